@@ -1,0 +1,119 @@
+"""Marshalling of Python shard lists into cfsec_shard arrays and back.
+
+A Go [][]byte becomes a Python list whose entries are 1-D uint8 buffers:
+numpy arrays (host memory, CFSEC_MEM_HOST) or torch uint8 tensors on a HIP
+device (CFSEC_MEM_DEVICE).  len(entry) == 0 or None marks a missing shard,
+as in KRS/reedsolomon.go:1416-1428.  Python buffers carry no Go capacity, so a
+missing entry is given a fresh zeroed buffer of the shard size before the call
+(what KRS does with AllocAligned when cap is short, reedsolomon.go:1514-1518,
+and ec.fillFullShards with make, encoder.go:199-210); after the call each
+list entry is re-sliced to the length the engine reported.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+
+
+def _is_torch(x) -> bool:
+    return type(x).__module__.startswith("torch")
+
+
+def _nbytes(x) -> int:
+    if x is None:
+        return 0
+    if _is_torch(x):
+        return x.numel() * x.element_size()
+    return int(x.size)
+
+
+def _ptr(x) -> int:
+    if _is_torch(x):
+        return x.data_ptr()
+    return x.ctypes.data
+
+
+class Marshal:
+    def __init__(self, shards, fill_size=None):
+        self.shards = shards
+        self.n = len(shards)
+        self.mem = None
+        self.like = None
+        for s in shards:
+            if s is not None and _nbytes(s) > 0:
+                kind = _lib.MEM_DEVICE if _is_torch(s) else _lib.MEM_HOST
+                if _is_torch(s) and not s.is_cuda:
+                    raise TypeError("torch shards must live on a HIP device")
+                if self.mem is None:
+                    self.mem, self.like = kind, s
+                elif self.mem != kind:
+                    raise TypeError("mixing host and device shards in one call")
+        if self.mem is None:
+            self.mem = _lib.MEM_HOST
+        self.arr = (_lib.Shard * max(self.n, 1))()
+        self.orig_len = []
+        self.alloc = {}
+        for i, s in enumerate(shards):
+            ln = _nbytes(s)
+            if s is not None and not _is_torch(s):
+                if s.dtype != np.uint8 or s.ndim != 1 or not s.flags.c_contiguous:
+                    raise TypeError("host shards must be 1-D contiguous uint8 numpy arrays")
+            if s is not None and _is_torch(s):
+                import torch
+                if s.dtype != torch.uint8 or s.dim() != 1 or not s.is_contiguous():
+                    raise TypeError("device shards must be 1-D contiguous uint8 tensors")
+            self.orig_len.append(ln)
+            if ln == 0 and fill_size:
+                buf = self._new(fill_size)
+                self.alloc[i] = buf
+                self.arr[i] = _lib.Shard(_ptr(buf), 0, fill_size)
+            elif ln == 0:
+                self.arr[i] = _lib.Shard(None, 0, 0)
+            else:
+                self.arr[i] = _lib.Shard(_ptr(s), ln, ln)
+
+    def _new(self, size):
+        if self.mem == _lib.MEM_DEVICE:
+            import torch
+            return torch.zeros(size, dtype=torch.uint8, device=self.like.device)
+        return np.zeros(size, np.uint8)
+
+    def ptr(self):
+        return self.arr
+
+    def writeback(self):
+        """Re-slice every entry to the length the engine left in its header."""
+        for i in range(self.n):
+            ln = self.arr[i].len
+            if ln == self.orig_len[i]:
+                continue
+            base = self.alloc.get(i)
+            if base is None:
+                base = self.shards[i]
+            if base is None:
+                continue
+            self.shards[i] = base[:ln]
+
+
+def shard_size(shards) -> int:
+    for s in shards:
+        ln = _nbytes(s)
+        if ln:
+            return ln
+    return 0
+
+
+def stream_ptr(stream):
+    if stream is None:
+        return None
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream  # torch.cuda.Stream
+
+
+def ptr_array(ptrs):
+    arr = (ctypes.c_void_p * len(ptrs))(*[int(p) for p in ptrs])
+    return arr

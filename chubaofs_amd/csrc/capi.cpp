@@ -1,0 +1,280 @@
+// capi.cpp -- extern "C" boundary declared in include/cfsec.h.
+#include <new>
+#include <vector>
+
+#include "engine.hpp"
+
+namespace cfsec {
+const char* last_error_cstr();
+}
+
+using cfsec::ECEncoder;
+using cfsec::RSEngine;
+
+struct cfsec_rs {
+  std::unique_ptr<RSEngine> e;
+};
+struct cfsec_ec {
+  std::unique_ptr<ECEncoder> e;
+};
+
+namespace {
+
+hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+template <class F>
+int guarded(F&& f) {
+  try {
+    return f();
+  } catch (const std::bad_alloc&) {
+    cfsec::set_last_error("host allocation failed");
+    return CFSEC_ERR_DEVICE;
+  } catch (...) {
+    cfsec::set_last_error("unexpected C++ exception");
+    return CFSEC_ERR_DEVICE;
+  }
+}
+
+// codemode.go:56-79 (the constCodeModeTactic table), keyed by the CodeMode values of
+// codemode.go:26-44.
+struct ModeRow {
+  int mode;
+  cfsec_tactic t;
+};
+const ModeRow kModes[] = {
+    {1, {15, 12, 0, 3, 24, 0, 2048}},   // EC15P12
+    {2, {6, 6, 0, 3, 11, 0, 2048}},     // EC6P6
+    {3, {16, 20, 2, 2, 34, 0, 2048}},   // EC16P20L2
+    {4, {6, 10, 2, 2, 14, 0, 2048}},    // EC6P10L2
+    {5, {6, 3, 3, 3, 9, 0, 2048}},      // EC6P3L3
+    {6, {6, 6, 0, 3, 11, 0, 0}},        // EC6P6Align0
+    {7, {6, 6, 0, 3, 11, 0, 512}},      // EC6P6Align512
+    {8, {4, 4, 2, 2, 6, 0, 2048}},      // EC4P4L2
+    {9, {12, 4, 0, 1, 15, 0, 2048}},    // EC12P4
+    {10, {16, 4, 0, 1, 19, 0, 2048}},   // EC16P4
+    {11, {3, 3, 0, 1, 5, 0, 2048}},     // EC3P3
+    {12, {10, 4, 0, 1, 13, 0, 2048}},   // EC10P4
+    {13, {6, 3, 0, 1, 8, 0, 2048}},     // EC6P3
+    {14, {12, 9, 0, 3, 20, 0, 2048}},   // EC12P9
+    {200, {6, 6, 9, 3, 11, 0, 2048}},   // EC6P6L9
+    {201, {6, 8, 10, 2, 13, 0, 0}},     // EC6P8L10
+};
+
+}  // namespace
+
+extern "C" {
+
+const char* cfsec_version(void) { return "cfsec 0.1.0 (gfx950)"; }
+
+const char* cfsec_last_error(void) { return cfsec::last_error_cstr(); }
+
+const char* cfsec_status_name(int status) {
+  switch (status) {
+    case CFSEC_OK: return "OK";
+    case CFSEC_ERR_TOO_FEW_SHARDS: return "ErrTooFewShards";
+    case CFSEC_ERR_SHARD_NO_DATA: return "ErrShardNoData";
+    case CFSEC_ERR_SHARD_SIZE: return "ErrShardSize";
+    case CFSEC_ERR_INV_SHARD_NUM: return "ErrInvShardNum";
+    case CFSEC_ERR_MAX_SHARD_NUM: return "ErrMaxShardNum";
+    case CFSEC_ERR_SHORT_DATA: return "ErrShortData";
+    case CFSEC_ERR_RECONSTRUCT_REQUIRED: return "ErrReconstructRequired";
+    case CFSEC_ERR_SINGULAR: return "errSingular";
+    case CFSEC_ERR_INVALID_CODE_MODE: return "ErrInvalidCodeMode";
+    case CFSEC_ERR_VERIFY: return "ErrVerify";
+    case CFSEC_ERR_INVALID_SHARDS: return "ErrInvalidShards";
+    case CFSEC_ERR_INVALID_ARG: return "ErrInvalidArg";
+    case CFSEC_ERR_DEVICE: return "ErrDevice";
+    case CFSEC_ERR_NOT_SUPPORTED: return "ErrNotSupported";
+    default: return "ErrUnknown";
+  }
+}
+
+int cfsec_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+// ---------------- reedsolomon.Encoder ----------------
+
+int cfsec_rs_new(int data_shards, int parity_shards, int device, cfsec_rs** out) {
+  if (!out) return CFSEC_ERR_INVALID_ARG;
+  *out = nullptr;
+  return guarded([&] {
+    std::unique_ptr<RSEngine> e;
+    int st = RSEngine::create(data_shards, parity_shards, device, &e);
+    if (st != CFSEC_OK) return st;
+    *out = new cfsec_rs{std::move(e)};
+    return (int)CFSEC_OK;
+  });
+}
+
+void cfsec_rs_free(cfsec_rs* h) { delete h; }
+
+int cfsec_rs_data_shards(const cfsec_rs* h) { return h ? h->e->k() : -1; }
+int cfsec_rs_parity_shards(const cfsec_rs* h) { return h ? h->e->m() : -1; }
+
+int cfsec_rs_matrix(const cfsec_rs* h, uint8_t* out, size_t out_len) {
+  if (!h || !out) return CFSEC_ERR_INVALID_ARG;
+  const auto& m = h->e->matrix();
+  if (out_len < m.v.size()) return CFSEC_ERR_INVALID_ARG;
+  std::copy(m.v.begin(), m.v.end(), out);
+  return CFSEC_OK;
+}
+
+int cfsec_rs_encode(cfsec_rs* h, cfsec_shard* shards, int n, int mem, void* stream) {
+  if (!h) return CFSEC_ERR_INVALID_ARG;
+  return guarded([&] { return h->e->encode(shards, n, mem, as_stream(stream)); });
+}
+
+int cfsec_rs_verify(cfsec_rs* h, cfsec_shard* shards, int n, int mem, void* stream, int* ok) {
+  if (!h || !ok) return CFSEC_ERR_INVALID_ARG;
+  return guarded([&] {
+    bool b = false;
+    int st = h->e->verify(shards, n, mem, as_stream(stream), &b);
+    *ok = b ? 1 : 0;
+    return st;
+  });
+}
+
+int cfsec_rs_reconstruct(cfsec_rs* h, cfsec_shard* shards, int n, int mem, void* stream) {
+  if (!h) return CFSEC_ERR_INVALID_ARG;
+  return guarded([&] { return h->e->reconstruct(shards, n, false, mem, as_stream(stream)); });
+}
+
+int cfsec_rs_reconstruct_data(cfsec_rs* h, cfsec_shard* shards, int n, int mem, void* stream) {
+  if (!h) return CFSEC_ERR_INVALID_ARG;
+  return guarded([&] { return h->e->reconstruct(shards, n, true, mem, as_stream(stream)); });
+}
+
+int cfsec_rs_split(cfsec_rs* h, uint8_t* data, size_t len, size_t cap, cfsec_shard* out,
+                   uint8_t* pad, size_t pad_len, size_t* pad_needed) {
+  if (!h) return CFSEC_ERR_INVALID_ARG;
+  return guarded([&] { return h->e->split(data, len, cap, out, pad, pad_len, pad_needed); });
+}
+
+int cfsec_rs_join(cfsec_rs* h, uint8_t* dst, size_t dst_len, const cfsec_shard* shards, int n,
+                  size_t out_size) {
+  if (!h || (!shards && n > 0)) return CFSEC_ERR_INVALID_ARG;
+  return guarded([&] { return h->e->join(dst, dst_len, shards, n, out_size); });
+}
+
+int cfsec_rs_encode_batch(cfsec_rs* h, uint8_t* const* ptrs, size_t shard_size, int nstripes,
+                          void* stream) {
+  if (!h) return CFSEC_ERR_INVALID_ARG;
+  return guarded([&] { return h->e->encode_batch(ptrs, shard_size, nstripes, as_stream(stream)); });
+}
+
+int cfsec_rs_verify_batch(cfsec_rs* h, uint8_t* const* ptrs, size_t shard_size, int nstripes,
+                          uint32_t* flags, void* stream) {
+  if (!h) return CFSEC_ERR_INVALID_ARG;
+  return guarded(
+      [&] { return h->e->verify_batch(ptrs, shard_size, nstripes, flags, as_stream(stream)); });
+}
+
+int cfsec_rs_reconstruct_batch(cfsec_rs* h, uint8_t* const* ptrs, size_t shard_size, int nstripes,
+                               const int* erased, int nerased, int data_only, void* stream) {
+  if (!h) return CFSEC_ERR_INVALID_ARG;
+  return guarded([&] {
+    return h->e->reconstruct_batch(ptrs, shard_size, nstripes, erased, nerased, data_only != 0,
+                                   as_stream(stream));
+  });
+}
+
+// ---------------- ec.Encoder ----------------
+
+int cfsec_codemode_tactic(int codemode, cfsec_tactic* t) {
+  if (!t) return CFSEC_ERR_INVALID_ARG;
+  for (const auto& r : kModes)
+    if (r.mode == codemode) {
+      *t = r.t;
+      return CFSEC_OK;
+    }
+  return CFSEC_ERR_INVALID_CODE_MODE;
+}
+
+int cfsec_ec_new(const cfsec_tactic* tactic, int enable_verify, int concurrency, int device,
+                 cfsec_ec** out) {
+  if (!out) return CFSEC_ERR_INVALID_ARG;
+  *out = nullptr;
+  if (!tactic) return CFSEC_ERR_INVALID_CODE_MODE;
+  return guarded([&] {
+    std::unique_ptr<ECEncoder> e;
+    int st = ECEncoder::create(*tactic, enable_verify != 0, concurrency, device, &e);
+    if (st != CFSEC_OK) return st;
+    *out = new cfsec_ec{std::move(e)};
+    return (int)CFSEC_OK;
+  });
+}
+
+void cfsec_ec_free(cfsec_ec* h) { delete h; }
+
+int cfsec_ec_encode(cfsec_ec* h, cfsec_shard* shards, int n, int mem, void* stream) {
+  if (!h) return CFSEC_ERR_INVALID_ARG;
+  return guarded([&] { return h->e->encode(shards, n, mem, as_stream(stream)); });
+}
+
+int cfsec_ec_reconstruct(cfsec_ec* h, cfsec_shard* shards, int n, const int* bad_idx, int nbad,
+                         int mem, void* stream) {
+  if (!h || (nbad > 0 && !bad_idx) || nbad < 0) return CFSEC_ERR_INVALID_ARG;
+  return guarded(
+      [&] { return h->e->reconstruct(shards, n, bad_idx, nbad, mem, as_stream(stream)); });
+}
+
+int cfsec_ec_reconstruct_data(cfsec_ec* h, cfsec_shard* shards, int n, const int* bad_idx,
+                              int nbad, int mem, void* stream) {
+  if (!h || (nbad > 0 && !bad_idx) || nbad < 0) return CFSEC_ERR_INVALID_ARG;
+  return guarded(
+      [&] { return h->e->reconstruct_data(shards, n, bad_idx, nbad, mem, as_stream(stream)); });
+}
+
+int cfsec_ec_verify(cfsec_ec* h, cfsec_shard* shards, int n, int mem, void* stream, int* ok) {
+  if (!h || !ok) return CFSEC_ERR_INVALID_ARG;
+  return guarded([&] {
+    bool b = false;
+    int st = h->e->verify(shards, n, mem, as_stream(stream), &b);
+    *ok = b ? 1 : 0;
+    return st;
+  });
+}
+
+int cfsec_ec_shards_in_idc(const cfsec_ec* h, int idx, int* out, int out_cap, int* count) {
+  if (!h || !count) return CFSEC_ERR_INVALID_ARG;
+  const std::vector<int> v = h->e->shards_in_idc(idx);
+  *count = (int)v.size();
+  if (out_cap < (int)v.size() || (!out && !v.empty())) return CFSEC_ERR_INVALID_ARG;
+  for (size_t i = 0; i < v.size(); ++i) out[i] = v[i];
+  return CFSEC_OK;
+}
+
+// ---------------- CRC32 ----------------
+
+int cfsec_crc32_ieee_batch(uint8_t* const* ptrs, size_t shard_size, int n, uint32_t* out,
+                           int device, void* stream) {
+  if ((!ptrs && n > 0) || !out || n < 0) return CFSEC_ERR_INVALID_ARG;
+  return guarded([&] {
+    if (device < 0 && hipGetDevice(&device) != hipSuccess) return (int)CFSEC_ERR_DEVICE;
+    cfsec::DeviceContext* ctx = cfsec::DeviceContext::get(device);
+    if (!ctx) {
+      cfsec::set_last_error("no HIP device available to the cfsec engine");
+      return (int)CFSEC_ERR_DEVICE;
+    }
+    cfsec::DeviceGuard g(device);
+    cfsec::DeviceContext::Workspace* ws = nullptr;
+    int st = ctx->acquire(0, (size_t)n, &ws);
+    if (st != CFSEC_OK) return st;
+    hipStream_t s = stream ? as_stream(stream) : ws->stream;
+    st = cfsec::hip_status(cfsec::launch_crc32(ptrs, shard_size, n, ws->dflags, s), "launch_crc32");
+    if (st == CFSEC_OK)
+      st = cfsec::hip_status(hipMemcpyAsync(ws->hflags, ws->dflags, 4 * (size_t)n, hipMemcpyDeviceToHost, s),
+                             "hipMemcpyAsync D2H");
+    const int sync = cfsec::hip_status(hipStreamSynchronize(s), "hipStreamSynchronize");
+    if (st == CFSEC_OK) st = sync;
+    if (st == CFSEC_OK)
+      for (int i = 0; i < n; ++i) out[i] = cfsec::crc32_finalize(ws->hflags[i], shard_size);
+    ctx->release(ws);
+    return st;
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,781 @@
+// engine.cpp -- RSEngine / ECEncoder / LrcEncoder host logic (see engine.hpp).
+#include "engine.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <unordered_map>
+
+namespace cfsec {
+
+namespace {
+thread_local std::string t_last_error;
+constexpr size_t kSlotAlign = 256;  // staging rows start on 256-B boundaries
+
+size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+// KRS/reedsolomon.go:1314-1339 checkShards / shardSize.
+Status check_shards(const cfsec_shard* shards, int n, bool nilok, size_t* size) {
+  size_t s = 0;
+  for (int i = 0; i < n; ++i)
+    if (shards[i].len != 0) {
+      s = shards[i].len;
+      break;
+    }
+  if (s == 0) return CFSEC_ERR_SHARD_NO_DATA;
+  for (int i = 0; i < n; ++i)
+    if (shards[i].len != s && (shards[i].len != 0 || !nilok)) return CFSEC_ERR_SHARD_SIZE;
+  *size = s;
+  return CFSEC_OK;
+}
+
+size_t first_size(const cfsec_shard* shards, int n) {
+  for (int i = 0; i < n; ++i)
+    if (shards[i].len != 0) return shards[i].len;
+  return 0;
+}
+
+// ec.fillFullShards (encoder.go:199-210).  Go allocates when cap is short; across the
+// C ABI the caller must hand in buffers with enough capacity.
+Status fill_full_shards(cfsec_shard* shards, int n) {
+  const size_t s = first_size(shards, n);
+  for (int i = 0; i < n; ++i)
+    if (shards[i].len == 0) {
+      if (s != 0 && (shards[i].cap < s || shards[i].data == nullptr)) {
+        set_last_error("fillFullShards: shard " + std::to_string(i) + " has cap < shard size");
+        return CFSEC_ERR_INVALID_ARG;
+      }
+      shards[i].len = s;
+    }
+  return CFSEC_OK;
+}
+
+// ec.initBadShards (encoder.go:182-188).
+Status init_bad_shards(cfsec_shard* shards, int n, const std::vector<int>& bad) {
+  for (int i : bad) {
+    if (i < 0 || i >= n) {
+      set_last_error("bad shard index out of range");
+      return CFSEC_ERR_INVALID_ARG;
+    }
+    if (shards[i].data != nullptr && shards[i].len != 0 && shards[i].cap > 0) shards[i].len = 0;
+  }
+  return CFSEC_OK;
+}
+
+// codemode.Tactic.IsValid (codemode.go:267-271).
+bool tactic_valid(const cfsec_tactic& t) {
+  return t.n > 0 && t.m > 0 && t.l >= 0 && t.az_count > 0 && t.put_quorum > 0 &&
+         t.get_quorum >= 0 && t.min_shard_size >= 0 && t.n % t.az_count == 0 &&
+         t.m % t.az_count == 0 && t.l % t.az_count == 0;
+}
+
+// codemode.Tactic.GetECLayoutByAZ (codemode.go:274-291).
+std::vector<std::vector<int>> layout_by_az(const cfsec_tactic& t) {
+  std::vector<std::vector<int>> az(t.az_count);
+  const int n = t.n / t.az_count, m = t.m / t.az_count, l = t.l / t.az_count;
+  for (int idx = 0; idx < t.az_count; ++idx) {
+    for (int i = 0; i < n; ++i) az[idx].push_back(idx * n + i);
+    for (int i = 0; i < m; ++i) az[idx].push_back(t.n + idx * m + i);
+    for (int i = 0; i < l; ++i) az[idx].push_back(t.n + t.m + idx * l + i);
+  }
+  return az;
+}
+}  // namespace
+
+void set_last_error(const std::string& msg) { t_last_error = msg; }
+const char* last_error_cstr() { return t_last_error.c_str(); }
+
+Status hip_status(hipError_t e, const char* what) {
+  if (e == hipSuccess) return CFSEC_OK;
+  set_last_error(std::string(what) + ": " + hipGetErrorString(e));
+  return CFSEC_ERR_DEVICE;
+}
+
+// ---------------------------------------------------------------- devices
+
+DeviceGuard::DeviceGuard(int device) {
+  if (hipGetDevice(&prev_) != hipSuccess) return;
+  if (prev_ != device && hipSetDevice(device) != hipSuccess) return;
+  ok_ = true;
+}
+DeviceGuard::~DeviceGuard() {
+  if (ok_) {
+    int cur = -1;
+    if (hipGetDevice(&cur) == hipSuccess && cur != prev_) (void)hipSetDevice(prev_);
+  }
+}
+
+DeviceContext* DeviceContext::get(int device) {
+  static std::mutex mu;
+  static std::unordered_map<int, std::unique_ptr<DeviceContext>> ctxs;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count) return nullptr;
+  std::lock_guard<std::mutex> l(mu);
+  auto& p = ctxs[device];
+  if (!p) p.reset(new DeviceContext(device));
+  return p.get();
+}
+
+Status DeviceContext::acquire(size_t bytes, size_t nflags, Workspace** out) {
+  Workspace* ws = nullptr;
+  {
+    std::lock_guard<std::mutex> l(mu_);
+    // best fit among the free workspaces
+    auto best = free_.end();
+    for (auto it = free_.begin(); it != free_.end(); ++it)
+      if ((*it)->cap >= bytes && (*it)->nflags >= nflags &&
+          (best == free_.end() || (*it)->cap < (*best)->cap))
+        best = it;
+    if (best == free_.end() && !free_.empty()) best = free_.begin();
+    if (best != free_.end()) {
+      ws = *best;
+      free_.erase(best);
+    } else {
+      all_.emplace_back(new Workspace());
+      ws = all_.back().get();
+    }
+  }
+  DeviceGuard g(device_);
+  if (!g.ok()) {
+    release(ws);
+    return hip_status(hipErrorInvalidDevice, "hipSetDevice");
+  }
+  Status st = CFSEC_OK;
+  if (!ws->stream) st = hip_status(hipStreamCreateWithFlags(&ws->stream, hipStreamNonBlocking), "hipStreamCreate");
+  if (st == CFSEC_OK && ws->cap < bytes) {
+    if (ws->dbuf) (void)hipFree(ws->dbuf);
+    ws->dbuf = nullptr;
+    ws->cap = 0;
+    st = hip_status(hipMalloc(reinterpret_cast<void**>(&ws->dbuf), bytes), "hipMalloc(staging)");
+    if (st == CFSEC_OK) ws->cap = bytes;
+  }
+  if (st == CFSEC_OK && ws->nflags < nflags) {
+    const size_t nf = std::max<size_t>(nflags, 64);
+    if (ws->dflags) (void)hipFree(ws->dflags);
+    if (ws->hflags) (void)hipHostFree(ws->hflags);
+    ws->dflags = nullptr;
+    ws->hflags = nullptr;
+    ws->nflags = 0;
+    st = hip_status(hipMalloc(reinterpret_cast<void**>(&ws->dflags), nf * 4), "hipMalloc(flags)");
+    if (st == CFSEC_OK)
+      st = hip_status(hipHostMalloc(reinterpret_cast<void**>(&ws->hflags), nf * 4, hipHostMallocDefault),
+                      "hipHostMalloc(flags)");
+    if (st == CFSEC_OK) ws->nflags = nf;
+  }
+  if (st != CFSEC_OK) {
+    release(ws);
+    return st;
+  }
+  *out = ws;
+  return CFSEC_OK;
+}
+
+void DeviceContext::release(Workspace* ws) {
+  std::lock_guard<std::mutex> l(mu_);
+  free_.push_back(ws);
+}
+
+// ---------------------------------------------------------------- inversion cache
+
+bool InversionCache::get(const std::vector<int>& invalid, Matrix* out) const {
+  std::shared_lock<std::shared_mutex> l(mu_);
+  auto it = map_.find(invalid);
+  if (it == map_.end()) return false;
+  *out = it->second;
+  return true;
+}
+
+void InversionCache::put(const std::vector<int>& invalid, const Matrix& m) {
+  std::unique_lock<std::shared_mutex> l(mu_);
+  map_.emplace(invalid, m);
+}
+
+// ---------------------------------------------------------------- RSEngine
+
+Status RSEngine::create(int k, int m, int device, std::unique_ptr<RSEngine>* out) {
+  // KRS/reedsolomon.go:413-447.  More than 256 shards switches the reference to its
+  // leopard GF(2^16) codec, which CubeFS never reaches (max 38 shards).
+  if (k + m > 256) return CFSEC_ERR_NOT_SUPPORTED;
+  if (k <= 0 || m < 0) return CFSEC_ERR_INV_SHARD_NUM;
+  std::unique_ptr<RSEngine> e(new RSEngine());
+  e->k_ = k;
+  e->m_ = m;
+  if (m > 0) {
+    if (!build_matrix(k, k + m, e->mat_)) return CFSEC_ERR_SINGULAR;
+  } else {
+    e->mat_ = Matrix(k, k);
+    for (int i = 0; i < k; ++i) e->mat_.at(i, i) = 1;
+  }
+  e->parity_ = Matrix(m, k);
+  for (int r = 0; r < m; ++r)
+    for (int c = 0; c < k; ++c) e->parity_.at(r, c) = e->mat_.at(k + r, c);
+  if (device < 0) {
+    int cur = 0;
+    int count = 0;
+    if (hipGetDeviceCount(&count) == hipSuccess && count > 0 && hipGetDevice(&cur) == hipSuccess)
+      device = cur;
+  }
+  // A missing device is reported by the first call that needs it (CFSEC_ERR_DEVICE); the
+  // host-only methods (matrix, Split, Join) work without one.
+  e->ctx_ = device >= 0 ? DeviceContext::get(device) : nullptr;
+  *out = std::move(e);
+  return CFSEC_OK;
+}
+
+Status RSEngine::run(const Matrix& rows, const std::vector<cfsec_shard*>& ins,
+                     const std::vector<cfsec_shard*>& outs, size_t S, int mem, hipStream_t stream,
+                     MatVecMode mode, bool* ok) {
+  if (ok) *ok = true;
+  if (outs.empty() || S == 0) return CFSEC_OK;
+  if (!ctx_) {
+    set_last_error("no HIP device available to the cfsec engine");
+    return CFSEC_ERR_DEVICE;
+  }
+  if (mem != CFSEC_MEM_HOST && mem != CFSEC_MEM_DEVICE) return CFSEC_ERR_INVALID_ARG;
+  for (auto* s : ins)
+    if (!s->data) return CFSEC_ERR_INVALID_ARG;
+  for (auto* s : outs)
+    if (!s->data) return CFSEC_ERR_INVALID_ARG;
+  const int nin = (int)ins.size(), nout = (int)outs.size();
+  if (rows.rows != nout || rows.cols != nin) return CFSEC_ERR_INVALID_ARG;
+
+  DeviceGuard g(ctx_->device());
+  if (!g.ok()) return hip_status(hipErrorInvalidDevice, "hipSetDevice");
+
+  const bool verify = mode == MatVecMode::kVerify;
+  const bool host = mem == CFSEC_MEM_HOST;
+  const size_t slot = align_up(S, kSlotAlign);
+  // Verify with more inputs than one launch carries: compute into staging, then compare.
+  const bool two_step_verify = verify && nin > 32;
+  size_t staging = host ? slot * size_t(nin + nout) : 0;
+  if (two_step_verify) staging += slot * size_t(nout);
+
+  DeviceContext::Workspace* ws = nullptr;
+  Status st = ctx_->acquire(staging, 1, &ws);
+  if (st != CFSEC_OK) return st;
+  hipStream_t s = (host || !stream) ? ws->stream : stream;
+
+  std::vector<const uint8_t*> din(nin);
+  std::vector<uint8_t*> dout(nout);
+  for (int i = 0; i < nin; ++i) {
+    if (host) {
+      din[i] = ws->dbuf + slot * i;
+      if (st == CFSEC_OK)
+        st = hip_status(hipMemcpyAsync(const_cast<uint8_t*>(din[i]), ins[i]->data, S, hipMemcpyHostToDevice, s),
+                        "hipMemcpyAsync H2D");
+    } else {
+      din[i] = ins[i]->data;
+    }
+  }
+  for (int r = 0; r < nout; ++r) {
+    if (host) {
+      dout[r] = ws->dbuf + slot * (nin + r);
+      if (st == CFSEC_OK && mode != MatVecMode::kStore)
+        st = hip_status(hipMemcpyAsync(dout[r], outs[r]->data, S, hipMemcpyHostToDevice, s),
+                        "hipMemcpyAsync H2D");
+    } else {
+      dout[r] = outs[r]->data;
+    }
+  }
+  if (st == CFSEC_OK && verify) st = hip_status(hipMemsetAsync(ws->dflags, 0, 4, s), "hipMemsetAsync");
+  if (st == CFSEC_OK) {
+    MatVecJob job;
+    job.k = nin;
+    job.m = nout;
+    job.coef = rows.v.data();
+    job.len = S;
+    job.nstripes = 1;
+    job.in = din.data();
+    job.flags = ws->dflags;
+    if (!two_step_verify) {
+      job.out = dout.data();
+      job.mode = mode;
+      st = hip_status(launch_matvec(job, s), "launch_matvec");
+    } else {
+      uint8_t* tmp0 = ws->dbuf + (host ? slot * size_t(nin + nout) : 0);
+      std::vector<uint8_t*> tmp(nout);
+      for (int r = 0; r < nout; ++r) tmp[r] = tmp0 + slot * r;
+      job.out = tmp.data();
+      job.mode = MatVecMode::kStore;
+      st = hip_status(launch_matvec(job, s), "launch_matvec");
+      if (st == CFSEC_OK) {
+        Matrix ident(nout, nout);
+        for (int r = 0; r < nout; ++r) ident.at(r, r) = 1;
+        std::vector<const uint8_t*> tin(tmp.begin(), tmp.end());
+        MatVecJob cmp = job;
+        cmp.k = nout;
+        cmp.coef = ident.v.data();
+        cmp.in = tin.data();
+        cmp.out = dout.data();
+        cmp.mode = MatVecMode::kVerify;
+        st = hip_status(launch_matvec(cmp, s), "launch_matvec(verify)");
+      }
+    }
+  }
+  if (st == CFSEC_OK && verify)
+    st = hip_status(hipMemcpyAsync(ws->hflags, ws->dflags, 4, hipMemcpyDeviceToHost, s), "hipMemcpyAsync D2H");
+  if (st == CFSEC_OK && host && !verify)
+    for (int r = 0; r < nout && st == CFSEC_OK; ++r)
+      st = hip_status(hipMemcpyAsync(outs[r]->data, dout[r], S, hipMemcpyDeviceToHost, s), "hipMemcpyAsync D2H");
+  const Status sync = hip_status(hipStreamSynchronize(s), "hipStreamSynchronize");
+  if (st == CFSEC_OK) st = sync;
+  if (st == CFSEC_OK && verify && ok) *ok = ws->hflags[0] == 0;
+  ctx_->release(ws);
+  return st;
+}
+
+Status RSEngine::encode(cfsec_shard* shards, int n, int mem, hipStream_t stream) {
+  if (!shards || n != total()) return CFSEC_ERR_TOO_FEW_SHARDS;
+  size_t S = 0;
+  Status st = check_shards(shards, n, false, &S);
+  if (st != CFSEC_OK) return st;
+  std::vector<cfsec_shard*> ins, outs;
+  for (int i = 0; i < k_; ++i) ins.push_back(&shards[i]);
+  for (int i = k_; i < n; ++i) outs.push_back(&shards[i]);
+  return run(parity_, ins, outs, S, mem, stream, MatVecMode::kStore, nullptr);
+}
+
+Status RSEngine::verify(cfsec_shard* shards, int n, int mem, hipStream_t stream, bool* ok) {
+  *ok = false;
+  if (!shards || n != total()) return CFSEC_ERR_TOO_FEW_SHARDS;
+  size_t S = 0;
+  Status st = check_shards(shards, n, false, &S);
+  if (st != CFSEC_OK) return st;
+  std::vector<cfsec_shard*> ins, outs;
+  for (int i = 0; i < k_; ++i) ins.push_back(&shards[i]);
+  for (int i = k_; i < n; ++i) outs.push_back(&shards[i]);
+  return run(parity_, ins, outs, S, mem, stream, MatVecMode::kVerify, ok);
+}
+
+Status RSEngine::plan_reconstruct(const std::vector<bool>& present, bool data_only, ReconPlan* plan) {
+  // KRS/reedsolomon.go:1453-1501: first k present rows in index order; cache key is
+  // the invalid rows met before the k-th valid one.
+  std::vector<int> invalid;
+  plan->valid.clear();
+  for (int row = 0; row < total() && (int)plan->valid.size() < k_; ++row) {
+    if (present[row]) plan->valid.push_back(row);
+    else invalid.push_back(row);
+  }
+  if ((int)plan->valid.size() < k_) return CFSEC_ERR_TOO_FEW_SHARDS;
+  Matrix dec;
+  if (!tree_.get(invalid, &dec)) {
+    Matrix sub(k_, k_);
+    for (int r = 0; r < k_; ++r)
+      for (int c = 0; c < k_; ++c) sub.at(r, c) = mat_.at(plan->valid[r], c);
+    if (!mat_invert(sub, dec)) return CFSEC_ERR_SINGULAR;
+    tree_.put(invalid, dec);
+  }
+  // Missing data rows: rows of inv(sub) (:1508-1524).  Missing parity rows: the
+  // reference recomputes them from all data shards (:1537-1550); the same linear map
+  // over the k survivors is parity_row x inv(sub), so one fused pass is bit-exact.
+  plan->outputs.clear();
+  std::vector<const uint8_t*> rowsrc;
+  for (int i = 0; i < k_; ++i)
+    if (!present[i]) plan->outputs.push_back(i);
+  if (!data_only)
+    for (int i = k_; i < total(); ++i)
+      if (!present[i]) plan->outputs.push_back(i);
+  plan->rows = Matrix((int)plan->outputs.size(), k_);
+  const GF& gf = GF::get();
+  for (size_t o = 0; o < plan->outputs.size(); ++o) {
+    const int idx = plan->outputs[o];
+    uint8_t* dst = plan->rows.row((int)o);
+    if (idx < k_) {
+      std::memcpy(dst, dec.row(idx), k_);
+    } else {
+      const uint8_t* p = parity_.row(idx - k_);
+      for (int c = 0; c < k_; ++c) {
+        uint8_t v = 0;
+        for (int j = 0; j < k_; ++j) v ^= gf.mul(p[j], dec.at(j, c));
+        dst[c] = v;
+      }
+    }
+  }
+  return CFSEC_OK;
+}
+
+Status RSEngine::reconstruct(cfsec_shard* shards, int n, bool data_only, int mem, hipStream_t stream) {
+  if (!shards || n != total()) return CFSEC_ERR_TOO_FEW_SHARDS;
+  size_t S = 0;
+  Status st = check_shards(shards, n, true, &S);
+  if (st != CFSEC_OK) return st;
+  std::vector<bool> present(n);
+  int npresent = 0, dpresent = 0;
+  for (int i = 0; i < n; ++i) {
+    present[i] = shards[i].len != 0;
+    if (present[i]) {
+      ++npresent;
+      if (i < k_) ++dpresent;
+    }
+  }
+  if (npresent == n || (data_only && dpresent == k_)) return CFSEC_OK;
+  if (npresent < k_) return CFSEC_ERR_TOO_FEW_SHARDS;
+  ReconPlan plan;
+  st = plan_reconstruct(present, data_only, &plan);
+  if (st != CFSEC_OK) return st;
+  for (int idx : plan.outputs)
+    if (!shards[idx].data || shards[idx].cap < S) {
+      set_last_error("reconstruct: missing shard " + std::to_string(idx) + " has cap < shard size");
+      return CFSEC_ERR_INVALID_ARG;
+    }
+  std::vector<cfsec_shard*> ins, outs;
+  for (int v : plan.valid) ins.push_back(&shards[v]);
+  for (int o : plan.outputs) outs.push_back(&shards[o]);
+  for (auto* o : outs) o->len = S;  // KRS/reedsolomon.go:1514-1518: shards[i] = shards[i][0:S]
+  return run(plan.rows, ins, outs, S, mem, stream, MatVecMode::kStore, nullptr);
+}
+
+Status RSEngine::split(uint8_t* data, size_t len, size_t cap, cfsec_shard* out, uint8_t* pad,
+                       size_t pad_len, size_t* pad_needed) {
+  // KRS/reedsolomon.go:1574-1632
+  if (pad_needed) *pad_needed = 0;
+  if (len == 0) return CFSEC_ERR_SHORT_DATA;
+  if (!data || !out) return CFSEC_ERR_INVALID_ARG;
+  if (cap < len) cap = len;
+  const int tot = total();
+  if (tot == 1) {
+    out[0] = cfsec_shard{data, len, cap};
+    return CFSEC_OK;
+  }
+  const size_t per = (len + k_ - 1) / k_;
+  const size_t need_total = per * tot;
+  size_t eff = len;
+  if (cap > len) {
+    eff = std::min(cap, need_total);
+    std::memset(data + len, 0, eff - len);
+  }
+  const size_t full = std::min<size_t>(eff / per, tot);
+  const size_t npad = tot - full;
+  if (pad_needed) *pad_needed = npad * per;
+  if (npad > 0 && (!pad || pad_len < npad * per)) return CFSEC_ERR_INVALID_ARG;
+  if (npad > 0) {
+    std::memset(pad, 0, npad * per);
+    if (len > per * full) std::memcpy(pad, data + per * full, len - per * full);
+  }
+  for (size_t i = 0; i < full; ++i) out[i] = cfsec_shard{data + i * per, per, per};
+  for (size_t j = 0; j < npad; ++j) out[full + j] = cfsec_shard{pad + j * per, per, per};
+  return CFSEC_OK;
+}
+
+Status RSEngine::join(uint8_t* dst, size_t dst_len, const cfsec_shard* shards, int n, size_t out_size) {
+  // KRS/reedsolomon.go:1646-1684
+  if (n < k_) return CFSEC_ERR_TOO_FEW_SHARDS;
+  size_t size = 0;
+  for (int i = 0; i < k_; ++i) {
+    if (shards[i].data == nullptr) return CFSEC_ERR_RECONSTRUCT_REQUIRED;
+    size += shards[i].len;
+    if (size >= out_size) break;
+  }
+  if (size < out_size) return CFSEC_ERR_SHORT_DATA;
+  if (!dst || dst_len < out_size) return CFSEC_ERR_INVALID_ARG;
+  size_t write = out_size;
+  for (int i = 0; i < k_ && write > 0; ++i) {
+    const size_t c = std::min(write, shards[i].len);
+    std::memcpy(dst + (out_size - write), shards[i].data, c);
+    write -= c;
+  }
+  return CFSEC_OK;
+}
+
+Status RSEngine::encode_batch(uint8_t* const* ptrs, size_t S, int nstripes, hipStream_t stream) {
+  if (!ctx_) return CFSEC_ERR_DEVICE;
+  if (!ptrs || nstripes < 0) return CFSEC_ERR_INVALID_ARG;
+  if (m_ == 0 || nstripes == 0 || S == 0) return CFSEC_OK;
+  std::vector<const uint8_t*> in(size_t(nstripes) * k_);
+  std::vector<uint8_t*> out(size_t(nstripes) * m_);
+  for (int s = 0; s < nstripes; ++s) {
+    for (int c = 0; c < k_; ++c) in[size_t(s) * k_ + c] = ptrs[size_t(s) * total() + c];
+    for (int r = 0; r < m_; ++r) out[size_t(s) * m_ + r] = ptrs[size_t(s) * total() + k_ + r];
+  }
+  DeviceGuard g(ctx_->device());
+  MatVecJob job;
+  job.k = k_;
+  job.m = m_;
+  job.coef = parity_.v.data();
+  job.len = S;
+  job.nstripes = nstripes;
+  job.in = in.data();
+  job.out = out.data();
+  return hip_status(launch_matvec(job, stream), "launch_matvec(encode_batch)");
+}
+
+Status RSEngine::verify_batch(uint8_t* const* ptrs, size_t S, int nstripes, uint32_t* flags,
+                              hipStream_t stream) {
+  if (!ctx_) return CFSEC_ERR_DEVICE;
+  if (!ptrs || !flags || nstripes < 0) return CFSEC_ERR_INVALID_ARG;
+  if (m_ == 0 || nstripes == 0 || S == 0) return CFSEC_OK;
+  if (k_ > 32) return CFSEC_ERR_NOT_SUPPORTED;
+  std::vector<const uint8_t*> in(size_t(nstripes) * k_);
+  std::vector<uint8_t*> out(size_t(nstripes) * m_);
+  for (int s = 0; s < nstripes; ++s) {
+    for (int c = 0; c < k_; ++c) in[size_t(s) * k_ + c] = ptrs[size_t(s) * total() + c];
+    for (int r = 0; r < m_; ++r) out[size_t(s) * m_ + r] = ptrs[size_t(s) * total() + k_ + r];
+  }
+  DeviceGuard g(ctx_->device());
+  MatVecJob job;
+  job.k = k_;
+  job.m = m_;
+  job.coef = parity_.v.data();
+  job.len = S;
+  job.nstripes = nstripes;
+  job.in = in.data();
+  job.out = out.data();
+  job.mode = MatVecMode::kVerify;
+  job.flags = flags;
+  return hip_status(launch_matvec(job, stream), "launch_matvec(verify_batch)");
+}
+
+Status RSEngine::reconstruct_batch(uint8_t* const* ptrs, size_t S, int nstripes, const int* erased,
+                                   int nerased, bool data_only, hipStream_t stream) {
+  if (!ctx_) return CFSEC_ERR_DEVICE;
+  if (!ptrs || nstripes < 0 || nerased < 0 || (nerased > 0 && !erased)) return CFSEC_ERR_INVALID_ARG;
+  std::vector<bool> present(total(), true);
+  for (int i = 0; i < nerased; ++i) {
+    if (erased[i] < 0 || erased[i] >= total()) return CFSEC_ERR_INVALID_ARG;
+    present[erased[i]] = false;
+  }
+  int np = 0, dp = 0;
+  for (int i = 0; i < total(); ++i)
+    if (present[i]) {
+      ++np;
+      if (i < k_) ++dp;
+    }
+  if (np == total() || (data_only && dp == k_) || nstripes == 0 || S == 0) return CFSEC_OK;
+  if (np < k_) return CFSEC_ERR_TOO_FEW_SHARDS;
+  ReconPlan plan;
+  Status st = plan_reconstruct(present, data_only, &plan);
+  if (st != CFSEC_OK) return st;
+  const int nout = (int)plan.outputs.size();
+  std::vector<const uint8_t*> in(size_t(nstripes) * k_);
+  std::vector<uint8_t*> out(size_t(nstripes) * nout);
+  for (int s = 0; s < nstripes; ++s) {
+    for (int c = 0; c < k_; ++c) in[size_t(s) * k_ + c] = ptrs[size_t(s) * total() + plan.valid[c]];
+    for (int r = 0; r < nout; ++r) out[size_t(s) * nout + r] = ptrs[size_t(s) * total() + plan.outputs[r]];
+  }
+  DeviceGuard g(ctx_->device());
+  MatVecJob job;
+  job.k = k_;
+  job.m = nout;
+  job.coef = plan.rows.v.data();
+  job.len = S;
+  job.nstripes = nstripes;
+  job.in = in.data();
+  job.out = out.data();
+  return hip_status(launch_matvec(job, stream), "launch_matvec(reconstruct_batch)");
+}
+
+// ---------------------------------------------------------------- ec.Encoder
+
+Status ECEncoder::create(const cfsec_tactic& t, bool enable_verify, int concurrency, int device,
+                         std::unique_ptr<ECEncoder>* out) {
+  // ec.NewEncoder, encoder.go:78-112
+  if (!tactic_valid(t)) return CFSEC_ERR_INVALID_CODE_MODE;
+  if (concurrency <= 0) concurrency = 100;  // defaultConcurrency, encoder.go:29
+  std::unique_ptr<RSEngine> engine;
+  Status st = RSEngine::create(t.n, t.m, device, &engine);
+  if (st != CFSEC_OK) return st;
+  std::unique_ptr<ECEncoder> enc;
+  if (t.l != 0) {
+    std::unique_ptr<RSEngine> local;
+    const int ln = (t.n + t.m) / t.az_count, lm = t.l / t.az_count;
+    st = RSEngine::create(ln, lm, device, &local);
+    if (st != CFSEC_OK) return st;
+    auto* lrc = new LrcEncoder();
+    // Fused LRC encode rows: global parity, then every AZ's local parity expressed over
+    // the N data shards (local parity = localRow x [AZ data, AZ global parity], and the
+    // global parity is itself parity_row x data).
+    const Matrix& G = engine->matrix();
+    const Matrix& Lm = local->matrix();
+    lrc->fused_ = Matrix(t.m + t.l, t.n);
+    for (int r = 0; r < t.m; ++r)
+      for (int c = 0; c < t.n; ++c) lrc->fused_.at(r, c) = G.at(t.n + r, c);
+    const GF& gf = GF::get();
+    const auto az = layout_by_az(t);
+    for (int a = 0; a < t.az_count; ++a)
+      for (int j = 0; j < lm; ++j) {
+        const int g = t.n + t.m + a * lm + j;
+        uint8_t* dst = lrc->fused_.row(t.m + (g - t.n - t.m));
+        for (int i = 0; i < ln; ++i) {
+          const uint8_t coef = Lm.at(ln + j, i);
+          const int member = az[a][i];
+          for (int c = 0; c < t.n; ++c) {
+            const uint8_t basis = member < t.n ? uint8_t(member == c) : G.at(member, c);
+            dst[c] ^= gf.mul(coef, basis);
+          }
+        }
+      }
+    lrc->local_ = std::move(local);
+    enc.reset(lrc);
+  } else {
+    enc.reset(new ECEncoder());
+  }
+  enc->t_ = t;
+  enc->enable_verify_ = enable_verify;
+  enc->pool_.reset(new BlockingCount(concurrency));
+  enc->engine_ = std::move(engine);
+  *out = std::move(enc);
+  return CFSEC_OK;
+}
+
+Status ECEncoder::encode(cfsec_shard* shards, int n, int mem, hipStream_t s) {
+  Slot slot(pool_.get());  // encoder.go:114-131
+  Status st = engine_->encode(shards, n, mem, s);
+  if (st != CFSEC_OK) return st;
+  if (enable_verify_) {
+    bool ok = false;
+    st = engine_->verify(shards, n, mem, s, &ok);
+    if (st != CFSEC_OK) return st;
+    if (!ok) return CFSEC_ERR_VERIFY;
+  }
+  return CFSEC_OK;
+}
+
+Status ECEncoder::verify(cfsec_shard* shards, int n, int mem, hipStream_t s, bool* ok) {
+  Slot slot(pool_.get());  // encoder.go:133-137
+  return engine_->verify(shards, n, mem, s, ok);
+}
+
+Status ECEncoder::reconstruct(cfsec_shard* shards, int n, const int* bad, int nbad, int mem,
+                              hipStream_t s) {
+  // encoder.go:139-144
+  Status st = init_bad_shards(shards, n, std::vector<int>(bad, bad + nbad));
+  if (st != CFSEC_OK) return st;
+  Slot slot(pool_.get());
+  return engine_->reconstruct(shards, n, false, mem, s);
+}
+
+Status ECEncoder::reconstruct_data(cfsec_shard* shards, int n, const int* bad, int nbad, int mem,
+                                   hipStream_t s) {
+  // encoder.go:146-151
+  Status st = init_bad_shards(shards, n, std::vector<int>(bad, bad + nbad));
+  if (st != CFSEC_OK) return st;
+  Slot slot(pool_.get());
+  return engine_->reconstruct(shards, n, true, mem, s);
+}
+
+std::vector<int> ECEncoder::shards_in_idc(int idx) const {
+  // encoder.go:169-176
+  std::vector<int> v;
+  const int ln = t_.n / t_.az_count, lm = t_.m / t_.az_count;
+  for (int i = idx * ln; i < (idx + 1) * ln; ++i) v.push_back(i);
+  for (int i = t_.n + lm * idx; i < t_.n + lm * (idx + 1); ++i) v.push_back(i);
+  return v;
+}
+
+// ---------------------------------------------------------------- lrcEncoder
+
+std::vector<int> LrcEncoder::shards_in_idc(int idx) const {
+  // lrcencoder.go:236-243 via codemode.LocalStripeInAZ (codemode.go:334-345)
+  if (idx < 0 || idx >= t_.az_count) return {};
+  return layout_by_az(t_)[idx];
+}
+
+Status LrcEncoder::encode(cfsec_shard* shards, int n, int mem, hipStream_t s) {
+  // lrcencoder.go:35-82
+  const int N = t_.n, M = t_.m, L = t_.l;
+  if (!shards || n != N + M + L) return CFSEC_ERR_INVALID_SHARDS;
+  Slot slot(pool_.get());
+  Status st = fill_full_shards(shards, n);
+  if (st != CFSEC_OK) return st;
+  size_t S = 0;
+  st = check_shards(shards, N + M, false, &S);  // global engine.Encode's checkShards
+  if (st != CFSEC_OK) return st;
+  Status local_err = CFSEC_OK;
+  for (int a = 0; a < t_.az_count && local_err == CFSEC_OK; ++a) {
+    std::vector<cfsec_shard> ls;
+    for (int g : shards_in_idc(a)) ls.push_back(shards[g]);
+    size_t ignored;
+    local_err = check_shards(ls.data(), (int)ls.size(), false, &ignored);
+  }
+  std::vector<cfsec_shard*> ins, outs;
+  for (int i = 0; i < N; ++i) ins.push_back(&shards[i]);
+  if (local_err != CFSEC_OK) {
+    // global parity is written before the local engine reports its error
+    st = engine_->encode(shards, N + M, mem, s);
+    return st != CFSEC_OK ? st : local_err;
+  }
+  for (int i = N; i < N + M + L; ++i) outs.push_back(&shards[i]);
+  st = engine_->run(fused_, ins, outs, S, mem, s, MatVecMode::kStore, nullptr);
+  if (st != CFSEC_OK) return st;
+  if (enable_verify_) {
+    bool ok = false;
+    st = engine_->run(fused_, ins, outs, S, mem, s, MatVecMode::kVerify, &ok);
+    if (st != CFSEC_OK) return st;
+    if (!ok) return CFSEC_ERR_VERIFY;
+  }
+  return CFSEC_OK;
+}
+
+Status LrcEncoder::verify(cfsec_shard* shards, int n, int mem, hipStream_t s, bool* ok) {
+  // lrcencoder.go:89-131
+  *ok = false;
+  Slot slot(pool_.get());
+  const int N = t_.n, M = t_.m, L = t_.l;
+  if (n == (N + M + L) / t_.az_count) return local_->verify(shards, n, mem, s, ok);
+  if (!shards || n != N + M + L) return CFSEC_ERR_INVALID_SHARDS;
+  Status st = engine_->verify(shards, N + M, mem, s, ok);
+  if (st != CFSEC_OK || !*ok) return st;
+  for (int a = 0; a < t_.az_count; ++a) {
+    std::vector<cfsec_shard> ls;
+    for (int g : shards_in_idc(a)) ls.push_back(shards[g]);
+    st = local_->verify(ls.data(), (int)ls.size(), mem, s, ok);
+    if (st != CFSEC_OK || !*ok) return st;
+  }
+  *ok = true;
+  return CFSEC_OK;
+}
+
+Status LrcEncoder::reconstruct(cfsec_shard* shards, int n, const int* bad, int nbad, int mem,
+                               hipStream_t s) {
+  // lrcencoder.go:133-186
+  const int N = t_.n, M = t_.m, L = t_.l, AZ = t_.az_count;
+  if (!shards || n <= 0) return CFSEC_ERR_INVALID_SHARDS;
+  Status st = fill_full_shards(shards, n);
+  if (st != CFSEC_OK) return st;
+  std::vector<int> global_bad;
+  for (int i = 0; i < nbad; ++i)
+    if (bad[i] < N + M) global_bad.push_back(bad[i]);
+  st = init_bad_shards(shards, n, global_bad);
+  if (st != CFSEC_OK) return st;
+  Slot slot(pool_.get());
+  if (n == (N + M + L) / AZ) return local_->reconstruct(shards, n, false, mem, s);
+  if (n != N + M + L) return CFSEC_ERR_INVALID_SHARDS;
+  st = engine_->reconstruct(shards, N + M, false, mem, s);
+  if (st != CFSEC_OK) return st;
+  std::map<int, std::vector<int>> local_bad;
+  for (int i = 0; i < nbad; ++i) {
+    const int b = bad[i];
+    if (b >= N + M) {
+      const int idc = (b - N - M) * AZ / L;
+      local_bad[idc].push_back(b - N - M - L / AZ * idc + (N + M) / AZ);
+    }
+  }
+  for (auto& kv : local_bad) {
+    // Go copies the slice headers into a fresh [][]byte (lrcencoder.go:236-243); the
+    // rebuilt bytes land in the shared buffers, the caller's headers keep their length.
+    std::vector<cfsec_shard> ls;
+    for (int g : shards_in_idc(kv.first)) ls.push_back(shards[g]);
+    st = init_bad_shards(ls.data(), (int)ls.size(), kv.second);
+    if (st != CFSEC_OK) return st;
+    st = local_->reconstruct(ls.data(), (int)ls.size(), false, mem, s);
+    if (st != CFSEC_OK) return st;
+  }
+  return CFSEC_OK;
+}
+
+Status LrcEncoder::reconstruct_data(cfsec_shard* shards, int n, const int* bad, int nbad, int mem,
+                                    hipStream_t s) {
+  // lrcencoder.go:188-201
+  const int N = t_.n, M = t_.m;
+  if (!shards || n < N + M) return CFSEC_ERR_INVALID_SHARDS;
+  Status st = fill_full_shards(shards, N + M);
+  if (st != CFSEC_OK) return st;
+  std::vector<int> global_bad;
+  for (int i = 0; i < nbad; ++i)
+    if (bad[i] < N + M) global_bad.push_back(bad[i]);
+  st = init_bad_shards(shards, n, global_bad);
+  if (st != CFSEC_OK) return st;
+  Slot slot(pool_.get());
+  return engine_->reconstruct(shards, N + M, true, mem, s);
+}
+
+}  // namespace cfsec

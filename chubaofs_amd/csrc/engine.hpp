@@ -1,0 +1,189 @@
+// engine.hpp -- the MI355X erasure-coding engine behind the cfsec C ABI.
+//
+//   RSEngine   restates reedsolomon.Encoder (KRS/reedsolomon.go) for the default
+//              Vandermonde code, with its arithmetic on the GPU.
+//   ECEncoder  restates ec.Encoder (blobstore/common/ec/encoder.go) and
+//   LrcEncoder the LRC variant (blobstore/common/ec/lrcencoder.go).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <condition_variable>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <shared_mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/cfsec.h"
+#include "gf256.hpp"
+#include "kernels.hpp"
+
+namespace cfsec {
+
+using Status = int;  // cfsec_status
+
+void set_last_error(const std::string& msg);
+Status hip_status(hipError_t e, const char* what);
+
+// Per-device streams and staging workspaces, shared by every engine on the device.
+class DeviceContext {
+ public:
+  static DeviceContext* get(int device);  // nullptr if the device does not exist
+  int device() const { return device_; }
+
+  struct Workspace {
+    uint8_t* dbuf = nullptr;   // device staging buffer
+    size_t cap = 0;
+    uint32_t* dflags = nullptr;  // device verify flags
+    uint32_t* hflags = nullptr;  // pinned host mirror
+    size_t nflags = 0;
+    hipStream_t stream = nullptr;
+  };
+  // Check out a workspace with at least `bytes` of staging and `nflags` flag words.
+  Status acquire(size_t bytes, size_t nflags, Workspace** out);
+  void release(Workspace* ws);
+
+ private:
+  explicit DeviceContext(int device) : device_(device) {}
+  int device_;
+  std::mutex mu_;
+  std::vector<std::unique_ptr<Workspace>> all_;
+  std::vector<Workspace*> free_;
+};
+
+// Makes `device` current for the scope, restoring the caller's device after.
+class DeviceGuard {
+ public:
+  explicit DeviceGuard(int device);
+  ~DeviceGuard();
+  bool ok() const { return ok_; }
+
+ private:
+  int prev_ = -1;
+  bool ok_ = false;
+};
+
+// KRS/inversion_tree.go:16-164: decode matrices keyed by the invalid indices seen
+// before k valid rows were found; RW-locked for concurrent readers.
+class InversionCache {
+ public:
+  bool get(const std::vector<int>& invalid, Matrix* out) const;
+  void put(const std::vector<int>& invalid, const Matrix& m);
+
+ private:
+  mutable std::shared_mutex mu_;
+  std::map<std::vector<int>, Matrix> map_;
+};
+
+// Rows to compute for one reconstruct call (shared by the single and batch paths).
+struct ReconPlan {
+  std::vector<int> valid;    // k surviving shard indices, first-present order
+  std::vector<int> outputs;  // shard indices to rebuild
+  Matrix rows;               // outputs.size() x k, over the shards in `valid`
+};
+
+class RSEngine {
+ public:
+  static Status create(int k, int m, int device, std::unique_ptr<RSEngine>* out);
+  int k() const { return k_; }
+  int m() const { return m_; }
+  int total() const { return k_ + m_; }
+  int device() const { return ctx_ ? ctx_->device() : -1; }
+  const Matrix& matrix() const { return mat_; }
+
+  Status encode(cfsec_shard* shards, int n, int mem, hipStream_t stream);
+  Status verify(cfsec_shard* shards, int n, int mem, hipStream_t stream, bool* ok);
+  Status reconstruct(cfsec_shard* shards, int n, bool data_only, int mem, hipStream_t stream);
+  Status split(uint8_t* data, size_t len, size_t cap, cfsec_shard* out, uint8_t* pad,
+               size_t pad_len, size_t* pad_needed);
+  Status join(uint8_t* dst, size_t dst_len, const cfsec_shard* shards, int n, size_t out_size);
+
+  Status encode_batch(uint8_t* const* ptrs, size_t S, int nstripes, hipStream_t stream);
+  Status verify_batch(uint8_t* const* ptrs, size_t S, int nstripes, uint32_t* flags,
+                      hipStream_t stream);
+  Status reconstruct_batch(uint8_t* const* ptrs, size_t S, int nstripes, const int* erased,
+                           int nerased, bool data_only, hipStream_t stream);
+
+  // Plan the rows of a reconstruct given which shards are present.
+  Status plan_reconstruct(const std::vector<bool>& present, bool data_only, ReconPlan* plan);
+
+  // Generic "outputs = rows x inputs" over caller shards (host or device memory).
+  // mode kVerify: *ok set; outputs are read, not written.
+  Status run(const Matrix& rows, const std::vector<cfsec_shard*>& ins,
+             const std::vector<cfsec_shard*>& outs, size_t S, int mem, hipStream_t stream,
+             MatVecMode mode, bool* ok);
+
+ private:
+  RSEngine() = default;
+  int k_ = 0, m_ = 0;
+  Matrix mat_;     // total x k
+  Matrix parity_;  // m x k (r.parity, KRS/reedsolomon.go:568-571)
+  InversionCache tree_;
+  DeviceContext* ctx_ = nullptr;
+};
+
+// Counting semaphore (util/limit/count.NewBlockingCount, encoder.go:90).
+class BlockingCount {
+ public:
+  explicit BlockingCount(int n) : left_(n) {}
+  void acquire() {
+    std::unique_lock<std::mutex> l(mu_);
+    cv_.wait(l, [&] { return left_ > 0; });
+    --left_;
+  }
+  void release() {
+    std::lock_guard<std::mutex> l(mu_);
+    ++left_;
+    cv_.notify_one();
+  }
+
+ private:
+  std::mutex mu_;
+  std::condition_variable cv_;
+  int left_;
+};
+
+class ECEncoder {
+ public:
+  static Status create(const cfsec_tactic& t, bool enable_verify, int concurrency, int device,
+                       std::unique_ptr<ECEncoder>* out);
+  virtual ~ECEncoder() = default;
+  virtual Status encode(cfsec_shard* shards, int n, int mem, hipStream_t s);
+  virtual Status reconstruct(cfsec_shard* shards, int n, const int* bad, int nbad, int mem,
+                             hipStream_t s);
+  virtual Status reconstruct_data(cfsec_shard* shards, int n, const int* bad, int nbad, int mem,
+                                  hipStream_t s);
+  virtual Status verify(cfsec_shard* shards, int n, int mem, hipStream_t s, bool* ok);
+  virtual std::vector<int> shards_in_idc(int idx) const;
+  const cfsec_tactic& tactic() const { return t_; }
+
+ protected:
+  struct Slot {
+    explicit Slot(BlockingCount* p) : p_(p) { p_->acquire(); }
+    ~Slot() { p_->release(); }
+    BlockingCount* p_;
+  };
+  cfsec_tactic t_{};
+  bool enable_verify_ = false;
+  std::unique_ptr<BlockingCount> pool_;
+  std::unique_ptr<RSEngine> engine_;
+};
+
+class LrcEncoder : public ECEncoder {
+ public:
+  Status encode(cfsec_shard* shards, int n, int mem, hipStream_t s) override;
+  Status reconstruct(cfsec_shard* shards, int n, const int* bad, int nbad, int mem,
+                     hipStream_t s) override;
+  Status reconstruct_data(cfsec_shard* shards, int n, const int* bad, int nbad, int mem,
+                          hipStream_t s) override;
+  Status verify(cfsec_shard* shards, int n, int mem, hipStream_t s, bool* ok) override;
+  std::vector<int> shards_in_idc(int idx) const override;
+
+ private:
+  friend class ECEncoder;
+  std::unique_ptr<RSEngine> local_;
+  Matrix fused_;  // (M+L) x N: global parity rows then local parity rows, over data
+};
+
+}  // namespace cfsec

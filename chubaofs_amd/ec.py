@@ -1,0 +1,166 @@
+"""ec -- mirror of blobstore/common/ec (encoder.go, lrcencoder.go, buf.go) over
+libcfsec.so's cfsec_ec_* entry points.  Method names, argument meaning and
+errors follow the Go interface so the tests read like encoder_test.go:
+
+    enc = NewEncoder(Config(CodeMode=codemode.GetTactic(codemode.EC6P10L2), EnableVerify=True))
+    shards = enc.Split(data)
+    enc.Encode(shards)
+    enc.Reconstruct(shards, [0, 17])
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from ._lib import ErrShortData, ErrInvalidCodeMode, ErrVerify, ErrInvalidShards  # noqa: F401 (re-export)
+from ._shards import Marshal, shard_size, stream_ptr
+from .codemode import Tactic
+from .reedsolomon import ReedSolomon
+
+DEFAULT_CONCURRENCY = 100  # encoder.go:29
+
+
+@dataclass
+class Config:
+    """ec.Config (encoder.go:65-69)."""
+
+    CodeMode: Tactic
+    EnableVerify: bool = False
+    Concurrency: int = 0
+
+
+def _tactic_c(t: Tactic) -> _lib.TacticC:
+    return _lib.TacticC(t.N, t.M, t.L, t.AZCount, t.PutQuorum, t.GetQuorum, t.MinShardSize)
+
+
+class Encoder:
+    """ec.Encoder (encoder.go:41-62); LRC modes behave as lrcEncoder (lrcencoder.go)."""
+
+    def __init__(self, cfg: Config, device: int = -1):
+        L = _lib.lib()
+        h = ctypes.c_void_p()
+        tc = _tactic_c(cfg.CodeMode)
+        _lib.check(L.cfsec_ec_new(ctypes.byref(tc), int(cfg.EnableVerify), cfg.Concurrency, device,
+                                  ctypes.byref(h)))
+        self._h, self._L, self.cfg = h, L, cfg
+        t = cfg.CodeMode
+        self._engine = ReedSolomon(t.N, t.M, device)  # host-side Split/Join only
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            self._L.cfsec_ec_free(h)
+            self._h = None
+
+    @property
+    def CodeMode(self) -> Tactic:
+        return self.cfg.CodeMode
+
+    # -- coding --
+    def Encode(self, shards, stream=None) -> None:
+        m = Marshal(shards, fill_size=shard_size(shards))
+        st = self._L.cfsec_ec_encode(self._h, m.ptr(), m.n, m.mem, stream_ptr(stream))
+        m.writeback()
+        _lib.check(st)
+
+    def _recon(self, fn, shards, badIdx, stream):
+        m = Marshal(shards, fill_size=shard_size(shards))
+        bad = (ctypes.c_int * max(len(badIdx), 1))(*badIdx)
+        st = fn(self._h, m.ptr(), m.n, bad, len(badIdx), m.mem, stream_ptr(stream))
+        m.writeback()
+        _lib.check(st)
+
+    def Reconstruct(self, shards, badIdx, stream=None) -> None:
+        self._recon(self._L.cfsec_ec_reconstruct, shards, list(badIdx), stream)
+
+    def ReconstructData(self, shards, badIdx, stream=None) -> None:
+        self._recon(self._L.cfsec_ec_reconstruct_data, shards, list(badIdx), stream)
+
+    def Verify(self, shards, stream=None) -> bool:
+        m = Marshal(shards)
+        ok = ctypes.c_int(0)
+        _lib.check(self._L.cfsec_ec_verify(self._h, m.ptr(), m.n, m.mem, stream_ptr(stream), ctypes.byref(ok)))
+        return bool(ok.value)
+
+    # -- slice bookkeeping (host) --
+    def Split(self, data, length: int | None = None):
+        """encoder.go:153-155 / lrcencoder.go:203-222.  data: uint8 array; data[:length] is the
+        payload, data.size its capacity."""
+        data = np.asarray(data, np.uint8) if not isinstance(data, np.ndarray) else data
+        shards = self._engine.Split(data, length)
+        t = self.CodeMode
+        if t.L:
+            shard_n, shard_len = len(shards), len(shards[0])
+            if data.size >= (t.L + shard_n) * shard_len:
+                shards += [data[(shard_n + i) * shard_len:(shard_n + i + 1) * shard_len] for i in range(t.L)]
+            else:
+                shards += [np.zeros(shard_len, np.uint8) for _ in range(t.L)]
+        return shards
+
+    def Join(self, dst, shards, outSize: int) -> None:
+        t = self.CodeMode
+        self._engine.Join(dst, shards[:t.N + t.M] if t.L else shards, outSize)
+
+    def GetDataShards(self, shards):
+        return shards[:self.CodeMode.N]
+
+    def GetParityShards(self, shards):
+        t = self.CodeMode
+        return shards[t.N:t.N + t.M] if t.L else shards[t.N:]
+
+    def GetLocalShards(self, shards):
+        t = self.CodeMode
+        return shards[t.N + t.M:] if t.L else []
+
+    def GetShardsInIdc(self, shards, idx: int):
+        t = self.CodeMode
+        if t.L:
+            # lrcencoder.go:236-243: a fresh list of the AZ's local stripe
+            return [shards[g] for g in self.shards_in_idc(idx)]
+        # encoder.go:169-176: Go's append(shards[a:b], shards[c:d]...) writes the parity
+        # headers into shards[b:] of the caller's slice (same backing array); kept as is.
+        ln, lm = t.N // t.AZCount, t.M // t.AZCount
+        b = (idx + 1) * ln
+        tail = list(shards[t.N + lm * idx:t.N + lm * (idx + 1)])
+        shards[b:b + len(tail)] = tail
+        return list(shards[idx * ln:b + len(tail)])
+
+    def shards_in_idc(self, idx: int):
+        out = (ctypes.c_int * 64)()
+        cnt = ctypes.c_int(0)
+        _lib.check(self._L.cfsec_ec_shards_in_idc(self._h, idx, out, 64, ctypes.byref(cnt)))
+        return [out[i] for i in range(cnt.value)]
+
+
+def NewEncoder(cfg: Config, device: int = -1) -> Encoder:
+    """ec.NewEncoder (encoder.go:78-112)."""
+    if not isinstance(cfg.CodeMode, Tactic) or not cfg.CodeMode.IsValid():
+        raise ErrInvalidCodeMode("ErrInvalidCodeMode")
+    return Encoder(cfg, device)
+
+
+@dataclass
+class BufferSizes:
+    """ec.BufferSizes (buf.go:52-59)."""
+
+    ShardSize: int = 0
+    DataSize: int = 0
+    ECDataSize: int = 0
+    ECSize: int = 0
+    From: int = 0
+    To: int = 0
+
+
+def GetBufferSizes(dataSize: int, tactic: Tactic) -> BufferSizes:
+    """ec.GetBufferSizes (buf.go:146-152 via newBuffer :67-133)."""
+    frm, to = 0, dataSize
+    if dataSize <= 0 or to < frm or frm < 0 or frm > dataSize or to < 0 or to > dataSize:
+        raise ErrShortData("ErrShortData")
+    if tactic.N <= 0:
+        raise ErrInvalidCodeMode("ErrInvalidCodeMode")
+    shard = (dataSize + tactic.N - 1) // tactic.N
+    shard = max(shard, tactic.MinShardSize)
+    return BufferSizes(shard, dataSize, shard * tactic.N, shard * (tactic.N + tactic.M + tactic.L), frm, to)

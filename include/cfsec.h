@@ -1,0 +1,157 @@
+/*
+ * cfsec.h -- C ABI of the MI355X-native erasure-coding engine for CubeFS blobstore.
+ *
+ * This is the drop-in boundary.  Two layers are exported, each replacing one Go
+ * interface of the reference (paths relative to the CubeFS tree):
+ *
+ *  1. cfsec_rs_*  replaces the reedsolomon.Encoder engine that blobstore/common/ec
+ *     constructs at blobstore/common/ec/encoder.go:86 (global) and :95 (local),
+ *     i.e. vendor/github.com/klauspost/reedsolomon/reedsolomon.go:25-131 with the
+ *     default (Vandermonde) matrix of reedsolomon.go:220-244.  Only the six methods
+ *     CubeFS uses are exported (Encode, Verify, Reconstruct, ReconstructData, Split,
+ *     Join), plus GPU batch entry points.
+ *
+ *  2. cfsec_ec_*  replaces ec.Encoder (blobstore/common/ec/encoder.go:41-62) as
+ *     returned by ec.NewEncoder (encoder.go:78-112), for both the plain RS encoder
+ *     (encoder.go:71-180) and the LRC encoder (lrcencoder.go:28-247).
+ *
+ * Shard vectors.  A Go [][]byte is passed as an array of cfsec_shard {data,len,cap}.
+ * len == 0 marks a missing shard (KRS/reedsolomon.go:1416-1428).  Reconstruct
+ * writes into a missing shard's buffer and sets its len to the shard size; the
+ * caller must have given it cap >= shard size (the cgo shim does what
+ * KRS/reedsolomon.go:1514-1518 does: reuse cap, else allocate 64-B aligned).
+ *
+ * Memory.  mem = CFSEC_MEM_HOST: plain host memory; the engine stages through HBM
+ * and returns after the results are back in host memory.  mem = CFSEC_MEM_DEVICE:
+ * pointers are HBM device pointers on the engine's device; the call is enqueued on
+ * `stream` (hipStream_t, NULL = an engine-owned stream) and returns after it
+ * completes.  *_batch entry points never synchronise: they enqueue on `stream`.
+ *
+ * Threading.  Every handle is safe for concurrent calls from many threads (the
+ * reference shares one encoder across goroutines, encoder.go:90,115-116).
+ * The library never retains a caller pointer after a call returns (cgo rule).
+ *
+ * Errors.  Return codes map 1:1 onto the Go sentinel errors named in each value.
+ */
+#ifndef CFSEC_H_
+#define CFSEC_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+  CFSEC_OK = 0,
+  CFSEC_ERR_TOO_FEW_SHARDS = 1,        /* reedsolomon.ErrTooFewShards   KRS/reedsolomon.go:601  */
+  CFSEC_ERR_SHARD_NO_DATA = 2,         /* reedsolomon.ErrShardNoData    KRS/reedsolomon.go:1305 */
+  CFSEC_ERR_SHARD_SIZE = 3,            /* reedsolomon.ErrShardSize      KRS/reedsolomon.go:1309 */
+  CFSEC_ERR_INV_SHARD_NUM = 4,         /* reedsolomon.ErrInvShardNum    KRS/reedsolomon.go:204  */
+  CFSEC_ERR_MAX_SHARD_NUM = 5,         /* reedsolomon.ErrMaxShardNum    KRS/reedsolomon.go:209  */
+  CFSEC_ERR_SHORT_DATA = 6,            /* reedsolomon.ErrShortData      KRS/reedsolomon.go:1556 (also ec.ErrShortData) */
+  CFSEC_ERR_RECONSTRUCT_REQUIRED = 7,  /* reedsolomon.ErrReconstructRequired KRS/reedsolomon.go:1636 */
+  CFSEC_ERR_SINGULAR = 8,              /* errSingular                   KRS/matrix.go:185       */
+  CFSEC_ERR_INVALID_CODE_MODE = 9,     /* ec.ErrInvalidCodeMode         common/ec/encoder.go:35 */
+  CFSEC_ERR_VERIFY = 10,               /* ec.ErrVerify                  common/ec/encoder.go:36 */
+  CFSEC_ERR_INVALID_SHARDS = 11,       /* ec.ErrInvalidShards           common/ec/encoder.go:37 */
+  CFSEC_ERR_INVALID_ARG = 12,          /* boundary misuse (NULL handle, cap < shard size, ...) */
+  CFSEC_ERR_DEVICE = 13,               /* HIP runtime failure; see cfsec_last_error()         */
+  CFSEC_ERR_NOT_SUPPORTED = 14         /* reedsolomon.ErrNotSupported   KRS/reedsolomon.go:212  */
+} cfsec_status;
+
+typedef enum { CFSEC_MEM_HOST = 0, CFSEC_MEM_DEVICE = 1 } cfsec_mem;
+
+/* One Go []byte: pointer, length, capacity. */
+typedef struct {
+  uint8_t* data;
+  size_t len;
+  size_t cap;
+} cfsec_shard;
+
+/* codemode.Tactic (blobstore/common/codemode/codemode.go:129-163). */
+typedef struct {
+  int n, m, l, az_count, put_quorum, get_quorum, min_shard_size;
+} cfsec_tactic;
+
+typedef struct cfsec_rs cfsec_rs;
+typedef struct cfsec_ec cfsec_ec;
+
+/* ---------------- library ---------------- */
+const char* cfsec_version(void);
+/* Message for the last CFSEC_ERR_DEVICE on this thread ("" if none). */
+const char* cfsec_last_error(void);
+/* Name of a status code, e.g. "ErrTooFewShards". */
+const char* cfsec_status_name(int status);
+/* Number of visible HIP devices (0 if none; never an error). */
+int cfsec_device_count(void);
+
+/* ---------------- reedsolomon.Encoder seam ---------------- */
+/* reedsolomon.New(dataShards, parityShards) -- KRS/reedsolomon.go:413-581.  The engine binds
+ * to `device` (-1 = the calling thread's current HIP device). */
+int cfsec_rs_new(int data_shards, int parity_shards, int device, cfsec_rs** out);
+void cfsec_rs_free(cfsec_rs* h);
+int cfsec_rs_data_shards(const cfsec_rs* h);
+int cfsec_rs_parity_shards(const cfsec_rs* h);
+/* Copy the (data+parity) x data encoding matrix (row-major) into out. */
+int cfsec_rs_matrix(const cfsec_rs* h, uint8_t* out, size_t out_len);
+
+/* Encode -- KRS/reedsolomon.go:609-625 */
+int cfsec_rs_encode(cfsec_rs* h, cfsec_shard* shards, int n, int mem, void* stream);
+/* Verify -- KRS/reedsolomon.go:770-784; *ok = 1 when every parity shard matches. */
+int cfsec_rs_verify(cfsec_rs* h, cfsec_shard* shards, int n, int mem, void* stream, int* ok);
+/* Reconstruct / ReconstructData -- KRS/reedsolomon.go:1377-1552 */
+int cfsec_rs_reconstruct(cfsec_rs* h, cfsec_shard* shards, int n, int mem, void* stream);
+int cfsec_rs_reconstruct_data(cfsec_rs* h, cfsec_shard* shards, int n, int mem, void* stream);
+/* Split -- KRS/reedsolomon.go:1574-1632 (host memory).  data has len/cap; the engine fills
+ * out[0..total) with views into data and, when cap is short, into pad (caller-owned, at least
+ * *pad_needed bytes; call once with pad == NULL to learn pad_needed). */
+int cfsec_rs_split(cfsec_rs* h, uint8_t* data, size_t len, size_t cap, cfsec_shard* out,
+                   uint8_t* pad, size_t pad_len, size_t* pad_needed);
+/* Join -- KRS/reedsolomon.go:1646-1684 (host memory): copies out_size bytes into dst. */
+int cfsec_rs_join(cfsec_rs* h, uint8_t* dst, size_t dst_len, const cfsec_shard* shards, int n,
+                  size_t out_size);
+
+/* GPU batch entry points (device memory, asynchronous on `stream`).
+ * ptrs holds nstripes * (data+parity) device pointers, stripe-major; every shard is
+ * shard_size bytes. */
+int cfsec_rs_encode_batch(cfsec_rs* h, uint8_t* const* ptrs, size_t shard_size, int nstripes,
+                          void* stream);
+/* flags: device array of nstripes uint32; flags[s] is OR-ed with 1 when stripe s mismatches
+ * (caller zeroes it). */
+int cfsec_rs_verify_batch(cfsec_rs* h, uint8_t* const* ptrs, size_t shard_size, int nstripes,
+                          uint32_t* flags, void* stream);
+/* Rebuild the shards listed in erased[] (same pattern for every stripe) from the first
+ * data_shards surviving shards, in one fused pass (missing data rows = inv(sub), missing
+ * parity rows = parity * inv(sub)).  data_only = 1 rebuilds only erased data shards. */
+int cfsec_rs_reconstruct_batch(cfsec_rs* h, uint8_t* const* ptrs, size_t shard_size, int nstripes,
+                               const int* erased, int nerased, int data_only, void* stream);
+
+/* ---------------- ec.Encoder ---------------- */
+/* Code-mode table (codemode.go:26-79): fill *t for a CodeMode value; CFSEC_ERR_INVALID_CODE_MODE
+ * when unknown. */
+int cfsec_codemode_tactic(int codemode, cfsec_tactic* t);
+/* ec.NewEncoder(Config{CodeMode, EnableVerify, Concurrency}) -- encoder.go:78-112 */
+int cfsec_ec_new(const cfsec_tactic* tactic, int enable_verify, int concurrency, int device,
+                 cfsec_ec** out);
+void cfsec_ec_free(cfsec_ec* h);
+int cfsec_ec_encode(cfsec_ec* h, cfsec_shard* shards, int n, int mem, void* stream);
+int cfsec_ec_reconstruct(cfsec_ec* h, cfsec_shard* shards, int n, const int* bad_idx, int nbad,
+                         int mem, void* stream);
+int cfsec_ec_reconstruct_data(cfsec_ec* h, cfsec_shard* shards, int n, const int* bad_idx,
+                              int nbad, int mem, void* stream);
+int cfsec_ec_verify(cfsec_ec* h, cfsec_shard* shards, int n, int mem, void* stream, int* ok);
+/* GetShardsInIdc index map (encoder.go:169-176 / lrcencoder.go:236-243): writes the global
+ * shard indices of AZ idx into out (capacity out_cap) and their count into *count. */
+int cfsec_ec_shards_in_idc(const cfsec_ec* h, int idx, int* out, int out_cap, int* count);
+
+/* ---------------- shard CRC32 (access/stream_put.go:249-253) ---------------- */
+/* crc32.ChecksumIEEE of each device shard; out: host array of n uint32. Synchronous. */
+int cfsec_crc32_ieee_batch(uint8_t* const* ptrs, size_t shard_size, int n, uint32_t* out,
+                           int device, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CFSEC_H_ */

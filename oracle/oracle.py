@@ -1,0 +1,130 @@
+"""TEST INFRASTRUCTURE: ctypes front end of the CPU oracle (oracle/gf_oracle.c).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this
+module; the product package (chubaofs_amd) never does.  Every function here is
+the checker, restating klauspost/reedsolomon v1.11.7 (see gf_oracle.c header for
+the file:line map).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+P_u8 = ctypes.POINTER(ctypes.c_uint8)
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        L = ctypes.CDLL(path)
+        L.oracle_tables.argtypes = [ctypes.c_void_p] * 7
+        L.oracle_gal_mul.argtypes = [ctypes.c_uint8, ctypes.c_uint8]
+        L.oracle_gal_mul.restype = ctypes.c_uint8
+        L.oracle_gal_exp.argtypes = [ctypes.c_uint8, ctypes.c_int]
+        L.oracle_gal_exp.restype = ctypes.c_uint8
+        L.oracle_invert.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_build_matrix.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        for fn in ("oracle_encode",):
+            getattr(L, fn).argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        L.oracle_verify.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                    ctypes.POINTER(ctypes.c_int)]
+        L.oracle_reconstruct.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                         ctypes.c_int, ctypes.c_void_p]
+        L.oracle_crc32_ieee.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+        L.oracle_crc32_ieee.restype = ctypes.c_uint32
+        L.oracle_crc32_update.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]
+        L.oracle_crc32_update.restype = ctypes.c_uint32
+        _LIB = L
+    return _LIB
+
+
+def tables() -> dict:
+    t = {
+        "logTable": np.zeros(256, np.uint8),
+        "expTable": np.zeros(510, np.uint8),
+        "invTable": np.zeros(256, np.uint8),
+        "mulTable": np.zeros((256, 256), np.uint8),
+        "mulTableLow": np.zeros((256, 16), np.uint8),
+        "mulTableHigh": np.zeros((256, 16), np.uint8),
+        "gf2p811dMulMatrices": np.zeros(256, np.uint64),
+    }
+    lib().oracle_tables(*[a.ctypes.data for a in t.values()])
+    return t
+
+
+def gal_mul(a: int, b: int) -> int:
+    return lib().oracle_gal_mul(a, b)
+
+
+def build_matrix(k: int, total: int) -> np.ndarray:
+    out = np.zeros((total, k), np.uint8)
+    err = lib().oracle_build_matrix(k, total, out.ctypes.data)
+    assert err == 0, err
+    return out
+
+
+def invert(mat: np.ndarray):
+    mat = np.ascontiguousarray(mat, np.uint8)
+    n = mat.shape[0]
+    out = np.zeros((n, n), np.uint8)
+    err = lib().oracle_invert(n, mat.ctypes.data, out.ctypes.data)
+    return err, out
+
+
+def _ptrs(shards):
+    arr = (ctypes.c_void_p * len(shards))()
+    for i, s in enumerate(shards):
+        arr[i] = s.ctypes.data if s is not None and s.size else 0
+    return arr
+
+
+def _lens(shards, lens=None):
+    if lens is None:
+        lens = [0 if s is None else s.size for s in shards]
+    return (ctypes.c_size_t * len(shards))(*lens)
+
+
+def encode(k: int, m: int, shards: list) -> int:
+    """shards: list of k+m uint8 numpy arrays; parity rows overwritten."""
+    return lib().oracle_encode(k, m, _ptrs(shards), _lens(shards), len(shards))
+
+
+def verify(k: int, m: int, shards: list):
+    ok = ctypes.c_int(0)
+    err = lib().oracle_verify(k, m, _ptrs(shards), _lens(shards), len(shards), ctypes.byref(ok))
+    return err, bool(ok.value)
+
+
+def reconstruct(k: int, m: int, shards: list, present: list, data_only: bool = False):
+    """shards: k+m equal-size buffers; present[i] False marks missing (buffer is scratch).
+
+    Returns (err, filled) where filled[i] is True for shards written."""
+    lens = [s.size if p else 0 for s, p in zip(shards, present)]
+    lens_c = _lens(shards, lens)
+    arr = (ctypes.c_void_p * len(shards))(*[s.ctypes.data for s in shards])
+    dec = np.zeros((k, k), np.uint8)
+    err = lib().oracle_reconstruct(k, m, arr, lens_c, len(shards), int(data_only), dec.ctypes.data)
+    filled = [(not p) and lens_c[i] != 0 for i, p in enumerate(present)]
+    return err, filled
+
+
+def crc32_ieee(buf) -> int:
+    b = np.ascontiguousarray(np.frombuffer(bytes(buf), np.uint8) if not isinstance(buf, np.ndarray) else buf)
+    return lib().oracle_crc32_ieee(b.ctypes.data, b.size)
+
+
+def encode_matrix_rows(k: int, total: int) -> np.ndarray:
+    return build_matrix(k, total)[k:]
