@@ -1,0 +1,272 @@
+#!/usr/bin/env python3
+"""bench.py -- EC12P4 encode + 4-erasure reconstruct throughput on MI355X.
+
+Workload (BASELINE.json configs[1]/[2], one GPU): a batch of `--stripes` EC12P4
+stripes of 64 MiB blobs (shard size S = ceil(64 MiB / 12) = 5,592,406 B), resident
+in HBM with a 256-B shard pitch.  One step = one pass of the hot path over the batch:
+  1. Encode       (cfsec_rs_encode_batch):      read 12*S, write 4*S per stripe
+  2. Reconstruct  erased {0,1,2,3}, the worst-case dense decode
+                  (cfsec_rs_reconstruct_batch): read 12*S, write 4*S per stripe
+value = data bytes through the engine per second = 2 * 12 * S * stripes * n_gpus / step
+time (each operation counts its stripe's 12*S data bytes once).  Multi-GPU: each rank
+codes its own stripes (weak scaling, no collective on the data path).
+
+    python bench.py [--gpus N --steps K --warmup W]
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import json
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+K_DATA, M_PARITY = 12, 4
+BLOB = 64 << 20
+S_DEFAULT = (BLOB + K_DATA - 1) // K_DATA  # 5,592,406 (common/ec/buf.go:77-81)
+ERASED = [0, 1, 2, 3]
+HBM_PEAK_GBPS = 8000.0  # MI355X spec (MI355X_MICROARCH.md)
+KERNEL = "gf_matvec_kernel<4"  # both step kernels: 12 inputs -> 4 outputs
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--stripes", type=int, default=8, help="stripes per GPU per step")
+    p.add_argument("--shard-size", type=int, default=S_DEFAULT)
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-pmc", action="store_true")
+    p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    return p.parse_args()
+
+
+# ----------------------------------------------------------------- PMC traffic
+def _read_counter_csv(d):
+    rows = []
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            rows += list(csv.DictReader(fh))
+    return rows
+
+
+def pmc_traffic(args):
+    """HBM bytes per launch of the step kernel from rocprofv3 FETCH_SIZE / WRITE_SIZE, one
+    counter per pass (MI355X_MICROARCH.md: FETCH_SIZE counts half of a 16-B/lane stream on
+    gfx950 -> doubled; both in KiB)."""
+    exe = shutil.which("rocprofv3")
+    if not exe:
+        return None, "rocprofv3 not found"
+    vals = {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+        cmd = ["timeout", "-s", "KILL", "120", exe, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "pmc",
+               "--", sys.executable, os.path.abspath(__file__), "--pmc-child", "--steps", "3", "--warmup", "1",
+               "--stripes", str(args.stripes), "--shard-size", str(args.shard_size)]
+        r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+        if r.returncode != 0:
+            return None, f"rocprofv3 --pmc {ctr} failed rc={r.returncode}: {r.stdout[-300:]}"
+        per = []
+        for row in _read_counter_csv(d):
+            name = row.get("Kernel_Name", "")
+            if KERNEL.replace(" ", "") in name.replace(" ", "") and row.get("Counter_Name", ctr) == ctr:
+                per.append(float(row["Counter_Value"]))
+        shutil.rmtree(d, ignore_errors=True)
+        if not per:
+            return None, f"no {ctr} rows for {KERNEL}"
+        vals[ctr] = sum(per) / len(per)
+    return (2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0, None
+
+
+# ----------------------------------------------------------------- CPU baseline
+def cpu_baseline(S, seconds):
+    """klauspost-strategy restatement (oracle/cpu_simd.c) on the host: the same EC12P4 encode +
+    4-erasure reconstruct of one stripe, repeated for ~`seconds`, with the reference's per-call
+    worker cap (4 with GFNI, else 8; KRS/reedsolomon.go:551-557)."""
+    import numpy as np
+
+    from oracle import oracle as O
+
+    feats = O.simd_features()
+    threads = 4 if feats["gfni"] else 8
+    rng = np.random.default_rng(0xCF5EC000)
+    data = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(K_DATA)]
+    parity = [np.zeros(S, np.uint8) for _ in range(M_PARITY)]
+    full = O.build_matrix(K_DATA, K_DATA + M_PARITY)
+    prow = full[K_DATA:]
+    err, dec = O.invert(full[4:16])  # survivors 4..15 after erasing {0,1,2,3}
+    assert err == 0
+    drows = dec[:4]
+    survivors = data[4:] + parity
+    rebuilt = [np.zeros(S, np.uint8) for _ in range(4)]
+    O.simd_code(prow, data, parity, threads)  # warm
+    ops, t0 = 0, time.perf_counter()
+    kind = 0
+    while True:
+        kind = O.simd_code(prow, data, parity, threads)
+        O.simd_code(drows, survivors, rebuilt, threads)
+        ops += 1
+        dt = time.perf_counter() - t0
+        if dt >= seconds:
+            break
+    for i in range(4):
+        assert np.array_equal(rebuilt[i], data[i]), "CPU baseline reconstruct mismatch"
+    value = 2 * K_DATA * S * ops / dt / 1e9
+    return {
+        "value": round(value, 3), "unit": "GB/s", "cores": threads, "kind": "port",
+        "sample": (f"EC12P4 encode + erase{{0,1,2,3}} reconstruct of one S={S} stripe x{ops} "
+                   f"({dt:.1f}s), klauspost v1.11.7 strategy restated in C "
+                   f"({'AVX2 10x4+2x4 tiles' if kind == 1 else 'GFNI tiles'}), {threads} worker threads"),
+        "host_cpus": os.cpu_count(),
+        "features": feats,
+    }
+
+
+# ----------------------------------------------------------------- GPU
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    S, nst = args.shard_size, args.stripes
+
+    traffic, pmc_note = None, "skipped"
+    if rank == 0 and world == 1 and not args.no_pmc and not args.pmc_child:
+        traffic, pmc_note = pmc_traffic(args)  # before this process touches the GPU
+
+    import torch
+
+    from chubaofs_amd import reedsolomon
+
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    total = K_DATA + M_PARITY
+    pitch = (S + 255) // 256 * 256
+    batch = torch.zeros((nst, total, pitch), dtype=torch.uint8, device=dev)
+    for s in range(nst):  # seeded synthetic data, one generator per stripe
+        g = torch.Generator(device=dev)
+        g.manual_seed(0xCF5EC000 + rank * nst + s)
+        batch[s, :K_DATA, :S] = torch.randint(0, 256, (K_DATA, S), generator=g, device=dev, dtype=torch.uint8)
+    base = batch.data_ptr()
+    ptrs = [base + (s * total + i) * pitch for s in range(nst) for i in range(total)]
+    enc = reedsolomon.New(K_DATA, M_PARITY, device=local_rank)
+    stream = torch.cuda.Stream(device=dev)
+
+    def step(evs=None):
+        if evs:
+            evs[0].record(stream)
+        enc.encode_batch(ptrs, S, nst, stream=stream)
+        if evs:
+            evs[1].record(stream)
+        enc.reconstruct_batch(ptrs, S, nst, ERASED, stream=stream)
+        if evs:
+            evs[2].record(stream)
+
+    if args.pmc_child:
+        for _ in range(args.warmup + args.steps):
+            step()
+        torch.cuda.synchronize()
+        return
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    golden = batch[:, :, :S].clone()
+
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(evs[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    enc_ms = [e[0].elapsed_time(e[1]) for e in evs]
+    rec_ms = [e[1].elapsed_time(e[2]) for e in evs]
+    # correctness gate: the stripes are unchanged codewords after K reconstructs
+    assert torch.equal(batch[:, :, :S], golden), "batch changed across reconstruct passes"
+    flags = torch.zeros(nst, dtype=torch.int32, device=dev)
+    e_v0, e_v1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e_v0.record(stream)
+    enc.verify_batch(ptrs, S, nst, flags.data_ptr(), stream=stream)
+    e_v1.record(stream)
+    torch.cuda.synchronize()
+    assert int(flags.sum().item()) == 0, "Verify failed after the timed region"
+    verify_ms = e_v0.elapsed_time(e_v1)
+
+    data_bytes = K_DATA * S * nst
+    launch_bytes = (K_DATA + M_PARITY) * S * nst  # algorithmic bytes per launch (read 12S + write 4S)
+    kern_ms = sorted(enc_ms + rec_ms)
+    avg_ms = sum(kern_ms) / len(kern_ms)
+    achieved = launch_bytes / (avg_ms * 1e-3) / 1e9
+    value = 2 * data_bytes * world * args.steps / elapsed / 1e9
+
+    if rank != 0:
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
+    cpu = None
+    if world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(S, args.cpu_seconds)
+    out = {
+        "metric": "EC12P4 encode + 4-erasure reconstruct data GB/s",
+        "value": round(value, 2),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic: seeded uniform bytes (torch Generator seed 0xCF5EC000 + stripe), HBM-resident",
+        "config": {
+            "workload": "EC12P4 Encode then Reconstruct(erased {0,1,2,3}) of 64 MiB-blob stripes",
+            "code_mode": "EC12P4", "shard_size": S, "shard_pitch": pitch, "stripes_per_gpu": nst,
+            "erased": ERASED, "parallelism": f"stripes sharded over {world} GPU(s), no collective",
+            "value_def": "2 * 12 * S * stripes * n_gpus / step time (encode and reconstruct each count the stripe's data once)",
+        },
+        "roofline": {
+            "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 4),
+            "traffic": None if traffic is None else int(traffic),
+            "kernel": "gf_matvec_kernel<4, kStore> (encode and reconstruct launches)",
+            "algorithmic_bytes_per_launch": launch_bytes,
+            "avg_launch_ms": round(avg_ms, 4),
+            "traffic_note": pmc_note if traffic is None else "rocprofv3 (2*FETCH_SIZE + WRITE_SIZE)*1024, per launch",
+        },
+        "encode_data_GBps": round(data_bytes / (sum(enc_ms) / len(enc_ms) * 1e-3) / 1e9, 1),
+        "reconstruct_data_GBps": round(data_bytes / (sum(rec_ms) / len(rec_ms) * 1e-3) / 1e9, 1),
+        "verify_data_GBps": round(data_bytes / (verify_ms * 1e-3) / 1e9, 1),
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -128,3 +128,33 @@ def crc32_ieee(buf) -> int:
 
 def encode_matrix_rows(k: int, total: int) -> np.ndarray:
     return build_matrix(k, total)[k:]
+
+
+# ---- klauspost-strategy SIMD baseline (bench.py cpu_baseline leg) ----
+def _simd():
+    L = lib()
+    if not getattr(L, "_simd_ready", False):
+        L.cpu_code_some_shards.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int]
+        L.cpu_code_some_shards.restype = ctypes.c_int
+        L.cpu_has_gfni.restype = ctypes.c_int
+        L.cpu_has_avx2.restype = ctypes.c_int
+        L._simd_ready = True
+    return L
+
+
+def simd_features() -> dict:
+    L = _simd()
+    return {"gfni": bool(L.cpu_has_gfni()), "avx2": bool(L.cpu_has_avx2())}
+
+
+def simd_code(rows: np.ndarray, inputs: list, outputs: list, threads: int, force: int = 0) -> int:
+    """outputs = rows x inputs with the AVX2/GFNI tile kernels; returns 1 (AVX2) or 2 (GFNI)."""
+    rows = np.ascontiguousarray(rows, np.uint8)
+    m, k = rows.shape
+    ins = (ctypes.c_void_p * k)(*[a.ctypes.data for a in inputs])
+    outs = (ctypes.c_void_p * m)(*[a.ctypes.data for a in outputs])
+    ret = _simd().cpu_code_some_shards(rows.ctypes.data, k, m, ins, outs, inputs[0].size, threads, force)
+    if ret < 0:
+        raise RuntimeError("SIMD path unavailable on this CPU")
+    return ret
