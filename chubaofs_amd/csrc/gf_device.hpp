@@ -1,0 +1,251 @@
+// gf_device.hpp -- device side of the GF(2^8) matrix x shard-vector kernel.
+//
+// Included by gf_kernels.hip (the product launcher) and by tools/gf_variants.hip
+// (the A/B tuning harness), so a tuned policy is exactly the code that ships.
+//
+// See gf_kernels.hip for the arithmetic (3-bit split tables + v_perm_b32) and the
+// data movement.  The policy knobs here:
+//   W   16-B chunks per lane per tile (chunk w sits w*kThreads*16 bytes further on,
+//       so each wave still touches whole 1 KiB runs of every row)
+//   G   input rows whose loads are issued together before any is consumed
+//   PERSIST  grid-stride over (stripe, tile) pairs; tables built once per workgroup
+//   NTL/NTS  non-temporal loads / stores (streaming data, touched once)
+//   XCD remap blockIdx so each XCD walks a contiguous run of tiles (T1 swizzle)
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+#include "kernels.hpp"
+
+namespace cfsec {
+namespace dev {
+
+constexpr int kMaxK = 32;       // inputs per launch
+constexpr int kMaxM = 32;       // outputs per launch
+constexpr int kPtrSlots = 300;  // shard pointers per launch
+constexpr int kThreads = 256;
+constexpr int kLaneBytes = 16;
+
+struct __attribute__((aligned(16))) GfArgs {
+  uint64_t len;
+  uint32_t k, m, nstripes, tiles_per_stripe;  // tiles_per_stripe: in units of the kernel's tile
+  uint32_t* flags;
+  uint8_t coef[kMaxM * kMaxK];    // m x k, row stride k
+  const uint8_t* ptr[kPtrSlots];  // [nstripes*k inputs][nstripes*m outputs]
+};
+static_assert(sizeof(GfArgs) <= 3584, "kernel argument block must stay below 4 KiB");
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef u32x4 u32x4_ua __attribute__((aligned(1)));  // shard rows may start at any byte
+
+__device__ __forceinline__ uint32_t gf_xtime(uint32_t v) {
+  v <<= 1;
+  return (v & 0x100u) ? (v ^ 0x11Du) : v;  // KRS/galois.go:25 polynomial 0x11D
+}
+
+template <bool NT>
+__device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4_ua*>(p));
+  else return *reinterpret_cast<const u32x4_ua*>(p);
+}
+
+template <bool NT>
+__device__ __forceinline__ void st16(uint8_t* p, u32x4 v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4_ua*>(p));
+  else *reinterpret_cast<u32x4_ua*>(p) = v;
+}
+
+// Bytes [0, rem) of a 16-byte chunk, zero above (the tail of a shard).
+__device__ __forceinline__ u32x4 ld_tail(const uint8_t* p, size_t rem) {
+  uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if ((size_t)i < rem) w[i >> 2] |= (uint32_t)p[i] << (8 * (i & 3));
+  return u32x4{w[0], w[1], w[2], w[3]};
+}
+
+__device__ __forceinline__ void st_tail(uint8_t* p, u32x4 v, size_t rem) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if ((size_t)i < rem) p[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+}
+
+// Product tables for coefficient (c, r) at LDS slot c*M + r:
+//   tab01 = {T0[0..3], T0[4..7], T1[0..3], T1[4..7]},  tab2 = T2[0..3]
+// with T0[e] = coef*e, T1[e] = coef*(e<<3), T2[e] = coef*(e<<6).
+template <int M>
+__device__ __forceinline__ void build_tables(const GfArgs& a, u32x4* tab01, uint32_t* tab2) {
+  const int k = (int)a.k;
+  for (int i = threadIdx.x; i < k * M; i += kThreads) {
+    const int c = i / M;
+    const int r = i - c * M;
+    uint32_t p[8];
+    p[0] = (r < (int)a.m) ? a.coef[r * k + c] : 0u;
+#pragma unroll
+    for (int j = 1; j < 8; ++j) p[j] = gf_xtime(p[j - 1]);  // coef * 2^j
+    uint32_t t0lo = 0, t0hi = 0, t1lo = 0, t1hi = 0, t2 = 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const uint32_t v0 = ((e & 1) ? p[0] : 0u) ^ ((e & 2) ? p[1] : 0u) ^ ((e & 4) ? p[2] : 0u);
+      const uint32_t v1 = ((e & 1) ? p[3] : 0u) ^ ((e & 2) ? p[4] : 0u) ^ ((e & 4) ? p[5] : 0u);
+      if (e < 4) {
+        const uint32_t v2 = ((e & 1) ? p[6] : 0u) ^ ((e & 2) ? p[7] : 0u);
+        t0lo |= v0 << (8 * e);
+        t1lo |= v1 << (8 * e);
+        t2 |= v2 << (8 * e);
+      } else {
+        t0hi |= v0 << (8 * (e - 4));
+        t1hi |= v1 << (8 * (e - 4));
+      }
+    }
+    tab01[i] = u32x4{t0lo, t0hi, t1lo, t1hi};
+    tab2[i] = t2;
+  }
+}
+
+// acc[r] ^= coef(c, r) * x for all M outputs; x is 16 bytes of input row c.
+template <int M>
+__device__ __forceinline__ void mac_row(u32x4 (&acc)[M], u32x4 x, const u32x4* __restrict__ tq,
+                                        const uint32_t* __restrict__ t2p) {
+  const u32x4 s0 = x & 0x07070707u;
+  const u32x4 s1 = (x >> 3) & 0x07070707u;
+  const u32x4 s2 = (x >> 6) & 0x03030303u;
+#pragma unroll
+  for (int r = 0; r < M; ++r) {
+    const u32x4 q = tq[r];
+    const uint32_t t2 = t2p[r];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const uint32_t p0 = __builtin_amdgcn_perm(q.y, q.x, s0[w]);
+      const uint32_t p1 = __builtin_amdgcn_perm(q.w, q.z, s1[w]);
+      const uint32_t p2 = __builtin_amdgcn_perm(0u, t2, s2[w]);
+      // acc ^ p0 ^ p1 in one v_bitop3_b32 (truth table 0x96 = 3-input XOR)
+      acc[r][w] = __builtin_amdgcn_bitop3_b32(acc[r][w], p0, p1, 0x96) ^ p2;
+    }
+  }
+}
+
+template <int M, MatVecMode MODE, bool NTL, bool NTS>
+__device__ __forceinline__ void finish(const GfArgs& a, u32x4 (&acc)[M], uint8_t* const* out,
+                                       size_t off, int stripe, uint32_t& diff) {
+  const int m = (int)a.m;
+#pragma unroll
+  for (int r = 0; r < M; ++r) {
+    if (r < m) {
+      if constexpr (MODE == MatVecMode::kVerify) {
+        const u32x4 d = acc[r] ^ ld16<NTL>(out[r] + off);
+        diff |= d.x | d.y | d.z | d.w;
+      } else {
+        u32x4 v = acc[r];
+        if constexpr (MODE == MatVecMode::kAccum) v ^= ld16<NTL>(out[r] + off);
+        st16<NTS>(out[r] + off, v);
+      }
+    }
+  }
+}
+
+// One lane's chunk at the end of a shard (rem < 16 bytes), byte-granular.
+template <int M, MatVecMode MODE>
+__device__ __forceinline__ void lane_tail(const GfArgs& a, const u32x4* tab01, const uint32_t* tab2,
+                                          const uint8_t* const* in, uint8_t* const* out, size_t off,
+                                          size_t rem, uint32_t& diff) {
+  const int k = (int)a.k, m = (int)a.m;
+  u32x4 acc[M];
+#pragma unroll
+  for (int r = 0; r < M; ++r) acc[r] = u32x4{0u, 0u, 0u, 0u};
+  for (int c = 0; c < k; ++c) mac_row<M>(acc, ld_tail(in[c] + off, rem), tab01 + c * M, tab2 + c * M);
+#pragma unroll
+  for (int r = 0; r < M; ++r) {
+    if (r < m) {
+      if constexpr (MODE == MatVecMode::kVerify) {
+        const u32x4 d = acc[r] ^ ld_tail(out[r] + off, rem);
+        diff |= d.x | d.y | d.z | d.w;
+      } else {
+        u32x4 v = acc[r];
+        if constexpr (MODE == MatVecMode::kAccum) v ^= ld_tail(out[r] + off, rem);
+        st_tail(out[r] + off, v, rem);
+      }
+    }
+  }
+}
+
+// Full tile: W chunks per lane, all in bounds.  Input rows are loaded G at a time.
+template <int M, MatVecMode MODE, int W, int G, bool NTL, bool NTS>
+__device__ __forceinline__ void lane_tile(const GfArgs& a, const u32x4* tab01, const uint32_t* tab2,
+                                          const uint8_t* const* in, uint8_t* const* out, size_t off,
+                                          int stripe, uint32_t& diff) {
+  constexpr size_t kStep = size_t(kThreads) * kLaneBytes;
+  const int k = (int)a.k;
+  u32x4 acc[W][M];
+#pragma unroll
+  for (int w = 0; w < W; ++w)
+#pragma unroll
+    for (int r = 0; r < M; ++r) acc[w][r] = u32x4{0u, 0u, 0u, 0u};
+  for (int c0 = 0; c0 < k; c0 += G) {
+    u32x4 x[G][W];
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+      if (c0 + g < k)
+#pragma unroll
+        for (int w = 0; w < W; ++w) x[g][w] = ld16<NTL>(in[c0 + g] + off + w * kStep);
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+      if (c0 + g < k)
+#pragma unroll
+        for (int w = 0; w < W; ++w) mac_row<M>(acc[w], x[g][w], tab01 + (c0 + g) * M, tab2 + (c0 + g) * M);
+  }
+#pragma unroll
+  for (int w = 0; w < W; ++w) finish<M, MODE, NTL, NTS>(a, acc[w], out, off + w * kStep, stripe, diff);
+}
+
+// Kernel body.  A tile is kThreads*16*W bytes of every row of one stripe.
+template <int M, MatVecMode MODE, int W, int G, bool PERSIST, bool NTL, bool NTS, bool XCD>
+__device__ __forceinline__ void matvec(const GfArgs& a) {
+  __shared__ u32x4 tab01[kMaxK * M];
+  __shared__ uint32_t tab2[kMaxK * M];
+  build_tables<M>(a, tab01, tab2);
+  __syncthreads();
+
+  constexpr size_t kStep = size_t(kThreads) * kLaneBytes;
+  constexpr size_t kTile = kStep * W;
+  const uint32_t tps = a.tiles_per_stripe;
+  const uint32_t ntiles = tps * a.nstripes;
+  uint32_t diff = 0;
+  uint32_t first = blockIdx.x;
+  if constexpr (XCD) {
+    // blocks b and b+8 share an XCD: give XCD x the contiguous run [x*per, (x+1)*per)
+    const uint32_t nb = gridDim.x, per = nb / 8;
+    if (per && blockIdx.x < per * 8) first = (blockIdx.x % 8) * per + blockIdx.x / 8;
+  }
+  for (uint32_t t = first; t < ntiles; t += (PERSIST ? gridDim.x : ntiles)) {
+    const int stripe = (int)(t / tps);
+    const size_t tile = t - (size_t)stripe * tps;
+    const uint8_t* const* in = a.ptr + (size_t)stripe * a.k;
+    uint8_t* const* out = const_cast<uint8_t* const*>(a.ptr + (size_t)a.nstripes * a.k + (size_t)stripe * a.m);
+    const size_t off = tile * kTile + (size_t)threadIdx.x * kLaneBytes;
+    if (off + (W - 1) * kStep + kLaneBytes <= a.len) {
+      lane_tile<M, MODE, W, G, NTL, NTS>(a, tab01, tab2, in, out, off, stripe, diff);
+    } else {
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        const size_t o = off + w * kStep;
+        if (o + kLaneBytes <= a.len)
+          lane_tile<M, MODE, 1, G, NTL, NTS>(a, tab01, tab2, in, out, o, stripe, diff);
+        else if (o < a.len)
+          lane_tail<M, MODE>(a, tab01, tab2, in, out, o, a.len - o, diff);
+      }
+    }
+    if constexpr (MODE == MatVecMode::kVerify) {
+      if (diff) {
+        atomicOr(a.flags + stripe, 1u);
+        diff = 0;
+      }
+    }
+  }
+}
+
+}  // namespace dev
+}  // namespace cfsec
