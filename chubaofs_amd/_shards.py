@@ -115,5 +115,8 @@ def stream_ptr(stream):
 
 
 def ptr_array(ptrs):
-    arr = (ctypes.c_void_p * len(ptrs))(*[int(p) for p in ptrs])
-    return arr
+    """A ctypes array of device pointers; an existing ctypes array passes through (callers
+    that launch the same batch repeatedly build it once)."""
+    if isinstance(ptrs, ctypes.Array):
+        return ptrs
+    return (ctypes.c_void_p * len(ptrs))(*[int(p) for p in ptrs])

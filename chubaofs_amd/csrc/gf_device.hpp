@@ -5,7 +5,7 @@
 //
 // See gf_kernels.hip for the arithmetic (3-bit split tables + v_perm_b32) and the
 // data movement.  The policy knobs here:
-//   W   16-B chunks per lane per tile (chunk w sits w*kThreads*16 bytes further on,
+//   W   16-B chunks per lane per tile (chunk w sits w*blockDim.x*16 bytes further on,
 //       so each wave still touches whole 1 KiB runs of every row)
 //   G   input rows whose loads are issued together before any is consumed
 //   PERSIST  grid-stride over (stripe, tile) pairs; tables built once per workgroup
@@ -79,7 +79,7 @@ __device__ __forceinline__ void st_tail(uint8_t* p, u32x4 v, size_t rem) {
 template <int M>
 __device__ __forceinline__ void build_tables(const GfArgs& a, u32x4* tab01, uint32_t* tab2) {
   const int k = (int)a.k;
-  for (int i = threadIdx.x; i < k * M; i += kThreads) {
+  for (int i = threadIdx.x; i < k * M; i += (int)blockDim.x) {
     const int c = i / M;
     const int r = i - c * M;
     uint32_t p[8];
@@ -176,8 +176,7 @@ __device__ __forceinline__ void lane_tail(const GfArgs& a, const u32x4* tab01, c
 template <int M, MatVecMode MODE, int W, int G, bool NTL, bool NTS>
 __device__ __forceinline__ void lane_tile(const GfArgs& a, const u32x4* tab01, const uint32_t* tab2,
                                           const uint8_t* const* in, uint8_t* const* out, size_t off,
-                                          int stripe, uint32_t& diff) {
-  constexpr size_t kStep = size_t(kThreads) * kLaneBytes;
+                                          size_t kStep, int stripe, uint32_t& diff) {
   const int k = (int)a.k;
   u32x4 acc[W][M];
 #pragma unroll
@@ -201,16 +200,21 @@ __device__ __forceinline__ void lane_tile(const GfArgs& a, const u32x4* tab01, c
   for (int w = 0; w < W; ++w) finish<M, MODE, NTL, NTS>(a, acc[w], out, off + w * kStep, stripe, diff);
 }
 
-// Kernel body.  A tile is kThreads*16*W bytes of every row of one stripe.
-template <int M, MatVecMode MODE, int W, int G, bool PERSIST, bool NTL, bool NTS, bool XCD>
+// Kernel body.  A tile is blockDim.x*16*W bytes of every row of one stripe.  Chunk w of a
+// lane sits w*blockDim.x*16 bytes on (WAVEC = false: the workgroup sweeps the tile W times)
+// or w*1 KiB on inside its wave's own W KiB run (WAVEC = true).
+template <int M, MatVecMode MODE, int W, int G, bool PERSIST, bool NTL, bool NTS, bool XCD,
+          bool WAVEC = false>
 __device__ __forceinline__ void matvec(const GfArgs& a) {
   __shared__ u32x4 tab01[kMaxK * M];
   __shared__ uint32_t tab2[kMaxK * M];
   build_tables<M>(a, tab01, tab2);
   __syncthreads();
 
-  constexpr size_t kStep = size_t(kThreads) * kLaneBytes;
-  constexpr size_t kTile = kStep * W;
+  const size_t kStep = WAVEC ? size_t(64) * kLaneBytes : size_t(blockDim.x) * kLaneBytes;
+  const size_t kTile = size_t(blockDim.x) * kLaneBytes * W;
+  const size_t lane_off = WAVEC ? (size_t)(threadIdx.x >> 6) * (64 * kLaneBytes * W) + (threadIdx.x & 63) * kLaneBytes
+                                : (size_t)threadIdx.x * kLaneBytes;
   const uint32_t tps = a.tiles_per_stripe;
   const uint32_t ntiles = tps * a.nstripes;
   uint32_t diff = 0;
@@ -225,15 +229,15 @@ __device__ __forceinline__ void matvec(const GfArgs& a) {
     const size_t tile = t - (size_t)stripe * tps;
     const uint8_t* const* in = a.ptr + (size_t)stripe * a.k;
     uint8_t* const* out = const_cast<uint8_t* const*>(a.ptr + (size_t)a.nstripes * a.k + (size_t)stripe * a.m);
-    const size_t off = tile * kTile + (size_t)threadIdx.x * kLaneBytes;
+    const size_t off = tile * kTile + lane_off;
     if (off + (W - 1) * kStep + kLaneBytes <= a.len) {
-      lane_tile<M, MODE, W, G, NTL, NTS>(a, tab01, tab2, in, out, off, stripe, diff);
+      lane_tile<M, MODE, W, G, NTL, NTS>(a, tab01, tab2, in, out, off, kStep, stripe, diff);
     } else {
 #pragma unroll
       for (int w = 0; w < W; ++w) {
         const size_t o = off + w * kStep;
         if (o + kLaneBytes <= a.len)
-          lane_tile<M, MODE, 1, G, NTL, NTS>(a, tab01, tab2, in, out, o, stripe, diff);
+          lane_tile<M, MODE, 1, G, NTL, NTS>(a, tab01, tab2, in, out, o, kStep, stripe, diff);
         else if (o < a.len)
           lane_tail<M, MODE>(a, tab01, tab2, in, out, o, a.len - o, diff);
       }

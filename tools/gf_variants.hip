@@ -30,17 +30,25 @@ using dev::GfArgs;
     }                                                                                  \
   } while (0)
 
-template <int M, MatVecMode MODE, int W, int G, bool PERSIST, bool NTL, bool NTS, bool XCD>
-__global__ __launch_bounds__(dev::kThreads) void kvar(const GfArgs a) {
-  dev::matvec<M, MODE, W, G, PERSIST, NTL, NTS, XCD>(a);
+template <int M, MatVecMode MODE, int W, int G, bool PERSIST, bool NTL, bool NTS, bool XCD, int LB, bool WC>
+__global__ __launch_bounds__(LB) void kvar(const GfArgs a) {
+  dev::matvec<M, MODE, W, G, PERSIST, NTL, NTS, XCD, WC>(a);
 }
 
 __global__ void fill_kernel(uint32_t* p, size_t n, uint32_t seed) {
   size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
   for (; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    uint32_t x = (uint32_t)i * 2654435761u ^ seed;
-    x ^= x << 13; x ^= x >> 17; x ^= x << 5;
-    p[i] = x;
+    if (seed == 0) {  // splitmix64 per 8-byte word (full-entropy bytes)
+      uint64_t z = (uint64_t)(i >> 1) * 0x9E3779B97F4A7C15ull + 0xCF5EC000ull;
+      z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+      z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+      z ^= z >> 31;
+      p[i] = (i & 1) ? (uint32_t)(z >> 32) : (uint32_t)z;
+    } else {
+      uint32_t x = (uint32_t)i * 2654435761u ^ seed;
+      x ^= x << 13; x ^= x >> 17; x ^= x << 5;
+      p[i] = x;
+    }
   }
 }
 
@@ -49,16 +57,20 @@ struct Variant {
   void (*kern)(GfArgs);
   int W;
   bool persist;
+  int bt = 256;
+  size_t lds = 0;
 };
 
-template <int W, int G, bool P, bool NTL, bool NTS = NTL, bool XCD = false>
-Variant mk(const char* name, MatVecMode mode) {
+template <int W, int G, bool P, bool NTL, bool NTS = NTL, bool XCD = false, int LB = 256, bool WC = false>
+Variant mk(const char* name, MatVecMode mode, int bt = 256, size_t lds = 0) {
   Variant v;
+  v.bt = bt;
+  v.lds = lds;
   v.name = name;
   v.W = W;
   v.persist = P;
-  if (mode == MatVecMode::kVerify) v.kern = kvar<4, MatVecMode::kVerify, W, G, P, NTL, NTS, XCD>;
-  else v.kern = kvar<4, MatVecMode::kStore, W, G, P, NTL, NTS, XCD>;
+  if (mode == MatVecMode::kVerify) v.kern = kvar<4, MatVecMode::kVerify, W, G, P, NTL, NTS, XCD, LB, WC>;
+  else v.kern = kvar<4, MatVecMode::kStore, W, G, P, NTL, NTS, XCD, LB, WC>;
   return v;
 }
 
@@ -72,7 +84,7 @@ int main(int argc, char** argv) {
   uint8_t* buf = nullptr;
   const size_t bytes = pitch * total * nst;
   CK(hipMalloc(&buf, bytes));
-  fill_kernel<<<4096, 256>>>((uint32_t*)buf, bytes / 4, 0xCF5EC000u);
+  fill_kernel<<<4096, 256>>>((uint32_t*)buf, bytes / 4, argc > 6 ? (uint32_t)atoi(argv[6]) : 0xCF5EC000u);
   uint32_t* flags = nullptr;
   CK(hipMalloc(&flags, 4 * nst));
   CK(hipDeviceSynchronize());
@@ -93,36 +105,34 @@ int main(int argc, char** argv) {
   }
 
   std::vector<Variant> vs = {
-      mk<1, 1, false, false>("W1 G1", mode),
-      mk<1, 1, false, true>("W1 G1 nt", mode),
-      mk<1, 2, false, true>("W1 G2 nt", mode),
-      mk<1, 4, false, true>("W1 G4 nt", mode),
-      mk<1, 12, false, true>("W1 G12 nt", mode),
-      mk<1, 12, false, true, false>("W1 G12 ntL", mode),
-      mk<1, 12, false, false, true>("W1 G12 ntS", mode),
-      mk<1, 1, false, true, false>("W1 G1 ntL", mode),
-      mk<1, 12, false, true, true, true>("W1 G12 nt xcd", mode),
-      mk<1, 1, false, true, true, true>("W1 G1 nt xcd", mode),
-      mk<2, 12, false, true, true, true>("W2 G12 nt xcd", mode),
-      mk<4, 4, false, true>("W4 G4 nt", mode),
-      mk<1, 12, true, true>("W1 G12 nt persist", mode),
+      mk<1, 1, false, true>("b256 W1 nt (ctl)", mode),
+      mk<2, 1, false, true, true, false, 256, true>("b256 W2 nt wavec", mode),
+      mk<4, 1, false, true, true, false, 256, true>("b256 W4 nt wavec", mode),
+      mk<2, 1, false, true, true, false, 256, true>("b128 W2 nt wavec", mode, 128),
+      mk<4, 1, false, true, true, false, 256, true>("b128 W4 nt wavec", mode, 128),
+      mk<2, 2, false, true, true, false, 256, true>("b128 W2 G2 nt wavec", mode, 128),
+      mk<2, 2, false, true>("b128 W2 G2 nt", mode, 128),
+      mk<1, 1, false, true>("b256 W1 nt (ctl2)", mode),
   };
+
+
+
 
   int ncu = 0;
   CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
 
   std::vector<uint8_t> golden, cur;
   auto launch = [&](const Variant& v) {
-    const size_t tile = size_t(dev::kThreads) * dev::kLaneBytes * v.W;
+    const size_t tile = size_t(v.bt) * dev::kLaneBytes * v.W;
     GfArgs b = a;
     b.tiles_per_stripe = (uint32_t)((S + tile - 1) / tile);
     unsigned grid = b.tiles_per_stripe * nst;
     if (v.persist) {
       int per = 0;
-      CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, v.kern, dev::kThreads, 0));
+      CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, v.kern, v.bt, v.lds));
       grid = std::min<unsigned>(grid, (unsigned)(per * ncu));
     }
-    hipLaunchKernelGGL(v.kern, dim3(grid), dim3(dev::kThreads), 0, 0, b);
+    hipLaunchKernelGGL(v.kern, dim3(grid), dim3(v.bt), v.lds, 0, b);
   };
   auto snapshot = [&](std::vector<uint8_t>& out) {
     out.resize(size_t(nst) * m * S);
@@ -174,6 +184,41 @@ int main(int argc, char** argv) {
     }
   const double algo = double(k + m) * S * nst;
   printf("S=%zu stripes=%d mode=%d  algorithmic bytes/launch=%.0f\n", S, nst, (int)mode, algo);
+  const int soak = argc > 5 ? atoi(argv[5]) : 0;
+  if (soak > 0) {
+    // Steady state: control variant, encode-only vs alternating encode / reconstruct({0,1,2,3}),
+    // mean per launch over consecutive windows of 100 launches.
+    GfArgs rec = a;
+    Matrix sub(k, k), dec;
+    for (int r = 0; r < k; ++r)
+      for (int c = 0; c < k; ++c) sub.at(r, c) = mat.at(4 + r, c);
+    mat_invert(sub, dec);
+    for (int r = 0; r < m; ++r)
+      for (int c = 0; c < k; ++c) rec.coef[r * k + c] = dec.at(r, c);
+    for (int s = 0; s < nst; ++s) {
+      for (int c = 0; c < k; ++c) rec.ptr[s * k + c] = buf + (s * total + 4 + c) * pitch;
+      for (int r = 0; r < m; ++r) rec.ptr[nst * k + s * m + r] = buf + (s * total + r) * pitch;
+    }
+    const Variant& v = vs[0];
+    for (int alt = 0; alt < 2; ++alt) {
+      printf("soak %s:", alt ? "alternating enc/rec" : "encode only");
+      for (int w = 0; w < soak / 100; ++w) {
+        CK(hipEventRecord(e0, 0));
+        for (int j = 0; j < 100; ++j) {
+          GfArgs b = (alt && (j & 1)) ? rec : a;
+          const size_t tile = size_t(v.bt) * dev::kLaneBytes * v.W;
+          b.tiles_per_stripe = (uint32_t)((S + tile - 1) / tile);
+          hipLaunchKernelGGL(v.kern, dim3(b.tiles_per_stripe * nst), dim3(v.bt), 0, 0, b);
+        }
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        printf(" %.1f", ms * 10);  // us per launch
+      }
+      printf("\n");
+    }
+  }
   for (size_t i = 0; i < vs.size(); ++i) {
     auto v = t[i];
     std::sort(v.begin(), v.end());
