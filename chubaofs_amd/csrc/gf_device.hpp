@@ -1,16 +1,21 @@
 // gf_device.hpp -- device side of the GF(2^8) matrix x shard-vector kernel.
 //
-// Included by gf_kernels.hip (the product launcher) and by tools/gf_variants.hip
-// (the A/B tuning harness), so a tuned policy is exactly the code that ships.
+// Included by gf_kernels.hip (the product launcher) and by the tools/ A/B harnesses, so a
+// tuned policy is exactly the code that ships.
 //
-// See gf_kernels.hip for the arithmetic (3-bit split tables + v_perm_b32) and the
-// data movement.  The policy knobs here:
-//   W   16-B chunks per lane per tile (chunk w sits w*blockDim.x*16 bytes further on,
-//       so each wave still touches whole 1 KiB runs of every row)
+// See gf_kernels.hip for the arithmetic (3-bit split tables + v_perm_b32) and the data
+// movement.  Policy knobs (template parameters of matvec):
+//   M   output rows per wave (accumulators live in VGPRs: 4*M)
+//   OS  waves of a workgroup that share one column chunk, each owning M of the M*OS output
+//       rows (large m: keeps per-wave accumulators + tables small; the inputs the sharing
+//       waves re-read come from L1)
+//   W   16-B chunks per lane per tile (chunk w sits w*step bytes further on)
 //   G   input rows whose loads are issued together before any is consumed
 //   PERSIST  grid-stride over (stripe, tile) pairs; tables built once per workgroup
 //   NTL/NTS  non-temporal loads / stores (streaming data, touched once)
 //   XCD remap blockIdx so each XCD walks a contiguous run of tiles (T1 swizzle)
+//   WAVEC    chunk w of a lane sits w*1 KiB on inside its wave's own run (else the
+//            workgroup sweeps the tile W times)
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -28,12 +33,18 @@ constexpr int kPtrSlots = 300;  // shard pointers per launch
 constexpr int kThreads = 256;
 constexpr int kLaneBytes = 16;
 
+// Shard pointers of stripe s, row j:
+//   explicit table (sstride == 0): ptr[s*k + j] (inputs), ptr[tab*k + s*m + r] (outputs)
+//   affine batch   (sstride != 0): ptr[j] + s*sstride, table holds stripe 0 only (tab == 1),
+//                                  so one launch covers any number of stripes.
 struct __attribute__((aligned(16))) GfArgs {
   uint64_t len;
   uint32_t k, m, nstripes, tiles_per_stripe;  // tiles_per_stripe: in units of the kernel's tile
   uint32_t* flags;
+  int64_t sstride;                 // byte distance between consecutive stripes (affine batch)
+  uint32_t tab, pad0;              // stripes held in ptr[]
   uint8_t coef[kMaxM * kMaxK];    // m x k, row stride k
-  const uint8_t* ptr[kPtrSlots];  // [nstripes*k inputs][nstripes*m outputs]
+  const uint8_t* ptr[kPtrSlots];  // [tab*k inputs][tab*m outputs]
 };
 static_assert(sizeof(GfArgs) <= 3584, "kernel argument block must stay below 4 KiB");
 
@@ -73,15 +84,15 @@ __device__ __forceinline__ void st_tail(uint8_t* p, u32x4 v, size_t rem) {
     if ((size_t)i < rem) p[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
 }
 
-// Product tables for coefficient (c, r) at LDS slot c*M + r:
+// Product tables for coefficient (c, r) at LDS slot c*MT + r (MT = output rows per block):
 //   tab01 = {T0[0..3], T0[4..7], T1[0..3], T1[4..7]},  tab2 = T2[0..3]
 // with T0[e] = coef*e, T1[e] = coef*(e<<3), T2[e] = coef*(e<<6).
-template <int M>
+template <int MT>
 __device__ __forceinline__ void build_tables(const GfArgs& a, u32x4* tab01, uint32_t* tab2) {
   const int k = (int)a.k;
-  for (int i = threadIdx.x; i < k * M; i += (int)blockDim.x) {
-    const int c = i / M;
-    const int r = i - c * M;
+  for (int i = threadIdx.x; i < k * MT; i += (int)blockDim.x) {
+    const int c = i / MT;
+    const int r = i - c * MT;
     uint32_t p[8];
     p[0] = (r < (int)a.m) ? a.coef[r * k + c] : 0u;
 #pragma unroll
@@ -106,7 +117,8 @@ __device__ __forceinline__ void build_tables(const GfArgs& a, u32x4* tab01, uint
   }
 }
 
-// acc[r] ^= coef(c, r) * x for all M outputs; x is 16 bytes of input row c.
+// acc[r] ^= coef(c, r) * x for the wave's M outputs; x is 16 bytes of input row c and
+// tq/t2p point at this wave's first output of input row c.
 template <int M>
 __device__ __forceinline__ void mac_row(u32x4 (&acc)[M], u32x4 x, const u32x4* __restrict__ tq,
                                         const uint32_t* __restrict__ t2p) {
@@ -128,55 +140,59 @@ __device__ __forceinline__ void mac_row(u32x4 (&acc)[M], u32x4 x, const u32x4* _
   }
 }
 
+// Store / accumulate / compare the wave's outputs og .. og+M-1 (rows past a.m are padding).
 template <int M, MatVecMode MODE, bool NTL, bool NTS>
 __device__ __forceinline__ void finish(const GfArgs& a, u32x4 (&acc)[M], uint8_t* const* out,
-                                       size_t off, int stripe, uint32_t& diff) {
+                                       int og, size_t off, uint32_t& diff) {
   const int m = (int)a.m;
 #pragma unroll
   for (int r = 0; r < M; ++r) {
-    if (r < m) {
+    if (og + r < m) {
+      uint8_t* p = out[og + r] + off;
       if constexpr (MODE == MatVecMode::kVerify) {
-        const u32x4 d = acc[r] ^ ld16<NTL>(out[r] + off);
+        const u32x4 d = acc[r] ^ ld16<NTL>(p);
         diff |= d.x | d.y | d.z | d.w;
       } else {
         u32x4 v = acc[r];
-        if constexpr (MODE == MatVecMode::kAccum) v ^= ld16<NTL>(out[r] + off);
-        st16<NTS>(out[r] + off, v);
+        if constexpr (MODE == MatVecMode::kAccum) v ^= ld16<NTL>(p);
+        st16<NTS>(p, v);
       }
     }
   }
 }
 
 // One lane's chunk at the end of a shard (rem < 16 bytes), byte-granular.
-template <int M, MatVecMode MODE>
+template <int M, int MT, MatVecMode MODE>
 __device__ __forceinline__ void lane_tail(const GfArgs& a, const u32x4* tab01, const uint32_t* tab2,
-                                          const uint8_t* const* in, uint8_t* const* out, size_t off,
-                                          size_t rem, uint32_t& diff) {
+                                          const uint8_t* const* in, uint8_t* const* out, int og,
+                                          size_t off, size_t rem, uint32_t& diff) {
   const int k = (int)a.k, m = (int)a.m;
   u32x4 acc[M];
 #pragma unroll
   for (int r = 0; r < M; ++r) acc[r] = u32x4{0u, 0u, 0u, 0u};
-  for (int c = 0; c < k; ++c) mac_row<M>(acc, ld_tail(in[c] + off, rem), tab01 + c * M, tab2 + c * M);
+  for (int c = 0; c < k; ++c)
+    mac_row<M>(acc, ld_tail(in[c] + off, rem), tab01 + c * MT + og, tab2 + c * MT + og);
 #pragma unroll
   for (int r = 0; r < M; ++r) {
-    if (r < m) {
+    if (og + r < m) {
+      uint8_t* p = out[og + r] + off;
       if constexpr (MODE == MatVecMode::kVerify) {
-        const u32x4 d = acc[r] ^ ld_tail(out[r] + off, rem);
+        const u32x4 d = acc[r] ^ ld_tail(p, rem);
         diff |= d.x | d.y | d.z | d.w;
       } else {
         u32x4 v = acc[r];
-        if constexpr (MODE == MatVecMode::kAccum) v ^= ld_tail(out[r] + off, rem);
-        st_tail(out[r] + off, v, rem);
+        if constexpr (MODE == MatVecMode::kAccum) v ^= ld_tail(p, rem);
+        st_tail(p, v, rem);
       }
     }
   }
 }
 
 // Full tile: W chunks per lane, all in bounds.  Input rows are loaded G at a time.
-template <int M, MatVecMode MODE, int W, int G, bool NTL, bool NTS>
+template <int M, int MT, MatVecMode MODE, int W, int G, bool NTL, bool NTS>
 __device__ __forceinline__ void lane_tile(const GfArgs& a, const u32x4* tab01, const uint32_t* tab2,
-                                          const uint8_t* const* in, uint8_t* const* out, size_t off,
-                                          size_t kStep, int stripe, uint32_t& diff) {
+                                          const uint8_t* const* in, uint8_t* const* out, int og,
+                                          size_t off, size_t kStep, uint32_t& diff) {
   const int k = (int)a.k;
   u32x4 acc[W][M];
 #pragma unroll
@@ -194,27 +210,32 @@ __device__ __forceinline__ void lane_tile(const GfArgs& a, const u32x4* tab01, c
     for (int g = 0; g < G; ++g)
       if (c0 + g < k)
 #pragma unroll
-        for (int w = 0; w < W; ++w) mac_row<M>(acc[w], x[g][w], tab01 + (c0 + g) * M, tab2 + (c0 + g) * M);
+        for (int w = 0; w < W; ++w)
+          mac_row<M>(acc[w], x[g][w], tab01 + (c0 + g) * MT + og, tab2 + (c0 + g) * MT + og);
   }
 #pragma unroll
-  for (int w = 0; w < W; ++w) finish<M, MODE, NTL, NTS>(a, acc[w], out, off + w * kStep, stripe, diff);
+  for (int w = 0; w < W; ++w) finish<M, MODE, NTL, NTS>(a, acc[w], out, og, off + w * kStep, diff);
 }
 
-// Kernel body.  A tile is blockDim.x*16*W bytes of every row of one stripe.  Chunk w of a
-// lane sits w*blockDim.x*16 bytes on (WAVEC = false: the workgroup sweeps the tile W times)
-// or w*1 KiB on inside its wave's own W KiB run (WAVEC = true).
+// Kernel body.  A tile is (blockDim.x/OS)*16*W bytes of every row of one stripe; wave v of the
+// workgroup covers column chunk v/OS of it and output rows (v%OS)*M .. +M.
 template <int M, MatVecMode MODE, int W, int G, bool PERSIST, bool NTL, bool NTS, bool XCD,
-          bool WAVEC = false>
+          bool WAVEC = false, int OS = 1>
 __device__ __forceinline__ void matvec(const GfArgs& a) {
-  __shared__ u32x4 tab01[kMaxK * M];
-  __shared__ uint32_t tab2[kMaxK * M];
-  build_tables<M>(a, tab01, tab2);
+  constexpr int MT = M * OS;  // output rows per workgroup
+  __shared__ u32x4 tab01[kMaxK * MT];
+  __shared__ uint32_t tab2[kMaxK * MT];
+  build_tables<MT>(a, tab01, tab2);
   __syncthreads();
 
-  const size_t kStep = WAVEC ? size_t(64) * kLaneBytes : size_t(blockDim.x) * kLaneBytes;
-  const size_t kTile = size_t(blockDim.x) * kLaneBytes * W;
-  const size_t lane_off = WAVEC ? (size_t)(threadIdx.x >> 6) * (64 * kLaneBytes * W) + (threadIdx.x & 63) * kLaneBytes
-                                : (size_t)threadIdx.x * kLaneBytes;
+  const int wave = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+  const int og = (wave % OS) * M;   // this wave's first output row
+  const int cw = wave / OS;         // this wave's column chunk
+  const size_t col_threads = size_t(blockDim.x) / OS;
+  const size_t kStep = WAVEC ? size_t(64) * kLaneBytes : col_threads * kLaneBytes;
+  const size_t kTile = col_threads * kLaneBytes * W;
+  const size_t lane_off = WAVEC ? (size_t)cw * (64 * kLaneBytes * W) + (size_t)lane * kLaneBytes
+                                : ((size_t)cw * 64 + lane) * kLaneBytes;
   const uint32_t tps = a.tiles_per_stripe;
   const uint32_t ntiles = tps * a.nstripes;
   uint32_t diff = 0;
@@ -227,19 +248,24 @@ __device__ __forceinline__ void matvec(const GfArgs& a) {
   for (uint32_t t = first; t < ntiles; t += (PERSIST ? gridDim.x : ntiles)) {
     const int stripe = (int)(t / tps);
     const size_t tile = t - (size_t)stripe * tps;
-    const uint8_t* const* in = a.ptr + (size_t)stripe * a.k;
-    uint8_t* const* out = const_cast<uint8_t* const*>(a.ptr + (size_t)a.nstripes * a.k + (size_t)stripe * a.m);
-    const size_t off = tile * kTile + lane_off;
-    if (off + (W - 1) * kStep + kLaneBytes <= a.len) {
-      lane_tile<M, MODE, W, G, NTL, NTS>(a, tab01, tab2, in, out, off, kStep, stripe, diff);
-    } else {
+    // explicit table: this stripe's own pointers; affine batch: stripe 0's plus a byte offset
+    const size_t tstripe = a.sstride ? 0 : (size_t)stripe;
+    const size_t soff = (size_t)((int64_t)stripe * a.sstride);
+    const uint8_t* const* in = a.ptr + tstripe * a.k;
+    uint8_t* const* out = const_cast<uint8_t* const*>(a.ptr + (size_t)a.tab * a.k + tstripe * a.m);
+    const size_t off = tile * kTile + lane_off;  // byte offset inside the shard
+    if (og < (int)a.m) {  // waves whose output rows are all padding have nothing to do
+      if (off + (W - 1) * kStep + kLaneBytes <= a.len) {
+        lane_tile<M, MT, MODE, W, G, NTL, NTS>(a, tab01, tab2, in, out, og, soff + off, kStep, diff);
+      } else {
 #pragma unroll
-      for (int w = 0; w < W; ++w) {
-        const size_t o = off + w * kStep;
-        if (o + kLaneBytes <= a.len)
-          lane_tile<M, MODE, 1, G, NTL, NTS>(a, tab01, tab2, in, out, o, kStep, stripe, diff);
-        else if (o < a.len)
-          lane_tail<M, MODE>(a, tab01, tab2, in, out, o, a.len - o, diff);
+        for (int w = 0; w < W; ++w) {
+          const size_t o = off + w * kStep;
+          if (o + kLaneBytes <= a.len)
+            lane_tile<M, MT, MODE, 1, G, NTL, NTS>(a, tab01, tab2, in, out, og, soff + o, kStep, diff);
+          else if (o < a.len)
+            lane_tail<M, MT, MODE>(a, tab01, tab2, in, out, og, soff + o, a.len - o, diff);
+        }
       }
     }
     if constexpr (MODE == MatVecMode::kVerify) {

@@ -39,40 +39,69 @@ namespace cfsec {
 namespace {
 
 using dev::GfArgs;
-constexpr int kStoreThreads = 256;
 constexpr int kStoreW = 1;
-constexpr int kVerifyThreads = 128;
 constexpr int kVerifyW = 2;
 
-template <int M, MatVecMode MODE>
+// (M output rows per wave, OS waves sharing a column chunk) for mc outputs: small m keeps every
+// output in one wave; larger m splits the outputs over 2 or 4 waves of the workgroup so each
+// wave's accumulators + tables stay under ~64-90 VGPRs (a single wave holding 20 outputs
+// needed 271 VGPRs = one wave per SIMD).
+struct Shape {
+  int M, OS;
+};
+Shape choose(int mc) {
+  if (mc <= 6) return {mc, 1};
+  if (mc <= 8) return {4, 2};
+  if (mc <= 12) return {(mc + 1) / 2, 2};
+  if (mc <= 24) return {(mc + 3) / 4, 4};
+  return {8, 4};
+}
+
+#ifndef CFSEC_SPLIT_G
+#define CFSEC_SPLIT_G 1  // input rows loaded together by output-split (compute-heavy) kernels
+#endif
+
+template <int M, int OS, MatVecMode MODE>
 __global__ __launch_bounds__(256) void gf_matvec_kernel(const GfArgs a) {
+  constexpr int G = OS > 1 ? CFSEC_SPLIT_G : 1;
   if constexpr (MODE == MatVecMode::kVerify)
-    dev::matvec<M, MODE, kVerifyW, 2, false, true, true, false>(a);
+    dev::matvec<M, MODE, kVerifyW, 2, false, true, true, false, false, OS>(a);
   else
-    dev::matvec<M, MODE, kStoreW, 1, false, true, true, false>(a);
+    dev::matvec<M, MODE, kStoreW, G, false, true, true, false, false, OS>(a);
 }
 
 template <MatVecMode MODE>
-hipError_t launch_mode(int mpad, const GfArgs& a, dim3 grid, int threads, hipStream_t st) {
-#define CFSEC_CASE(MV)                                                                   \
-  case MV:                                                                               \
-    hipLaunchKernelGGL((gf_matvec_kernel<MV, MODE>), grid, dim3(threads), 0, st, a);     \
+hipError_t launch_mode(Shape sh, const GfArgs& a, dim3 grid, int threads, hipStream_t st) {
+#define CFSEC_CASE(MV, OSV)                                                                      \
+  case MV * 8 + OSV:                                                                             \
+    hipLaunchKernelGGL((gf_matvec_kernel<MV, OSV, MODE>), grid, dim3(threads), 0, st, a);        \
     break;
-  switch (mpad) {
-    CFSEC_CASE(1) CFSEC_CASE(2) CFSEC_CASE(3) CFSEC_CASE(4) CFSEC_CASE(5) CFSEC_CASE(6)
-    CFSEC_CASE(8) CFSEC_CASE(10) CFSEC_CASE(12) CFSEC_CASE(16) CFSEC_CASE(20)
-    CFSEC_CASE(24) CFSEC_CASE(32)
+  switch (sh.M * 8 + sh.OS) {
+    CFSEC_CASE(1, 1) CFSEC_CASE(2, 1) CFSEC_CASE(3, 1) CFSEC_CASE(4, 1) CFSEC_CASE(5, 1)
+    CFSEC_CASE(6, 1) CFSEC_CASE(4, 2) CFSEC_CASE(5, 2) CFSEC_CASE(6, 2) CFSEC_CASE(4, 4)
+    CFSEC_CASE(5, 4) CFSEC_CASE(6, 4) CFSEC_CASE(8, 4)
     default: return hipErrorInvalidValue;
   }
 #undef CFSEC_CASE
   return hipGetLastError();
 }
 
-int pad_outputs(int m) {
-  static const int kSizes[] = {1, 2, 3, 4, 5, 6, 8, 10, 12, 16, 20, 24, 32};
-  for (int s : kSizes)
-    if (s >= m) return s;
-  return -1;
+// Byte distance between consecutive stripes when every stripe of the job has the same
+// relative row layout (input rows c0..c0+kc, output rows r0..r0+mc); 0 otherwise.  Such a
+// batch (e.g. stripes carved from one pitched HBM buffer) runs as a single launch whatever its
+// stripe count; anything else is carried as an explicit pointer table, kPtrSlots per launch.
+int64_t affine_stride(const MatVecJob& job, int c0, int kc, int r0, int mc) {
+  if (job.nstripes < 2) return 0;
+  const auto addr = [](const void* p) { return (int64_t)(uintptr_t)p; };
+  const int64_t ss = addr(job.in[job.k + c0]) - addr(job.in[c0]);
+  if (ss == 0) return 0;
+  for (int s = 1; s < job.nstripes; ++s) {
+    for (int c = c0; c < c0 + kc; ++c)
+      if (addr(job.in[(size_t)s * job.k + c]) != addr(job.in[c]) + s * ss) return 0;
+    for (int r = r0; r < r0 + mc; ++r)
+      if (addr(job.out[(size_t)s * job.m + r]) != addr(job.out[r]) + s * ss) return 0;
+  }
+  return ss;
 }
 
 }  // namespace
@@ -94,38 +123,44 @@ hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
       MatVecMode mode = job.mode;
       if (mode == MatVecMode::kStore && c0 > 0) mode = MatVecMode::kAccum;
       const bool verify = mode == MatVecMode::kVerify;
-      const int threads = verify ? kVerifyThreads : kStoreThreads;
-      const size_t tile = size_t(threads) * dev::kLaneBytes * (verify ? kVerifyW : kStoreW);
+      const Shape sh = choose(mc);
+      // verify: 128-thread workgroups (2 chunks per lane) unless the outputs are split over waves
+      const int threads = (verify && sh.OS == 1) ? 128 : 256;
+      const size_t tile = size_t(threads / sh.OS) * dev::kLaneBytes * (verify ? kVerifyW : kStoreW);
       const size_t tiles = (job.len + tile - 1) / tile;
       const int per_stripe = kc + mc;
-      int stripes_per_launch = kPtrSlots / per_stripe;
+      const int64_t sstride = affine_stride(job, c0, kc, r0, mc);
+      int stripes_per_launch = sstride ? job.nstripes : kPtrSlots / per_stripe;
       // one launch covers tiles * stripes workgroups: keep that in a 32-bit grid
       stripes_per_launch = (int)std::min<size_t>(stripes_per_launch, std::max<size_t>(1, 0x7fffffffu / tiles));
       if (tiles > 0x7fffffffu) return hipErrorInvalidValue;
       for (int s0 = 0; s0 < job.nstripes; s0 += stripes_per_launch) {
         const int ns = std::min(stripes_per_launch, job.nstripes - s0);
+        const int tab = sstride ? 1 : ns;  // stripes held in the pointer table
         a.len = job.len;
         a.k = (uint32_t)kc;
         a.m = (uint32_t)mc;
         a.nstripes = (uint32_t)ns;
         a.tiles_per_stripe = (uint32_t)tiles;
         a.flags = job.flags ? job.flags + s0 : nullptr;
+        a.sstride = sstride;
+        a.tab = (uint32_t)tab;
+        a.pad0 = 0;
         for (int r = 0; r < mc; ++r)
           for (int c = 0; c < kc; ++c)
             a.coef[r * kc + c] = job.coef[(size_t)(r0 + r) * job.k + (c0 + c)];
-        for (int s = 0; s < ns; ++s) {
+        for (int s = 0; s < tab; ++s) {
           for (int c = 0; c < kc; ++c)
             a.ptr[s * kc + c] = job.in[(size_t)(s0 + s) * job.k + c0 + c];
           for (int r = 0; r < mc; ++r)
-            a.ptr[ns * kc + s * mc + r] = job.out[(size_t)(s0 + s) * job.m + r0 + r];
+            a.ptr[tab * kc + s * mc + r] = job.out[(size_t)(s0 + s) * job.m + r0 + r];
         }
         const dim3 grid((unsigned)(tiles * ns));
-        const int mpad = pad_outputs(mc);
         hipError_t e;
         switch (mode) {
-          case MatVecMode::kStore: e = launch_mode<MatVecMode::kStore>(mpad, a, grid, threads, stream); break;
-          case MatVecMode::kAccum: e = launch_mode<MatVecMode::kAccum>(mpad, a, grid, threads, stream); break;
-          default: e = launch_mode<MatVecMode::kVerify>(mpad, a, grid, threads, stream); break;
+          case MatVecMode::kStore: e = launch_mode<MatVecMode::kStore>(sh, a, grid, threads, stream); break;
+          case MatVecMode::kAccum: e = launch_mode<MatVecMode::kAccum>(sh, a, grid, threads, stream); break;
+          default: e = launch_mode<MatVecMode::kVerify>(sh, a, grid, threads, stream); break;
         }
         if (e != hipSuccess) return e;
       }

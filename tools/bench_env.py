@@ -1,7 +1,9 @@
-"""Dev tool: isolate what makes the step kernel slower inside the bench process.
+"""Dev tool: isolate what makes the step kernel slower inside bench.py.
 
-Times 200 back-to-back EC12P4 encode launches (8 x 64 MiB-blob stripes) for each combination
-of {torch-allocated, hipMalloc-allocated} buffer x {torch stream, null stream}, in one process.
+Runs the bench's setup with switchable pieces, then times N back-to-back launches of
+encode (E), alternating encode/reconstruct (A), in one process, printing us/launch.
+
+    python tools/bench_env.py [N] [setup...]   setup in {randfull, perstripe, clone}
 """
 import ctypes
 import os
@@ -15,39 +17,48 @@ from chubaofs_amd import reedsolomon  # noqa: E402
 K, M, S, NST = 12, 4, 5592406, 8
 TOTAL = K + M
 PITCH = (S + 255) // 256 * 256
-NBYTES = NST * TOTAL * PITCH
-
-hip = ctypes.CDLL("libamdhip64.so")
-hip.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
-hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
 
 
 def main():
-    dev = torch.device("cuda", 0)
-    tbuf = torch.randint(0, 256, (NBYTES,), dtype=torch.uint8, device=dev)
-    hptr = ctypes.c_void_p()
-    assert hip.hipMalloc(ctypes.byref(hptr), NBYTES) == 0
-    assert hip.hipMemcpy(hptr, ctypes.c_void_p(tbuf.data_ptr()), NBYTES, 3) == 0  # D2D
-    torch.cuda.synchronize()
-    enc = reedsolomon.New(K, M, device=0)
-    tstream = torch.cuda.Stream(device=dev)
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 200
-    for rnd in range(2):
-        for bname, base in (("torch-buf", tbuf.data_ptr()), ("hipMalloc-buf", hptr.value)):
-            ptrs = (ctypes.c_void_p * (NST * TOTAL))(*[base + i * PITCH for i in range(NST * TOTAL)])
-            for sname, st in (("torch-stream", tstream), ("null-stream", None)):
-                s = tstream if st is not None else torch.cuda.default_stream(dev)
-                for _ in range(10):
-                    enc.encode_batch(ptrs, S, NST, stream=st)
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(s)
-                for _ in range(n):
-                    enc.encode_batch(ptrs, S, NST, stream=st)
-                e1.record(s)
-                torch.cuda.synchronize()
-                us = e0.elapsed_time(e1) / n * 1e3
-                print(f"round {rnd} {bname:14s} {sname:13s} {us:7.1f} us/launch  "
-                      f"{TOTAL * S * NST / (us * 1e-6) / 1e9:7.1f} GB/s", flush=True)
+    setup = set(sys.argv[2:])
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    if "perstripe" in setup:  # exactly bench.py's fill
+        batch = torch.zeros((NST, TOTAL, PITCH), dtype=torch.uint8, device=dev)
+        for s in range(NST):
+            g = torch.Generator(device=dev)
+            g.manual_seed(0xCF5EC000 + s)
+            batch[s, :K, :S] = torch.randint(0, 256, (K, S), generator=g, device=dev, dtype=torch.uint8)
+    else:
+        batch = torch.randint(0, 256, (NST, TOTAL, PITCH), dtype=torch.uint8, device=dev)
+    base = batch.data_ptr()
+    ptrs = (ctypes.c_void_p * (NST * TOTAL))(*[base + i * PITCH for i in range(NST * TOTAL)])
+    enc = reedsolomon.New(K, M, device=0)
+    st = torch.cuda.Stream(device=dev)
+    enc.encode_batch(ptrs, S, NST, stream=st)
+    enc.reconstruct_batch(ptrs, S, NST, [0, 1, 2, 3], stream=st)
+    torch.cuda.synchronize()
+    if "clone" in setup:
+        golden = batch.clone()  # noqa: F841
+    torch.cuda.synchronize()
+
+    def run(kind, reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for i in range(reps):
+            if kind == "E" or i % 2 == 0:
+                enc.encode_batch(ptrs, S, NST, stream=st)
+            else:
+                enc.reconstruct_batch(ptrs, S, NST, [0, 1, 2, 3], stream=st)
+        e1.record(st)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps * 1e3
+
+    for rnd in range(3):
+        for kind in ("E", "A"):
+            print(f"setup={sorted(setup)} round {rnd} {kind}: {run(kind, n):7.1f} us/launch  "
+                  f"windows of 20: {[round(run(kind, 20), 1) for _ in range(5)]}", flush=True)
 
 
 if __name__ == "__main__":

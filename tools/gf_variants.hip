@@ -96,6 +96,7 @@ int main(int argc, char** argv) {
   a.k = k;
   a.m = m;
   a.nstripes = nst;
+  a.tab = nst;
   a.flags = flags;
   for (int r = 0; r < m; ++r)
     for (int c = 0; c < k; ++c) a.coef[r * k + c] = mat.at(k + r, c);
