@@ -217,6 +217,132 @@ __device__ __forceinline__ void lane_tile(const GfArgs& a, const u32x4* tab01, c
   for (int w = 0; w < W; ++w) finish<M, MODE, NTL, NTS>(a, acc[w], out, og, off + w * kStep, diff);
 }
 
+// acc[r][w] ^= coef(c, r) * x[w] on plain dword arrays (the fixed-K tile's form of mac_row).
+template <int M>
+__device__ __forceinline__ void mac_row_k(uint32_t (&acc)[M][4], const uint32_t (&x)[4],
+                                          const u32x4* __restrict__ tq, const uint32_t* __restrict__ t2p) {
+  uint32_t s0[4], s1[4], s2[4];
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    s0[w] = x[w] & 0x07070707u;
+    s1[w] = (x[w] >> 3) & 0x07070707u;
+    s2[w] = (x[w] >> 6) & 0x03030303u;
+  }
+#pragma unroll
+  for (int r = 0; r < M; ++r) {
+    const u32x4 q = tq[r];
+    const uint32_t t2 = t2p[r];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const uint32_t p0 = __builtin_amdgcn_perm(q.y, q.x, s0[w]);
+      const uint32_t p1 = __builtin_amdgcn_perm(q.w, q.z, s1[w]);
+      const uint32_t p2 = __builtin_amdgcn_perm(0u, t2, s2[w]);
+      acc[r][w] = __builtin_amdgcn_bitop3_b32(acc[r][w], p0, p1, 0x96) ^ p2;
+    }
+  }
+}
+
+// Full tile for a compile-time input count K, one 16-B chunk per lane at byte `loff` of every row.
+// The rows a lane touches (K inputs, then in verify mode the M rows it compares) form one load
+// sequence in which row c+D is issued before row c is consumed, so D loads per wave stay in
+// flight while the multiply runs.  The order is enforced, not hoped for: with the whole tile in
+// one basic block the scheduler otherwise hoists every load and table read to the top (270-356
+// VGPRs for K=12, M=4: one or two waves per SIMD), so each row ends by pinning the accumulators
+// (empty asm) behind a sched_barrier, and the row pointers (uniform: SGPR bases, 32-bit lane
+// offsets) are loaded once up front.  tools/gf_pipe.hip measured the effect.
+template <int K, int M, int MT, MatVecMode MODE, int D, bool NTL, bool NTS>
+__device__ __forceinline__ void lane_tile_k(int m, const u32x4* tab01, const uint32_t* tab2,
+                                            const uint8_t* const* in, uint8_t* const* out, int og,
+                                            int64_t sbase, uint32_t loff, uint32_t& diff) {
+  constexpr bool kVer = MODE == MatVecMode::kVerify;
+  constexpr int R = K + (kVer ? M : 0);  // rows loaded
+  const uint8_t* row[R];
+#pragma unroll
+  for (int c = 0; c < K; ++c) row[c] = in[c] + sbase;
+#pragma unroll
+  for (int r = 0; r < R - K; ++r) row[K + r] = out[og + r < m ? og + r : og] + sbase;
+  __builtin_amdgcn_sched_barrier(0);
+
+  uint32_t acc[M][4];
+#pragma unroll
+  for (int r = 0; r < M; ++r)
+#pragma unroll
+    for (int w = 0; w < 4; ++w) acc[r][w] = 0u;
+  uint32_t x[R][4];
+  const auto load = [&](int c) {
+    if (c >= K && og + (c - K) >= m) return;  // verify padding row
+    const u32x4 v = ld16<NTL>(row[c] + loff);
+    x[c][0] = v.x;
+    x[c][1] = v.y;
+    x[c][2] = v.z;
+    x[c][3] = v.w;
+  };
+#pragma unroll
+  for (int c = 0; c < D && c < R; ++c) load(c);
+#pragma unroll
+  for (int c = 0; c < R; ++c) {
+    if (c + D < R) load(c + D);
+    __builtin_amdgcn_sched_barrier(0);
+    if (c < K) {
+      mac_row_k<M>(acc, x[c], tab01 + c * MT + og, tab2 + c * MT + og);
+#pragma unroll
+      for (int r = 0; r < M; ++r)
+        asm volatile("" : "+v"(acc[r][0]), "+v"(acc[r][1]), "+v"(acc[r][2]), "+v"(acc[r][3]));
+    } else if (og + (c - K) < m) {
+      const int r = c - K;
+      diff |= (acc[r][0] ^ x[c][0]) | (acc[r][1] ^ x[c][1]) | (acc[r][2] ^ x[c][2]) | (acc[r][3] ^ x[c][3]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if constexpr (!kVer) {
+#pragma unroll
+    for (int r = 0; r < M; ++r) {
+      if (og + r < m) {
+        uint8_t* p = out[og + r] + sbase + loff;
+        u32x4 v = u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
+        if constexpr (MODE == MatVecMode::kAccum) v ^= ld16<NTL>(p);
+        st16<NTS>(p, v);
+      }
+    }
+  }
+}
+
+// Kernel body for a compile-time input count (a.k == K, a.len < 4 GiB): 256-thread workgroups,
+// one 16-B chunk per lane, tile = (256/OS)*16 bytes of every row, grid (tiles, stripes);
+// otherwise as matvec below.
+template <int K, int M, MatVecMode MODE, int D, int OS>
+__device__ __forceinline__ void matvec_k(const GfArgs& a) {
+  constexpr int MT = M * OS;
+  __shared__ u32x4 tab01[K * MT];
+  __shared__ uint32_t tab2[K * MT];
+  build_tables<MT>(a, tab01, tab2);
+  __syncthreads();
+
+  const int wave = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+  const int og = (wave % OS) * M;
+  const int cw = wave / OS;
+  constexpr uint32_t kTile = uint32_t(kThreads / OS) * kLaneBytes;
+  // 2-D grid (x: tiles of a stripe, y: stripes): a division of blockIdx.x would expand to VALU
+  // code and drag the row pointers into VGPRs
+  const uint32_t stripe = blockIdx.y;
+  const uint32_t tile = blockIdx.x;
+  const size_t tstripe = a.sstride ? 0 : (size_t)stripe;
+  const int64_t sbase = (int64_t)stripe * a.sstride;
+  const uint8_t* const* in = a.ptr + tstripe * K;
+  uint8_t* const* out = const_cast<uint8_t* const*>(a.ptr + (size_t)a.tab * K + tstripe * a.m);
+  const uint32_t off = tile * kTile + (uint32_t)(cw * 64 + lane) * kLaneBytes;
+  uint32_t diff = 0;
+  if (og < (int)a.m) {
+    if ((uint64_t)off + kLaneBytes <= a.len)
+      lane_tile_k<K, M, MT, MODE, D, true, true>((int)a.m, tab01, tab2, in, out, og, sbase, off, diff);
+    else if (off < a.len)
+      lane_tail<M, MT, MODE>(a, tab01, tab2, in, out, og, (size_t)sbase + off, a.len - off, diff);
+  }
+  if constexpr (MODE == MatVecMode::kVerify) {
+    if (diff) atomicOr(a.flags + stripe, 1u);
+  }
+}
+
 // Kernel body.  A tile is (blockDim.x/OS)*16*W bytes of every row of one stripe; wave v of the
 // workgroup covers column chunk v/OS of it and output rows (v%OS)*M .. +M.
 template <int M, MatVecMode MODE, int W, int G, bool PERSIST, bool NTL, bool NTS, bool XCD,

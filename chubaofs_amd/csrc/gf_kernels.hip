@@ -26,13 +26,18 @@
 // launch free of device allocations and host->device copies (safe under
 // concurrent callers and hipGraph capture).
 //
-// Policies (tools/gf_variants.hip, interleaved A/B on MI355X, EC12P4 8x64 MiB):
-//   store/accum: 256-thread workgroups, 1 chunk per lane, loads one row at a time
-//                (deeper per-lane load batches and persistent grids measured slower)
-//   verify:      128-thread workgroups, 2 chunks per lane, rows loaded in pairs
+// Two kernel families:
+//   fixed-K (gf_fixed.hpp, k in {6, 8, 12, 16, 18}: every CubeFS code mode and local stripe):
+//                256-thread workgroups, 1 chunk per lane, rows pipelined 2 ahead with the issue
+//                order pinned (tools/gf_pipe.hip: +6% over the runtime-k loop on EC12P4, at
+//                the trivial-arithmetic ceiling of the same access pattern)
+//   runtime-k (any other k, or k > 32 chunked with accumulate): policies from
+//                tools/gf_variants.hip -- store/accum 256-thread, 1 chunk per lane, one row at a
+//                time; verify 128-thread, 2 chunks per lane, rows loaded in pairs
 #include <algorithm>
 
 #include "gf_device.hpp"
+#include "gf_launch.hpp"
 #include "kernels.hpp"
 
 namespace cfsec {
@@ -41,21 +46,6 @@ namespace {
 using dev::GfArgs;
 constexpr int kStoreW = 1;
 constexpr int kVerifyW = 2;
-
-// (M output rows per wave, OS waves sharing a column chunk) for mc outputs: small m keeps every
-// output in one wave; larger m splits the outputs over 2 or 4 waves of the workgroup so each
-// wave's accumulators + tables stay under ~64-90 VGPRs (a single wave holding 20 outputs
-// needed 271 VGPRs = one wave per SIMD).
-struct Shape {
-  int M, OS;
-};
-Shape choose(int mc) {
-  if (mc <= 6) return {mc, 1};
-  if (mc <= 8) return {4, 2};
-  if (mc <= 12) return {(mc + 1) / 2, 2};
-  if (mc <= 24) return {(mc + 3) / 4, 4};
-  return {8, 4};
-}
 
 #ifndef CFSEC_SPLIT_G
 #define CFSEC_SPLIT_G 1  // input rows loaded together by output-split (compute-heavy) kernels
@@ -68,6 +58,18 @@ __global__ __launch_bounds__(256) void gf_matvec_kernel(const GfArgs a) {
     dev::matvec<M, MODE, kVerifyW, 2, false, true, true, false, false, OS>(a);
   else
     dev::matvec<M, MODE, kStoreW, G, false, true, true, false, false, OS>(a);
+}
+
+template <MatVecMode MODE>
+hipError_t launch_fixed(int k, Shape sh, const GfArgs& a, dim3 grid, hipStream_t st) {
+  switch (k) {
+    case 6: return launch_k<6, MODE>(sh, a, grid, st);
+    case 8: return launch_k<8, MODE>(sh, a, grid, st);
+    case 12: return launch_k<12, MODE>(sh, a, grid, st);
+    case 16: return launch_k<16, MODE>(sh, a, grid, st);
+    case 18: return launch_k<18, MODE>(sh, a, grid, st);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 template <MatVecMode MODE>
@@ -124,15 +126,21 @@ hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
       if (mode == MatVecMode::kStore && c0 > 0) mode = MatVecMode::kAccum;
       const bool verify = mode == MatVecMode::kVerify;
       const Shape sh = choose(mc);
-      // verify: 128-thread workgroups (2 chunks per lane) unless the outputs are split over waves
-      const int threads = (verify && sh.OS == 1) ? 128 : 256;
-      const size_t tile = size_t(threads / sh.OS) * dev::kLaneBytes * (verify ? kVerifyW : kStoreW);
+      // the code-mode input counts take the fixed-K pipelined kernels (all 256-thread, 1 chunk
+      // per lane); anything else the runtime-k kernel, whose verify policy is 128-thread
+      // workgroups with 2 chunks per lane unless the outputs are split over waves
+      const bool fixed = fixed_k(kc) && kc == job.k && mode != MatVecMode::kAccum &&
+                         job.len <= 0xFFFFFFFFull - 4096;  // 32-bit lane offsets
+      const int threads = (!fixed && verify && sh.OS == 1) ? 128 : 256;
+      const size_t tile =
+          size_t(threads / sh.OS) * dev::kLaneBytes * ((verify && !fixed) ? kVerifyW : kStoreW);
       const size_t tiles = (job.len + tile - 1) / tile;
       const int per_stripe = kc + mc;
       const int64_t sstride = affine_stride(job, c0, kc, r0, mc);
       int stripes_per_launch = sstride ? job.nstripes : kPtrSlots / per_stripe;
       // one launch covers tiles * stripes workgroups: keep that in a 32-bit grid
       stripes_per_launch = (int)std::min<size_t>(stripes_per_launch, std::max<size_t>(1, 0x7fffffffu / tiles));
+      if (fixed) stripes_per_launch = std::min(stripes_per_launch, 65535);  // grid.y = stripes
       if (tiles > 0x7fffffffu) return hipErrorInvalidValue;
       for (int s0 = 0; s0 < job.nstripes; s0 += stripes_per_launch) {
         const int ns = std::min(stripes_per_launch, job.nstripes - s0);
@@ -157,6 +165,13 @@ hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
         }
         const dim3 grid((unsigned)(tiles * ns));
         hipError_t e;
+        if (fixed) {
+          const dim3 grid2((unsigned)tiles, (unsigned)ns);
+          e = verify ? launch_fixed<MatVecMode::kVerify>(kc, sh, a, grid2, stream)
+                     : launch_fixed<MatVecMode::kStore>(kc, sh, a, grid2, stream);
+          if (e != hipSuccess) return e;
+          continue;
+        }
         switch (mode) {
           case MatVecMode::kStore: e = launch_mode<MatVecMode::kStore>(sh, a, grid, threads, stream); break;
           case MatVecMode::kAccum: e = launch_mode<MatVecMode::kAccum>(sh, a, grid, threads, stream); break;

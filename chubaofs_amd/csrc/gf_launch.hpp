@@ -1,0 +1,47 @@
+// gf_launch.hpp -- launcher internals shared by gf_kernels.hip and the fixed-K translation
+// units gf_k{6,8,12,16,18}.hip (one TU per input count so the instantiations build in parallel).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "gf_device.hpp"
+#include "kernels.hpp"
+
+namespace cfsec {
+
+// (M output rows per wave, OS waves sharing a column chunk) for mc outputs: small m keeps every
+// output in one wave; larger m splits the outputs over 2 or 4 waves of the workgroup so each
+// wave's accumulators + tables stay under ~64-90 VGPRs (a single wave holding 20 outputs
+// needed 271 VGPRs = one wave per SIMD).
+struct Shape {
+  int M, OS;
+};
+inline Shape choose(int mc) {
+  if (mc <= 6) return {mc, 1};
+  if (mc <= 8) return {4, 2};
+  if (mc <= 12) return {(mc + 1) / 2, 2};
+  if (mc <= 24) return {(mc + 3) / 4, 4};
+  return {8, 4};
+}
+
+// Fixed-K kernels for the input counts of the CubeFS code modes: k = 6 (EC6P6, EC6P10), 8 (the
+// EC6P10L2 local stripe), 12 (EC12P4), 16 (EC16P20), 18 (the EC16P20L2 local stripe).
+inline bool fixed_k(int k) { return k == 6 || k == 8 || k == 12 || k == 16 || k == 18; }
+
+// Launch gf_matvec_k_kernel<K, M, OS, MODE> for shape sh (defined in gf_fixed.hpp, instantiated
+// for kStore and kVerify in gf_k<K>.hip).
+template <int K, MatVecMode MODE>
+hipError_t launch_k(Shape sh, const dev::GfArgs& a, dim3 grid, hipStream_t st);
+
+#define CFSEC_EXTERN_K(K)                                                                       \
+  extern template hipError_t launch_k<K, MatVecMode::kStore>(Shape, const dev::GfArgs&, dim3, \
+                                                             hipStream_t);                    \
+  extern template hipError_t launch_k<K, MatVecMode::kVerify>(Shape, const dev::GfArgs&, dim3, \
+                                                              hipStream_t);
+CFSEC_EXTERN_K(6)
+CFSEC_EXTERN_K(8)
+CFSEC_EXTERN_K(12)
+CFSEC_EXTERN_K(16)
+CFSEC_EXTERN_K(18)
+#undef CFSEC_EXTERN_K
+
+}  // namespace cfsec

@@ -5,8 +5,9 @@
 // VALU lane-op estimate of the v_perm arithmetic.  Correctness of the same kernels is covered
 // by tests/test_gpu_parity.py; this tool only times.
 //
+// Encode (kStore) and Verify (kVerify) per shape.  Links the shipped library:
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../chubaofs_amd/csrc gf_shapes.hip \
-//         ../chubaofs_amd/csrc/gf_kernels.hip -o gf_shapes
+//         -L../chubaofs_amd -lcfsec -Wl,-rpath,'$ORIGIN/../chubaofs_amd' -o gf_shapes
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -66,7 +67,10 @@ int main() {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  printf("%-30s %3s %3s %9s %4s %9s %8s %6s %9s\n", "shape", "k", "m", "S", "nst", "us/launch", "GB/s", "%8TB", "Tlaneop/s");
+  uint32_t* flags;
+  CK(hipMalloc(&flags, 4096));
+  printf("%-30s %3s %3s %9s %4s %9s %8s %6s %9s %9s %6s\n", "shape", "k", "m", "S", "nst", "us/launch", "GB/s",
+         "%8TB", "Tlaneop/s", "verify us", "%8TB");
   for (auto& sh : shapes) {
     const size_t pitch = (sh.S + 255) / 256 * 256;
     Matrix mat;
@@ -91,6 +95,9 @@ int main() {
     job.in = in.data();
     job.out = out.data();
     auto launch_all = [&]() { CK(launch_matvec(job, 0)); };  // the shipped launcher
+    MatVecJob vjob = job;
+    vjob.mode = MatVecMode::kVerify;
+    vjob.flags = flags;
     static float settled = 0;  // ~300 ms of load once, so clocks leave their idle state
     while (settled < 300) {
       CK(hipEventRecord(e0, 0));
@@ -110,11 +117,19 @@ int main() {
     float ms;
     CK(hipEventElapsedTime(&ms, e0, e1));
     const double us = ms * 1e3 / reps;
+    CK(hipEventRecord(e0, 0));
+    for (int i = 0; i < reps; ++i) CK(launch_matvec(vjob, 0));
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float vms;
+    CK(hipEventElapsedTime(&vms, e0, e1));
+    const double vus = vms * 1e3 / reps;
     const double bytes = double(sh.k + sh.m) * sh.S * sh.stripes;
     // lane-ops: per 16-B lane chunk, k inputs x (20 selector ops + m x 20 perm/xor ops)
     const double laneops = double(sh.S) / 16 * sh.stripes * sh.k * (20.0 + 20.0 * sh.m);
-    printf("%-30s %3d %3d %9zu %4d %9.1f %8.1f %6.1f %9.1f\n", sh.name, sh.k, sh.m, sh.S, sh.stripes, us,
-           bytes / (us * 1e-6) / 1e9, 100 * bytes / (us * 1e-6) / 8e12, laneops / (us * 1e-6) / 1e12);
+    printf("%-30s %3d %3d %9zu %4d %9.1f %8.1f %6.1f %9.1f %9.1f %6.1f\n", sh.name, sh.k, sh.m, sh.S, sh.stripes,
+           us, bytes / (us * 1e-6) / 1e9, 100 * bytes / (us * 1e-6) / 8e12, laneops / (us * 1e-6) / 1e12, vus,
+           100 * bytes / (vus * 1e-6) / 8e12);
   }
   return 0;
 }
