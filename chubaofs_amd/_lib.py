@@ -91,6 +91,8 @@ SIGNATURES = {
     "cfsec_rs_encode_batch": ([_V, _V, _S, _I, _V], _I),
     "cfsec_rs_verify_batch": ([_V, _V, _S, _I, _V, _V], _I),
     "cfsec_rs_reconstruct_batch": ([_V, _V, _S, _I, _V, _I, _I, _V], _I),
+    "cfsec_rs_encode_crc_batch": ([_V, _V, _S, _I, _V, _V], _I),
+    "cfsec_rs_reconstruct_crc_batch": ([_V, _V, _S, _I, _V, _I, _I, _V, _V], _I),
     "cfsec_codemode_tactic": ([_I, _P(TacticC)], _I),
     "cfsec_ec_new": ([_P(TacticC), _I, _I, _I, _P(_V)], _I),
     "cfsec_ec_free": ([_V], None),

@@ -181,6 +181,22 @@ int cfsec_rs_reconstruct_batch(cfsec_rs* h, uint8_t* const* ptrs, size_t shard_s
   });
 }
 
+int cfsec_rs_encode_crc_batch(cfsec_rs* h, uint8_t* const* ptrs, size_t shard_size, int nstripes,
+                              uint32_t* crcs, void* stream) {
+  if (!h) return CFSEC_ERR_INVALID_ARG;
+  return guarded([&] { return h->e->encode_crc_batch(ptrs, shard_size, nstripes, crcs, as_stream(stream)); });
+}
+
+int cfsec_rs_reconstruct_crc_batch(cfsec_rs* h, uint8_t* const* ptrs, size_t shard_size, int nstripes,
+                                   const int* erased, int nerased, int data_only, uint32_t* crcs,
+                                   void* stream) {
+  if (!h) return CFSEC_ERR_INVALID_ARG;
+  return guarded([&] {
+    return h->e->reconstruct_crc_batch(ptrs, shard_size, nstripes, erased, nerased, data_only != 0, crcs,
+                                       as_stream(stream));
+  });
+}
+
 // ---------------- ec.Encoder ----------------
 
 int cfsec_codemode_tactic(int codemode, cfsec_tactic* t) {

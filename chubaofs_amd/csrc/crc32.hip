@@ -19,12 +19,14 @@ namespace {
 constexpr uint32_t kPoly = 0xEDB88320u;
 constexpr int kThreads = 256;
 constexpr size_t kChunk = 1024;
-constexpr int kSlots = 400;
+constexpr int kSlots = 280;
 
 struct __attribute__((aligned(16))) CrcArgs {
   uint64_t len;
   uint32_t* out;
+  uint32_t fin, pad;            // XOR-ed in once per shard (0: leave the raw word)
   const uint8_t* ptr[kSlots];
+  uint32_t idx[kSlots];         // output word of shard i
 };
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -99,32 +101,43 @@ __global__ __launch_bounds__(kThreads) void crc32_chunks_kernel(const CrcArgs a)
   }
   for (; i < end; ++i) crc = (crc >> 8) ^ tab[0][(crc ^ p[i]) & 0xFF];
   if (end < a.len) crc = multmodp(x8nmodp(a.len - end, d_x2n.t), crc);
-  atomicXor(a.out + blockIdx.y, crc);
+  if (start == 0) crc ^= a.fin;
+  atomicXor(a.out + a.idx[blockIdx.y], crc);
 }
 
 }  // namespace
 
-hipError_t launch_crc32(const uint8_t* const* ptrs, size_t len, int n, uint32_t* out,
-                        hipStream_t stream) {
+hipError_t launch_crc32_to(const uint8_t* const* ptrs, size_t len, int n, uint32_t* out, const uint32_t* idx,
+                           uint32_t fin, hipStream_t stream) {
   static const X2n host_x2n = make_x2n();
   hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(d_x2n), &host_x2n, sizeof(X2n), 0,
                                         hipMemcpyHostToDevice, stream);
-  if (e != hipSuccess) return e;
-  e = hipMemsetAsync(out, 0, sizeof(uint32_t) * (size_t)n, stream);
   if (e != hipSuccess || len == 0 || n == 0) return e;
   const size_t blocks = (len + kChunk * kThreads - 1) / (kChunk * kThreads);
   CrcArgs a;
   a.len = len;
+  a.out = out;
+  a.fin = fin;
+  a.pad = 0;
   for (int s0 = 0; s0 < n; s0 += kSlots) {
     const int ns = std::min(kSlots, n - s0);
-    a.out = out + s0;
-    for (int s = 0; s < ns; ++s) a.ptr[s] = ptrs[s0 + s];
+    for (int s = 0; s < ns; ++s) {
+      a.ptr[s] = ptrs[s0 + s];
+      a.idx[s] = idx ? idx[s0 + s] : (uint32_t)(s0 + s);
+    }
     hipLaunchKernelGGL(crc32_chunks_kernel, dim3((unsigned)blocks, (unsigned)ns), dim3(kThreads), 0,
                        stream, a);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
+}
+
+hipError_t launch_crc32(const uint8_t* const* ptrs, size_t len, int n, uint32_t* out,
+                        hipStream_t stream) {
+  hipError_t e = hipMemsetAsync(out, 0, sizeof(uint32_t) * (size_t)n, stream);
+  if (e != hipSuccess) return e;
+  return launch_crc32_to(ptrs, len, n, out, nullptr, 0u, stream);
 }
 
 uint32_t crc32_finalize(uint32_t raw, size_t len) {

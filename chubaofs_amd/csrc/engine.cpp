@@ -563,6 +563,102 @@ Status RSEngine::reconstruct_batch(uint8_t* const* ptrs, size_t S, int nstripes,
   return hip_status(launch_matvec(job, stream), "launch_matvec(reconstruct_batch)");
 }
 
+// Product + checksums: the fused kernel where it exists, else the product then the standalone
+// CRC kernel over the same shards (one more read of each).
+static Status matvec_with_crc(const MatVecJob& job, uint8_t* const* ptrs, int total, const std::vector<int>& slot,
+                              size_t S, uint32_t* crcs, hipStream_t stream) {
+  if (matvec_crc_supported(job.k, job.m, S))
+    return hip_status(launch_matvec_crc(job, crcs, total, slot.data(), stream), "launch_matvec_crc");
+  Status st = hip_status(launch_matvec(job, stream), "launch_matvec");
+  if (st != CFSEC_OK) return st;
+  st = hip_status(hipMemsetAsync(crcs, 0, sizeof(uint32_t) * (size_t)total * job.nstripes, stream), "hipMemsetAsync");
+  if (st != CFSEC_OK || S == 0) return st;
+  std::vector<const uint8_t*> p;
+  std::vector<uint32_t> idx;
+  const bool cin = slot[0] >= 0;
+  for (int s = 0; s < job.nstripes; ++s)
+    for (int i = 0; i < job.k + job.m; ++i) {
+      if (i < job.k && !cin) continue;
+      p.push_back(i < job.k ? job.in[(size_t)s * job.k + i] : job.out[(size_t)s * job.m + i - job.k]);
+      idx.push_back((uint32_t)(s * total + slot[i]));
+    }
+  return hip_status(launch_crc32_to(p.data(), S, (int)p.size(), crcs, idx.data(), crc32_shift_ones(S), stream),
+                    "launch_crc32_to");
+}
+
+Status RSEngine::encode_crc_batch(uint8_t* const* ptrs, size_t S, int nstripes, uint32_t* crcs,
+                                  hipStream_t stream) {
+  if (!ctx_) return CFSEC_ERR_DEVICE;
+  if (!ptrs || !crcs || nstripes < 0) return CFSEC_ERR_INVALID_ARG;
+  if (nstripes == 0) return CFSEC_OK;
+  DeviceGuard g(ctx_->device());
+  if (m_ == 0 || S == 0) {
+    Status st = hip_status(hipMemsetAsync(crcs, 0, 4 * (size_t)total() * nstripes, stream), "hipMemsetAsync");
+    if (st != CFSEC_OK || S == 0) return st;
+    std::vector<const uint8_t*> p(ptrs, ptrs + (size_t)total() * nstripes);
+    return hip_status(launch_crc32_to(p.data(), S, (int)p.size(), crcs, nullptr, crc32_shift_ones(S), stream),
+                      "launch_crc32_to");
+  }
+  std::vector<const uint8_t*> in(size_t(nstripes) * k_);
+  std::vector<uint8_t*> out(size_t(nstripes) * m_);
+  for (int s = 0; s < nstripes; ++s) {
+    for (int c = 0; c < k_; ++c) in[size_t(s) * k_ + c] = ptrs[size_t(s) * total() + c];
+    for (int r = 0; r < m_; ++r) out[size_t(s) * m_ + r] = ptrs[size_t(s) * total() + k_ + r];
+  }
+  MatVecJob job;
+  job.k = k_;
+  job.m = m_;
+  job.coef = parity_.v.data();
+  job.len = S;
+  job.nstripes = nstripes;
+  job.in = in.data();
+  job.out = out.data();
+  std::vector<int> slot(total());
+  for (int i = 0; i < total(); ++i) slot[i] = i;
+  return matvec_with_crc(job, ptrs, total(), slot, S, crcs, stream);
+}
+
+Status RSEngine::reconstruct_crc_batch(uint8_t* const* ptrs, size_t S, int nstripes, const int* erased,
+                                       int nerased, bool data_only, uint32_t* crcs, hipStream_t stream) {
+  if (!ctx_) return CFSEC_ERR_DEVICE;
+  if (!ptrs || !crcs || nstripes < 0 || nerased < 0 || (nerased > 0 && !erased)) return CFSEC_ERR_INVALID_ARG;
+  std::vector<bool> present(total(), true);
+  for (int i = 0; i < nerased; ++i) {
+    if (erased[i] < 0 || erased[i] >= total()) return CFSEC_ERR_INVALID_ARG;
+    present[erased[i]] = false;
+  }
+  int np = 0;
+  for (int i = 0; i < total(); ++i) np += present[i] ? 1 : 0;
+  if (np < k_ && nstripes > 0) return CFSEC_ERR_TOO_FEW_SHARDS;
+  DeviceGuard g(ctx_->device());
+  if (nstripes == 0) return CFSEC_OK;
+  ReconPlan plan;
+  if (np < total()) {
+    Status st = plan_reconstruct(present, data_only, &plan);
+    if (st != CFSEC_OK) return st;
+  }
+  const int nout = (int)plan.outputs.size();
+  if (nout == 0 || S == 0)
+    return hip_status(hipMemsetAsync(crcs, 0, 4 * (size_t)total() * nstripes, stream), "hipMemsetAsync");
+  std::vector<const uint8_t*> in(size_t(nstripes) * k_);
+  std::vector<uint8_t*> out(size_t(nstripes) * nout);
+  for (int s = 0; s < nstripes; ++s) {
+    for (int c = 0; c < k_; ++c) in[size_t(s) * k_ + c] = ptrs[size_t(s) * total() + plan.valid[c]];
+    for (int r = 0; r < nout; ++r) out[size_t(s) * nout + r] = ptrs[size_t(s) * total() + plan.outputs[r]];
+  }
+  MatVecJob job;
+  job.k = k_;
+  job.m = nout;
+  job.coef = plan.rows.v.data();
+  job.len = S;
+  job.nstripes = nstripes;
+  job.in = in.data();
+  job.out = out.data();
+  std::vector<int> slot(k_ + nout, -1);
+  for (int r = 0; r < nout; ++r) slot[k_ + r] = plan.outputs[r];
+  return matvec_with_crc(job, ptrs, total(), slot, S, crcs, stream);
+}
+
 // ---------------------------------------------------------------- ec.Encoder
 
 Status ECEncoder::create(const cfsec_tactic& t, bool enable_verify, int concurrency, int device,

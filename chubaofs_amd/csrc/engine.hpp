@@ -104,6 +104,12 @@ class RSEngine {
                       hipStream_t stream);
   Status reconstruct_batch(uint8_t* const* ptrs, size_t S, int nstripes, const int* erased,
                            int nerased, bool data_only, hipStream_t stream);
+  // The same with crc32.ChecksumIEEE of the shards (fused into the kernel where supported):
+  // crcs = device [nstripes * total()]; encode checksums every shard, reconstruct the rebuilt ones
+  // (other words 0).
+  Status encode_crc_batch(uint8_t* const* ptrs, size_t S, int nstripes, uint32_t* crcs, hipStream_t stream);
+  Status reconstruct_crc_batch(uint8_t* const* ptrs, size_t S, int nstripes, const int* erased, int nerased,
+                               bool data_only, uint32_t* crcs, hipStream_t stream);
 
   // Plan the rows of a reconstruct given which shards are present.
   Status plan_reconstruct(const std::vector<bool>& present, bool data_only, ReconPlan* plan);

@@ -1,0 +1,188 @@
+// gf_crc.hip -- host side of the fused matvec + shard CRC32 kernels (device code: gf_crc.hpp).
+#include <algorithm>
+#include <map>
+#include <mutex>
+#include <vector>
+
+#include "gf_crc.hpp"
+#include "gf_launch.hpp"
+
+namespace cfsec {
+namespace crcdev {
+CFSEC_CRC_EXTERN(6)
+CFSEC_CRC_EXTERN(8)
+CFSEC_CRC_EXTERN(12)
+CFSEC_CRC_EXTERN(16)
+CFSEC_CRC_EXTERN(18)
+}  // namespace crcdev
+
+namespace {
+
+using crcdev::GfCrcArgs;
+constexpr uint32_t kX0 = 0x80000000u;    // x^0 (reflected)
+constexpr uint32_t kX1 = 0x40000000u;    // x^1
+constexpr uint32_t kXInv = 0xDB710641u;  // x^-1 mod P: the y with y*x = x^0 (P has a constant term)
+
+uint32_t mulmod(uint32_t a, uint32_t b) {
+  uint32_t p = 0;
+  for (uint32_t bit = kX0; bit; bit >>= 1) {
+    if (a & bit) p ^= b;
+    b = (b >> 1) ^ ((b & 1u) ? crcdev::kPoly : 0u);
+  }
+  return p;
+}
+
+// x^e mod P for any integer e (e < 0: powers of x^-1).
+uint32_t xpow(int64_t e) {
+  uint32_t base = e >= 0 ? kX1 : kXInv;
+  uint64_t n = e >= 0 ? (uint64_t)e : (uint64_t)(-e);
+  uint32_t p = kX0;
+  while (n) {
+    if (n & 1) p = mulmod(p, base);
+    base = mulmod(base, base);
+    n >>= 1;
+  }
+  return p;
+}
+
+std::vector<uint32_t> host_tables() {
+  std::vector<uint32_t> t(crcdev::kTabWords + crcdev::kBasisWords);
+  for (uint32_t b = 0; b < 256; ++b) {  // T0: the byte-at-a-time table of hash/crc32
+    uint32_t c = b;
+    for (int i = 0; i < 8; ++i) c = (c & 1u) ? (c >> 1) ^ crcdev::kPoly : c >> 1;
+    t[b] = c;
+  }
+  for (int n = 1; n < 8; ++n)  // Tn[b] = f(0, b followed by n zero bytes)
+    for (int b = 0; b < 256; ++b) {
+      const uint32_t v = t[(n - 1) * 256 + b];
+      t[n * 256 + b] = (v >> 8) ^ t[v & 0xFF];
+    }
+  const uint32_t k4080 = xpow(8 * 4080);
+  for (int q = 0; q < 4; ++q)  // Hq[b] = shift(b << 8q, 4080)
+    for (uint32_t b = 0; b < 256; ++b) t[(8 + q) * 256 + b] = mulmod(k4080, b << (8 * q));
+  for (int j = 0; j < 256; ++j) {  // basis of shift(., 16*(255-j)) for thread j
+    const uint32_t kj = xpow(8LL * 16 * (255 - j));
+    for (int i = 0; i < 32; ++i) t[crcdev::kTabWords + j * 32 + i] = mulmod(kj, 1u << i);
+  }
+  return t;
+}
+
+// The lookup tables on the current device, uploaded once per device.
+hipError_t device_tables(const uint32_t** out) {
+  static std::mutex mu;
+  static std::map<int, uint32_t*> per_device;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> l(mu);
+  auto it = per_device.find(dev);
+  if (it == per_device.end()) {
+    static const std::vector<uint32_t> host = host_tables();
+    uint32_t* d = nullptr;
+    e = hipMalloc(reinterpret_cast<void**>(&d), host.size() * 4);
+    if (e != hipSuccess) return e;
+    e = hipMemcpy(d, host.data(), host.size() * 4, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      (void)hipFree(d);
+      return e;
+    }
+    it = per_device.emplace(dev, d).first;
+  }
+  *out = it->second;
+  return hipSuccess;
+}
+
+// As gf_kernels.hip's affine_stride, for the whole job.
+int64_t affine_stride(const MatVecJob& job) {
+  if (job.nstripes < 2) return 0;
+  const auto addr = [](const void* p) { return (int64_t)(uintptr_t)p; };
+  const int64_t ss = addr(job.in[job.k]) - addr(job.in[0]);
+  if (ss == 0) return 0;
+  for (int s = 1; s < job.nstripes; ++s) {
+    for (int c = 0; c < job.k; ++c)
+      if (addr(job.in[(size_t)s * job.k + c]) != addr(job.in[c]) + s * ss) return 0;
+    for (int r = 0; r < job.m; ++r)
+      if (addr(job.out[(size_t)s * job.m + r]) != addr(job.out[r]) + s * ss) return 0;
+  }
+  return ss;
+}
+
+template <bool CIN>
+hipError_t launch_crc(int k, int m, const GfCrcArgs& a, dim3 grid, hipStream_t st) {
+  switch (k) {
+    case 6: return crcdev::launch_crc_k<6, CIN>(m, a, grid, st);
+    case 8: return crcdev::launch_crc_k<8, CIN>(m, a, grid, st);
+    case 12: return crcdev::launch_crc_k<12, CIN>(m, a, grid, st);
+    case 16: return crcdev::launch_crc_k<16, CIN>(m, a, grid, st);
+    case 18: return crcdev::launch_crc_k<18, CIN>(m, a, grid, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace
+
+bool matvec_crc_supported(int k, int m, size_t len) {
+  return fixed_k(k) && m >= 1 && m <= crcdev::kMaxM && len <= 0xFFFFFFFFull - crcdev::kTile;
+}
+
+uint32_t crc32_shift_ones(size_t len) { return mulmod(xpow(8 * (int64_t)len), 0xFFFFFFFFu) ^ 0xFFFFFFFFu; }
+
+hipError_t launch_matvec_crc(const MatVecJob& job, uint32_t* crc, int crc_stride, const int* slot,
+                             hipStream_t stream) {
+  if (job.mode != MatVecMode::kStore || !matvec_crc_supported(job.k, job.m, job.len) || !crc || !slot ||
+      crc_stride <= 0 || crc_stride > 256 || job.nstripes < 0 || !job.coef || !job.in || !job.out)
+    return hipErrorInvalidValue;
+  const int k = job.k, m = job.m;
+  const bool cin = slot[0] >= 0;
+  for (int i = 0; i < k + m; ++i) {
+    const bool want = i >= k || cin;
+    if (want && (slot[i] < 0 || slot[i] >= crc_stride)) return hipErrorInvalidValue;
+  }
+  hipError_t e = hipMemsetAsync(crc, 0, sizeof(uint32_t) * (size_t)crc_stride * job.nstripes, stream);
+  if (e != hipSuccess || job.nstripes == 0 || job.len == 0) return e;
+
+  GfCrcArgs a{};
+  e = device_tables(&a.tabs);
+  if (e != hipSuccess) return e;
+  const uint32_t tiles = (uint32_t)((job.len + crcdev::kTile - 1) / crcdev::kTile);
+  const int64_t sstride = affine_stride(job);
+  const int per = sstride ? job.nstripes : crcdev::kPtrSlots / (k + m);
+  const int stripes_per_launch = std::min(per, 65535);
+  // ~2048 workgroups per launch (8 per CU) while each keeps >= 1 tile; at most kMaxGroups per stripe
+  const uint32_t want = std::max<uint32_t>(1, 2048u / (uint32_t)std::min(job.nstripes, stripes_per_launch));
+  uint32_t groups = std::min<uint32_t>({tiles, want, (uint32_t)crcdev::kMaxGroups});
+  const uint32_t tpw = (tiles + groups - 1) / groups;
+  groups = (tiles + tpw - 1) / tpw;
+
+  a.len = job.len;
+  a.k = (uint32_t)k;
+  a.m = (uint32_t)m;
+  a.tiles = tiles;
+  a.tpw = tpw;
+  a.sstride = sstride;
+  a.fin = crc32_shift_ones(job.len);
+  a.crc_stride = (uint32_t)crc_stride;
+  for (int i = 0; i < k + m; ++i) a.slot[i] = (uint8_t)std::max(slot[i], 0);
+  for (int r = 0; r < m; ++r)
+    for (int c = 0; c < k; ++c) a.coef[r * k + c] = job.coef[(size_t)r * k + c];
+  for (uint32_t g = 0; g < groups; ++g) {
+    const int64_t end = (int64_t)std::min<uint64_t>((uint64_t)(g + 1) * tpw, tiles) * crcdev::kTile;
+    a.gconst[g] = xpow(8 * ((int64_t)job.len - end));
+  }
+  for (int s0 = 0; s0 < job.nstripes; s0 += stripes_per_launch) {
+    const int ns = std::min(stripes_per_launch, job.nstripes - s0);
+    const int tab = sstride ? 1 : ns;
+    a.tab = (uint32_t)tab;
+    a.crc = crc + (size_t)s0 * crc_stride;
+    for (int s = 0; s < tab; ++s) {
+      for (int c = 0; c < k; ++c) a.ptr[s * k + c] = job.in[(size_t)(s0 + s) * k + c];
+      for (int r = 0; r < m; ++r) a.ptr[tab * k + s * m + r] = job.out[(size_t)(s0 + s) * m + r];
+    }
+    const dim3 grid(groups, (unsigned)ns);
+    e = cin ? launch_crc<true>(k, m, a, grid, stream) : launch_crc<false>(k, m, a, grid, stream);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+}  // namespace cfsec

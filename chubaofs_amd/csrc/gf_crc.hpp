@@ -1,0 +1,242 @@
+// gf_crc.hpp -- fused GF(2^8) matrix x shard-vector product + shard CRC32-IEEE (gfx950).
+//
+// CubeFS checksums every shard right after coding it: access computes crc32.ChecksumIEEE of
+// each data and parity shard after Encode (blobstore/access/stream_put.go:249-253) and blobnode
+// checksums shards around a repair (blobnode/work_shard_recover.go:335-342, 668-683).  As a
+// separate pass that re-reads every shard from HBM.  This kernel checksums the 16-byte pieces
+// the GF tile already holds in registers, so an encode with checksums moves exactly the bytes
+// of the plain encode ("CRC fused: +0 bytes").
+//
+// CRC algebra (Go hash/crc32 IEEE: reflected polynomial 0xEDB88320, bit 31 = x^0).  f(r, B) is
+// the register after feeding bytes B from register r with no pre/post inversion; f(r, B) =
+// shift(r, |B|) ^ f(0, B) with shift(v, n) = v * x^(8n) mod P, and
+// ChecksumIEEE(M) = f(0, M) ^ shift(~0, |M|) ^ ~0.
+//
+// Work split.  A workgroup owns `tpw` consecutive 4 KiB tiles of one stripe; thread j holds
+// bytes [16j, 16j+16) of every row of each tile (the fixed-K GF tile of gf_device.hpp).  Per
+// checksummed row it keeps a Horner register over its pieces, R <- f(shift(R, 4080), piece):
+// four byte lookups for the shift, then slice-by-8 twice -- 20 LDS lookups per 16 bytes.  After
+// its last tile the thread moves R from its piece end to the tile end e (x^(8*16*(255-j)), a
+// 32-column GF(2) basis read once from global memory), the 256 threads XOR-reduce, and one
+// multiply by x^(8(S - e)) moves the sum to the shard end (a host constant per workgroup;
+// negative for the zero-padded last tile -- x is invertible mod P).  Workgroups XOR their words
+// into the shard's word (atomicXor) and workgroup 0 also folds in shift(~0, S) ^ ~0, so the word
+// ends as crc32.ChecksumIEEE with no finalize pass.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "gf_device.hpp"
+#include "kernels.hpp"
+
+namespace cfsec {
+namespace crcdev {
+
+using dev::u32x4;
+
+constexpr uint32_t kPoly = 0xEDB88320u;
+constexpr int kTile = 4096;            // bytes per row per tile: 256 threads x 16 B
+constexpr int kMaxK = 18, kMaxM = 6, kPtrSlots = 96, kMaxGroups = 384;
+constexpr int kTabWords = 12 * 256;    // T0..T7: slice-by-8;  H0..H3: shift by 4080 bytes
+constexpr int kBasisWords = 256 * 32;  // thread j: the 32 columns of shift(., 16*(255-j))
+
+struct __attribute__((aligned(16))) GfCrcArgs {
+  uint64_t len;
+  uint32_t k, m, tiles, tpw;
+  int64_t sstride;       // affine batch: byte distance between stripes (0: explicit table)
+  uint32_t tab, fin;     // stripes held in ptr[]; shift(~0, len) ^ ~0
+  uint32_t* crc;         // [stripe][crc_stride] checksum words, zeroed by the launcher
+  const uint32_t* tabs;  // device: kTabWords + kBasisWords
+  uint32_t crc_stride, pad0;
+  uint8_t slot[kMaxK + kMaxM];  // checksum word of kernel row i (inputs 0..k-1, outputs k..)
+  uint8_t coef[kMaxM * kMaxK];
+  const uint8_t* ptr[kPtrSlots];  // [tab*k inputs][tab*m outputs], as GfArgs
+  uint32_t gconst[kMaxGroups];    // x^(8(len - e_g)) mod P for workgroup g
+};
+static_assert(sizeof(GfCrcArgs) <= 3584, "kernel argument block must stay below 4 KiB");
+
+// f(r, 8 bytes w0|w1): slice-by-8 with ct[n*256 + b] = f(0, b followed by n zero bytes).
+__device__ __forceinline__ uint32_t slice8(const uint32_t* ct, uint32_t r, uint32_t w0, uint32_t w1) {
+  w0 ^= r;
+  return ct[7 * 256 + (w0 & 0xFF)] ^ ct[6 * 256 + ((w0 >> 8) & 0xFF)] ^ ct[5 * 256 + ((w0 >> 16) & 0xFF)] ^
+         ct[4 * 256 + (w0 >> 24)] ^ ct[3 * 256 + (w1 & 0xFF)] ^ ct[2 * 256 + ((w1 >> 8) & 0xFF)] ^
+         ct[1 * 256 + ((w1 >> 16) & 0xFF)] ^ ct[w1 >> 24];
+}
+
+// R <- f(shift(R, 4080), d): the next piece of this thread sits 4080 bytes after the last one.
+__device__ __forceinline__ uint32_t crc_step(const uint32_t* ct, uint32_t r, const uint32_t (&d)[4]) {
+  const uint32_t s = ct[8 * 256 + (r & 0xFF)] ^ ct[9 * 256 + ((r >> 8) & 0xFF)] ^
+                     ct[10 * 256 + ((r >> 16) & 0xFF)] ^ ct[11 * 256 + (r >> 24)];
+  return slice8(ct, slice8(ct, s, d[0], d[1]), d[2], d[3]);
+}
+
+// a * b mod P (reflected: bit 31 = x^0)
+__device__ __forceinline__ uint32_t mulmod(uint32_t a, uint32_t b) {
+  uint32_t p = 0;
+  for (uint32_t bit = 0x80000000u; bit; bit >>= 1) {
+    if (a & bit) p ^= b;
+    b = (b >> 1) ^ ((b & 1u) ? kPoly : 0u);
+  }
+  return p;
+}
+
+// One tile of the product for this thread (bytes [off, off+16) of every row) plus the Horner
+// step of every checksummed row.  Full pieces take the pipelined path of lane_tile_k; the
+// thread holding the shard end (or past it) reads/writes only bytes < len and checksums the
+// piece zero-padded, which is what the negative group shift undoes.
+template <int K, int M, bool CIN>
+__device__ __forceinline__ void crc_tile(uint64_t len, const u32x4* tab01, const uint32_t* tab2,
+                                         const uint32_t* ct, const uint8_t* const (&row)[K + M],
+                                         uint32_t off, uint32_t (&R)[(CIN ? K : 0) + M]) {
+  constexpr int RO = CIN ? K : 0;  // register of output row 0
+  uint32_t acc[M][4];
+#pragma unroll
+  for (int r = 0; r < M; ++r)
+#pragma unroll
+    for (int w = 0; w < 4; ++w) acc[r][w] = 0u;
+  const auto pin = [&]() {
+#pragma unroll
+    for (int r = 0; r < M; ++r)
+      asm volatile("" : "+v"(acc[r][0]), "+v"(acc[r][1]), "+v"(acc[r][2]), "+v"(acc[r][3]));
+  };
+  if ((uint64_t)off + dev::kLaneBytes <= len) {
+    uint32_t x[K][4];
+    const auto load = [&](int c) {
+      const u32x4 v = dev::ld16<true>(row[c] + off);
+      x[c][0] = v.x;
+      x[c][1] = v.y;
+      x[c][2] = v.z;
+      x[c][3] = v.w;
+    };
+    load(0);
+    load(1);
+#pragma unroll
+    for (int c = 0; c < K; c += 2) {
+      if (c + 2 < K) load(c + 2);
+      if (c + 3 < K) load(c + 3);
+      __builtin_amdgcn_sched_barrier(0);
+      dev::mac_pair_k<M>(acc, x[c], x[c + 1], tab01 + c * M, tab2 + c * M, tab01 + (c + 1) * M,
+                         tab2 + (c + 1) * M);
+      pin();
+      if constexpr (CIN) {
+        R[c] = crc_step(ct, R[c], x[c]);
+        R[c + 1] = crc_step(ct, R[c + 1], x[c + 1]);
+        asm volatile("" : "+v"(R[c]), "+v"(R[c + 1]));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int r = 0; r < M; ++r)
+      dev::st16<true>(const_cast<uint8_t*>(row[K + r]) + off, u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]});
+  } else {
+    const size_t rem = off < len ? (size_t)(len - off) : 0;
+    for (int c = 0; c < K; ++c) {
+      uint32_t xv[4] = {0u, 0u, 0u, 0u};
+      if (rem) {
+        const u32x4 v = dev::ld_tail(row[c] + off, rem);
+        xv[0] = v.x;
+        xv[1] = v.y;
+        xv[2] = v.z;
+        xv[3] = v.w;
+      }
+      dev::mac_row_k<M>(acc, xv, tab01 + c * M, tab2 + c * M);
+      if constexpr (CIN) R[c] = crc_step(ct, R[c], xv);
+    }
+    if (rem)
+#pragma unroll
+      for (int r = 0; r < M; ++r)
+        dev::st_tail(const_cast<uint8_t*>(row[K + r]) + off, u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]},
+                     rem);
+  }
+#pragma unroll
+  for (int r = 0; r < M; ++r) R[RO + r] = crc_step(ct, R[RO + r], acc[r]);
+}
+
+// grid (groups, stripes), 256 threads.  a.k == K, a.m == M.
+template <int K, int M, bool CIN>
+__global__ __launch_bounds__(256) void gf_crc_kernel(const GfCrcArgs a) {
+  constexpr int NR = (CIN ? K : 0) + M;  // checksummed rows
+  __shared__ u32x4 tab01[K * M];
+  __shared__ uint32_t tab2[K * M];
+  __shared__ uint32_t ct[kTabWords];
+  __shared__ uint32_t red[4][NR];
+  dev::build_tables<M>(K, M, a.coef, tab01, tab2);
+  for (int i = threadIdx.x; i < kTabWords; i += 256) ct[i] = a.tabs[i];
+  __syncthreads();
+
+  const uint32_t g = blockIdx.x, stripe = blockIdx.y;
+  const size_t ts = a.sstride ? 0 : (size_t)stripe;
+  const int64_t sbase = (int64_t)stripe * a.sstride;
+  const uint8_t* row[K + M];
+#pragma unroll
+  for (int c = 0; c < K; ++c) row[c] = a.ptr[ts * K + c] + sbase;
+#pragma unroll
+  for (int r = 0; r < M; ++r) row[K + r] = a.ptr[(size_t)a.tab * K + ts * M + r] + sbase;
+  uint32_t R[NR];
+#pragma unroll
+  for (int i = 0; i < NR; ++i) R[i] = 0u;
+  const uint32_t t0 = g * a.tpw;
+  const uint32_t t1 = min(t0 + a.tpw, a.tiles);
+  const uint32_t lanepos = threadIdx.x * dev::kLaneBytes;
+  for (uint32_t t = t0; t < t1; ++t) crc_tile<K, M, CIN>(a.len, tab01, tab2, ct, row, t * kTile + lanepos, R);
+
+  // move every register from this thread's last piece end to the tile end t1*4096
+  const u32x4* basis = reinterpret_cast<const u32x4*>(a.tabs + kTabWords + threadIdx.x * 32);
+  uint32_t col[32];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const u32x4 v = basis[q];
+    col[4 * q] = v.x;
+    col[4 * q + 1] = v.y;
+    col[4 * q + 2] = v.z;
+    col[4 * q + 3] = v.w;
+  }
+  const int wave = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int b = 0; b < 32; ++b) o ^= (0u - ((R[i] >> b) & 1u)) & col[b];
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) o ^= (uint32_t)__shfl_xor((int)o, d);
+    if (lane == 0) red[wave][i] = o;
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < NR) {
+    const int i = (int)threadIdx.x;
+    uint32_t v = red[0][i] ^ red[1][i] ^ red[2][i] ^ red[3][i];
+    v = mulmod(a.gconst[g], v);
+    if (g == 0) v ^= a.fin;
+    atomicXor(a.crc + (size_t)stripe * a.crc_stride + a.slot[CIN ? i : K + i], v);
+  }
+}
+
+// Launch gf_crc_kernel<K, m, CIN> (instantiated for m = 1..6 in gf_crc_k<K>.hip).
+template <int K, bool CIN>
+hipError_t launch_crc_k(int m, const GfCrcArgs& a, dim3 grid, hipStream_t st) {
+  switch (m) {
+#define CFSEC_CRC_CASE(MV)                                                                       \
+  case MV:                                                                                       \
+    hipLaunchKernelGGL((gf_crc_kernel<K, MV, CIN>), grid, dim3(256), 0, st, a);                  \
+    break;
+    CFSEC_CRC_CASE(1) CFSEC_CRC_CASE(2) CFSEC_CRC_CASE(3) CFSEC_CRC_CASE(4) CFSEC_CRC_CASE(5)
+    CFSEC_CRC_CASE(6)
+#undef CFSEC_CRC_CASE
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+#define CFSEC_CRC_EXTERN(K)                                                                         \
+  extern template hipError_t launch_crc_k<K, true>(int, const GfCrcArgs&, dim3, hipStream_t);       \
+  extern template hipError_t launch_crc_k<K, false>(int, const GfCrcArgs&, dim3, hipStream_t);
+
+}  // namespace crcdev
+}  // namespace cfsec
+
+#define CFSEC_CRC_INSTANTIATE(K)                                                                     \
+  namespace cfsec {                                                                                  \
+  namespace crcdev {                                                                                 \
+  template hipError_t launch_crc_k<K, true>(int, const GfCrcArgs&, dim3, hipStream_t);              \
+  template hipError_t launch_crc_k<K, false>(int, const GfCrcArgs&, dim3, hipStream_t);             \
+  }                                                                                                  \
+  }

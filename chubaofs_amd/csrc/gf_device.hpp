@@ -88,13 +88,12 @@ __device__ __forceinline__ void st_tail(uint8_t* p, u32x4 v, size_t rem) {
 //   tab01 = {T0[0..3], T0[4..7], T1[0..3], T1[4..7]},  tab2 = T2[0..3]
 // with T0[e] = coef*e, T1[e] = coef*(e<<3), T2[e] = coef*(e<<6).
 template <int MT>
-__device__ __forceinline__ void build_tables(const GfArgs& a, u32x4* tab01, uint32_t* tab2) {
-  const int k = (int)a.k;
+__device__ __forceinline__ void build_tables(int k, int m, const uint8_t* coef, u32x4* tab01, uint32_t* tab2) {
   for (int i = threadIdx.x; i < k * MT; i += (int)blockDim.x) {
     const int c = i / MT;
     const int r = i - c * MT;
     uint32_t p[8];
-    p[0] = (r < (int)a.m) ? a.coef[r * k + c] : 0u;
+    p[0] = (r < m) ? coef[r * k + c] : 0u;
 #pragma unroll
     for (int j = 1; j < 8; ++j) p[j] = gf_xtime(p[j - 1]);  // coef * 2^j
     uint32_t t0lo = 0, t0hi = 0, t1lo = 0, t1hi = 0, t2 = 0;
@@ -115,6 +114,11 @@ __device__ __forceinline__ void build_tables(const GfArgs& a, u32x4* tab01, uint
     tab01[i] = u32x4{t0lo, t0hi, t1lo, t1hi};
     tab2[i] = t2;
   }
+}
+
+template <int MT>
+__device__ __forceinline__ void build_tables(const GfArgs& a, u32x4* tab01, uint32_t* tab2) {
+  build_tables<MT>((int)a.k, (int)a.m, a.coef, tab01, tab2);
 }
 
 // acc[r] ^= coef(c, r) * x for the wave's M outputs; x is 16 bytes of input row c and
@@ -242,6 +246,41 @@ __device__ __forceinline__ void mac_row_k(uint32_t (&acc)[M][4], const uint32_t 
   }
 }
 
+// Two input rows at once: acc ^= coef(a, r)*xa ^ coef(b, r)*xb.  The six table lookups per output
+// dword fold into acc with three 3-input XORs (v_bitop3_b32 0x96) instead of four XOR ops for
+// two single rows: 9 VALU ops per (output, dword, row pair) instead of 10.
+template <int M>
+__device__ __forceinline__ void mac_pair_k(uint32_t (&acc)[M][4], const uint32_t (&xa)[4],
+                                           const uint32_t (&xb)[4], const u32x4* __restrict__ tqa,
+                                           const uint32_t* __restrict__ t2a, const u32x4* __restrict__ tqb,
+                                           const uint32_t* __restrict__ t2b) {
+  uint32_t a0[4], a1[4], a2[4], b0[4], b1[4], b2[4];
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    a0[w] = xa[w] & 0x07070707u;
+    a1[w] = (xa[w] >> 3) & 0x07070707u;
+    a2[w] = (xa[w] >> 6) & 0x03030303u;
+    b0[w] = xb[w] & 0x07070707u;
+    b1[w] = (xb[w] >> 3) & 0x07070707u;
+    b2[w] = (xb[w] >> 6) & 0x03030303u;
+  }
+#pragma unroll
+  for (int r = 0; r < M; ++r) {
+    const u32x4 qa = tqa[r], qb = tqb[r];
+    const uint32_t ta = t2a[r], tb = t2b[r];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const uint32_t u = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_perm(qa.y, qa.x, a0[w]),
+                                                     __builtin_amdgcn_perm(qa.w, qa.z, a1[w]),
+                                                     __builtin_amdgcn_perm(0u, ta, a2[w]), 0x96);
+      const uint32_t v = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_perm(qb.y, qb.x, b0[w]),
+                                                     __builtin_amdgcn_perm(qb.w, qb.z, b1[w]),
+                                                     __builtin_amdgcn_perm(0u, tb, b2[w]), 0x96);
+      acc[r][w] = __builtin_amdgcn_bitop3_b32(acc[r][w], u, v, 0x96);
+    }
+  }
+}
+
 // Full tile for a compile-time input count K, one 16-B chunk per lane at byte `loff` of every row.
 // The rows a lane touches (K inputs, then in verify mode the M rows it compares) form one load
 // sequence in which row c+D is issued before row c is consumed, so D loads per wave stay in
@@ -250,10 +289,11 @@ __device__ __forceinline__ void mac_row_k(uint32_t (&acc)[M][4], const uint32_t 
 // VGPRs for K=12, M=4: one or two waves per SIMD), so each row ends by pinning the accumulators
 // (empty asm) behind a sched_barrier, and the row pointers (uniform: SGPR bases, 32-bit lane
 // offsets) are loaded once up front.  tools/gf_pipe.hip measured the effect.
-template <int K, int M, int MT, MatVecMode MODE, int D, bool NTL, bool NTS>
+template <int K, int M, int MT, MatVecMode MODE, int D, bool NTL, bool NTS, bool PAIR = true>
 __device__ __forceinline__ void lane_tile_k(int m, const u32x4* tab01, const uint32_t* tab2,
                                             const uint8_t* const* in, uint8_t* const* out, int og,
                                             int64_t sbase, uint32_t loff, uint32_t& diff) {
+  static_assert(K % 2 == 0 && D >= 2, "the fixed-K tile consumes input rows in pairs, a pair ahead");
   constexpr bool kVer = MODE == MatVecMode::kVerify;
   constexpr int R = K + (kVer ? M : 0);  // rows loaded
   const uint8_t* row[R];
@@ -277,18 +317,36 @@ __device__ __forceinline__ void lane_tile_k(int m, const u32x4* tab01, const uin
     x[c][2] = v.z;
     x[c][3] = v.w;
   };
+  const auto pin = [&]() {
+#pragma unroll
+    for (int r = 0; r < M; ++r)
+      asm volatile("" : "+v"(acc[r][0]), "+v"(acc[r][1]), "+v"(acc[r][2]), "+v"(acc[r][3]));
+  };
 #pragma unroll
   for (int c = 0; c < D && c < R; ++c) load(c);
+  // inputs two rows per step (K is even for every fixed K)
 #pragma unroll
-  for (int c = 0; c < R; ++c) {
+  for (int c = 0; c < K; c += 2) {
+    if (c + D < R) load(c + D);
+    if (c + D + 1 < R) load(c + D + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (PAIR) {
+      mac_pair_k<M>(acc, x[c], x[c + 1], tab01 + c * MT + og, tab2 + c * MT + og, tab01 + (c + 1) * MT + og,
+                    tab2 + (c + 1) * MT + og);
+    } else {
+      mac_row_k<M>(acc, x[c], tab01 + c * MT + og, tab2 + c * MT + og);
+      pin();
+      mac_row_k<M>(acc, x[c + 1], tab01 + (c + 1) * MT + og, tab2 + (c + 1) * MT + og);
+    }
+    pin();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // verify: compare the computed rows with the stored ones
+#pragma unroll
+  for (int c = K; c < R; ++c) {
     if (c + D < R) load(c + D);
     __builtin_amdgcn_sched_barrier(0);
-    if (c < K) {
-      mac_row_k<M>(acc, x[c], tab01 + c * MT + og, tab2 + c * MT + og);
-#pragma unroll
-      for (int r = 0; r < M; ++r)
-        asm volatile("" : "+v"(acc[r][0]), "+v"(acc[r][1]), "+v"(acc[r][2]), "+v"(acc[r][3]));
-    } else if (og + (c - K) < m) {
+    if (og + (c - K) < m) {
       const int r = c - K;
       diff |= (acc[r][0] ^ x[c][0]) | (acc[r][1] ^ x[c][1]) | (acc[r][2] ^ x[c][2]) | (acc[r][3] ^ x[c][3]);
     }
@@ -310,7 +368,7 @@ __device__ __forceinline__ void lane_tile_k(int m, const u32x4* tab01, const uin
 // Kernel body for a compile-time input count (a.k == K, a.len < 4 GiB): 256-thread workgroups,
 // one 16-B chunk per lane, tile = (256/OS)*16 bytes of every row, grid (tiles, stripes);
 // otherwise as matvec below.
-template <int K, int M, MatVecMode MODE, int D, int OS>
+template <int K, int M, MatVecMode MODE, int D, int OS, bool NTL = true, bool NTS = true, bool PAIR = true>
 __device__ __forceinline__ void matvec_k(const GfArgs& a) {
   constexpr int MT = M * OS;
   __shared__ u32x4 tab01[K * MT];
@@ -334,7 +392,7 @@ __device__ __forceinline__ void matvec_k(const GfArgs& a) {
   uint32_t diff = 0;
   if (og < (int)a.m) {
     if ((uint64_t)off + kLaneBytes <= a.len)
-      lane_tile_k<K, M, MT, MODE, D, true, true>((int)a.m, tab01, tab2, in, out, og, sbase, off, diff);
+      lane_tile_k<K, M, MT, MODE, D, NTL, NTS, PAIR>((int)a.m, tab01, tab2, in, out, og, sbase, off, diff);
     else if (off < a.len)
       lane_tail<M, MT, MODE>(a, tab01, tab2, in, out, og, (size_t)sbase + off, a.len - off, diff);
   }

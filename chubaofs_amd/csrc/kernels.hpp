@@ -43,5 +43,21 @@ hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream);
 hipError_t launch_crc32(const uint8_t* const* ptrs, size_t len, int n, uint32_t* out,
                         hipStream_t stream);
 uint32_t crc32_finalize(uint32_t raw, size_t len);
+// Standalone form with scattered outputs: shard i's word is out[idx[i]] (idx NULL: out[i]),
+// accumulated with atomicXor into words the caller has zeroed, `fin` XOR-ed in once per shard
+// (crc32_shift_ones(len) gives crc32.ChecksumIEEE directly).
+hipError_t launch_crc32_to(const uint8_t* const* ptrs, size_t len, int n, uint32_t* out, const uint32_t* idx,
+                           uint32_t fin, hipStream_t stream);
+
+// Encode / reconstruct (kStore) with crc32.ChecksumIEEE of the rows the product touches, fused
+// into the product kernel (gf_crc.hpp): row i of the product (inputs 0..k-1, then outputs) has its
+// checksum in device word crc[s * crc_stride + slot[i]] of stripe s.  slot[0] < 0 skips the inputs
+// (checksum the outputs only).  Every word of crc[0 .. nstripes*crc_stride) is zeroed first, so
+// words no row maps to read 0.  Only for matvec_crc_supported shapes (k in {6,8,12,16,18}, m <= 6).
+bool matvec_crc_supported(int k, int m, size_t len);
+hipError_t launch_matvec_crc(const MatVecJob& job, uint32_t* crc, int crc_stride, const int* slot,
+                             hipStream_t stream);
+// shift(~0, len) ^ ~0: XOR it into a raw (zero-preset) CRC of len bytes to get crc32.ChecksumIEEE.
+uint32_t crc32_shift_ones(size_t len);
 
 }  // namespace cfsec

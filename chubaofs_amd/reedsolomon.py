@@ -121,6 +121,21 @@ class ReedSolomon:
         _lib.check(self._L.cfsec_rs_reconstruct_batch(self._h, ptr_array(ptrs), shard_len, nstripes, er,
                                                       len(erased), int(data_only), stream_ptr(stream)))
 
+    def encode_crc_batch(self, ptrs, shard_len: int, nstripes: int, crcs_ptr: int, stream=None) -> None:
+        """encode_batch + crc32.ChecksumIEEE of every shard into the device uint32 array at
+        crcs_ptr, [stripe][shard] (access/stream_put.go:249-253), fused where supported."""
+        _lib.check(self._L.cfsec_rs_encode_crc_batch(self._h, ptr_array(ptrs), shard_len, nstripes, crcs_ptr,
+                                                     stream_ptr(stream)))
+
+    def reconstruct_crc_batch(self, ptrs, shard_len: int, nstripes: int, erased, crcs_ptr: int,
+                              data_only=False, stream=None) -> None:
+        """reconstruct_batch + crc32.ChecksumIEEE of each rebuilt shard ([stripe][shard]; other
+        words 0)."""
+        er = (ctypes.c_int * max(len(erased), 1))(*erased)
+        _lib.check(self._L.cfsec_rs_reconstruct_crc_batch(self._h, ptr_array(ptrs), shard_len, nstripes, er,
+                                                          len(erased), int(data_only), crcs_ptr,
+                                                          stream_ptr(stream)))
+
 
 def New(data_shards: int, parity_shards: int, device: int = -1) -> ReedSolomon:
     """reedsolomon.New with default options (KRS/reedsolomon.go:413)."""

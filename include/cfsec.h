@@ -128,6 +128,18 @@ int cfsec_rs_verify_batch(cfsec_rs* h, uint8_t* const* ptrs, size_t shard_size, 
 int cfsec_rs_reconstruct_batch(cfsec_rs* h, uint8_t* const* ptrs, size_t shard_size, int nstripes,
                                const int* erased, int nerased, int data_only, void* stream);
 
+/* Encode / reconstruct with the shard checksums CubeFS computes right after coding
+ * (crc32.ChecksumIEEE, access/stream_put.go:249-253; blobnode/work_shard_recover.go:335-342),
+ * fused into the coding kernel where the shape allows (k in {6,8,12,16,18}, <= 6 outputs): no
+ * extra pass over the shards.  crcs: device array of nstripes * (data+parity) uint32, indexed
+ * [stripe][shard].  Encode fills every word; reconstruct fills the words of the shards it rebuilt
+ * and zeroes the rest.  Asynchronous on `stream`. */
+int cfsec_rs_encode_crc_batch(cfsec_rs* h, uint8_t* const* ptrs, size_t shard_size, int nstripes,
+                              uint32_t* crcs, void* stream);
+int cfsec_rs_reconstruct_crc_batch(cfsec_rs* h, uint8_t* const* ptrs, size_t shard_size, int nstripes,
+                                   const int* erased, int nerased, int data_only, uint32_t* crcs,
+                                   void* stream);
+
 /* ---------------- ec.Encoder ---------------- */
 /* Code-mode table (codemode.go:26-79): fill *t for a CodeMode value; CFSEC_ERR_INVALID_CODE_MODE
  * when unknown. */

@@ -1,0 +1,133 @@
+"""Encode / reconstruct with fused shard checksums (cfsec_rs_{encode,reconstruct}_crc_batch).
+
+CubeFS computes crc32.ChecksumIEEE of every shard right after Encode (access/stream_put.go:249-253)
+and of repaired shards (blobnode/work_shard_recover.go:335-342).  The GPU computes them inside the
+coding kernel; every word must equal zlib's CRC-32 (the same polynomial, preset and final inversion
+as Go's hash/crc32 IEEE) of the shard bytes, and the coded bytes must still match the oracle.
+Shapes outside the fused kernel's range (m > 6, k not a code-mode count) take the product + the
+standalone CRC kernel and must give the same words.
+"""
+import zlib
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+# fused: (12,4) (6,6) (8,1) (18,1) (16,4); fallback: (6,10) (10,4) (16,20)
+SHAPES = [(12, 4), (6, 6), (8, 1), (18, 1), (16, 4), (6, 10), (10, 4), (16, 20)]
+SIZES = [1, 15, 16, 17, 4095, 4096, 4097, 8191, 65539, 174763]
+
+
+@pytest.fixture(scope="module")
+def rs():
+    from chubaofs_amd import reedsolomon
+    return reedsolomon
+
+
+def crc(a: np.ndarray) -> int:
+    return zlib.crc32(a.tobytes()) & 0xFFFFFFFF
+
+
+def batch(k, m, S, nstripes, seed, pitch=None):
+    total = k + m
+    pitch = pitch or (S + 255) // 256 * 256
+    r = np.random.default_rng(seed)
+    host = np.zeros((nstripes, total, pitch), np.uint8)
+    host[:, :k, :S] = r.integers(0, 256, (nstripes, k, S), dtype=np.uint8)
+    dev = torch.from_numpy(host).cuda()
+    base = dev.data_ptr()
+    ptrs = [base + (s * total + i) * pitch for s in range(nstripes) for i in range(total)]
+    return host, dev, ptrs
+
+
+@pytest.mark.parametrize("k,m", SHAPES)
+@pytest.mark.parametrize("S", SIZES)
+def test_encode_crc_batch(rs, k, m, S):
+    nst = 3
+    host, dev, ptrs = batch(k, m, S, nst, seed=k * 100 + m + S)
+    crcs = torch.full((nst * (k + m),), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+    enc = rs.New(k, m)
+    enc.encode_crc_batch(ptrs, S, nst, crcs.data_ptr())
+    got = dev.cpu().numpy()
+    words = crcs.cpu().numpy().view(np.uint32).reshape(nst, k + m)
+    for s in range(nst):
+        want = [host[s, i, :S].copy() for i in range(k + m)]
+        assert O.encode(k, m, want) == 0
+        for i in range(k + m):
+            assert np.array_equal(got[s, i, :S], want[i]), (s, i)
+            assert int(words[s, i]) == crc(want[i]), (s, i, hex(int(words[s, i])), hex(crc(want[i])))
+            assert int(words[s, i]) == O.crc32_ieee(want[i])
+
+
+@pytest.mark.parametrize("k,m,S", [(12, 4, 100003), (6, 6, 4097), (16, 4, 262144)])
+def test_encode_crc_explicit_pointer_table(rs, k, m, S):
+    """Shards in separate allocations (no common stripe stride): the pointer-table path."""
+    nst = 5
+    r = np.random.default_rng(S)
+    shards = [[torch.from_numpy(r.integers(0, 256, S, dtype=np.uint8)).cuda() if i < k
+               else torch.zeros(S, dtype=torch.uint8, device="cuda") for i in range(k + m)] for _ in range(nst)]
+    ptrs = [t.data_ptr() for st in shards for t in st]
+    crcs = torch.zeros(nst * (k + m), dtype=torch.int32, device="cuda")
+    rs.New(k, m).encode_crc_batch(ptrs, S, nst, crcs.data_ptr())
+    words = crcs.cpu().numpy().view(np.uint32).reshape(nst, k + m)
+    for s in range(nst):
+        want = [t.cpu().numpy() for t in shards[s]]
+        host = [w.copy() for w in want]
+        assert O.encode(k, m, host) == 0
+        for i in range(k + m):
+            assert np.array_equal(want[i], host[i])
+            assert int(words[s, i]) == crc(host[i]), (s, i)
+
+
+@pytest.mark.parametrize("k,m,erased", [(12, 4, [0, 1, 2, 3]), (12, 4, [3, 13]), (6, 6, [0, 5, 6, 11]),
+                                        (8, 1, [4]), (18, 1, [17]), (16, 20, [0, 1, 16, 17]), (6, 10, [2, 9])])
+@pytest.mark.parametrize("S", [17, 4096, 70001])
+def test_reconstruct_crc_batch(rs, k, m, erased, S):
+    nst = 4
+    host, dev, ptrs = batch(k, m, S, nst, seed=S + len(erased))
+    enc = rs.New(k, m)
+    enc.encode_batch(ptrs, S, nst)
+    golden = dev.clone()
+    dev[:, erased, :] = 0
+    crcs = torch.full((nst * (k + m),), -1, dtype=torch.int32, device="cuda")
+    enc.reconstruct_crc_batch(ptrs, S, nst, erased, crcs.data_ptr())
+    assert torch.equal(dev[:, :, :S], golden[:, :, :S])
+    g = golden.cpu().numpy()
+    words = crcs.cpu().numpy().view(np.uint32).reshape(nst, k + m)
+    for s in range(nst):
+        for i in range(k + m):
+            want = crc(g[s, i, :S]) if i in erased else 0
+            assert int(words[s, i]) == want, (s, i)
+
+
+def test_crc_large_stripe_ec12p4(rs):
+    """BASELINE C2 shape (S = 5,592,406): every shard's checksum after a fused encode, then the
+    rebuilt shards' checksums after the worst-case reconstruct equal the originals'."""
+    k, m, S, nst = 12, 4, 5592406, 2
+    host, dev, ptrs = batch(k, m, S, nst, seed=0xCF5EC000)
+    enc = rs.New(k, m)
+    crcs = torch.zeros(nst * (k + m), dtype=torch.int32, device="cuda")
+    enc.encode_crc_batch(ptrs, S, nst, crcs.data_ptr())
+    g = dev.cpu().numpy()
+    words = crcs.cpu().numpy().view(np.uint32).reshape(nst, k + m)
+    for s in range(nst):
+        for i in range(k + m):
+            assert int(words[s, i]) == crc(g[s, i, :S]), (s, i)
+    want = words.copy()
+    dev[:, 0:4, :] = 0
+    rc = torch.zeros_like(crcs)
+    enc.reconstruct_crc_batch(ptrs, S, nst, [0, 1, 2, 3], rc.data_ptr())
+    rw = rc.cpu().numpy().view(np.uint32).reshape(nst, k + m)
+    assert (rw[:, :4] == want[:, :4]).all() and (rw[:, 4:] == 0).all()
+
+
+def test_crc_zero_length_and_empty(rs):
+    enc = rs.New(12, 4)
+    crcs = torch.full((16,), 7, dtype=torch.int32, device="cuda")
+    t = torch.zeros(16, dtype=torch.uint8, device="cuda")
+    enc.encode_crc_batch([t.data_ptr()] * 16, 0, 1, crcs.data_ptr())
+    assert crcs.cpu().tolist() == [0] * 16  # crc32.ChecksumIEEE(nil) == 0

@@ -192,6 +192,39 @@ __global__ __launch_bounds__(256) void kpats(const GfArgs a) {
   }
 }
 
+
+// Store cache-policy probes: the pattern kernel (12 -> 4, trivial arithmetic) and the shipped
+// fixed-K tile, with the output stores issued as inline asm carrying the given modifiers.
+template <int SP>
+__device__ __forceinline__ void st_pol(uint8_t* p, u32x4 v) {
+  if constexpr (SP == 0) asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(p), "v"(v) : "memory");
+  else if constexpr (SP == 1) asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(p), "v"(v) : "memory");
+  else if constexpr (SP == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+  else if constexpr (SP == 3) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+  else if constexpr (SP == 4) asm volatile("global_store_dwordx4 %0, %1, off nt sc1" ::"v"(p), "v"(v) : "memory");
+  else if constexpr (SP == 5) asm volatile("global_store_dwordx4 %0, %1, off nt sc0 sc1" ::"v"(p), "v"(v) : "memory");
+  else asm volatile("global_store_dwordx4 %0, %1, off sc0" ::"v"(p), "v"(v) : "memory");
+}
+
+template <int SP>
+__global__ __launch_bounds__(256) void kpatp(const GfArgs a) {
+  const uint32_t stripe = blockIdx.y;
+  const size_t base = (size_t)blockIdx.x * 4096 + threadIdx.x * 16;
+  const size_t soff = (size_t)stripe * a.sstride;
+  if (base + 16 > a.len) return;
+  u32x4 acc = u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int c = 0; c < 12; ++c) acc ^= dev::ld16<true>(a.ptr[c] + soff + base);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) st_pol<SP>(const_cast<uint8_t*>(a.ptr[12 + r]) + soff + base, acc + (uint32_t)r);
+}
+
+
+template <int D, bool NTL, bool NTS, bool PAIR = true, int K = 12, int M = 4, int OS = 1>
+__global__ __launch_bounds__(256) void kfix(const GfArgs a) {
+  dev::matvec_k<K, M, MatVecMode::kStore, D, OS, NTL, NTS, PAIR>(a);
+}
+
 __global__ __launch_bounds__(256) void kcopy(const u32x4* __restrict__ src, u32x4* __restrict__ dst, size_t n) {
   const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
   if (i < n) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
@@ -284,36 +317,25 @@ int main(int argc, char** argv) {
   for (int r = 0; r < m; ++r) a.ptr[k + r] = buf + (k + r) * pitch;
 
   std::vector<Variant> vs = {
-      {"ctl (shipped)", kctl, true},
-      mk<3, false>("gf12 D=3"),
-      {"gfw D=2 W=1", kgfw<12, 4, 2, 1>, false, 4},
-      {"gfw D=3 W=1", kgfw<12, 4, 3, 1>, false, 4},
-      {"gfw D=3 W=1 plainS", kgfw<12, 4, 3, 1, false>, false, 4},
-      {"gfw D=2 W=2", kgfw<12, 4, 2, 2>, false, 8},
-      {"gfw D=3 W=2", kgfw<12, 4, 3, 2>, false, 8},
-      {"gfw D=4 W=2", kgfw<12, 4, 4, 2>, false, 8},
-      {"gfw D=2 W=4", kgfw<12, 4, 2, 4>, false, 16},
-      {"gfw D=3 W=4", kgfw<12, 4, 3, 4>, false, 16},
-      {"xor12 D=4 sb", kpipe<12, 4, 4, true, true>, false},
+      {"ctl (runtime k)", kctl, true},
+      {"fix D2 pair", kfix<2, true, true, true>, true, -4},
+      {"fix D2 single", kfix<2, true, true, false>, true, -4},
+      {"fix D4 pair", kfix<4, true, true, true>, true, -4},
+      {"fix D4 single", kfix<4, true, true, false>, true, -4},
+      {"fix D2 pair (2)", kfix<2, true, true, true>, true, -4},
+      {"fix D2 single (2)", kfix<2, true, true, false>, true, -4},
+      {"pat2d st plain", kpatp<0>, false, -4},
       {"copy (float4)", nullptr, false},
-      {"pat 12->4 W1", kpat<12, 4, 1>, false, 4},
-      {"pat 12->4 W4", kpat<12, 4, 4>, false, 16},
-      {"pats 12->4 T4 nt", kpats<12, 4, 4, true>, false, 16},
-      {"pats 12->4 T4 plain", kpats<12, 4, 4, false>, false, 16},
-      {"pats 12->4 T16 nt", kpats<12, 4, 16, true>, false, 64},
-      {"pats 0->4 T1 nt", kpats<0, 4, 1, true>, false, 4, 4.0 / 16},
-      {"pats 0->4 T1 plain", kpats<0, 4, 1, false>, false, 4, 4.0 / 16},
-      {"pats 0->4 T16 nt", kpats<0, 4, 16, true>, false, 64, 4.0 / 16},
-      {"pats 0->1 T1 nt", kpats<0, 1, 1, true>, false, 4, 1.0 / 16},
-      {"pats 1->1 T1 nt", kpats<1, 1, 1, true>, false, 4, 2.0 / 16},
-      {"pats 8->8 T1 nt", kpats<8, 8, 1, true>, false, 4},
-      {"pat 16->0 W4", kpat<16, 0, 4>, false, 16},
   };
   uint32_t* flags = nullptr;
   CK(hipMalloc(&flags, 64));
   a.flags = flags;
   auto launch = [&](const Variant& v) {
-    if (v.kern) {
+    if (v.kern && v.tilekb < 0) {  // 2-D grid (tiles, stripes)
+      GfArgs b = a;
+      b.tiles_per_stripe = (uint32_t)((S - v.tilekb * 1024 - 1) / (-v.tilekb * 1024));
+      hipLaunchKernelGGL(v.kern, dim3(b.tiles_per_stripe, nst), dim3(256), 0, 0, b);
+    } else if (v.kern) {
       GfArgs b = a;
       b.tiles_per_stripe = (uint32_t)((S + v.tilekb * 1024 - 1) / (v.tilekb * 1024));
       hipLaunchKernelGGL(v.kern, dim3(b.tiles_per_stripe * nst), dim3(256), 0, 0, b);

@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "gf256.hpp"
@@ -69,8 +70,10 @@ int main() {
   CK(hipEventCreate(&e1));
   uint32_t* flags;
   CK(hipMalloc(&flags, 4096));
-  printf("%-30s %3s %3s %9s %4s %9s %8s %6s %9s %9s %6s\n", "shape", "k", "m", "S", "nst", "us/launch", "GB/s",
-         "%8TB", "Tlaneop/s", "verify us", "%8TB");
+  uint32_t* crcs;
+  CK(hipMalloc(&crcs, 4 * 64 * 1024));
+  printf("%-30s %3s %3s %9s %4s %9s %8s %6s %9s %9s %6s %9s %6s %11s\n", "shape", "k", "m", "S", "nst", "us/launch", "GB/s",
+         "%8TB", "Tlaneop/s", "verify us", "%8TB", "+crc us", "%8TB", "crc-only us");
   for (auto& sh : shapes) {
     const size_t pitch = (sh.S + 255) / 256 * 256;
     Matrix mat;
@@ -98,7 +101,7 @@ int main() {
     MatVecJob vjob = job;
     vjob.mode = MatVecMode::kVerify;
     vjob.flags = flags;
-    static float settled = 0;  // ~300 ms of load once, so clocks leave their idle state
+    static float settled = getenv("GF_SHAPES_NOSETTLE") ? 1e9f : 0.f;  // ~300 ms of load once (clock ramp)
     while (settled < 300) {
       CK(hipEventRecord(e0, 0));
       for (int i = 0; i < 20; ++i) launch_all();
@@ -109,7 +112,7 @@ int main() {
       settled += ms;
     }
     for (int i = 0; i < 5; ++i) launch_all();
-    const int reps = 100;
+    const int reps = getenv("GF_SHAPES_REPS") ? atoi(getenv("GF_SHAPES_REPS")) : 100;
     CK(hipEventRecord(e0, 0));
     for (int i = 0; i < reps; ++i) launch_all();
     CK(hipEventRecord(e1, 0));
@@ -124,12 +127,44 @@ int main() {
     float vms;
     CK(hipEventElapsedTime(&vms, e0, e1));
     const double vus = vms * 1e3 / reps;
+    // encode + crc32.ChecksumIEEE of every shard, fused (same algorithmic bytes as the encode)
+    double cus = 0;
+    if (matvec_crc_supported(sh.k, sh.m, sh.S)) {
+      std::vector<int> slot(sh.k + sh.m);
+      for (int i = 0; i < sh.k + sh.m; ++i) slot[i] = i;
+      for (int i = 0; i < 5; ++i) CK(launch_matvec_crc(job, crcs, sh.k + sh.m, slot.data(), 0));
+      CK(hipEventRecord(e0, 0));
+      for (int i = 0; i < reps; ++i) CK(launch_matvec_crc(job, crcs, sh.k + sh.m, slot.data(), 0));
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float cms;
+      CK(hipEventElapsedTime(&cms, e0, e1));
+      cus = cms * 1e3 / reps;
+    }
+    // the standalone checksum pass over the same shards (what the fused kernel saves)
+    double ous = 0;
+    {
+      std::vector<const uint8_t*> all;
+      for (int s = 0; s < sh.stripes; ++s) {
+        for (int c = 0; c < sh.k; ++c) all.push_back(in[(size_t)s * sh.k + c]);
+        for (int r = 0; r < sh.m; ++r) all.push_back(out[(size_t)s * sh.m + r]);
+      }
+      for (int i = 0; i < 3; ++i) CK(launch_crc32(all.data(), sh.S, (int)all.size(), crcs, 0));
+      const int creps = std::max(5, reps / 4);
+      CK(hipEventRecord(e0, 0));
+      for (int i = 0; i < creps; ++i) CK(launch_crc32(all.data(), sh.S, (int)all.size(), crcs, 0));
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float oms;
+      CK(hipEventElapsedTime(&oms, e0, e1));
+      ous = oms * 1e3 / creps;
+    }
     const double bytes = double(sh.k + sh.m) * sh.S * sh.stripes;
     // lane-ops: per 16-B lane chunk, k inputs x (20 selector ops + m x 20 perm/xor ops)
     const double laneops = double(sh.S) / 16 * sh.stripes * sh.k * (20.0 + 20.0 * sh.m);
-    printf("%-30s %3d %3d %9zu %4d %9.1f %8.1f %6.1f %9.1f %9.1f %6.1f\n", sh.name, sh.k, sh.m, sh.S, sh.stripes,
-           us, bytes / (us * 1e-6) / 1e9, 100 * bytes / (us * 1e-6) / 8e12, laneops / (us * 1e-6) / 1e12, vus,
-           100 * bytes / (vus * 1e-6) / 8e12);
+    printf("%-30s %3d %3d %9zu %4d %9.1f %8.1f %6.1f %9.1f %9.1f %6.1f %9.1f %6.1f %11.1f\n", sh.name, sh.k, sh.m, sh.S,
+           sh.stripes, us, bytes / (us * 1e-6) / 1e9, 100 * bytes / (us * 1e-6) / 8e12, laneops / (us * 1e-6) / 1e12,
+           vus, 100 * bytes / (vus * 1e-6) / 8e12, cus, cus > 0 ? 100 * bytes / (cus * 1e-6) / 8e12 : 0.0, ous);
   }
   return 0;
 }
