@@ -1,132 +1,131 @@
-// crc32.hip -- shard CRC32-IEEE on gfx950 (the checksum access computes per shard after
-// encode, blobstore/access/stream_put.go:249-253, and blobnode recomputes on repair,
-// blobnode/work_shard_recover.go:336-342).  Go's crc32.ChecksumIEEE: reflected polynomial
-// 0xEDB88320, register preset ~0 and final inversion.
+// crc32.hip -- standalone shard CRC32-IEEE on gfx950: Go's crc32.ChecksumIEEE of each shard
+// (reflected polynomial 0xEDB88320, register preset ~0, final inversion), for shards no coding
+// kernel touches -- cfsec_crc32_ieee_batch, and the checksum pass after a product whose shape
+// the fused kernel (gf_crc.hpp) does not cover.
 //
-// Parallel form.  Write f(r, B) for the register after feeding bytes B from register r
-// (no pre/post inversion).  f is affine: f(r, B) = shift(r, |B|) ^ f(0, B), where
-// shift(v, n) multiplies v by x^(8n) mod P.  For a shard split into chunks C_i ending at
-// byte e_i:  crc = ~( shift(~0, S) ^ XOR_i shift(f(0, C_i), S - e_i) ).
-// Each lane folds one 1 KiB chunk with slice-by-4 tables in LDS, shifts its remainder to
-// the end of the shard, and XORs it into the shard's word; the host applies the ~0 terms.
-#include "kernels.hpp"
-
+// Same algebra and work split as the fused kernel, without the product: a workgroup owns `tpw`
+// consecutive 4 KiB tiles of one shard, thread j a 16-byte piece of each (coalesced 16-B loads,
+// the next tile's piece in flight while this one is folded), Horner R <- f(shift(R, 4080), piece)
+// with slice-by-8 LDS tables, a per-thread basis multiply to the tile end, a workgroup XOR
+// reduction and one multiply by x^(8(S - e)) to the shard end, then atomicXor into the shard's
+// word.  `fin` (crc32_shift_ones(S), or 0 for the raw word) is folded in by workgroup 0.
 #include <algorithm>
+#include <vector>
+
+#include "gf_crc.hpp"
+#include "kernels.hpp"
 
 namespace cfsec {
 namespace {
 
-constexpr uint32_t kPoly = 0xEDB88320u;
-constexpr int kThreads = 256;
-constexpr size_t kChunk = 1024;
-constexpr int kSlots = 280;
+using crcdev::kBasisWords;
+using crcdev::kMaxGroups;
+using crcdev::kTabWords;
+using crcdev::kTile;
+using dev::u32x4;
+constexpr int kSlots = 160;
 
 struct __attribute__((aligned(16))) CrcArgs {
   uint64_t len;
+  int64_t sstride;               // affine list: shard i at ptr[0] + i*sstride, word idx[0] + i
+  uint32_t tiles, tpw;
   uint32_t* out;
-  uint32_t fin, pad;            // XOR-ed in once per shard (0: leave the raw word)
+  const uint32_t* tabs;
+  uint32_t fin, pad;
   const uint8_t* ptr[kSlots];
-  uint32_t idx[kSlots];         // output word of shard i
+  uint32_t idx[kSlots];          // output word of shard i
+  uint32_t gconst[kMaxGroups];   // x^(8(len - e_g)) mod P
 };
+static_assert(sizeof(CrcArgs) <= 3584, "kernel argument block must stay below 4 KiB");
 
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef u32x4 u32x4_ua __attribute__((aligned(1)));
-
-// a * b mod P, reflected bit order (bit 31 = x^0).
-__host__ __device__ inline uint32_t multmodp(uint32_t a, uint32_t b) {
-  uint32_t p = 0;
-  for (uint32_t m = 1u << 31; m; m >>= 1) {
-    if (a & m) p ^= b;
-    b = (b & 1u) ? (b >> 1) ^ kPoly : b >> 1;
+__device__ __forceinline__ void piece(const uint8_t* p, uint64_t len, uint32_t off, uint32_t (&d)[4]) {
+  if ((uint64_t)off + dev::kLaneBytes <= len) {
+    const u32x4 v = dev::ld16<true>(p + off);
+    d[0] = v.x, d[1] = v.y, d[2] = v.z, d[3] = v.w;
+  } else {
+    const size_t rem = off < len ? (size_t)(len - off) : 0;  // zero padding past the shard end
+    const u32x4 v = rem ? dev::ld_tail(p + off, rem) : u32x4{0u, 0u, 0u, 0u};
+    d[0] = v.x, d[1] = v.y, d[2] = v.z, d[3] = v.w;
   }
-  return p;
 }
 
-struct X2n {
-  uint32_t t[64];  // t[k] = x^(2^k) mod P
-};
-
-X2n make_x2n() {
-  X2n x{};
-  uint32_t p = 1u << 30;  // x^1
-  x.t[0] = p;
-  for (int k = 1; k < 64; ++k) x.t[k] = p = multmodp(p, p);
-  return x;
-}
-
-__constant__ X2n d_x2n;
-
-// x^(8n) mod P
-__host__ __device__ inline uint32_t x8nmodp(uint64_t n, const uint32_t* t) {
-  uint32_t p = 1u << 31;  // x^0
-  int k = 3;
-  while (n) {
-    if (n & 1) p = multmodp(t[k], p);
-    n >>= 1;
-    ++k;
-  }
-  return p;
-}
-
-__global__ __launch_bounds__(kThreads) void crc32_chunks_kernel(const CrcArgs a) {
-  __shared__ uint32_t tab[4][256];
-  for (int i = threadIdx.x; i < 256; i += kThreads) {
-    uint32_t c = (uint32_t)i;
-    for (int j = 0; j < 8; ++j) c = (c & 1u) ? (c >> 1) ^ kPoly : c >> 1;
-    tab[0][i] = c;
-  }
+__global__ __launch_bounds__(256) void crc32_horner_kernel(const CrcArgs a) {
+  __shared__ uint32_t ct[kTabWords];
+  __shared__ uint32_t red[4];
+  for (int i = threadIdx.x; i < kTabWords; i += 256) ct[i] = a.tabs[i];
   __syncthreads();
-  for (int i = threadIdx.x; i < 256; i += kThreads) {
-    uint32_t c = tab[0][i];
-    for (int s = 1; s < 4; ++s) {
-      c = (c >> 8) ^ tab[0][c & 0xFF];
-      tab[s][i] = c;
-    }
-  }
-  __syncthreads();
-
-  const size_t start = ((size_t)blockIdx.x * kThreads + threadIdx.x) * kChunk;
-  if (start >= a.len) return;
-  const size_t end = start + kChunk < a.len ? start + kChunk : a.len;
-  const uint8_t* p = a.ptr[blockIdx.y];
-  uint32_t crc = 0;
-  size_t i = start;
-  for (; i + 16 <= end; i += 16) {
-    const u32x4 v = *reinterpret_cast<const u32x4_ua*>(p + i);
+  const uint32_t g = blockIdx.x, sh = blockIdx.y;
+  const uint8_t* p = a.sstride ? a.ptr[0] + (int64_t)sh * a.sstride : a.ptr[sh];
+  const uint32_t t0 = g * a.tpw, t1 = min(t0 + a.tpw, a.tiles);
+  const uint32_t lanepos = threadIdx.x * dev::kLaneBytes;
+  uint32_t R = 0, cur[4], nxt[4];
+  piece(p, a.len, t0 * kTile + lanepos, cur);
+  for (uint32_t t = t0; t < t1; ++t) {
+    if (t + 1 < t1) piece(p, a.len, (t + 1) * kTile + lanepos, nxt);
+    R = crcdev::crc_step(ct, R, cur);
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      crc ^= v[w];
-      crc = tab[3][crc & 0xFF] ^ tab[2][(crc >> 8) & 0xFF] ^ tab[1][(crc >> 16) & 0xFF] ^ tab[0][crc >> 24];
-    }
+    for (int w = 0; w < 4; ++w) cur[w] = nxt[w];
   }
-  for (; i < end; ++i) crc = (crc >> 8) ^ tab[0][(crc ^ p[i]) & 0xFF];
-  if (end < a.len) crc = multmodp(x8nmodp(a.len - end, d_x2n.t), crc);
-  if (start == 0) crc ^= a.fin;
-  atomicXor(a.out + a.idx[blockIdx.y], crc);
+  const u32x4* basis = reinterpret_cast<const u32x4*>(a.tabs + kTabWords + threadIdx.x * 32);
+  uint32_t o = 0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const u32x4 v = basis[q];
+    o ^= (0u - ((R >> (4 * q)) & 1u)) & v.x;
+    o ^= (0u - ((R >> (4 * q + 1)) & 1u)) & v.y;
+    o ^= (0u - ((R >> (4 * q + 2)) & 1u)) & v.z;
+    o ^= (0u - ((R >> (4 * q + 3)) & 1u)) & v.w;
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) o ^= (uint32_t)__shfl_xor((int)o, d);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = o;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t v = crcdev::mulmod(a.gconst[g], red[0] ^ red[1] ^ red[2] ^ red[3]);
+    if (g == 0) v ^= a.fin;
+    atomicXor(a.out + (a.sstride ? a.idx[0] + sh : a.idx[sh]), v);
+  }
 }
 
 }  // namespace
 
 hipError_t launch_crc32_to(const uint8_t* const* ptrs, size_t len, int n, uint32_t* out, const uint32_t* idx,
                            uint32_t fin, hipStream_t stream) {
-  static const X2n host_x2n = make_x2n();
-  hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(d_x2n), &host_x2n, sizeof(X2n), 0,
-                                        hipMemcpyHostToDevice, stream);
-  if (e != hipSuccess || len == 0 || n == 0) return e;
-  const size_t blocks = (len + kChunk * kThreads - 1) / (kChunk * kThreads);
-  CrcArgs a;
+  if (len == 0 || n == 0) return hipSuccess;
+  if (len > 0xFFFFFFFFull - kTile || !ptrs || !out) return hipErrorInvalidValue;
+  CrcArgs a{};
+  hipError_t e = crc_device_tables(&a.tabs);
+  if (e != hipSuccess) return e;
+  const uint32_t tiles = (uint32_t)((len + kTile - 1) / kTile);
+  // one launch for an equally spaced list (a pitched stripe batch) with consecutive words
+  const auto at = [&](int i) { return (int64_t)(uintptr_t)ptrs[i]; };
+  int64_t stride = n > 1 ? at(1) - at(0) : 0;
+  for (int i = 1; i < n && stride; ++i)
+    if (at(i) - at(0) != stride * i || (idx && idx[i] != idx[0] + (uint32_t)i)) stride = 0;
+  if (n > 65535) stride = 0;
+  const int per_launch = stride ? n : kSlots;
+  // ~2048 workgroups in all, each keeping >= 1 tile
+  const uint32_t want = std::max<uint32_t>(1, 2048u / (uint32_t)n);
+  uint32_t groups = std::min<uint32_t>({tiles, want, (uint32_t)kMaxGroups});
+  const uint32_t tpw = (tiles + groups - 1) / groups;
+  groups = (tiles + tpw - 1) / tpw;
   a.len = len;
+  a.sstride = stride;
+  a.tiles = tiles;
+  a.tpw = tpw;
   a.out = out;
   a.fin = fin;
-  a.pad = 0;
-  for (int s0 = 0; s0 < n; s0 += kSlots) {
-    const int ns = std::min(kSlots, n - s0);
-    for (int s = 0; s < ns; ++s) {
+  for (uint32_t g = 0; g < groups; ++g) {
+    const int64_t end = (int64_t)std::min<uint64_t>((uint64_t)(g + 1) * tpw, tiles) * kTile;
+    a.gconst[g] = crc_xpow(8 * ((int64_t)len - end));
+  }
+  for (int s0 = 0; s0 < n; s0 += per_launch) {
+    const int ns = std::min(per_launch, n - s0);
+    for (int s = 0; s < std::min(ns, kSlots); ++s) {
       a.ptr[s] = ptrs[s0 + s];
       a.idx[s] = idx ? idx[s0 + s] : (uint32_t)(s0 + s);
     }
-    hipLaunchKernelGGL(crc32_chunks_kernel, dim3((unsigned)blocks, (unsigned)ns), dim3(kThreads), 0,
-                       stream, a);
+    hipLaunchKernelGGL(crc32_horner_kernel, dim3(groups, (unsigned)ns), dim3(256), 0, stream, a);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
@@ -141,9 +140,8 @@ hipError_t launch_crc32(const uint8_t* const* ptrs, size_t len, int n, uint32_t*
 }
 
 uint32_t crc32_finalize(uint32_t raw, size_t len) {
-  static const X2n host_x2n = make_x2n();
   if (len == 0) return 0;
-  return ~(multmodp(x8nmodp(len, host_x2n.t), 0xFFFFFFFFu) ^ raw);
+  return raw ^ crc32_shift_ones(len);
 }
 
 }  // namespace cfsec

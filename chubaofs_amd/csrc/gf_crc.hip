@@ -67,8 +67,10 @@ std::vector<uint32_t> host_tables() {
   return t;
 }
 
+}  // namespace
+
 // The lookup tables on the current device, uploaded once per device.
-hipError_t device_tables(const uint32_t** out) {
+hipError_t crc_device_tables(const uint32_t** out) {
   static std::mutex mu;
   static std::map<int, uint32_t*> per_device;
   int dev = 0;
@@ -91,6 +93,10 @@ hipError_t device_tables(const uint32_t** out) {
   *out = it->second;
   return hipSuccess;
 }
+
+uint32_t crc_xpow(int64_t e) { return xpow(e); }
+
+namespace {
 
 // As gf_kernels.hip's affine_stride, for the whole job.
 int64_t affine_stride(const MatVecJob& job) {
@@ -142,7 +148,7 @@ hipError_t launch_matvec_crc(const MatVecJob& job, uint32_t* crc, int crc_stride
   if (e != hipSuccess || job.nstripes == 0 || job.len == 0) return e;
 
   GfCrcArgs a{};
-  e = device_tables(&a.tabs);
+  e = crc_device_tables(&a.tabs);
   if (e != hipSuccess) return e;
   const uint32_t tiles = (uint32_t)((job.len + crcdev::kTile - 1) / crcdev::kTile);
   const int64_t sstride = affine_stride(job);

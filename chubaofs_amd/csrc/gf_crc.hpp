@@ -226,6 +226,15 @@ hipError_t launch_crc_k(int m, const GfCrcArgs& a, dim3 grid, hipStream_t st) {
   return hipGetLastError();
 }
 
+}  // namespace crcdev
+
+// gf_crc.hip: the lookup tables (kTabWords + kBasisWords) on the current device, uploaded once
+// per device; x^e mod P for any integer e (negative: powers of x^-1).
+hipError_t crc_device_tables(const uint32_t** out);
+uint32_t crc_xpow(int64_t e);
+
+namespace crcdev {
+
 #define CFSEC_CRC_EXTERN(K)                                                                         \
   extern template hipError_t launch_crc_k<K, true>(int, const GfCrcArgs&, dim3, hipStream_t);       \
   extern template hipError_t launch_crc_k<K, false>(int, const GfCrcArgs&, dim3, hipStream_t);

@@ -131,3 +131,22 @@ def test_crc_zero_length_and_empty(rs):
     t = torch.zeros(16, dtype=torch.uint8, device="cuda")
     enc.encode_crc_batch([t.data_ptr()] * 16, 0, 1, crcs.data_ptr())
     assert crcs.cpu().tolist() == [0] * 16  # crc32.ChecksumIEEE(nil) == 0
+
+
+@pytest.mark.parametrize("layout", ["pitched", "separate"])
+@pytest.mark.parametrize("n,S", [(170, 4097), (2048, 300), (7, 349526)])
+def test_standalone_crc_many_shards(rs, layout, n, S):
+    """cfsec_crc32_ieee_batch over many shards: an equally spaced list runs as one launch, a
+    scattered list in pointer-table launches of 160."""
+    r = np.random.default_rng(n + S)
+    if layout == "pitched":
+        pitch = (S + 255) // 256 * 256
+        host = r.integers(0, 256, (n, pitch), dtype=np.uint8)
+        dev = torch.from_numpy(host).cuda()
+        ptrs = [dev.data_ptr() + i * pitch for i in range(n)]
+        arrs = [host[i, :S] for i in range(n)]
+    else:
+        arrs = [r.integers(0, 256, S, dtype=np.uint8) for _ in range(n)]
+        dev = [torch.from_numpy(a).cuda() for a in arrs]
+        ptrs = [t.data_ptr() for t in dev]
+    assert rs.crc32_ieee_batch(ptrs, S) == [crc(a) for a in arrs]
