@@ -257,6 +257,10 @@ def main():
     flags = torch.zeros(nst, dtype=torch.int32, device=dev)
     verify_ms = timed(lambda: enc.verify_batch(ptrs, S, nst, flags.data_ptr(), stream=stream), n_op)
     assert int(flags.sum().item()) == 0, "Verify failed after the timed region"
+    # Encode + crc32.ChecksumIEEE of all 16 shards (access/stream_put.go:249-253), fused into the
+    # coding kernel: same algorithmic bytes as the encode
+    crcs = torch.zeros(nst * total, dtype=torch.int32, device=dev)
+    crc_ms = timed(lambda: enc.encode_crc_batch(ptrs, S, nst, crcs.data_ptr(), stream=stream), n_op)
 
     data_bytes = K_DATA * S * nst
     launch_bytes = (K_DATA + M_PARITY) * S * nst  # algorithmic bytes per launch (read 12S + write 4S)
@@ -304,6 +308,8 @@ def main():
         "reconstruct_data_GBps": round(data_bytes / (rec_ms * 1e-3) / 1e9, 1),
         "verify_data_GBps": round(data_bytes / (verify_ms * 1e-3) / 1e9, 1),
         "verify_roofline_frac": round(launch_bytes / (verify_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+        "encode_crc_data_GBps": round(data_bytes / (crc_ms * 1e-3) / 1e9, 1),
+        "encode_crc_roofline_frac": round(launch_bytes / (crc_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
         "cpu_baseline": cpu,
     }
     print(json.dumps(out), flush=True)
