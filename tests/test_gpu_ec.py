@@ -251,3 +251,35 @@ def test_concurrent_encoders_threads():
     with cf.ThreadPoolExecutor(8) as ex:
         assert all(ex.map(job, range(24)))
     del rng
+
+
+@pytest.mark.parametrize("mode", [cm.EC6P6, cm.EC12P4, cm.EC6P10L2, cm.EC16P20L2])
+@pytest.mark.parametrize("memory", ["host", "device"])
+def test_segment_reconstruct_data(mode, memory):
+    """access/stream_get.go:420-431: a ranged Get rebuilds only the requested byte range of the
+    data shards -- ReconstructData over sub-slices shards[i][off:off+size] of the full shards,
+    with the bad shards' segments rebuilt in place inside the original buffers."""
+    t = cm.GetTactic(mode)
+    enc = new(mode, verify=False)
+    rng = np.random.default_rng(mode * 7 + (memory == "device"))
+    data = rng.integers(0, 256, 200003, dtype=np.uint8)
+    shards = enc.Split(data)
+    if memory == "device":
+        shards = to_dev(shards)
+    enc.Encode(shards)
+    origin = host(copy_shards(shards))
+    S = len(origin[0])
+    for off, size in [(0, 1), (17, 4096), (S // 3, 1000), (S - 5, 5), (4095, 8193)]:
+        size = min(size, S - off)
+        bad = sorted(rng.choice(t.N + t.M, t.M, replace=False).tolist())
+        work = copy_shards(shards)
+        for i in bad:
+            work[i][off:off + size] = 0  # the bad shards' bytes in the range are unknown
+        segments = [s[off:off + size] for s in work]
+        enc.ReconstructData(segments, bad)
+        got = host(work)
+        for i in range(t.N):  # every data segment restored, inside the original buffer
+            assert np.array_equal(got[i][off:off + size], origin[i][off:off + size]), (off, size, i, bad)
+        for i in range(t.N + t.M + t.L):  # nothing outside the range was touched
+            assert np.array_equal(got[i][:off], origin[i][:off] if i not in bad else got[i][:off])
+            assert np.array_equal(got[i][off + size:], origin[i][off + size:]), (off, size, i)
