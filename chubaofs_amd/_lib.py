@@ -102,6 +102,8 @@ SIGNATURES = {
     "cfsec_ec_verify": ([_V, P_SHARD, _I, _I, _V, _P(_I)], _I),
     "cfsec_ec_shards_in_idc": ([_V, _I, _V, _I, _P(_I)], _I),
     "cfsec_crc32_ieee_batch": ([_V, _S, _I, _V, _I, _V], _I),
+    "cfsec_host_alloc": ([_S, _P(_V)], _I),
+    "cfsec_host_free": ([_V], _I),
 }
 
 _LIB = None
@@ -125,3 +127,31 @@ def lib():
 
 def device_count() -> int:
     return lib().cfsec_device_count()
+
+
+class _Pinned:
+    """Owner of one cfsec_host_alloc block; frees it when the last numpy view is gone."""
+
+    def __init__(self, size: int):
+        p = ctypes.c_void_p()
+        check(lib().cfsec_host_alloc(size, ctypes.byref(p)))
+        self.ptr, self.size = p.value, size
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            lib().cfsec_host_free(self.ptr)
+            self.ptr = None
+
+
+def pinned_empty(size: int):
+    """A uint8 numpy array in page-locked host memory (cfsec_host_alloc): host-memory calls on it
+    DMA straight to HBM.  The array keeps the allocation alive."""
+    import numpy as np
+
+    if size == 0:
+        return np.zeros(0, np.uint8)
+    owner = _Pinned(size)
+    buf = (ctypes.c_uint8 * size).from_address(owner.ptr)
+    arr = np.frombuffer(buf, dtype=np.uint8)
+    buf._cfsec_owner = owner  # the ctypes buffer (referenced by arr.base) holds the owner
+    return arr

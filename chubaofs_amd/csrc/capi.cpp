@@ -263,6 +263,22 @@ int cfsec_ec_shards_in_idc(const cfsec_ec* h, int idx, int* out, int out_cap, in
   return CFSEC_OK;
 }
 
+// ---------------- pinned host memory ----------------
+
+int cfsec_host_alloc(size_t size, void** out) {
+  if (!out) return CFSEC_ERR_INVALID_ARG;
+  *out = nullptr;
+  if (size == 0) return CFSEC_OK;
+  return guarded([&] {
+    return (int)cfsec::hip_status(hipHostMalloc(out, size, hipHostMallocPortable), "hipHostMalloc");
+  });
+}
+
+int cfsec_host_free(void* p) {
+  if (!p) return CFSEC_OK;
+  return guarded([&] { return (int)cfsec::hip_status(hipHostFree(p), "hipHostFree"); });
+}
+
 // ---------------- CRC32 ----------------
 
 int cfsec_crc32_ieee_batch(uint8_t* const* ptrs, size_t shard_size, int n, uint32_t* out,

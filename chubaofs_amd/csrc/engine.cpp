@@ -141,6 +141,10 @@ Status DeviceContext::acquire(size_t bytes, size_t nflags, Workspace** out) {
   }
   Status st = CFSEC_OK;
   if (!ws->stream) st = hip_status(hipStreamCreateWithFlags(&ws->stream, hipStreamNonBlocking), "hipStreamCreate");
+  if (st == CFSEC_OK && !ws->stream2)
+    st = hip_status(hipStreamCreateWithFlags(&ws->stream2, hipStreamNonBlocking), "hipStreamCreate");
+  if (st == CFSEC_OK && !ws->ev)
+    st = hip_status(hipEventCreateWithFlags(&ws->ev, hipEventDisableTiming), "hipEventCreate");
   if (st == CFSEC_OK && ws->cap < bytes) {
     if (ws->dbuf) (void)hipFree(ws->dbuf);
     ws->dbuf = nullptr;
@@ -221,6 +225,22 @@ Status RSEngine::create(int k, int m, int device, std::unique_ptr<RSEngine>* out
   return CFSEC_OK;
 }
 
+namespace {
+// The device address of page-locked host memory (hipHostMalloc / cfsec_host_alloc); false for
+// pageable memory.
+bool device_alias(uint8_t* p, uint8_t** dptr) {
+  hipPointerAttribute_t attr;
+  if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  if (attr.type != hipMemoryTypeHost || !attr.devicePointer) return false;
+  const uint8_t* hbase = static_cast<const uint8_t*>(attr.hostPointer);
+  *dptr = static_cast<uint8_t*>(attr.devicePointer) + (hbase ? p - hbase : 0);
+  return true;
+}
+}  // namespace
+
 Status RSEngine::run(const Matrix& rows, const std::vector<cfsec_shard*>& ins,
                      const std::vector<cfsec_shard*>& outs, size_t S, int mem, hipStream_t stream,
                      MatVecMode mode, bool* ok) {
@@ -246,6 +266,28 @@ Status RSEngine::run(const Matrix& rows, const std::vector<cfsec_shard*>& ins,
   const size_t slot = align_up(S, kSlotAlign);
   // Verify with more inputs than one launch carries: compute into staging, then compare.
   const bool two_step_verify = verify && nin > 32;
+  if (host) {
+    // Page-locked buffers (cfsec_host_alloc) are device-addressable: the kernel reads and writes
+    // them over PCIe with no staging copies (tools/bench_host.py: 50.7 GB/s of data for EC12P4
+    // encode vs 32.4 through the staged pipeline and 26.7 from pageable memory).
+    std::vector<cfsec_shard> zin(nin), zout(nout);
+    bool zero_copy = true;
+    for (int i = 0; i < nin && zero_copy; ++i) {
+      zin[i] = *ins[i];
+      zero_copy = device_alias(ins[i]->data, &zin[i].data);
+    }
+    for (int r = 0; r < nout && zero_copy; ++r) {
+      zout[r] = *outs[r];
+      zero_copy = device_alias(outs[r]->data, &zout[r].data);
+    }
+    if (zero_copy) {
+      std::vector<cfsec_shard*> pin(nin), pout(nout);
+      for (int i = 0; i < nin; ++i) pin[i] = &zin[i];
+      for (int r = 0; r < nout; ++r) pout[r] = &zout[r];
+      return run(rows, pin, pout, S, CFSEC_MEM_DEVICE, nullptr, mode, ok);
+    }
+    if (!two_step_verify) return run_host(rows, ins, outs, S, mode, ok);
+  }
   size_t staging = host ? slot * size_t(nin + nout) : 0;
   if (two_step_verify) staging += slot * size_t(nout);
 
@@ -318,6 +360,103 @@ Status RSEngine::run(const Matrix& rows, const std::vector<cfsec_shard*>& ins,
       st = hip_status(hipMemcpyAsync(outs[r]->data, dout[r], S, hipMemcpyDeviceToHost, s), "hipMemcpyAsync D2H");
   const Status sync = hip_status(hipStreamSynchronize(s), "hipStreamSynchronize");
   if (st == CFSEC_OK) st = sync;
+  if (st == CFSEC_OK && verify && ok) *ok = ws->hflags[0] == 0;
+  ctx_->release(ws);
+  return st;
+}
+
+namespace {
+// Rows of a host call that sit at one stride from each other (ec.Buffer carves its shards at
+// stride S from one allocation, common/ec/buf.go:83-84): one 2-D copy moves all of them.
+int64_t host_row_stride(const std::vector<cfsec_shard*>& rows) {
+  if (rows.size() < 2) return 0;
+  const int64_t st = (int64_t)(uintptr_t)rows[1]->data - (int64_t)(uintptr_t)rows[0]->data;
+  if (st <= 0) return 0;
+  for (size_t i = 2; i < rows.size(); ++i)
+    if ((int64_t)(uintptr_t)rows[i]->data - (int64_t)(uintptr_t)rows[0]->data != st * (int64_t)i) return 0;
+  return st;
+}
+
+hipError_t copy_rows(const std::vector<cfsec_shard*>& rows, int64_t hstride, size_t off, size_t len,
+                     uint8_t* dev, size_t dpitch, bool h2d, hipStream_t s) {
+  if (rows.empty()) return hipSuccess;
+  if (hstride > 0 && (size_t)hstride >= len) {
+    return h2d ? hipMemcpy2DAsync(dev, dpitch, rows[0]->data + off, (size_t)hstride, len, rows.size(),
+                                  hipMemcpyHostToDevice, s)
+               : hipMemcpy2DAsync(rows[0]->data + off, (size_t)hstride, dev, dpitch, len, rows.size(),
+                                  hipMemcpyDeviceToHost, s);
+  }
+  for (size_t i = 0; i < rows.size(); ++i) {
+    hipError_t e = h2d ? hipMemcpyAsync(dev + i * dpitch, rows[i]->data + off, len, hipMemcpyHostToDevice, s)
+                       : hipMemcpyAsync(rows[i]->data + off, dev + i * dpitch, len, hipMemcpyDeviceToHost, s);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+}  // namespace
+
+// Host-memory call: the shard columns go through HBM in chunks of kHostChunk bytes per row,
+// alternating over two streams, so chunk j+1's host->device copies, chunk j's kernel and chunk
+// j-1's device->host copies overlap (the copy engines of each direction and the CUs run
+// concurrently; PCIe Gen5 x16 is the bound).  Buffers from cfsec_host_alloc (pinned) DMA
+// directly; pageable ones go through HIP's staging.  Chunks of one stream reuse its staging
+// region, which that stream's order makes safe.
+Status RSEngine::run_host(const Matrix& rows, const std::vector<cfsec_shard*>& ins,
+                          const std::vector<cfsec_shard*>& outs, size_t S, MatVecMode mode, bool* ok) {
+  const int nin = (int)ins.size(), nout = (int)outs.size();
+  const bool verify = mode == MatVecMode::kVerify;
+  const size_t chunk = std::min(align_up(S, kSlotAlign), kHostChunk);
+  const size_t nchunks = (S + chunk - 1) / chunk;
+  const int nlanes = nchunks > 1 ? 2 : 1;
+  const size_t per_lane = chunk * size_t(nin + nout);
+  DeviceContext::Workspace* ws = nullptr;
+  Status st = ctx_->acquire(per_lane * nlanes, 1, &ws);
+  if (st != CFSEC_OK) return st;
+  hipStream_t lane[2] = {ws->stream, ws->stream2};
+  const int64_t in_stride = host_row_stride(ins), out_stride = host_row_stride(outs);
+  if (verify) {
+    st = hip_status(hipMemsetAsync(ws->dflags, 0, 4, lane[0]), "hipMemsetAsync");
+    if (st == CFSEC_OK && nlanes > 1) st = hip_status(hipEventRecord(ws->ev, lane[0]), "hipEventRecord");
+    if (st == CFSEC_OK && nlanes > 1) st = hip_status(hipStreamWaitEvent(lane[1], ws->ev, 0), "hipStreamWaitEvent");
+  }
+  std::vector<const uint8_t*> din(nin);
+  std::vector<uint8_t*> dout(nout);
+  for (size_t j = 0; j < nchunks && st == CFSEC_OK; ++j) {
+    const int l = (int)(j % nlanes);
+    hipStream_t s = lane[l];
+    uint8_t* base = ws->dbuf + per_lane * l;
+    const size_t off = j * chunk, len = std::min(chunk, S - off);
+    for (int i = 0; i < nin; ++i) din[i] = base + chunk * i;
+    for (int r = 0; r < nout; ++r) dout[r] = base + chunk * (nin + r);
+    st = hip_status(copy_rows(ins, in_stride, off, len, base, chunk, true, s), "hipMemcpyAsync H2D");
+    if (st == CFSEC_OK && verify)
+      st = hip_status(copy_rows(outs, out_stride, off, len, base + chunk * nin, chunk, true, s), "hipMemcpyAsync H2D");
+    if (st == CFSEC_OK) {
+      MatVecJob job;
+      job.k = nin;
+      job.m = nout;
+      job.coef = rows.v.data();
+      job.len = len;
+      job.nstripes = 1;
+      job.in = din.data();
+      job.out = dout.data();
+      job.mode = mode;
+      job.flags = ws->dflags;
+      st = hip_status(launch_matvec(job, s), "launch_matvec");
+    }
+    if (st == CFSEC_OK && !verify)
+      st = hip_status(copy_rows(outs, out_stride, off, len, base + chunk * nin, chunk, false, s), "hipMemcpyAsync D2H");
+  }
+  if (st == CFSEC_OK && verify && nlanes > 1) {
+    st = hip_status(hipEventRecord(ws->ev, lane[1]), "hipEventRecord");
+    if (st == CFSEC_OK) st = hip_status(hipStreamWaitEvent(lane[0], ws->ev, 0), "hipStreamWaitEvent");
+  }
+  if (st == CFSEC_OK && verify)
+    st = hip_status(hipMemcpyAsync(ws->hflags, ws->dflags, 4, hipMemcpyDeviceToHost, lane[0]), "hipMemcpyAsync D2H");
+  for (int l = 0; l < nlanes; ++l) {
+    const Status sync = hip_status(hipStreamSynchronize(lane[l]), "hipStreamSynchronize");
+    if (st == CFSEC_OK) st = sync;
+  }
   if (st == CFSEC_OK && verify && ok) *ok = ws->hflags[0] == 0;
   ctx_->release(ws);
   return st;

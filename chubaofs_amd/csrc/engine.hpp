@@ -39,6 +39,8 @@ class DeviceContext {
     uint32_t* hflags = nullptr;  // pinned host mirror
     size_t nflags = 0;
     hipStream_t stream = nullptr;
+    hipStream_t stream2 = nullptr;  // second lane of the chunked host pipeline
+    hipEvent_t ev = nullptr;        // orders stream2 after work enqueued on stream
   };
   // Check out a workspace with at least `bytes` of staging and `nflags` flag words.
   Status acquire(size_t bytes, size_t nflags, Workspace** out);
@@ -119,6 +121,15 @@ class RSEngine {
   Status run(const Matrix& rows, const std::vector<cfsec_shard*>& ins,
              const std::vector<cfsec_shard*>& outs, size_t S, int mem, hipStream_t stream,
              MatVecMode mode, bool* ok);
+
+  // Columns of a host-memory call per chunk (bytes per row) through the two-stream pipeline.
+  static constexpr size_t kHostChunk = 1 << 20;
+
+ private:
+  Status run_host(const Matrix& rows, const std::vector<cfsec_shard*>& ins,
+                  const std::vector<cfsec_shard*>& outs, size_t S, MatVecMode mode, bool* ok);
+
+ public:
 
  private:
   RSEngine() = default;

@@ -158,6 +158,14 @@ int cfsec_ec_verify(cfsec_ec* h, cfsec_shard* shards, int n, int mem, void* stre
  * shard indices of AZ idx into out (capacity out_cap) and their count into *count. */
 int cfsec_ec_shards_in_idc(const cfsec_ec* h, int idx, int* out, int out_cap, int* count);
 
+/* ---------------- pinned host memory ---------------- */
+/* Page-locked host memory for shard buffers (the hook is resourcepool.NewMemPoolWith,
+ * common/resourcepool/mempool.go:60, which ec.Buffer draws from, common/ec/buf.go:93-117).
+ * CFSEC_MEM_HOST calls on such buffers DMA straight to HBM instead of through the runtime's
+ * staging copies.  C memory: safe to hand to cgo. */
+int cfsec_host_alloc(size_t size, void** out);
+int cfsec_host_free(void* p);
+
 /* ---------------- shard CRC32 (access/stream_put.go:249-253) ---------------- */
 /* crc32.ChecksumIEEE of each device shard; out: host array of n uint32. Synchronous. */
 int cfsec_crc32_ieee_batch(uint8_t* const* ptrs, size_t shard_size, int n, uint32_t* out,
