@@ -84,35 +84,40 @@ __device__ __forceinline__ void st_tail(uint8_t* p, u32x4 v, size_t rem) {
     if ((size_t)i < rem) p[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
 }
 
-// Product tables for coefficient (c, r) at LDS slot c*MT + r (MT = output rows per block):
-//   tab01 = {T0[0..3], T0[4..7], T1[0..3], T1[4..7]},  tab2 = T2[0..3]
+// Product tables of one coefficient:
+//   t01 = {T0[0..3], T0[4..7], T1[0..3], T1[4..7]},  t2 = T2[0..3]
 // with T0[e] = coef*e, T1[e] = coef*(e<<3), T2[e] = coef*(e<<6).
+__device__ __forceinline__ void coef_tables(uint32_t coef, u32x4& t01, uint32_t& t2) {
+  uint32_t p[8];
+  p[0] = coef;
+#pragma unroll
+  for (int j = 1; j < 8; ++j) p[j] = gf_xtime(p[j - 1]);  // coef * 2^j
+  uint32_t t0lo = 0, t0hi = 0, t1lo = 0, t1hi = 0, tt2 = 0;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const uint32_t v0 = ((e & 1) ? p[0] : 0u) ^ ((e & 2) ? p[1] : 0u) ^ ((e & 4) ? p[2] : 0u);
+    const uint32_t v1 = ((e & 1) ? p[3] : 0u) ^ ((e & 2) ? p[4] : 0u) ^ ((e & 4) ? p[5] : 0u);
+    if (e < 4) {
+      const uint32_t v2 = ((e & 1) ? p[6] : 0u) ^ ((e & 2) ? p[7] : 0u);
+      t0lo |= v0 << (8 * e);
+      t1lo |= v1 << (8 * e);
+      tt2 |= v2 << (8 * e);
+    } else {
+      t0hi |= v0 << (8 * (e - 4));
+      t1hi |= v1 << (8 * (e - 4));
+    }
+  }
+  t01 = u32x4{t0lo, t0hi, t1lo, t1hi};
+  t2 = tt2;
+}
+
+// Product tables for coefficient (c, r) at LDS slot c*MT + r (MT = output rows per block).
 template <int MT>
 __device__ __forceinline__ void build_tables(int k, int m, const uint8_t* coef, u32x4* tab01, uint32_t* tab2) {
   for (int i = threadIdx.x; i < k * MT; i += (int)blockDim.x) {
     const int c = i / MT;
     const int r = i - c * MT;
-    uint32_t p[8];
-    p[0] = (r < m) ? coef[r * k + c] : 0u;
-#pragma unroll
-    for (int j = 1; j < 8; ++j) p[j] = gf_xtime(p[j - 1]);  // coef * 2^j
-    uint32_t t0lo = 0, t0hi = 0, t1lo = 0, t1hi = 0, t2 = 0;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const uint32_t v0 = ((e & 1) ? p[0] : 0u) ^ ((e & 2) ? p[1] : 0u) ^ ((e & 4) ? p[2] : 0u);
-      const uint32_t v1 = ((e & 1) ? p[3] : 0u) ^ ((e & 2) ? p[4] : 0u) ^ ((e & 4) ? p[5] : 0u);
-      if (e < 4) {
-        const uint32_t v2 = ((e & 1) ? p[6] : 0u) ^ ((e & 2) ? p[7] : 0u);
-        t0lo |= v0 << (8 * e);
-        t1lo |= v1 << (8 * e);
-        t2 |= v2 << (8 * e);
-      } else {
-        t0hi |= v0 << (8 * (e - 4));
-        t1hi |= v1 << (8 * (e - 4));
-      }
-    }
-    tab01[i] = u32x4{t0lo, t0hi, t1lo, t1hi};
-    tab2[i] = t2;
+    coef_tables((r < m) ? coef[r * k + c] : 0u, tab01[i], tab2[i]);
   }
 }
 

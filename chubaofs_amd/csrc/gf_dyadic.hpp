@@ -1,0 +1,298 @@
+// gf_dyadic.hpp -- GF(2^8) matrix x shard-vector products for matrices made of dyadic blocks.
+//
+// The parity rows of the Vandermonde-derived systematic matrix of klauspost/reedsolomon
+// (KRS/reedsolomon.go:220-244, evaluation points 0..n-1) have block structure: M[r][c] =
+// L(p_r) / ((p_r + p_c) L'(p_c)) is a scaled Cauchy form, and where the points of a block of B
+// rows and B columns are cosets of {0..B-1} (an additive subgroup of GF(2^8)) the scale is
+// constant on the block and 1/(p_r + p_c) depends on r ^ c only:  M[r0+i][c0+j] = h[i ^ j].
+// EC12P4, EC16P4 and EC16P20 parity are made of 4x4 dyadic blocks, EC6P6 / EC6P10 / EC10P4 of
+// 2x2 ones, and so are the decode matrices of coset-aligned erasures (EC12P4's worst case
+// {0,1,2,3} included).  A dyadic block needs fewer products:
+//   [a b; b a] [x; y] = [a(x+y) + (a+b)y ; b(x+y) + (a+b)y]            3 products instead of 4
+//   [A B; B A] [X; Y] = [A(X+Y) + (A+B)Y ; B(X+Y) + (A+B)Y]            on 2x2 blocks: 9 instead of 16
+// GF(2^8) arithmetic is exact, so the bytes are those of the plain product; the launcher checks
+// the structure on the actual coefficient matrix and takes these kernels only when it holds.
+//
+// Per 4x4 block and dword: multiplicands u = x0^x1^x2^x3, s = x1^x3, v = x2^x3, x3 (their
+// v_perm selectors cost what 4 input rows cost), then 27 v_perm_b32 + 19 three-input XORs for 4
+// outputs, against 48 + 24 for the plain tile (gf_device.hpp lane_tile_k).
+#pragma once
+#include "gf_device.hpp"
+
+namespace cfsec {
+namespace dev {
+
+template <int B>
+struct Dy;
+template <>
+struct Dy<2> {
+  static constexpr int NC = 3;  // a, b, a^b
+};
+template <>
+struct Dy<4> {
+  static constexpr int NC = 9;  // h0, h1, h0^h1, h2, h3, h2^h3, g0=h0^h2, g1=h1^h3, g0^g1
+};
+
+template <int B>
+__device__ __forceinline__ uint32_t dy_coef(const uint8_t* h, int q) {
+  if constexpr (B == 2) {
+    return q == 0 ? h[0] : q == 1 ? h[1] : (uint32_t)(h[0] ^ h[1]);
+  } else {
+    switch (q) {
+      case 0: return h[0];
+      case 1: return h[1];
+      case 2: return h[0] ^ h[1];
+      case 3: return h[2];
+      case 4: return h[3];
+      case 5: return h[2] ^ h[3];
+      case 6: return h[0] ^ h[2];
+      case 7: return h[1] ^ h[3];
+      default: return h[0] ^ h[1] ^ h[2] ^ h[3];
+    }
+  }
+}
+
+// Product tables of every derived coefficient: slot (rb*KB + cb)*NC + q for row block rb, column
+// block cb (coef: m x K row-major, first row of each block read).  Row blocks MB .. MBP-1 pad the
+// last wave's share with zero tables, so no wave indexes past the arrays.
+template <int K, int M, int B, int MBP>
+__device__ __forceinline__ void build_dy_tables(const uint8_t* coef, u32x4* tab01, uint32_t* tab2) {
+  constexpr int KB = K / B, MB = M / B, NC = Dy<B>::NC;
+  for (int i = threadIdx.x; i < MBP * KB * NC; i += (int)blockDim.x) {
+    const int q = i % NC, blk = i / NC, cb = blk % KB, rb = blk / KB;
+    coef_tables(rb < MB ? dy_coef<B>(coef + (rb * B) * K + cb * B, q) : 0u, tab01[i], tab2[i]);
+  }
+}
+
+struct Sel {
+  uint32_t s0[4], s1[4], s2[4];
+};
+
+__device__ __forceinline__ void selectors(const uint32_t (&x)[4], Sel& s) {
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    s.s0[w] = x[w] & 0x07070707u;
+    s.s1[w] = (x[w] >> 3) & 0x07070707u;
+    s.s2[w] = (x[w] >> 6) & 0x03030303u;
+  }
+}
+
+// The three partial lookups of coefficient q times the multiplicand whose selectors are s.
+struct Prod {
+  uint32_t a[4], b[4], c[4];
+};
+__device__ __forceinline__ void lookups(const u32x4 q, uint32_t t2, const Sel& s, Prod& p) {
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    p.a[w] = __builtin_amdgcn_perm(q.y, q.x, s.s0[w]);
+    p.b[w] = __builtin_amdgcn_perm(q.w, q.z, s.s1[w]);
+    p.c[w] = __builtin_amdgcn_perm(0u, t2, s.s2[w]);
+  }
+}
+
+__device__ __forceinline__ uint32_t x3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// B = 2, all row blocks of one column block: tq/t2p point at (rb=0, cb) slot 0; row blocks are
+// kb*NC slots apart.
+template <int MB>
+__device__ __forceinline__ void dy_col2(uint32_t (&acc)[2 * MB][4], const uint32_t (&x0)[4],
+                                        const uint32_t (&x1)[4], const u32x4* tq, const uint32_t* t2p,
+                                        int stride) {
+  uint32_t u[4];
+#pragma unroll
+  for (int w = 0; w < 4; ++w) u[w] = x0[w] ^ x1[w];
+  Sel su, sy;
+  selectors(u, su);
+  selectors(x1, sy);
+#pragma unroll
+  for (int rb = 0; rb < MB; ++rb) {
+    const u32x4* q = tq + rb * stride;
+    const uint32_t* t = t2p + rb * stride;
+    Prod pa, pb, pc;
+    lookups(q[0], t[0], su, pa);
+    lookups(q[1], t[1], su, pb);
+    lookups(q[2], t[2], sy, pc);
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const uint32_t c = x3(pc.a[w], pc.b[w], pc.c[w]);
+      acc[2 * rb][w] = x3(x3(acc[2 * rb][w], pa.a[w], pa.b[w]), pa.c[w], c);
+      acc[2 * rb + 1][w] = x3(x3(acc[2 * rb + 1][w], pb.a[w], pb.b[w]), pb.c[w], c);
+    }
+  }
+}
+
+// B = 4, all row blocks of one column block.
+template <int MB>
+__device__ __forceinline__ void dy_col4(uint32_t (&acc)[4 * MB][4], const uint32_t (&x0)[4],
+                                        const uint32_t (&x1)[4], const uint32_t (&x2)[4],
+                                        const uint32_t (&x3v)[4], const u32x4* tq, const uint32_t* t2p,
+                                        int stride) {
+  uint32_t u[4], s[4], v[4];
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    s[w] = x1[w] ^ x3v[w];
+    v[w] = x2[w] ^ x3v[w];
+    u[w] = x3(x0[w], x2[w], s[w]);  // x0^x1^x2^x3
+  }
+  Sel su, ss, sv, sy;
+#pragma unroll
+  for (int rb = 0; rb < MB; ++rb) {
+    const u32x4* q = tq + rb * stride;
+    const uint32_t* t = t2p + rb * stride;
+    uint32_t ps[4], ps2[4], c0[4], c1[4];
+    {
+      Prod p;
+      selectors(s, ss);
+      lookups(q[2], t[2], ss, p);  // (h0^h1) s
+#pragma unroll
+      for (int w = 0; w < 4; ++w) ps[w] = x3(p.a[w], p.b[w], p.c[w]);
+      lookups(q[5], t[5], ss, p);  // (h2^h3) s
+#pragma unroll
+      for (int w = 0; w < 4; ++w) ps2[w] = x3(p.a[w], p.b[w], p.c[w]);
+      asm volatile("" : "+v"(ps[0]), "+v"(ps[1]), "+v"(ps[2]), "+v"(ps[3]), "+v"(ps2[0]), "+v"(ps2[1]), "+v"(ps2[2]), "+v"(ps2[3]));
+      __builtin_amdgcn_sched_barrier(0);
+      Prod py, p6, p7;
+      selectors(x3v, sy);
+      selectors(v, sv);
+      lookups(q[8], t[8], sy, py);  // (g0^g1) x3
+      lookups(q[6], t[6], sv, p6);  // g0 v
+      lookups(q[7], t[7], sv, p7);  // g1 v
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const uint32_t qy = x3(py.a[w], py.b[w], py.c[w]);
+        c0[w] = x3(p6.a[w], p6.b[w], p6.c[w]) ^ qy;
+        c1[w] = x3(p7.a[w], p7.b[w], p7.c[w]) ^ qy;
+      }
+    }
+    asm volatile("" : "+v"(c0[0]), "+v"(c0[1]), "+v"(c0[2]), "+v"(c0[3]), "+v"(c1[0]), "+v"(c1[1]), "+v"(c1[2]), "+v"(c1[3]));
+    __builtin_amdgcn_sched_barrier(0);
+    selectors(u, su);
+    // one output at a time: out_j ^= h_j u ^ (shared s term) ^ (shared x3/v term)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      Prod p;
+      const int qi = j < 2 ? j : j + 1;  // h0, h1, h2, h3 live at slots 0, 1, 3, 4
+      lookups(q[qi], t[qi], su, p);
+      const uint32_t* sh = j < 2 ? ps : ps2;
+      const uint32_t* cc = (j & 1) ? c1 : c0;
+#pragma unroll
+      for (int w = 0; w < 4; ++w)
+        acc[4 * rb + j][w] = x3(x3(acc[4 * rb + j][w], p.a[w], p.b[w]), x3(p.c[w], sh[w], cc[w]), 0u);
+      asm volatile("" : "+v"(acc[4 * rb + j][0]), "+v"(acc[4 * rb + j][1]), "+v"(acc[4 * rb + j][2]),
+                   "+v"(acc[4 * rb + j][3]));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
+// Waves per column chunk (OS) and column chunks per workgroup (CW) of the dyadic kernels: each
+// wave owns RBW row blocks (4x4 blocks: one, so a wave's accumulators + the block's selectors
+// stay near 120 VGPRs; 2x2 blocks: two), and a workgroup holds at most 320 threads.
+template <int M, int B>
+struct DyShape {
+  static constexpr int MB = M / B;
+  static constexpr int RBW = B == 4 ? 1 : 2;
+  static constexpr int OS = (MB + RBW - 1) / RBW;
+  static constexpr int CW = OS >= 4 ? 1 : 4 / OS;
+  static constexpr int kThreadsPerWg = 64 * OS * CW;
+  static constexpr int kTileBytes = 64 * kLaneBytes * CW;
+};
+
+// Kernel body: compile-time K inputs, M outputs, dyadic blocks of B; grid (tiles, stripes),
+// DyShape threads; wave w handles column chunk w / OS and row blocks (w % OS) * RBW .. +RBW,
+// one 16-byte chunk per lane per row, column blocks loaded one block ahead.
+template <int K, int M, int B, MatVecMode MODE>
+__device__ __forceinline__ void matvec_dy(const GfArgs& a) {
+  static_assert(K % B == 0 && M % B == 0 && (B == 2 || B == 4), "dyadic shape");
+  using Sh = DyShape<M, B>;
+  constexpr int KB = K / B, MB = M / B, NC = Dy<B>::NC, RBW = Sh::RBW, MW = RBW * B;
+  constexpr int MBP = Sh::OS * RBW;  // row blocks incl. the last wave's padding
+  constexpr bool kVer = MODE == MatVecMode::kVerify;
+  __shared__ u32x4 tab01[MBP * KB * NC];
+  __shared__ uint32_t tab2[MBP * KB * NC];
+  build_dy_tables<K, M, B, MBP>(a.coef, tab01, tab2);
+  __syncthreads();
+
+  const int wave = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+  const int rb0 = (wave % Sh::OS) * RBW;  // first row block of this wave
+  const int cw = wave / Sh::OS;
+  if (rb0 >= MB) return;  // padding wave (no barrier follows)
+  const int nrb = MB - rb0 < RBW ? MB - rb0 : RBW;
+  const uint32_t stripe = blockIdx.y, tile = blockIdx.x;
+  const size_t ts = a.sstride ? 0 : (size_t)stripe;
+  const int64_t sbase = (int64_t)stripe * a.sstride;
+  const uint32_t off = tile * (uint32_t)Sh::kTileBytes + (uint32_t)(cw * 64 + lane) * kLaneBytes;
+  const uint8_t* row[K + MW];
+#pragma unroll
+  for (int c = 0; c < K; ++c) row[c] = a.ptr[ts * K + c] + sbase;
+#pragma unroll
+  for (int r = 0; r < MW; ++r) {
+    const int o = rb0 * B + (r < nrb * B ? r : 0);
+    row[K + r] = a.ptr[(size_t)a.tab * K + ts * M + o] + sbase;
+  }
+  __builtin_amdgcn_sched_barrier(0);
+
+  uint32_t acc[MW][4];
+#pragma unroll
+  for (int r = 0; r < MW; ++r)
+#pragma unroll
+    for (int w = 0; w < 4; ++w) acc[r][w] = 0u;
+  const auto pin = [&]() {
+#pragma unroll
+    for (int r = 0; r < MW; ++r)
+      asm volatile("" : "+v"(acc[r][0]), "+v"(acc[r][1]), "+v"(acc[r][2]), "+v"(acc[r][3]));
+  };
+  const bool full = (uint64_t)off + kLaneBytes <= a.len;
+  const size_t rem = off < a.len ? (size_t)(a.len - off) : 0;
+  uint32_t diff = 0;
+  if (full || rem) {
+    uint32_t x[K][4];
+    const auto load = [&](int c) {
+      const u32x4 v = full ? ld16<true>(row[c] + off) : ld_tail(row[c] + off, rem);
+      x[c][0] = v.x;
+      x[c][1] = v.y;
+      x[c][2] = v.z;
+      x[c][3] = v.w;
+    };
+#pragma unroll
+    for (int c = 0; c < B; ++c) load(c);
+    const u32x4* tq = tab01 + rb0 * KB * NC;
+    const uint32_t* tt = tab2 + rb0 * KB * NC;
+#pragma unroll
+    for (int cb = 0; cb < KB; ++cb) {
+      if (cb + 1 < KB)
+#pragma unroll
+        for (int c = 0; c < B; ++c) load((cb + 1) * B + c);
+      __builtin_amdgcn_sched_barrier(0);
+      const int c0 = cb * B;
+      if constexpr (B == 2)
+        dy_col2<RBW>(acc, x[c0], x[c0 + 1], tq + cb * NC, tt + cb * NC, KB * NC);
+      else
+        dy_col4<RBW>(acc, x[c0], x[c0 + 1], x[c0 + 2], x[c0 + 3], tq + cb * NC, tt + cb * NC, KB * NC);
+      pin();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int r = 0; r < MW; ++r) {
+      if (r >= nrb * B) continue;
+      uint8_t* p = const_cast<uint8_t*>(row[K + r]) + off;
+      const u32x4 v = u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
+      if constexpr (kVer) {
+        const u32x4 d = v ^ (full ? ld16<true>(p) : ld_tail(p, rem));
+        diff |= d.x | d.y | d.z | d.w;
+      } else if (full) {
+        st16<true>(p, v);
+      } else {
+        st_tail(p, v, rem);
+      }
+    }
+  }
+  if constexpr (kVer) {
+    if (diff) atomicOr(a.flags + stripe, 1u);
+  }
+}
+
+}  // namespace dev
+}  // namespace cfsec

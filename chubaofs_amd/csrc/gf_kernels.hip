@@ -35,6 +35,7 @@
 //                tools/gf_variants.hip -- store/accum 256-thread, 1 chunk per lane, one row at a
 //                time; verify 128-thread, 2 chunks per lane, rows loaded in pairs
 #include <algorithm>
+#include <vector>
 
 #include "gf_device.hpp"
 #include "gf_launch.hpp"
@@ -132,6 +133,15 @@ hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
       const bool fixed = fixed_k(kc) && kc == job.k && mode != MatVecMode::kAccum &&
                          job.len <= 0xFFFFFFFFull - 4096;  // 32-bit lane offsets
       const int threads = (!fixed && verify && sh.OS == 1) ? 128 : 256;
+      // 4-output matrices of 4x4 dyadic blocks (EC12P4 / EC16P4 encode, coset-aligned reconstructs
+      // such as EC12P4's worst case) take the reduced-product kernel
+      int dyB = 0;
+      if (fixed && r0 == 0 && mc == job.m) {
+        std::vector<uint8_t> sub((size_t)mc * kc);
+        for (int r = 0; r < mc; ++r)
+          for (int c = 0; c < kc; ++c) sub[(size_t)r * kc + c] = job.coef[(size_t)r * job.k + c];
+        dyB = dyadic_block(sub.data(), mc, kc);
+      }
       const size_t tile =
           size_t(threads / sh.OS) * dev::kLaneBytes * ((verify && !fixed) ? kVerifyW : kStoreW);
       const size_t tiles = (job.len + tile - 1) / tile;
@@ -165,6 +175,12 @@ hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
         }
         const dim3 grid((unsigned)(tiles * ns));
         hipError_t e;
+        if (fixed && dyB) {
+          e = kc == 12 ? launch_dy<12>(mc, dyB, mode, a, (unsigned)ns, stream)
+                       : launch_dy<16>(mc, dyB, mode, a, (unsigned)ns, stream);
+          if (e != hipSuccess) return e;
+          continue;
+        }
         if (fixed) {
           const dim3 grid2((unsigned)tiles, (unsigned)ns);
           e = verify ? launch_fixed<MatVecMode::kVerify>(kc, sh, a, grid2, stream)

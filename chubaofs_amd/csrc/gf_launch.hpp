@@ -32,6 +32,28 @@ inline bool fixed_k(int k) { return k == 6 || k == 8 || k == 12 || k == 16 || k 
 template <int K, MatVecMode MODE>
 hipError_t launch_k(Shape sh, const dev::GfArgs& a, dim3 grid, hipStream_t st);
 
+// Dyadic-block kernels (gf_dyadic.hpp) for an m x k matrix whose B x B blocks satisfy
+// M[r0+i][c0+j] = M[r0][c0 + (i ^ j)]; specialised in gf_dy_k<K>.hip for K in {12, 16}, B = 4, m = 4.
+template <int K>
+hipError_t launch_dy(int m, int B, MatVecMode mode, const dev::GfArgs& a, unsigned ns, hipStream_t st);
+template <>
+hipError_t launch_dy<12>(int, int, MatVecMode, const dev::GfArgs&, unsigned, hipStream_t);
+template <>
+hipError_t launch_dy<16>(int, int, MatVecMode, const dev::GfArgs&, unsigned, hipStream_t);
+
+// The dyadic block size a shipped kernel can use for this matrix (4), or 0.
+inline int dyadic_block(const uint8_t* coef, int m, int k) {
+  int B = 0;
+  if ((k == 12 || k == 16) && m == 4) B = 4;
+  if (!B) return 0;
+  for (int r0 = 0; r0 < m; r0 += B)
+    for (int c0 = 0; c0 < k; c0 += B)
+      for (int i = 0; i < B; ++i)
+        for (int j = 0; j < B; ++j)
+          if (coef[(size_t)(r0 + i) * k + c0 + j] != coef[(size_t)r0 * k + c0 + (i ^ j)]) return 0;
+  return B;
+}
+
 #define CFSEC_EXTERN_K(K)                                                                       \
   extern template hipError_t launch_k<K, MatVecMode::kStore>(Shape, const dev::GfArgs&, dim3, \
                                                              hipStream_t);                    \

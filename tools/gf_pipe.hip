@@ -18,6 +18,7 @@
 
 #include "gf256.hpp"
 #include "gf_device.hpp"
+#include "gf_dyadic.hpp"
 
 using namespace cfsec;
 using dev::GfArgs;
@@ -225,6 +226,12 @@ __global__ __launch_bounds__(256) void kfix(const GfArgs a) {
   dev::matvec_k<K, M, MatVecMode::kStore, D, OS, NTL, NTS, PAIR>(a);
 }
 
+
+template <int K, int M, int B>
+__global__ __launch_bounds__(256) void kdy(const GfArgs a) {
+  dev::matvec_dy<K, M, B, MatVecMode::kStore>(a);
+}
+
 __global__ __launch_bounds__(256) void kcopy(const u32x4* __restrict__ src, u32x4* __restrict__ dst, size_t n) {
   const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
   if (i < n) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
@@ -319,12 +326,11 @@ int main(int argc, char** argv) {
   std::vector<Variant> vs = {
       {"ctl (runtime k)", kctl, true},
       {"fix D2 pair", kfix<2, true, true, true>, true, -4},
-      {"fix D2 single", kfix<2, true, true, false>, true, -4},
-      {"fix D4 pair", kfix<4, true, true, true>, true, -4},
-      {"fix D4 single", kfix<4, true, true, false>, true, -4},
+      {"dyadic B4", kdy<12, 4, 4>, true, -4},
       {"fix D2 pair (2)", kfix<2, true, true, true>, true, -4},
-      {"fix D2 single (2)", kfix<2, true, true, false>, true, -4},
+      {"dyadic B4 (2)", kdy<12, 4, 4>, true, -4},
       {"pat2d st plain", kpatp<0>, false, -4},
+      {"pat2d st nt", kpatp<1>, false, -4},
       {"copy (float4)", nullptr, false},
   };
   uint32_t* flags = nullptr;
