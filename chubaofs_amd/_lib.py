@@ -91,6 +91,7 @@ SIGNATURES = {
     "cfsec_rs_encode_batch": ([_V, _V, _S, _I, _V], _I),
     "cfsec_rs_verify_batch": ([_V, _V, _S, _I, _V, _V], _I),
     "cfsec_rs_reconstruct_batch": ([_V, _V, _S, _I, _V, _I, _I, _V], _I),
+    "cfsec_rs_encode_crc": ([_V, P_SHARD, _I, _I, _V, _V], _I),
     "cfsec_rs_encode_crc_batch": ([_V, _V, _S, _I, _V, _V], _I),
     "cfsec_rs_reconstruct_crc_batch": ([_V, _V, _S, _I, _V, _I, _I, _V, _V], _I),
     "cfsec_codemode_tactic": ([_I, _P(TacticC)], _I),

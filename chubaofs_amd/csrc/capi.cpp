@@ -181,6 +181,11 @@ int cfsec_rs_reconstruct_batch(cfsec_rs* h, uint8_t* const* ptrs, size_t shard_s
   });
 }
 
+int cfsec_rs_encode_crc(cfsec_rs* h, cfsec_shard* shards, int n, int mem, void* stream, uint32_t* crcs) {
+  if (!h) return CFSEC_ERR_INVALID_ARG;
+  return guarded([&] { return h->e->encode_crc(shards, n, mem, as_stream(stream), crcs); });
+}
+
 int cfsec_rs_encode_crc_batch(cfsec_rs* h, uint8_t* const* ptrs, size_t shard_size, int nstripes,
                               uint32_t* crcs, void* stream) {
   if (!h) return CFSEC_ERR_INVALID_ARG;

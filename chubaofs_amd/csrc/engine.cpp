@@ -225,6 +225,9 @@ Status RSEngine::create(int k, int m, int device, std::unique_ptr<RSEngine>* out
   return CFSEC_OK;
 }
 
+static Status matvec_with_crc(const MatVecJob& job, uint8_t* const* ptrs, int total, const std::vector<int>& slot,
+                              size_t S, uint32_t* crcs, hipStream_t stream);
+
 namespace {
 // The device address of page-locked host memory (hipHostMalloc / cfsec_host_alloc); false for
 // pageable memory.
@@ -471,6 +474,71 @@ Status RSEngine::encode(cfsec_shard* shards, int n, int mem, hipStream_t stream)
   for (int i = 0; i < k_; ++i) ins.push_back(&shards[i]);
   for (int i = k_; i < n; ++i) outs.push_back(&shards[i]);
   return run(parity_, ins, outs, S, mem, stream, MatVecMode::kStore, nullptr);
+}
+
+Status RSEngine::encode_crc(cfsec_shard* shards, int n, int mem, hipStream_t stream, uint32_t* crcs) {
+  if (!shards || n != total()) return CFSEC_ERR_TOO_FEW_SHARDS;
+  if (!crcs) return CFSEC_ERR_INVALID_ARG;
+  size_t S = 0;
+  Status st = check_shards(shards, n, false, &S);
+  if (st != CFSEC_OK) return st;
+  if (!ctx_) {
+    set_last_error("no HIP device available to the cfsec engine");
+    return CFSEC_ERR_DEVICE;
+  }
+  if (mem != CFSEC_MEM_HOST && mem != CFSEC_MEM_DEVICE) return CFSEC_ERR_INVALID_ARG;
+  for (int i = 0; i < n; ++i)
+    if (!shards[i].data) return CFSEC_ERR_INVALID_ARG;
+  DeviceGuard g(ctx_->device());
+  if (!g.ok()) return hip_status(hipErrorInvalidDevice, "hipSetDevice");
+  // device addresses of the shards: device memory as is, pinned host pages aliased (zero-copy),
+  // pageable host memory staged whole through the workspace
+  std::vector<uint8_t*> dptr(n);
+  bool staged = false;
+  if (mem == CFSEC_MEM_HOST)
+    for (int i = 0; i < n && !staged; ++i) staged = !device_alias(shards[i].data, &dptr[i]);
+  else
+    for (int i = 0; i < n; ++i) dptr[i] = shards[i].data;
+  const size_t slot = align_up(S, kSlotAlign);
+  DeviceContext::Workspace* ws = nullptr;
+  st = ctx_->acquire(staged ? slot * n : 0, (size_t)n, &ws);
+  if (st != CFSEC_OK) return st;
+  hipStream_t s = (mem == CFSEC_MEM_HOST || !stream) ? ws->stream : stream;
+  if (staged)
+    for (int i = 0; i < n; ++i) {
+      dptr[i] = ws->dbuf + slot * i;
+      if (i < k_ && st == CFSEC_OK)
+        st = hip_status(hipMemcpyAsync(dptr[i], shards[i].data, S, hipMemcpyHostToDevice, s), "hipMemcpyAsync H2D");
+    }
+  if (st == CFSEC_OK && m_ > 0) {
+    MatVecJob job;
+    job.k = k_;
+    job.m = m_;
+    job.coef = parity_.v.data();
+    job.len = S;
+    job.nstripes = 1;
+    std::vector<const uint8_t*> in(dptr.begin(), dptr.begin() + k_);
+    job.in = in.data();
+    job.out = dptr.data() + k_;
+    std::vector<int> slots(n);
+    for (int i = 0; i < n; ++i) slots[i] = i;
+    st = matvec_with_crc(job, dptr.data(), n, slots, S, ws->dflags, s);
+  } else if (st == CFSEC_OK) {
+    st = hip_status(hipMemsetAsync(ws->dflags, 0, 4 * (size_t)n, s), "hipMemsetAsync");
+    std::vector<const uint8_t*> p(dptr.begin(), dptr.end());
+    if (st == CFSEC_OK)
+      st = hip_status(launch_crc32_to(p.data(), S, n, ws->dflags, nullptr, crc32_shift_ones(S), s), "launch_crc32_to");
+  }
+  if (st == CFSEC_OK && staged)
+    for (int r = k_; r < n && st == CFSEC_OK; ++r)
+      st = hip_status(hipMemcpyAsync(shards[r].data, dptr[r], S, hipMemcpyDeviceToHost, s), "hipMemcpyAsync D2H");
+  if (st == CFSEC_OK)
+    st = hip_status(hipMemcpyAsync(ws->hflags, ws->dflags, 4 * (size_t)n, hipMemcpyDeviceToHost, s), "hipMemcpyAsync D2H");
+  const Status sync = hip_status(hipStreamSynchronize(s), "hipStreamSynchronize");
+  if (st == CFSEC_OK) st = sync;
+  if (st == CFSEC_OK) std::memcpy(crcs, ws->hflags, 4 * (size_t)n);
+  ctx_->release(ws);
+  return st;
 }
 
 Status RSEngine::verify(cfsec_shard* shards, int n, int mem, hipStream_t stream, bool* ok) {

@@ -95,6 +95,8 @@ class RSEngine {
   const Matrix& matrix() const { return mat_; }
 
   Status encode(cfsec_shard* shards, int n, int mem, hipStream_t stream);
+  // Encode + crc32.ChecksumIEEE of every shard into host crcs[n], one fused pass.
+  Status encode_crc(cfsec_shard* shards, int n, int mem, hipStream_t stream, uint32_t* crcs);
   Status verify(cfsec_shard* shards, int n, int mem, hipStream_t stream, bool* ok);
   Status reconstruct(cfsec_shard* shards, int n, bool data_only, int mem, hipStream_t stream);
   Status split(uint8_t* data, size_t len, size_t cap, cfsec_shard* out, uint8_t* pad,

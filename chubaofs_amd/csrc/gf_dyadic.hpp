@@ -203,7 +203,7 @@ struct DyShape {
 // Kernel body: compile-time K inputs, M outputs, dyadic blocks of B; grid (tiles, stripes),
 // DyShape threads; wave w handles column chunk w / OS and row blocks (w % OS) * RBW .. +RBW,
 // one 16-byte chunk per lane per row, column blocks loaded one block ahead.
-template <int K, int M, int B, MatVecMode MODE>
+template <int K, int M, int B, MatVecMode MODE, bool NTS = true, bool NTL = true>
 __device__ __forceinline__ void matvec_dy(const GfArgs& a) {
   static_assert(K % B == 0 && M % B == 0 && (B == 2 || B == 4), "dyadic shape");
   using Sh = DyShape<M, B>;
@@ -250,7 +250,7 @@ __device__ __forceinline__ void matvec_dy(const GfArgs& a) {
   if (full || rem) {
     uint32_t x[K][4];
     const auto load = [&](int c) {
-      const u32x4 v = full ? ld16<true>(row[c] + off) : ld_tail(row[c] + off, rem);
+      const u32x4 v = full ? ld16<NTL>(row[c] + off) : ld_tail(row[c] + off, rem);
       x[c][0] = v.x;
       x[c][1] = v.y;
       x[c][2] = v.z;
@@ -283,7 +283,7 @@ __device__ __forceinline__ void matvec_dy(const GfArgs& a) {
         const u32x4 d = v ^ (full ? ld16<true>(p) : ld_tail(p, rem));
         diff |= d.x | d.y | d.z | d.w;
       } else if (full) {
-        st16<true>(p, v);
+        st16<NTS>(p, v);
       } else {
         st_tail(p, v, rem);
       }

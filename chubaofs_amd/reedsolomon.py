@@ -40,6 +40,14 @@ class ReedSolomon:
         m = Marshal(shards)
         _lib.check(self._L.cfsec_rs_encode(self._h, m.ptr(), m.n, m.mem, stream_ptr(stream)))
 
+    def EncodeCRC(self, shards, stream=None):
+        """Encode + crc32.ChecksumIEEE of every shard, fused (cfsec_rs_encode_crc); returns the
+        n checksums (what access computes per shard after Encode, stream_put.go:249-253)."""
+        m = Marshal(shards)
+        out = (ctypes.c_uint32 * max(m.n, 1))()
+        _lib.check(self._L.cfsec_rs_encode_crc(self._h, m.ptr(), m.n, m.mem, stream_ptr(stream), out))
+        return [int(out[i]) for i in range(m.n)]
+
     def Verify(self, shards, stream=None) -> bool:
         m = Marshal(shards)
         ok = ctypes.c_int(0)

@@ -137,6 +137,45 @@ func (e *Engine) Encode(shards [][]byte) error {
 	return toError(C.cfsec_rs_encode(e.h, v.ptr(), C.int(v.n), C.CFSEC_MEM_HOST, nil))
 }
 
+// EncodeCRC is Encode followed by crc32.ChecksumIEEE of every shard -- what access computes
+// right after encoding (blobstore/access/stream_put.go:249-253) -- in one fused GPU pass.
+func (e *Engine) EncodeCRC(shards [][]byte) ([]uint32, error) {
+	v := newShardVec(shards)
+	defer v.free()
+	crcs := make([]uint32, v.n)
+	if v.n == 0 {
+		return crcs, toError(C.cfsec_rs_encode(e.h, v.ptr(), 0, C.CFSEC_MEM_HOST, nil))
+	}
+	var pin runtime.Pinner
+	pin.Pin(&crcs[0])
+	defer pin.Unpin()
+	err := toError(C.cfsec_rs_encode_crc(e.h, v.ptr(), C.int(v.n), C.CFSEC_MEM_HOST, nil,
+		(*C.uint32_t)(unsafe.Pointer(&crcs[0]))))
+	return crcs, err
+}
+
+// HostAlloc returns size bytes of page-locked C memory (cfsec_host_alloc) as a byte slice: the
+// allocation hook for resourcepool.NewMemPoolWith (common/resourcepool/mempool.go:60), so
+// ec.Buffer shards are coded in place over PCIe.  Release it with HostFree.
+func HostAlloc(size int) ([]byte, error) {
+	if size <= 0 {
+		return nil, nil
+	}
+	var p unsafe.Pointer
+	if err := toError(C.cfsec_host_alloc(C.size_t(size), &p)); err != nil {
+		return nil, err
+	}
+	return unsafe.Slice((*byte)(p), size), nil
+}
+
+// HostFree releases a slice from HostAlloc.
+func HostFree(b []byte) error {
+	if cap(b) == 0 {
+		return nil
+	}
+	return toError(C.cfsec_host_free(unsafe.Pointer(unsafe.SliceData(b[:1]))))
+}
+
 func (e *Engine) Verify(shards [][]byte) (bool, error) {
 	v := newShardVec(shards)
 	defer v.free()

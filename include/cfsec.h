@@ -99,6 +99,10 @@ int cfsec_rs_matrix(const cfsec_rs* h, uint8_t* out, size_t out_len);
 
 /* Encode -- KRS/reedsolomon.go:609-625 */
 int cfsec_rs_encode(cfsec_rs* h, cfsec_shard* shards, int n, int mem, void* stream);
+/* Encode followed by crc32.ChecksumIEEE of every shard (access/stream_put.go:125-143 then
+ * :249-253) in one fused pass: crcs is a host array of n words.  Host memory from
+ * cfsec_host_alloc is coded in place over PCIe; other host memory is staged through HBM. */
+int cfsec_rs_encode_crc(cfsec_rs* h, cfsec_shard* shards, int n, int mem, void* stream, uint32_t* crcs);
 /* Verify -- KRS/reedsolomon.go:770-784; *ok = 1 when every parity shard matches. */
 int cfsec_rs_verify(cfsec_rs* h, cfsec_shard* shards, int n, int mem, void* stream, int* ok);
 /* Reconstruct / ReconstructData -- KRS/reedsolomon.go:1377-1552 */

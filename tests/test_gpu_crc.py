@@ -150,3 +150,28 @@ def test_standalone_crc_many_shards(rs, layout, n, S):
         dev = [torch.from_numpy(a).cuda() for a in arrs]
         ptrs = [t.data_ptr() for t in dev]
     assert rs.crc32_ieee_batch(ptrs, S) == [crc(a) for a in arrs]
+
+
+@pytest.mark.parametrize("memory", ["pageable", "pinned", "device"])
+@pytest.mark.parametrize("k,m,S", [(12, 4, 5592406), (12, 4, 17), (6, 6, 174763), (16, 20, 4097), (8, 1, 65536)])
+def test_encode_crc_single_call(rs, memory, k, m, S):
+    """cfsec_rs_encode_crc: the access Put path's Encode + per-shard ChecksumIEEE in one call, for
+    Go-side host buffers (pageable or from cfsec_host_alloc) and device shards."""
+    from chubaofs_amd import _lib
+    r = np.random.default_rng(S + k)
+    want = [r.integers(0, 256, S, dtype=np.uint8) for _ in range(k)] + [np.zeros(S, np.uint8) for _ in range(m)]
+    assert O.encode(k, m, want) == 0
+    if memory == "device":
+        sh = [torch.from_numpy(w.copy()).cuda() for w in want]
+        for p in sh[k:]:
+            p.zero_()
+    else:
+        buf = _lib.pinned_empty((k + m) * S) if memory == "pinned" else np.zeros((k + m) * S, np.uint8)
+        sh = [buf[i * S:(i + 1) * S] for i in range(k + m)]
+        for i in range(k):
+            sh[i][:] = want[i]
+    words = rs.New(k, m).EncodeCRC(sh)
+    got = [s.cpu().numpy() if hasattr(s, "cpu") else s for s in sh]
+    for i in range(k + m):
+        assert np.array_equal(got[i], want[i]), i
+        assert words[i] == crc(want[i]), i

@@ -227,9 +227,9 @@ __global__ __launch_bounds__(256) void kfix(const GfArgs a) {
 }
 
 
-template <int K, int M, int B>
+template <int K, int M, int B, bool NTS = true, bool NTL = true>
 __global__ __launch_bounds__(256) void kdy(const GfArgs a) {
-  dev::matvec_dy<K, M, B, MatVecMode::kStore>(a);
+  dev::matvec_dy<K, M, B, MatVecMode::kStore, NTS, NTL>(a);
 }
 
 __global__ __launch_bounds__(256) void kcopy(const u32x4* __restrict__ src, u32x4* __restrict__ dst, size_t n) {
@@ -325,13 +325,14 @@ int main(int argc, char** argv) {
 
   std::vector<Variant> vs = {
       {"ctl (runtime k)", kctl, true},
-      {"fix D2 pair", kfix<2, true, true, true>, true, -4},
       {"dyadic B4", kdy<12, 4, 4>, true, -4},
-      {"fix D2 pair (2)", kfix<2, true, true, true>, true, -4},
+      {"dyadic B4 plainS", kdy<12, 4, 4, false>, true, -4},
+      {"dyadic B4 plainL", kdy<12, 4, 4, true, false>, true, -4},
+      {"dyadic B4 plain LS", kdy<12, 4, 4, false, false>, true, -4},
       {"dyadic B4 (2)", kdy<12, 4, 4>, true, -4},
+      {"dyadic B4 plainS (2)", kdy<12, 4, 4, false>, true, -4},
       {"pat2d st plain", kpatp<0>, false, -4},
       {"pat2d st nt", kpatp<1>, false, -4},
-      {"copy (float4)", nullptr, false},
   };
   uint32_t* flags = nullptr;
   CK(hipMalloc(&flags, 64));
