@@ -19,18 +19,26 @@ hipError_t launch_dy_one(const dev::GfArgs& a, unsigned ns, hipStream_t st) {
   return hipGetLastError();
 }
 
+// Launch the kernel for output count m, one of Ms.
+template <int K, int B, MatVecMode MODE, int... Ms>
+hipError_t launch_dy_m(int m, const dev::GfArgs& a, unsigned ns, hipStream_t st) {
+  hipError_t e = hipErrorInvalidValue;
+  (void)((m == Ms ? (e = launch_dy_one<K, Ms, B, MODE>(a, ns, st), true) : false) || ...);
+  return e;
+}
+
 }  // namespace cfsec
 
-// K with 4x4 blocks, 4 outputs (one wave per column chunk).  Wider outputs (EC16P20) and the 2x2
-// kernels are slower than the plain tile on MI355X (shape sweep: the multi-wave split halves the
-// occupancy at ~120 VGPRs), so only this shape ships.
-#define CFSEC_DY_INSTANTIATE_B4(K)                                                                  \
+// launch_dy<K> for block size BV and the output counts listed after it (dyadic_shape in
+// gf_launch.hpp must list the same ones).
+#define CFSEC_DY_INSTANTIATE(K, BV, ...)                                                            \
   namespace cfsec {                                                                                 \
   template <>                                                                                       \
   hipError_t launch_dy<K>(int m, int B, MatVecMode mode, const dev::GfArgs& a, unsigned ns,         \
                           hipStream_t st) {                                                         \
-    if (B != 4 || m != 4) return hipErrorInvalidValue;                                              \
-    return mode == MatVecMode::kVerify ? launch_dy_one<K, 4, 4, MatVecMode::kVerify>(a, ns, st)     \
-                                       : launch_dy_one<K, 4, 4, MatVecMode::kStore>(a, ns, st);     \
+    if (B != BV || dyadic_shape(K, m) != BV) return hipErrorInvalidValue;                           \
+    return mode == MatVecMode::kVerify                                                              \
+               ? launch_dy_m<K, BV, MatVecMode::kVerify, __VA_ARGS__>(m, a, ns, st)                 \
+               : launch_dy_m<K, BV, MatVecMode::kStore, __VA_ARGS__>(m, a, ns, st);                 \
   }                                                                                                 \
   }

@@ -1,4 +1,5 @@
-// gf_dy_k12.hip -- 4x4-dyadic kernels for k = 12 (EC12P4); see gf_dyadic.hpp.
+// gf_dy_k12.hip -- 4x4-dyadic kernels for k = 12 (EC12P4 encode and coset-aligned repairs); see
+// gf_dyadic.hpp.
 #include "gf_dy_fixed.hpp"
 
-CFSEC_DY_INSTANTIATE_B4(12)
+CFSEC_DY_INSTANTIATE(12, 4, 4, 8, 12)

@@ -188,12 +188,13 @@ __device__ __forceinline__ void dy_col4(uint32_t (&acc)[4 * MB][4], const uint32
 }
 
 // Waves per column chunk (OS) and column chunks per workgroup (CW) of the dyadic kernels: each
-// wave owns RBW row blocks (4x4 blocks: one, so a wave's accumulators + the block's selectors
-// stay near 120 VGPRs; 2x2 blocks: two), and a workgroup holds at most 320 threads.
-template <int M, int B>
+// wave owns RBW row blocks.  The shipped kernels keep all row blocks in one wave (RBW = MB, OS = 1):
+// splitting them over waves re-reads every input once per wave and lost 25 % on EC16P20 even
+// though one wave holding 20 accumulators runs at 1-2 waves per SIMD (tools/gf_dy_probe.hip).
+template <int M, int B, int RBW_ = 64>
 struct DyShape {
   static constexpr int MB = M / B;
-  static constexpr int RBW = B == 4 ? 1 : 2;
+  static constexpr int RBW = RBW_ < MB ? RBW_ : MB;
   static constexpr int OS = (MB + RBW - 1) / RBW;
   static constexpr int CW = OS >= 4 ? 1 : 4 / OS;
   static constexpr int kThreadsPerWg = 64 * OS * CW;
@@ -203,10 +204,10 @@ struct DyShape {
 // Kernel body: compile-time K inputs, M outputs, dyadic blocks of B; grid (tiles, stripes),
 // DyShape threads; wave w handles column chunk w / OS and row blocks (w % OS) * RBW .. +RBW,
 // one 16-byte chunk per lane per row, column blocks loaded one block ahead.
-template <int K, int M, int B, MatVecMode MODE, bool NTS = true, bool NTL = true>
+template <int K, int M, int B, MatVecMode MODE, bool NTS = true, bool NTL = true, int RBW_ = 64>
 __device__ __forceinline__ void matvec_dy(const GfArgs& a) {
   static_assert(K % B == 0 && M % B == 0 && (B == 2 || B == 4), "dyadic shape");
-  using Sh = DyShape<M, B>;
+  using Sh = DyShape<M, B, RBW_>;
   constexpr int KB = K / B, MB = M / B, NC = Dy<B>::NC, RBW = Sh::RBW, MW = RBW * B;
   constexpr int MBP = Sh::OS * RBW;  // row blocks incl. the last wave's padding
   constexpr bool kVer = MODE == MatVecMode::kVerify;

@@ -1,7 +1,10 @@
 // gf_fixed.hpp -- definition of the fixed-K kernels (included only by gf_k<K>.hip).
 //
 // Rows are prefetched kFixedD ahead (tools/gf_pipe.hip, EC12P4 8 x 64 MiB on MI355X: D=2
-// fastest; the runtime-k kernel waits for each row before multiplying it).
+// fastest; the runtime-k kernel waits for each row before multiplying it).  Every output row of a
+// column chunk stays in one wave (OS = 1) up to fixed_max_m(K): splitting the rows over 2 or 4
+// waves re-reads the inputs once per wave from L2/LDS and was 8-22 % slower for m in 10..22
+// (profiles/r01/wide_output_probe.txt) even though the single wave runs at 1-2 waves per SIMD.
 #pragma once
 #include "gf_launch.hpp"
 
@@ -9,31 +12,28 @@ namespace cfsec {
 
 constexpr int kFixedD = 2;
 
-template <int K, int M, int OS, MatVecMode MODE>
+template <int K, int M, MatVecMode MODE>
 __global__ __launch_bounds__(256) void gf_matvec_k_kernel(const dev::GfArgs a) {
-  dev::matvec_k<K, M, MODE, kFixedD, OS>(a);
+  dev::matvec_k<K, M, MODE, kFixedD, 1>(a);
 }
 
-template <int K, MatVecMode MODE>
-hipError_t launch_k(Shape sh, const dev::GfArgs& a, dim3 grid, hipStream_t st) {
-#define CFSEC_KCASE(MV, OSV)                                                                  \
-  case MV * 8 + OSV:                                                                          \
-    hipLaunchKernelGGL((gf_matvec_k_kernel<K, MV, OSV, MODE>), grid, dim3(256), 0, st, a);    \
-    break;
-  switch (sh.M * 8 + sh.OS) {
-    CFSEC_KCASE(1, 1) CFSEC_KCASE(2, 1) CFSEC_KCASE(3, 1) CFSEC_KCASE(4, 1) CFSEC_KCASE(5, 1)
-    CFSEC_KCASE(6, 1) CFSEC_KCASE(4, 2) CFSEC_KCASE(5, 2) CFSEC_KCASE(6, 2) CFSEC_KCASE(4, 4)
-    CFSEC_KCASE(5, 4) CFSEC_KCASE(6, 4) CFSEC_KCASE(8, 4)
-    default: return hipErrorInvalidValue;
+template <int K, MatVecMode MODE, int M>
+hipError_t launch_k(int m, const dev::GfArgs& a, dim3 grid, hipStream_t st) {
+  if constexpr (M == 0) {
+    return hipErrorInvalidValue;
+  } else {
+    if (m != M) return launch_k<K, MODE, M - 1>(m, a, grid, st);
+    hipLaunchKernelGGL((gf_matvec_k_kernel<K, M, MODE>), grid, dim3(256), 0, st, a);
+    return hipGetLastError();
   }
-#undef CFSEC_KCASE
-  return hipGetLastError();
 }
 
 }  // namespace cfsec
 
-#define CFSEC_INSTANTIATE_K(K)                                                                  \
-  namespace cfsec {                                                                             \
-  template hipError_t launch_k<K, MatVecMode::kStore>(Shape, const dev::GfArgs&, dim3, hipStream_t); \
-  template hipError_t launch_k<K, MatVecMode::kVerify>(Shape, const dev::GfArgs&, dim3, hipStream_t); \
+#define CFSEC_INSTANTIATE_K(K)                                                                   \
+  namespace cfsec {                                                                              \
+  template hipError_t launch_k<K, MatVecMode::kStore, fixed_max_m(K)>(int, const dev::GfArgs&, dim3, \
+                                                                     hipStream_t);                  \
+  template hipError_t launch_k<K, MatVecMode::kVerify, fixed_max_m(K)>(int, const dev::GfArgs&, dim3, \
+                                                                      hipStream_t);                 \
   }

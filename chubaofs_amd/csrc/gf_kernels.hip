@@ -62,13 +62,13 @@ __global__ __launch_bounds__(256) void gf_matvec_kernel(const GfArgs a) {
 }
 
 template <MatVecMode MODE>
-hipError_t launch_fixed(int k, Shape sh, const GfArgs& a, dim3 grid, hipStream_t st) {
+hipError_t launch_fixed(int k, int m, const GfArgs& a, dim3 grid, hipStream_t st) {
   switch (k) {
-    case 6: return launch_k<6, MODE>(sh, a, grid, st);
-    case 8: return launch_k<8, MODE>(sh, a, grid, st);
-    case 12: return launch_k<12, MODE>(sh, a, grid, st);
-    case 16: return launch_k<16, MODE>(sh, a, grid, st);
-    case 18: return launch_k<18, MODE>(sh, a, grid, st);
+    case 6: return launch_k<6, MODE>(m, a, grid, st);
+    case 8: return launch_k<8, MODE>(m, a, grid, st);
+    case 12: return launch_k<12, MODE>(m, a, grid, st);
+    case 16: return launch_k<16, MODE>(m, a, grid, st);
+    case 18: return launch_k<18, MODE>(m, a, grid, st);
     default: return hipErrorInvalidValue;
   }
 }
@@ -127,14 +127,15 @@ hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
       if (mode == MatVecMode::kStore && c0 > 0) mode = MatVecMode::kAccum;
       const bool verify = mode == MatVecMode::kVerify;
       const Shape sh = choose(mc);
-      // the code-mode input counts take the fixed-K pipelined kernels (all 256-thread, 1 chunk
-      // per lane); anything else the runtime-k kernel, whose verify policy is 128-thread
-      // workgroups with 2 chunks per lane unless the outputs are split over waves
-      const bool fixed = fixed_k(kc) && kc == job.k && mode != MatVecMode::kAccum &&
+      // the code-mode input counts take the fixed-K pipelined kernels (256 threads, one wave per
+      // column chunk holding every output, 1 chunk per lane); anything else the runtime-k
+      // kernel, whose verify policy is 128-thread workgroups with 2 chunks per lane unless the
+      // outputs are split over waves
+      const bool fixed = fixed_k(kc) && kc == job.k && mc <= fixed_max_m(kc) && mode != MatVecMode::kAccum &&
                          job.len <= 0xFFFFFFFFull - 4096;  // 32-bit lane offsets
       const int threads = (!fixed && verify && sh.OS == 1) ? 128 : 256;
-      // 4-output matrices of 4x4 dyadic blocks (EC12P4 / EC16P4 encode, coset-aligned reconstructs
-      // such as EC12P4's worst case) take the reduced-product kernel
+      // matrices of 4x4 / 2x2 dyadic blocks (encode of every code mode but the LRC local stripes,
+      // coset-aligned reconstructs such as EC12P4's worst case) take the reduced-product kernel
       int dyB = 0;
       if (fixed && r0 == 0 && mc == job.m) {
         std::vector<uint8_t> sub((size_t)mc * kc);
@@ -142,8 +143,8 @@ hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
           for (int c = 0; c < kc; ++c) sub[(size_t)r * kc + c] = job.coef[(size_t)r * job.k + c];
         dyB = dyadic_block(sub.data(), mc, kc);
       }
-      const size_t tile =
-          size_t(threads / sh.OS) * dev::kLaneBytes * ((verify && !fixed) ? kVerifyW : kStoreW);
+      const size_t tile = fixed ? size_t(256) * dev::kLaneBytes
+                                : size_t(threads / sh.OS) * dev::kLaneBytes * (verify ? kVerifyW : kStoreW);
       const size_t tiles = (job.len + tile - 1) / tile;
       const int per_stripe = kc + mc;
       const int64_t sstride = affine_stride(job, c0, kc, r0, mc);
@@ -176,15 +177,16 @@ hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
         const dim3 grid((unsigned)(tiles * ns));
         hipError_t e;
         if (fixed && dyB) {
-          e = kc == 12 ? launch_dy<12>(mc, dyB, mode, a, (unsigned)ns, stream)
-                       : launch_dy<16>(mc, dyB, mode, a, (unsigned)ns, stream);
+          e = kc == 6    ? launch_dy<6>(mc, dyB, mode, a, (unsigned)ns, stream)
+              : kc == 12 ? launch_dy<12>(mc, dyB, mode, a, (unsigned)ns, stream)
+                         : launch_dy<16>(mc, dyB, mode, a, (unsigned)ns, stream);
           if (e != hipSuccess) return e;
           continue;
         }
         if (fixed) {
           const dim3 grid2((unsigned)tiles, (unsigned)ns);
-          e = verify ? launch_fixed<MatVecMode::kVerify>(kc, sh, a, grid2, stream)
-                     : launch_fixed<MatVecMode::kStore>(kc, sh, a, grid2, stream);
+          e = verify ? launch_fixed<MatVecMode::kVerify>(kc, mc, a, grid2, stream)
+                     : launch_fixed<MatVecMode::kStore>(kc, mc, a, grid2, stream);
           if (e != hipSuccess) return e;
           continue;
         }

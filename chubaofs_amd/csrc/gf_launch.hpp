@@ -27,24 +27,39 @@ inline Shape choose(int mc) {
 // EC6P10L2 local stripe), 12 (EC12P4), 16 (EC16P20), 18 (the EC16P20L2 local stripe).
 inline bool fixed_k(int k) { return k == 6 || k == 8 || k == 12 || k == 16 || k == 18; }
 
-// Launch gf_matvec_k_kernel<K, M, OS, MODE> for shape sh (defined in gf_fixed.hpp, instantiated
-// for kStore and kVerify in gf_k<K>.hip).
-template <int K, MatVecMode MODE>
-hipError_t launch_k(Shape sh, const dev::GfArgs& a, dim3 grid, hipStream_t st);
+// Largest output count with a fixed-K kernel: EC6P10L2's 10 global + 2 local parities (6 x 12),
+// EC12P4 repairs of up to 12 rows, EC16P20L2's 20 + 2 (16 x 22) and up to 24 EC16P20 repair rows.
+constexpr int fixed_max_m(int k) {
+  return k == 6 ? 12 : k == 8 ? 8 : k == 12 ? 12 : k == 16 ? 24 : k == 18 ? 4 : 0;
+}
+
+// Launch gf_matvec_k_kernel<K, m, MODE> on a (tiles of 4096 B, stripes) grid (defined in
+// gf_fixed.hpp, instantiated for kStore and kVerify in gf_k<K>.hip).
+template <int K, MatVecMode MODE, int M = fixed_max_m(K)>
+hipError_t launch_k(int m, const dev::GfArgs& a, dim3 grid, hipStream_t st);
 
 // Dyadic-block kernels (gf_dyadic.hpp) for an m x k matrix whose B x B blocks satisfy
-// M[r0+i][c0+j] = M[r0][c0 + (i ^ j)]; specialised in gf_dy_k<K>.hip for K in {12, 16}, B = 4, m = 4.
+// M[r0+i][c0+j] = M[r0][c0 + (i ^ j)]; specialised in gf_dy_k<K>.hip: B = 4 for K = 12 (m = 4, 8,
+// 12) and K = 16 (m = 4 .. 20 in steps of 4), B = 2 for K = 6 (m = 6 .. 12 even).
 template <int K>
 hipError_t launch_dy(int m, int B, MatVecMode mode, const dev::GfArgs& a, unsigned ns, hipStream_t st);
+template <>
+hipError_t launch_dy<6>(int, int, MatVecMode, const dev::GfArgs&, unsigned, hipStream_t);
 template <>
 hipError_t launch_dy<12>(int, int, MatVecMode, const dev::GfArgs&, unsigned, hipStream_t);
 template <>
 hipError_t launch_dy<16>(int, int, MatVecMode, const dev::GfArgs&, unsigned, hipStream_t);
 
-// The dyadic block size a shipped kernel can use for this matrix (4), or 0.
+// The block size of the shipped dyadic kernel for an m x k matrix (4 or 2), or 0.
+constexpr int dyadic_shape(int k, int m) {
+  return ((k == 12 && m <= 12) || (k == 16 && m <= 20)) && m % 4 == 0 ? 4
+         : k == 6 && m >= 6 && m <= 12 && m % 2 == 0                  ? 2
+                                                                      : 0;
+}
+
+// The dyadic block size a shipped kernel can use for this matrix, or 0.
 inline int dyadic_block(const uint8_t* coef, int m, int k) {
-  int B = 0;
-  if ((k == 12 || k == 16) && m == 4) B = 4;
+  const int B = dyadic_shape(k, m);
   if (!B) return 0;
   for (int r0 = 0; r0 < m; r0 += B)
     for (int c0 = 0; c0 < k; c0 += B)
@@ -54,11 +69,11 @@ inline int dyadic_block(const uint8_t* coef, int m, int k) {
   return B;
 }
 
-#define CFSEC_EXTERN_K(K)                                                                       \
-  extern template hipError_t launch_k<K, MatVecMode::kStore>(Shape, const dev::GfArgs&, dim3, \
-                                                             hipStream_t);                    \
-  extern template hipError_t launch_k<K, MatVecMode::kVerify>(Shape, const dev::GfArgs&, dim3, \
-                                                              hipStream_t);
+#define CFSEC_EXTERN_K(K)                                                                         \
+  extern template hipError_t launch_k<K, MatVecMode::kStore, fixed_max_m(K)>(int, const dev::GfArgs&, \
+                                                                            dim3, hipStream_t);     \
+  extern template hipError_t launch_k<K, MatVecMode::kVerify, fixed_max_m(K)>(int, const dev::GfArgs&, \
+                                                                             dim3, hipStream_t);
 CFSEC_EXTERN_K(6)
 CFSEC_EXTERN_K(8)
 CFSEC_EXTERN_K(12)

@@ -133,6 +133,31 @@ def test_encode_many_inputs_chunked(rs):
         assert np.array_equal(got[i], want[i])
 
 
+FIXED_MAX_M = {6: 12, 8: 8, 12: 12, 16: 24, 18: 4}  # gf_launch.hpp fixed_max_m
+
+
+@pytest.mark.parametrize("k,m", [(k, m) for k, top in FIXED_MAX_M.items() for m in range(1, top + 2)])
+def test_every_fixed_kernel_output_count(rs, k, m):
+    """Every output count of the fixed-K kernels (plain and dyadic-block, store and verify), plus the
+    first count past them (runtime-k kernel): encode, verify with and without a flipped parity
+    byte, the worst-case data erasure (coset-aligned, dyadic for k = 6, 12, 16) and a random
+    erasure set of size m (a general matrix) -- all against the oracle."""
+    size = 8209  # two 4 KiB tiles + a ragged tail
+    want = oracle_encoded(k, m, size, seed=k * 64 + m)
+    enc = rs.New(k, m)
+    d = to_dev([s if i < k else np.full(size, 0x5A, np.uint8) for i, s in enumerate(want)])
+    enc.Encode(d)
+    got = to_host(d)
+    for i in range(k, k + m):
+        assert np.array_equal(got[i], want[i]), i
+    assert enc.Verify(d)
+    d[k + m - 1][size - 1] ^= 0x10
+    assert not enc.Verify(d)
+    r = random.Random(k * 100 + m)
+    for erased in (set(range(min(m, k))), set(r.sample(range(k + m), m))):
+        _check_recon(rs, k, m, size, erased, False, seed=m)
+
+
 def _check_recon(rs, k, m, size, erased, data_only, seed, consistent=True):
     if consistent:
         full = oracle_encoded(k, m, size, seed)
