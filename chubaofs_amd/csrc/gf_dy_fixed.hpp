@@ -6,39 +6,41 @@
 
 namespace cfsec {
 
-template <int K, int M, int B, MatVecMode MODE>
-__global__ __launch_bounds__((dev::DyShape<M, B>::kThreadsPerWg)) void gf_dy_kernel(const dev::GfArgs a) {
-  dev::matvec_dy<K, M, B, MODE>(a);
+template <int K, int M, int B, MatVecMode MODE, int E>
+__global__ __launch_bounds__((dev::DyShape<M - E, B>::kThreadsPerWg)) void gf_dy_kernel(const dev::GfArgs a) {
+  dev::matvec_dy<K, M, B, MODE, true, true, 64, E>(a);
 }
 
-template <int K, int M, int B, MatVecMode MODE>
+template <int K, int M, int B, MatVecMode MODE, int E>
 hipError_t launch_dy_one(const dev::GfArgs& a, unsigned ns, hipStream_t st) {
-  using Sh = dev::DyShape<M, B>;
+  using Sh = dev::DyShape<M - E, B>;
   const unsigned tiles = (unsigned)((a.len + Sh::kTileBytes - 1) / Sh::kTileBytes);
-  hipLaunchKernelGGL((gf_dy_kernel<K, M, B, MODE>), dim3(tiles, ns), dim3(Sh::kThreadsPerWg), 0, st, a);
+  hipLaunchKernelGGL((gf_dy_kernel<K, M, B, MODE, E>), dim3(tiles, ns), dim3(Sh::kThreadsPerWg), 0, st, a);
   return hipGetLastError();
 }
 
 // Launch the kernel for output count m, one of Ms.
-template <int K, int B, MatVecMode MODE, int... Ms>
+template <int K, int B, MatVecMode MODE, int E, int... Ms>
 hipError_t launch_dy_m(int m, const dev::GfArgs& a, unsigned ns, hipStream_t st) {
   hipError_t e = hipErrorInvalidValue;
-  (void)((m == Ms ? (e = launch_dy_one<K, Ms, B, MODE>(a, ns, st), true) : false) || ...);
+  (void)((m == Ms ? (e = launch_dy_one<K, Ms, B, MODE, E>(a, ns, st), true) : false) || ...);
   return e;
 }
 
-}  // namespace cfsec
+template <int... M>
+struct Ms {};
 
-// launch_dy<K> for block size BV and the output counts listed after it (dyadic_shape in
-// gf_launch.hpp must list the same ones).
-#define CFSEC_DY_INSTANTIATE(K, BV, ...)                                                            \
-  namespace cfsec {                                                                                 \
-  template <>                                                                                       \
-  hipError_t launch_dy<K>(int m, int B, MatVecMode mode, const dev::GfArgs& a, unsigned ns,         \
-                          hipStream_t st) {                                                         \
-    if (B != BV || dyadic_shape(K, m) != BV) return hipErrorInvalidValue;                           \
-    return mode == MatVecMode::kVerify                                                              \
-               ? launch_dy_m<K, BV, MatVecMode::kVerify, __VA_ARGS__>(m, a, ns, st)                 \
-               : launch_dy_m<K, BV, MatVecMode::kStore, __VA_ARGS__>(m, a, ns, st);                 \
-  }                                                                                                 \
-  }
+// launch_dy<K> body: block size BV, all-dyadic output counts M0, output counts M2 with 2 plain
+// rows (dyadic_plan in gf_launch.hpp must list the same ones).
+template <int K, int BV, int... M0, int... M2>
+hipError_t dy_dispatch(Ms<M0...>, Ms<M2...>, int m, int B, int E, MatVecMode mode, const dev::GfArgs& a,
+                       unsigned ns, hipStream_t st) {
+  constexpr MatVecMode kV = MatVecMode::kVerify, kS = MatVecMode::kStore;
+  if (B != BV) return hipErrorInvalidValue;
+  const bool v = mode == kV;
+  if (E == 0) return v ? launch_dy_m<K, BV, kV, 0, M0...>(m, a, ns, st) : launch_dy_m<K, BV, kS, 0, M0...>(m, a, ns, st);
+  if (E == 2) return v ? launch_dy_m<K, BV, kV, 2, M2...>(m, a, ns, st) : launch_dy_m<K, BV, kS, 2, M2...>(m, a, ns, st);
+  return hipErrorInvalidValue;
+}
+
+}  // namespace cfsec

@@ -2,4 +2,9 @@
 // gf_dyadic.hpp.
 #include "gf_dy_fixed.hpp"
 
-CFSEC_DY_INSTANTIATE(12, 4, 4, 8, 12)
+namespace cfsec {
+template <>
+hipError_t launch_dy<12>(int m, int B, int E, MatVecMode mode, const dev::GfArgs& a, unsigned ns, hipStream_t st) {
+  return dy_dispatch<12, 4>(Ms<4, 8, 12>{}, Ms<>{}, m, B, E, mode, a, ns, st);
+}
+}  // namespace cfsec

@@ -53,14 +53,22 @@ __device__ __forceinline__ uint32_t dy_coef(const uint8_t* h, int q) {
 }
 
 // Product tables of every derived coefficient: slot (rb*KB + cb)*NC + q for row block rb, column
-// block cb (coef: m x K row-major, first row of each block read).  Row blocks MB .. MBP-1 pad the
-// last wave's share with zero tables, so no wave indexes past the arrays.
-template <int K, int M, int B, int MBP>
+// block cb (coef: (MD + E) x K row-major, first row of each block read).  Row blocks MB .. MBP-1 pad
+// the last wave's share with zero tables, so no wave indexes past the arrays.  The E plain rows
+// after the MD dyadic ones follow at slot MBP*KB*NC + c*E + e.
+template <int K, int MD, int B, int MBP, int E>
 __device__ __forceinline__ void build_dy_tables(const uint8_t* coef, u32x4* tab01, uint32_t* tab2) {
-  constexpr int KB = K / B, MB = M / B, NC = Dy<B>::NC;
-  for (int i = threadIdx.x; i < MBP * KB * NC; i += (int)blockDim.x) {
-    const int q = i % NC, blk = i / NC, cb = blk % KB, rb = blk / KB;
-    coef_tables(rb < MB ? dy_coef<B>(coef + (rb * B) * K + cb * B, q) : 0u, tab01[i], tab2[i]);
+  constexpr int KB = K / B, MB = MD / B, NC = Dy<B>::NC, ND = MBP * KB * NC;
+  for (int i = threadIdx.x; i < ND + K * E; i += (int)blockDim.x) {
+    uint32_t cf = 0;
+    if (i < ND) {
+      const int q = i % NC, blk = i / NC, cb = blk % KB, rb = blk / KB;
+      cf = rb < MB ? dy_coef<B>(coef + (rb * B) * K + cb * B, q) : 0u;
+    } else if constexpr (E > 0) {
+      const int c = (i - ND) / E, e = (i - ND) % E;
+      cf = coef[(MD + e) * K + c];
+    }
+    coef_tables(cf, tab01[i], tab2[i]);
   }
 }
 
@@ -201,19 +209,24 @@ struct DyShape {
   static constexpr int kTileBytes = 64 * kLaneBytes * CW;
 };
 
-// Kernel body: compile-time K inputs, M outputs, dyadic blocks of B; grid (tiles, stripes),
-// DyShape threads; wave w handles column chunk w / OS and row blocks (w % OS) * RBW .. +RBW,
+// Kernel body: compile-time K inputs, M outputs of which the first M - E are made of dyadic blocks
+// of B and the last E are plain rows (the local parities of a fused LRC encode: EC16P20L2 is 20
+// dyadic global rows + 2 local rows); grid (tiles, stripes), DyShape threads; wave w handles
+// column chunk w / OS and row blocks (w % OS) * RBW .. +RBW (plain rows: single-wave shapes only),
 // one 16-byte chunk per lane per row, column blocks loaded one block ahead.
-template <int K, int M, int B, MatVecMode MODE, bool NTS = true, bool NTL = true, int RBW_ = 64>
+template <int K, int M, int B, MatVecMode MODE, bool NTS = true, bool NTL = true, int RBW_ = 64, int E = 0>
 __device__ __forceinline__ void matvec_dy(const GfArgs& a) {
-  static_assert(K % B == 0 && M % B == 0 && (B == 2 || B == 4), "dyadic shape");
-  using Sh = DyShape<M, B, RBW_>;
-  constexpr int KB = K / B, MB = M / B, NC = Dy<B>::NC, RBW = Sh::RBW, MW = RBW * B;
+  constexpr int MD = M - E;
+  static_assert(K % B == 0 && MD % B == 0 && (B == 2 || B == 4), "dyadic shape");
+  using Sh = DyShape<MD, B, RBW_>;
+  static_assert(E == 0 || Sh::OS == 1, "plain rows ride along single-wave shapes only");
+  constexpr int KB = K / B, MB = MD / B, NC = Dy<B>::NC, RBW = Sh::RBW, MW = RBW * B;
   constexpr int MBP = Sh::OS * RBW;  // row blocks incl. the last wave's padding
+  constexpr int ND = MBP * KB * NC;  // dyadic table slots; the plain rows' follow
   constexpr bool kVer = MODE == MatVecMode::kVerify;
-  __shared__ u32x4 tab01[MBP * KB * NC];
-  __shared__ uint32_t tab2[MBP * KB * NC];
-  build_dy_tables<K, M, B, MBP>(a.coef, tab01, tab2);
+  __shared__ u32x4 tab01[ND + K * E];
+  __shared__ uint32_t tab2[ND + K * E];
+  build_dy_tables<K, MD, B, MBP, E>(a.coef, tab01, tab2);
   __syncthreads();
 
   const int wave = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
@@ -225,7 +238,7 @@ __device__ __forceinline__ void matvec_dy(const GfArgs& a) {
   const size_t ts = a.sstride ? 0 : (size_t)stripe;
   const int64_t sbase = (int64_t)stripe * a.sstride;
   const uint32_t off = tile * (uint32_t)Sh::kTileBytes + (uint32_t)(cw * 64 + lane) * kLaneBytes;
-  const uint8_t* row[K + MW];
+  const uint8_t* row[K + MW + E];
 #pragma unroll
   for (int c = 0; c < K; ++c) row[c] = a.ptr[ts * K + c] + sbase;
 #pragma unroll
@@ -233,16 +246,19 @@ __device__ __forceinline__ void matvec_dy(const GfArgs& a) {
     const int o = rb0 * B + (r < nrb * B ? r : 0);
     row[K + r] = a.ptr[(size_t)a.tab * K + ts * M + o] + sbase;
   }
+#pragma unroll
+  for (int e = 0; e < E; ++e) row[K + MW + e] = a.ptr[(size_t)a.tab * K + ts * M + MD + e] + sbase;
   __builtin_amdgcn_sched_barrier(0);
 
-  uint32_t acc[MW][4];
+  constexpr int MA = MW + E;  // accumulators: dyadic rows, then plain rows
+  uint32_t acc[MA][4];
 #pragma unroll
-  for (int r = 0; r < MW; ++r)
+  for (int r = 0; r < MA; ++r)
 #pragma unroll
     for (int w = 0; w < 4; ++w) acc[r][w] = 0u;
   const auto pin = [&]() {
 #pragma unroll
-    for (int r = 0; r < MW; ++r)
+    for (int r = 0; r < MA; ++r)
       asm volatile("" : "+v"(acc[r][0]), "+v"(acc[r][1]), "+v"(acc[r][2]), "+v"(acc[r][3]));
   };
   const bool full = (uint64_t)off + kLaneBytes <= a.len;
@@ -268,16 +284,27 @@ __device__ __forceinline__ void matvec_dy(const GfArgs& a) {
         for (int c = 0; c < B; ++c) load((cb + 1) * B + c);
       __builtin_amdgcn_sched_barrier(0);
       const int c0 = cb * B;
+      auto& dacc = reinterpret_cast<uint32_t(&)[MW][4]>(acc);
       if constexpr (B == 2)
-        dy_col2<RBW>(acc, x[c0], x[c0 + 1], tq + cb * NC, tt + cb * NC, KB * NC);
+        dy_col2<RBW>(dacc, x[c0], x[c0 + 1], tq + cb * NC, tt + cb * NC, KB * NC);
       else
-        dy_col4<RBW>(acc, x[c0], x[c0 + 1], x[c0 + 2], x[c0 + 3], tq + cb * NC, tt + cb * NC, KB * NC);
+        dy_col4<RBW>(dacc, x[c0], x[c0 + 1], x[c0 + 2], x[c0 + 3], tq + cb * NC, tt + cb * NC, KB * NC);
       pin();
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr (E > 0) {
+        auto& eacc = reinterpret_cast<uint32_t(&)[E][4]>(acc[MW]);
+#pragma unroll
+        for (int c = c0; c < c0 + B; c += 2) {
+          mac_pair_k<E>(eacc, x[c], x[c + 1], tab01 + ND + c * E, tab2 + ND + c * E, tab01 + ND + (c + 1) * E,
+                        tab2 + ND + (c + 1) * E);
+          pin();
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
     }
 #pragma unroll
-    for (int r = 0; r < MW; ++r) {
-      if (r >= nrb * B) continue;
+    for (int r = 0; r < MA; ++r) {
+      if (r < MW && r >= nrb * B) continue;
       uint8_t* p = const_cast<uint8_t*>(row[K + r]) + off;
       const u32x4 v = u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
       if constexpr (kVer) {

@@ -136,12 +136,12 @@ hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
       const int threads = (!fixed && verify && sh.OS == 1) ? 128 : 256;
       // matrices of 4x4 / 2x2 dyadic blocks (encode of every code mode but the LRC local stripes,
       // coset-aligned reconstructs such as EC12P4's worst case) take the reduced-product kernel
-      int dyB = 0;
+      DyPlan dy{0, 0};
       if (fixed && r0 == 0 && mc == job.m) {
         std::vector<uint8_t> sub((size_t)mc * kc);
         for (int r = 0; r < mc; ++r)
           for (int c = 0; c < kc; ++c) sub[(size_t)r * kc + c] = job.coef[(size_t)r * job.k + c];
-        dyB = dyadic_block(sub.data(), mc, kc);
+        dy = dyadic_plan(sub.data(), mc, kc);
       }
       const size_t tile = fixed ? size_t(256) * dev::kLaneBytes
                                 : size_t(threads / sh.OS) * dev::kLaneBytes * (verify ? kVerifyW : kStoreW);
@@ -176,10 +176,10 @@ hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
         }
         const dim3 grid((unsigned)(tiles * ns));
         hipError_t e;
-        if (fixed && dyB) {
-          e = kc == 6    ? launch_dy<6>(mc, dyB, mode, a, (unsigned)ns, stream)
-              : kc == 12 ? launch_dy<12>(mc, dyB, mode, a, (unsigned)ns, stream)
-                         : launch_dy<16>(mc, dyB, mode, a, (unsigned)ns, stream);
+        if (fixed && dy.B) {
+          e = kc == 6    ? launch_dy<6>(mc, dy.B, dy.E, mode, a, (unsigned)ns, stream)
+              : kc == 12 ? launch_dy<12>(mc, dy.B, dy.E, mode, a, (unsigned)ns, stream)
+                         : launch_dy<16>(mc, dy.B, dy.E, mode, a, (unsigned)ns, stream);
           if (e != hipSuccess) return e;
           continue;
         }

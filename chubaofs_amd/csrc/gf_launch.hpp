@@ -38,35 +38,48 @@ constexpr int fixed_max_m(int k) {
 template <int K, MatVecMode MODE, int M = fixed_max_m(K)>
 hipError_t launch_k(int m, const dev::GfArgs& a, dim3 grid, hipStream_t st);
 
-// Dyadic-block kernels (gf_dyadic.hpp) for an m x k matrix whose B x B blocks satisfy
-// M[r0+i][c0+j] = M[r0][c0 + (i ^ j)]; specialised in gf_dy_k<K>.hip: B = 4 for K = 12 (m = 4, 8,
-// 12) and K = 16 (m = 4 .. 20 in steps of 4), B = 2 for K = 6 (m = 6 .. 12 even).
+// Dyadic-block kernels (gf_dyadic.hpp) for an m x k matrix whose first m - E rows are made of
+// B x B blocks with M[r0+i][c0+j] = M[r0][c0 + (i ^ j)] (E plain rows follow); specialised in
+// gf_dy_k<K>.hip for the shapes dyadic_plan lists.
 template <int K>
-hipError_t launch_dy(int m, int B, MatVecMode mode, const dev::GfArgs& a, unsigned ns, hipStream_t st);
+hipError_t launch_dy(int m, int B, int E, MatVecMode mode, const dev::GfArgs& a, unsigned ns, hipStream_t st);
 template <>
-hipError_t launch_dy<6>(int, int, MatVecMode, const dev::GfArgs&, unsigned, hipStream_t);
+hipError_t launch_dy<6>(int, int, int, MatVecMode, const dev::GfArgs&, unsigned, hipStream_t);
 template <>
-hipError_t launch_dy<12>(int, int, MatVecMode, const dev::GfArgs&, unsigned, hipStream_t);
+hipError_t launch_dy<12>(int, int, int, MatVecMode, const dev::GfArgs&, unsigned, hipStream_t);
 template <>
-hipError_t launch_dy<16>(int, int, MatVecMode, const dev::GfArgs&, unsigned, hipStream_t);
+hipError_t launch_dy<16>(int, int, int, MatVecMode, const dev::GfArgs&, unsigned, hipStream_t);
 
-// The block size of the shipped dyadic kernel for an m x k matrix (4 or 2), or 0.
-constexpr int dyadic_shape(int k, int m) {
+// The block size of the shipped dyadic kernel for an m x k matrix with e trailing plain rows, or 0:
+// 4x4 blocks for k = 12 (m = 4, 8, 12) and k = 16 (m = 4 .. 20), 2x2 for k = 6 (m = 6 .. 12), and
+// the fused LRC encodes with their 2 local rows (EC6P10L2: 6 x (10 + 2), EC16P20L2: 16 x (20 + 2)).
+constexpr int dyadic_shape(int k, int m, int e = 0) {
+  if (e == 2) return k == 16 && m == 22 ? 4 : k == 6 && m == 12 ? 2 : 0;
+  if (e != 0) return 0;
   return ((k == 12 && m <= 12) || (k == 16 && m <= 20)) && m % 4 == 0 ? 4
          : k == 6 && m >= 6 && m <= 12 && m % 2 == 0                  ? 2
                                                                       : 0;
 }
 
-// The dyadic block size a shipped kernel can use for this matrix, or 0.
-inline int dyadic_block(const uint8_t* coef, int m, int k) {
-  const int B = dyadic_shape(k, m);
-  if (!B) return 0;
-  for (int r0 = 0; r0 < m; r0 += B)
-    for (int c0 = 0; c0 < k; c0 += B)
-      for (int i = 0; i < B; ++i)
-        for (int j = 0; j < B; ++j)
-          if (coef[(size_t)(r0 + i) * k + c0 + j] != coef[(size_t)r0 * k + c0 + (i ^ j)]) return 0;
-  return B;
+struct DyPlan {
+  int B, E;  // B = 0: no dyadic kernel
+};
+
+// The dyadic kernel a matrix can take: all rows dyadic, else all but the last 2.
+inline DyPlan dyadic_plan(const uint8_t* coef, int m, int k) {
+  const auto blocks_hold = [&](int B, int md) {
+    for (int r0 = 0; r0 < md; r0 += B)
+      for (int c0 = 0; c0 < k; c0 += B)
+        for (int i = 0; i < B; ++i)
+          for (int j = 0; j < B; ++j)
+            if (coef[(size_t)(r0 + i) * k + c0 + j] != coef[(size_t)r0 * k + c0 + (i ^ j)]) return false;
+    return true;
+  };
+  for (int e : {0, 2}) {
+    const int B = dyadic_shape(k, m, e);
+    if (B && blocks_hold(B, m - e)) return {B, e};
+  }
+  return {0, 0};
 }
 
 #define CFSEC_EXTERN_K(K)                                                                         \
