@@ -50,11 +50,13 @@ ErrInvalidShards = _mk("ErrInvalidShards", 11, "ec.ErrInvalidShards")
 ErrInvalidArg = _mk("ErrInvalidArg", 12, "boundary misuse")
 ErrDevice = _mk("ErrDevice", 13, "HIP runtime failure")
 ErrNotSupported = _mk("ErrNotSupported", 14, "reedsolomon.ErrNotSupported")
+ErrInvalidBlock = _mk("ErrInvalidBlock", 15, "crc32block.ErrInvalidBlock")
+ErrMismatchedCrc = _mk("ErrMismatchedCrc", 16, "crc32block.ErrMismatchedCrc")
 
 _BY_CODE = {c.status: c for c in (
     ErrTooFewShards, ErrShardNoData, ErrShardSize, ErrInvShardNum, ErrMaxShardNum, ErrShortData,
     ErrReconstructRequired, ErrSingular, ErrInvalidCodeMode, ErrVerify, ErrInvalidShards,
-    ErrInvalidArg, ErrDevice, ErrNotSupported)}
+    ErrInvalidArg, ErrDevice, ErrNotSupported, ErrInvalidBlock, ErrMismatchedCrc)}
 
 
 def check(status: int) -> None:
@@ -105,6 +107,11 @@ SIGNATURES = {
     "cfsec_crc32_ieee_batch": ([_V, _S, _I, _V, _I, _V], _I),
     "cfsec_host_alloc": ([_S, _P(_V)], _I),
     "cfsec_host_free": ([_V], _I),
+    "cfsec_crc32block_encode_size": ([ctypes.c_int64, ctypes.c_int64], ctypes.c_int64),
+    "cfsec_crc32block_decode_size": ([ctypes.c_int64, ctypes.c_int64], ctypes.c_int64),
+    "cfsec_crc32block_encode": ([_V, ctypes.c_int64, ctypes.c_int64, _V, _P(ctypes.c_uint32), _I, _I, _V], _I),
+    "cfsec_crc32block_decode": ([_V, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _V,
+                                 _P(ctypes.c_int64), _I, _I, _V], _I),
 }
 
 _LIB = None

@@ -1,4 +1,6 @@
 // capi.cpp -- extern "C" boundary declared in include/cfsec.h.
+#include <algorithm>
+#include <cstdint>
 #include <new>
 #include <vector>
 
@@ -60,6 +62,98 @@ const ModeRow kModes[] = {
     {201, {6, 8, 10, 2, 13, 0, 0}},     // EC6P8L10
 };
 
+// EncodeSize (common/crc32block/util.go:50-57) for a valid block length.
+int64_t crc32block_framed(int64_t size, int64_t block_len) {
+  const int64_t p = block_len - 4;
+  return size + 4 * ((size + p - 1) / p);
+}
+
+// Encoder.Encode / Decoder.Reader through launch_crc32block: device pointers in place, page-locked
+// host buffers in place (device aliases), other host memory staged through the workspace.
+int crc32block_call(bool encode, const uint8_t* src, int64_t size, int64_t block_len, int64_t from, int64_t to,
+                    uint8_t* dst, uint32_t* shard_crc, int64_t* bad_block, int mem, int device, void* stream) {
+  if (!cfsec::crc32block_valid_len(block_len)) return CFSEC_ERR_INVALID_BLOCK;
+  if (size < 0 || (mem != CFSEC_MEM_HOST && mem != CFSEC_MEM_DEVICE)) return CFSEC_ERR_INVALID_ARG;
+  if (!encode && (from < 0 || from > to || to > size)) return CFSEC_ERR_INVALID_ARG;
+  if (bad_block) *bad_block = -1;
+  if (shard_crc) *shard_crc = 0;  // crc32.ChecksumIEEE(nil)
+  const int64_t P = block_len - 4;
+  int64_t b0 = 0, nb = (size + P - 1) / P;  // blocks the call touches
+  if (!encode) {
+    b0 = from / P;
+    const int64_t b1 = from < to ? (to - 1) / P : (from % P ? b0 : b0 - 1);  // see crc32block.hip
+    nb = b1 - b0 + 1;
+  }
+  if (nb <= 0) return CFSEC_OK;
+  const int64_t framed = crc32block_framed(size, block_len);
+  const int64_t f0 = b0 * block_len, f1 = std::min(framed, (b0 + nb) * block_len);
+  const int64_t in_bytes = encode ? size : f1 - f0;
+  const int64_t out_bytes = encode ? framed : to - from;
+  if (!src || (!dst && out_bytes > 0)) return CFSEC_ERR_INVALID_ARG;
+  return guarded([&] {
+    if (device < 0 && hipGetDevice(&device) != hipSuccess) return (int)CFSEC_ERR_DEVICE;
+    cfsec::DeviceContext* ctx = cfsec::DeviceContext::get(device);
+    if (!ctx) {
+      cfsec::set_last_error("no HIP device available to the cfsec engine");
+      return (int)CFSEC_ERR_DEVICE;
+    }
+    cfsec::DeviceGuard g(device);
+    const uint8_t* din = src;
+    uint8_t* dout = dst;
+    bool stage = false;
+    if (mem == CFSEC_MEM_HOST) {
+      uint8_t *pi = nullptr, *po = nullptr;
+      const bool pin_in = cfsec::device_alias(const_cast<uint8_t*>(src) + (encode ? 0 : f0), &pi);
+      const bool pin_out = out_bytes == 0 || cfsec::device_alias(dst, &po);
+      stage = !(pin_in && pin_out);
+      if (!stage) {
+        din = encode ? pi : reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(pi) - (uintptr_t)f0);
+        dout = po;
+      }
+    }
+    cfsec::DeviceContext::Workspace* ws = nullptr;
+    int st = ctx->acquire(stage ? (size_t)(in_bytes + out_bytes) : 0, 2, &ws);
+    if (st != CFSEC_OK) return st;
+    hipStream_t s = stream ? as_stream(stream) : ws->stream;
+    if (stage) {
+      st = cfsec::hip_status(hipMemcpyAsync(ws->dbuf, src + (encode ? 0 : f0), (size_t)in_bytes, hipMemcpyHostToDevice, s),
+                             "hipMemcpyAsync H2D");
+      // the launch addresses the framed object from its start; the staged copy begins at block b0
+      din = encode ? ws->dbuf : reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(ws->dbuf) - (uintptr_t)f0);
+      dout = ws->dbuf + in_bytes;
+    }
+    if (st == CFSEC_OK) st = cfsec::hip_status(hipMemsetAsync(ws->dflags, 0xFF, 4, s), "hipMemsetAsync");
+    if (st == CFSEC_OK) st = cfsec::hip_status(hipMemsetAsync(ws->dflags + 1, 0, 4, s), "hipMemsetAsync");
+    cfsec::Crc32BlockJob j;
+    j.encode = encode;
+    j.in = din;
+    j.out = dout;
+    j.size = size;
+    j.block_len = block_len;
+    j.from = from;
+    j.to = to;
+    j.bad = ws->dflags;
+    j.whole = (encode && shard_crc) ? ws->dflags + 1 : nullptr;
+    if (st == CFSEC_OK) st = cfsec::hip_status(cfsec::launch_crc32block(j, s), "launch_crc32block");
+    if (st == CFSEC_OK && stage && out_bytes > 0)
+      st = cfsec::hip_status(hipMemcpyAsync(dst, dout, (size_t)out_bytes, hipMemcpyDeviceToHost, s),
+                             "hipMemcpyAsync D2H");
+    if (st == CFSEC_OK)
+      st = cfsec::hip_status(hipMemcpyAsync(ws->hflags, ws->dflags, 8, hipMemcpyDeviceToHost, s), "hipMemcpyAsync D2H");
+    const int sync = cfsec::hip_status(hipStreamSynchronize(s), "hipStreamSynchronize");
+    if (st == CFSEC_OK) st = sync;
+    if (st == CFSEC_OK) {
+      if (encode && shard_crc) *shard_crc = ws->hflags[1] ^ cfsec::crc32_shift_ones((size_t)size);
+      if (!encode && ws->hflags[0] != 0xFFFFFFFFu) {
+        if (bad_block) *bad_block = b0 + (int64_t)ws->hflags[0];
+        st = CFSEC_ERR_MISMATCHED_CRC;
+      }
+    }
+    ctx->release(ws);
+    return st;
+  });
+}
+
 }  // namespace
 
 extern "C" {
@@ -85,6 +179,8 @@ const char* cfsec_status_name(int status) {
     case CFSEC_ERR_INVALID_ARG: return "ErrInvalidArg";
     case CFSEC_ERR_DEVICE: return "ErrDevice";
     case CFSEC_ERR_NOT_SUPPORTED: return "ErrNotSupported";
+    case CFSEC_ERR_INVALID_BLOCK: return "ErrInvalidBlock";
+    case CFSEC_ERR_MISMATCHED_CRC: return "ErrMismatchedCrc";
     default: return "ErrUnknown";
   }
 }
@@ -312,6 +408,28 @@ int cfsec_crc32_ieee_batch(uint8_t* const* ptrs, size_t shard_size, int n, uint3
     ctx->release(ws);
     return st;
   });
+}
+
+// ---------------- crc32block ----------------
+
+int64_t cfsec_crc32block_encode_size(int64_t size, int64_t block_len) {
+  if (!cfsec::crc32block_valid_len(block_len) || size < 0) return -1;
+  return crc32block_framed(size, block_len);
+}
+
+int64_t cfsec_crc32block_decode_size(int64_t total, int64_t block_len) {
+  if (!cfsec::crc32block_valid_len(block_len) || total < 0) return -1;
+  return total - 4 * ((total + block_len - 1) / block_len);  // util.go:59-65
+}
+
+int cfsec_crc32block_encode(const uint8_t* src, int64_t size, int64_t block_len, uint8_t* dst,
+                            uint32_t* shard_crc, int mem, int device, void* stream) {
+  return crc32block_call(true, src, size, block_len, 0, size, dst, shard_crc, nullptr, mem, device, stream);
+}
+
+int cfsec_crc32block_decode(const uint8_t* src, int64_t size, int64_t block_len, int64_t from, int64_t to,
+                            uint8_t* dst, int64_t* bad_block, int mem, int device, void* stream) {
+  return crc32block_call(false, src, size, block_len, from, to, dst, nullptr, bad_block, mem, device, stream);
 }
 
 }  // extern "C"

@@ -228,7 +228,6 @@ Status RSEngine::create(int k, int m, int device, std::unique_ptr<RSEngine>* out
 static Status matvec_with_crc(const MatVecJob& job, uint8_t* const* ptrs, int total, const std::vector<int>& slot,
                               size_t S, uint32_t* crcs, hipStream_t stream);
 
-namespace {
 // The device address of page-locked host memory (hipHostMalloc / cfsec_host_alloc); false for
 // pageable memory.
 bool device_alias(uint8_t* p, uint8_t** dptr) {
@@ -242,7 +241,6 @@ bool device_alias(uint8_t* p, uint8_t** dptr) {
   *dptr = static_cast<uint8_t*>(attr.devicePointer) + (hbase ? p - hbase : 0);
   return true;
 }
-}  // namespace
 
 Status RSEngine::run(const Matrix& rows, const std::vector<cfsec_shard*>& ins,
                      const std::vector<cfsec_shard*>& outs, size_t S, int mem, hipStream_t stream,

@@ -25,6 +25,9 @@ using Status = int;  // cfsec_status
 
 void set_last_error(const std::string& msg);
 Status hip_status(hipError_t e, const char* what);
+// The device address of page-locked host memory (hipHostMalloc / cfsec_host_alloc); false for
+// pageable memory.
+bool device_alias(uint8_t* p, uint8_t** dptr);
 
 // Per-device streams and staging workspaces, shared by every engine on the device.
 class DeviceContext {

@@ -128,7 +128,9 @@ hipError_t launch_crc(int k, int m, const GfCrcArgs& a, dim3 grid, hipStream_t s
 }  // namespace
 
 bool matvec_crc_supported(int k, int m, size_t len) {
-  return fixed_k(k) && m >= 1 && m <= crcdev::kMaxM && len <= 0xFFFFFFFFull - crcdev::kTile;
+  // the fused kernels exist for the input counts of the code modes of SURVEY §8
+  const bool crc_k = k == 6 || k == 8 || k == 12 || k == 16 || k == 18;
+  return crc_k && m >= 1 && m <= crcdev::kMaxM && len <= 0xFFFFFFFFull - crcdev::kTile;
 }
 
 uint32_t crc32_shift_ones(size_t len) { return mulmod(xpow(8 * (int64_t)len), 0xFFFFFFFFu) ^ 0xFFFFFFFFu; }

@@ -298,7 +298,7 @@ template <int K, int M, int MT, MatVecMode MODE, int D, bool NTL, bool NTS, bool
 __device__ __forceinline__ void lane_tile_k(int m, const u32x4* tab01, const uint32_t* tab2,
                                             const uint8_t* const* in, uint8_t* const* out, int og,
                                             int64_t sbase, uint32_t loff, uint32_t& diff) {
-  static_assert(K % 2 == 0 && D >= 2, "the fixed-K tile consumes input rows in pairs, a pair ahead");
+  static_assert(D >= 2, "the fixed-K tile consumes input rows in pairs, a pair ahead");
   constexpr bool kVer = MODE == MatVecMode::kVerify;
   constexpr int R = K + (kVer ? M : 0);  // rows loaded
   const uint8_t* row[R];
@@ -329,9 +329,9 @@ __device__ __forceinline__ void lane_tile_k(int m, const u32x4* tab01, const uin
   };
 #pragma unroll
   for (int c = 0; c < D && c < R; ++c) load(c);
-  // inputs two rows per step (K is even for every fixed K)
+  // inputs two rows per step, an odd K's last row alone
 #pragma unroll
-  for (int c = 0; c < K; c += 2) {
+  for (int c = 0; c + 1 < K; c += 2) {
     if (c + D < R) load(c + D);
     if (c + D + 1 < R) load(c + D + 1);
     __builtin_amdgcn_sched_barrier(0);
@@ -343,6 +343,14 @@ __device__ __forceinline__ void lane_tile_k(int m, const u32x4* tab01, const uin
       pin();
       mac_row_k<M>(acc, x[c + 1], tab01 + (c + 1) * MT + og, tab2 + (c + 1) * MT + og);
     }
+    pin();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if constexpr (K % 2 == 1) {
+    constexpr int c = K - 1;  // rows up to c + D - 1 are loaded or in flight
+    if (c + D < R) load(c + D);
+    __builtin_amdgcn_sched_barrier(0);
+    mac_row_k<M>(acc, x[c], tab01 + c * MT + og, tab2 + c * MT + og);
     pin();
     __builtin_amdgcn_sched_barrier(0);
   }

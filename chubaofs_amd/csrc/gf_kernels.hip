@@ -64,8 +64,13 @@ __global__ __launch_bounds__(256) void gf_matvec_kernel(const GfArgs a) {
 template <MatVecMode MODE>
 hipError_t launch_fixed(int k, int m, const GfArgs& a, dim3 grid, hipStream_t st) {
   switch (k) {
+    case 3: return launch_k<3, MODE>(m, a, grid, st);
+    case 4: return launch_k<4, MODE>(m, a, grid, st);
     case 6: return launch_k<6, MODE>(m, a, grid, st);
+    case 7: return launch_k<7, MODE>(m, a, grid, st);
     case 8: return launch_k<8, MODE>(m, a, grid, st);
+    case 10: return launch_k<10, MODE>(m, a, grid, st);
+    case 15: return launch_k<15, MODE>(m, a, grid, st);
     case 12: return launch_k<12, MODE>(m, a, grid, st);
     case 16: return launch_k<16, MODE>(m, a, grid, st);
     case 18: return launch_k<18, MODE>(m, a, grid, st);

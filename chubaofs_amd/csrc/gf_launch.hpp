@@ -23,14 +23,23 @@ inline Shape choose(int mc) {
   return {8, 4};
 }
 
-// Fixed-K kernels for the input counts of the CubeFS code modes: k = 6 (EC6P6, EC6P10), 8 (the
-// EC6P10L2 local stripe), 12 (EC12P4), 16 (EC16P20), 18 (the EC16P20L2 local stripe).
-inline bool fixed_k(int k) { return k == 6 || k == 8 || k == 12 || k == 16 || k == 18; }
+// Fixed-K kernels for the input counts of the CubeFS code modes (codemode.go:40-120): k = 6
+// (EC6P6, EC6P10, EC6P3), 8 (the EC6P10L2 local stripe), 12 (EC12P4, EC12P9), 16 (EC16P20,
+// EC16P4), 18 (the EC16P20L2 local stripe), 15 (EC15P12), 10 (EC10P4), 3 (EC3P3, the EC6P3L3
+// local stripe), 4 (EC4P4L2 and its local stripe, the EC6P6L9 local stripe), 7 (the EC6P8L10
+// local stripe).
+inline bool fixed_k(int k) {
+  switch (k) {
+    case 3: case 4: case 6: case 7: case 8: case 10: case 12: case 15: case 16: case 18: return true;
+    default: return false;
+  }
+}
 
 // Largest output count with a fixed-K kernel: EC6P10L2's 10 global + 2 local parities (6 x 12),
-// EC12P4 repairs of up to 12 rows, EC16P20L2's 20 + 2 (16 x 22) and up to 24 EC16P20 repair rows.
+// up to 12 EC12P4 / EC12P9 / EC15P12 repair rows, EC16P20L2's 20 + 2 (16 x 22) and up to 24
+// EC16P20 repair rows; 6 for the small stripes.
 constexpr int fixed_max_m(int k) {
-  return k == 6 ? 12 : k == 8 ? 8 : k == 12 ? 12 : k == 16 ? 24 : k == 18 ? 4 : 0;
+  return k == 6 || k == 12 || k == 15 ? 12 : k == 16 ? 24 : k == 8 ? 8 : k == 18 ? 4 : 6;
 }
 
 // Launch gf_matvec_k_kernel<K, m, MODE> on a (tiles of 4096 B, stripes) grid (defined in
@@ -87,8 +96,13 @@ inline DyPlan dyadic_plan(const uint8_t* coef, int m, int k) {
                                                                             dim3, hipStream_t);     \
   extern template hipError_t launch_k<K, MatVecMode::kVerify, fixed_max_m(K)>(int, const dev::GfArgs&, \
                                                                              dim3, hipStream_t);
+CFSEC_EXTERN_K(3)
+CFSEC_EXTERN_K(4)
 CFSEC_EXTERN_K(6)
+CFSEC_EXTERN_K(7)
 CFSEC_EXTERN_K(8)
+CFSEC_EXTERN_K(10)
+CFSEC_EXTERN_K(15)
 CFSEC_EXTERN_K(12)
 CFSEC_EXTERN_K(16)
 CFSEC_EXTERN_K(18)

@@ -60,4 +60,22 @@ hipError_t launch_matvec_crc(const MatVecJob& job, uint32_t* crc, int crc_stride
 // shift(~0, len) ^ ~0: XOR it into a raw (zero-preset) CRC of len bytes to get crc32.ChecksumIEEE.
 uint32_t crc32_shift_ones(size_t len);
 
+// blobstore/common/crc32block framing (crc32block.hip): blocks of block_len bytes, each the
+// little-endian crc32.ChecksumIEEE of its payload (block_len - 4 bytes, less in the last block)
+// followed by the payload.  Device pointers.
+struct Crc32BlockJob {
+  bool encode = true;
+  const uint8_t* in = nullptr;  // encode: the payload; decode: the framed object
+  uint8_t* out = nullptr;       // encode: the framed object (EncodeSize bytes); decode: to - from bytes
+  int64_t size = 0;             // payload bytes of the object
+  int64_t block_len = 0;        // positive multiple of 4096
+  int64_t from = 0, to = 0;     // decode: payload range (Decoder.Reader(from, to))
+  uint32_t* bad = nullptr;      // decode: device word preset to ~0; receives the smallest mismatching
+                                // block index relative to block from / (block_len - 4)
+  uint32_t* whole = nullptr;    // encode, optional: device word preset to 0; receives the raw
+                                // (zero-preset) CRC of the whole payload
+};
+bool crc32block_valid_len(int64_t block_len);  // util.go:34-36
+hipError_t launch_crc32block(const Crc32BlockJob& job, hipStream_t stream);
+
 }  // namespace cfsec

@@ -58,7 +58,9 @@ typedef enum {
   CFSEC_ERR_INVALID_SHARDS = 11,       /* ec.ErrInvalidShards           common/ec/encoder.go:37 */
   CFSEC_ERR_INVALID_ARG = 12,          /* boundary misuse (NULL handle, cap < shard size, ...) */
   CFSEC_ERR_DEVICE = 13,               /* HIP runtime failure; see cfsec_last_error()         */
-  CFSEC_ERR_NOT_SUPPORTED = 14         /* reedsolomon.ErrNotSupported   KRS/reedsolomon.go:212  */
+  CFSEC_ERR_NOT_SUPPORTED = 14,        /* reedsolomon.ErrNotSupported   KRS/reedsolomon.go:212  */
+  CFSEC_ERR_INVALID_BLOCK = 15,        /* crc32block.ErrInvalidBlock    common/crc32block/util.go:29 */
+  CFSEC_ERR_MISMATCHED_CRC = 16        /* crc32block.ErrMismatchedCrc   common/crc32block/util.go:30 */
 } cfsec_status;
 
 typedef enum { CFSEC_MEM_HOST = 0, CFSEC_MEM_DEVICE = 1 } cfsec_mem;
@@ -174,6 +176,32 @@ int cfsec_host_free(void* p);
 /* crc32.ChecksumIEEE of each device shard; out: host array of n uint32. Synchronous. */
 int cfsec_crc32_ieee_batch(uint8_t* const* ptrs, size_t shard_size, int n, uint32_t* out,
                            int device, void* stream);
+
+/* ---------------- crc32block framing (blobstore/common/crc32block) ---------------- */
+/* A framed object is a run of block_len-byte blocks (default 64 KiB; block_len a positive multiple
+ * of 4096), each the little-endian crc32.ChecksumIEEE of its payload followed by the payload
+ * (block_len - 4 bytes; fewer in the last block) -- block.go:34-49, encode.go:87-109.
+ * Sizes: EncodeSize / DecodeSize (util.go:50-65); -1 when block_len is invalid (the Go functions
+ * panic with ErrInvalidBlock) or the size is negative. */
+int64_t cfsec_crc32block_encode_size(int64_t size, int64_t block_len);
+int64_t cfsec_crc32block_decode_size(int64_t total, int64_t block_len);
+/* Encoder.Encode (encode.go:48-58, blobnode core/storage/datafile.go:345-373): frame `size` payload
+ * bytes of src into dst (cfsec_crc32block_encode_size bytes).  shard_crc (host, may be NULL)
+ * receives crc32.ChecksumIEEE of the whole payload, which datafile.go:345-373 computes on the way
+ * (shard.Crc).  One pass: every payload byte is read once and written once.  mem as for cfsec_rs_*:
+ * CFSEC_MEM_DEVICE pointers run on `stream` (NULL = an internal stream) on `device` (-1 = current);
+ * CFSEC_MEM_HOST buffers from cfsec_host_alloc are read and written in place, other host memory is
+ * staged through HBM.  Returns after completion. */
+int cfsec_crc32block_encode(const uint8_t* src, int64_t size, int64_t block_len, uint8_t* dst,
+                            uint32_t* shard_crc, int mem, int device, void* stream);
+/* Decoder.Reader(from, to) (decode.go:122-146; blobnode datafile.go:406-426): check the blocks of
+ * the framed object src (payload size `size`) that hold payload bytes [from, to) -- and the block
+ * holding `from` when from == to is not block-aligned, as the reference's skip does -- and copy
+ * those bytes to dst (to - from bytes; may be NULL when from == to).  CFSEC_ERR_MISMATCHED_CRC when a
+ * checked block's checksum differs; *bad_block (may be NULL) = index of the first such block, -1
+ * otherwise. */
+int cfsec_crc32block_decode(const uint8_t* src, int64_t size, int64_t block_len, int64_t from, int64_t to,
+                            uint8_t* dst, int64_t* bad_block, int mem, int device, void* stream);
 
 #ifdef __cplusplus
 }

@@ -158,3 +158,63 @@ def simd_code(rows: np.ndarray, inputs: list, outputs: list, threads: int, force
     if ret < 0:
         raise RuntimeError("SIMD path unavailable on this CPU")
     return ret
+
+
+# ---- crc32block framing (blobstore/common/crc32block), restated over the CRC above ----
+CRC32BLOCK_DEFAULT = 64 * 1024  # defaultCrc32BlockSize, block.go:22-24
+
+
+def crc32block_valid_len(block_len: int) -> bool:
+    """isValidBlockLen, util.go:34-36 (baseBlockLen = 1 << 12)."""
+    return block_len > 0 and block_len % 4096 == 0
+
+
+def crc32block_encode_size(size: int, block_len: int) -> int:
+    """EncodeSize, util.go:50-57."""
+    if not crc32block_valid_len(block_len):
+        raise ValueError("ErrInvalidBlock")
+    payload = block_len - 4
+    return size + 4 * ((size + payload - 1) // payload)
+
+
+def crc32block_decode_size(total: int, block_len: int) -> int:
+    """DecodeSize, util.go:59-65."""
+    if not crc32block_valid_len(block_len):
+        raise ValueError("ErrInvalidBlock")
+    return total - 4 * ((total + block_len - 1) // block_len)
+
+
+def crc32block_encode(payload: np.ndarray, block_len: int = CRC32BLOCK_DEFAULT) -> np.ndarray:
+    """limitEncoderReader.nextBlock (encode.go:87-109) + blockUnit.writeCrc (block.go:46-49): each
+    block is [LE crc32.ChecksumIEEE(payload piece)][payload piece of <= block_len - 4 bytes]."""
+    payload = np.ascontiguousarray(payload, np.uint8)
+    out = np.empty(crc32block_encode_size(payload.size, block_len), np.uint8)
+    P = block_len - 4
+    for b, q in enumerate(range(0, payload.size, P)):
+        piece = payload[q:q + P]
+        o = b * block_len
+        out[o:o + 4] = np.frombuffer(int(crc32_ieee(piece)).to_bytes(4, "little"), np.uint8)
+        out[o + 4:o + 4 + piece.size] = piece
+    return out
+
+
+def crc32block_decode(framed: np.ndarray, size: int, from_: int, to: int, block_len: int = CRC32BLOCK_DEFAULT):
+    """Decoder.Reader(from, to) read to EOF (decode.go:122-146): blockReader.nextBlock checks each
+    block it reads (decode.go:85-108) starting at the block holding `from`; rangeReader skips
+    from % payload bytes (reading -- and checking -- that block even when from == to) and stops
+    after to - from bytes.  Returns (bytes, index of the first bad block or -1)."""
+    P = block_len - 4
+    if not crc32block_valid_len(block_len) or not 0 <= from_ <= to <= size:
+        raise ValueError("invalid range")
+    b0 = from_ // P
+    b1 = (to - 1) // P if from_ < to else (b0 if from_ % P else b0 - 1)
+    got = bytearray()
+    for b in range(b0, b1 + 1):
+        plen = min(P, size - b * P)
+        blk = framed[b * block_len:b * block_len + 4 + plen]
+        if int.from_bytes(bytes(blk[:4]), "little") != crc32_ieee(np.ascontiguousarray(blk[4:])):
+            return np.frombuffer(bytes(got), np.uint8), b
+        lo, hi = max(from_, b * P), min(to, b * P + plen)
+        if lo < hi:
+            got += bytes(blk[4 + lo - b * P:4 + hi - b * P])
+    return np.frombuffer(bytes(got), np.uint8), -1

@@ -133,7 +133,7 @@ def test_encode_many_inputs_chunked(rs):
         assert np.array_equal(got[i], want[i])
 
 
-FIXED_MAX_M = {6: 12, 8: 8, 12: 12, 16: 24, 18: 4}  # gf_launch.hpp fixed_max_m
+FIXED_MAX_M = {3: 6, 4: 6, 6: 12, 7: 6, 8: 8, 10: 6, 12: 12, 15: 12, 16: 24, 18: 4}  # gf_launch.hpp fixed_max_m
 
 
 @pytest.mark.parametrize("k,m", [(k, m) for k, top in FIXED_MAX_M.items() for m in range(1, top + 2)])
