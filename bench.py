@@ -261,6 +261,25 @@ def main():
     # coding kernel: same algorithmic bytes as the encode
     crcs = torch.zeros(nst * total, dtype=torch.int32, device=dev)
     crc_ms = timed(lambda: enc.encode_crc_batch(ptrs, S, nst, crcs.data_ptr(), stream=stream), n_op)
+    # Blobnode's write path frames each shard in 64 KiB crc32block blocks and takes the shard's
+    # checksum on the way (core/storage/datafile.go:345-373); its read path checks and unframes them
+    # (datafile.go:406-426).  All 16 shards of every stripe in one framing / one checking launch.
+    from chubaofs_amd import crc32block
+    nsh = nst * total
+    flen = crc32block.EncodeSize(S)
+    framed = torch.empty((nsh, flen), dtype=torch.uint8, device=dev)
+    unframed = torch.empty((nsh, S), dtype=torch.uint8, device=dev)
+    fptrs = (ctypes.c_void_p * nsh)(*[framed[i].data_ptr() for i in range(nsh)])
+    uptrs = (ctypes.c_void_p * nsh)(*[unframed[i].data_ptr() for i in range(nsh)])
+    fcrc = torch.zeros(nsh, dtype=torch.int32, device=dev)
+    fbad = torch.zeros(nsh, dtype=torch.int32, device=dev)
+    blk_enc_ms = timed(lambda: crc32block.encode_batch(ptrs, fptrs, S, shard_crcs_ptr=fcrc.data_ptr(),
+                                                       stream=stream), n_op)
+    blk_dec_ms = timed(lambda: crc32block.decode_batch(fptrs, uptrs, S, fbad.data_ptr(), stream=stream), n_op)
+    assert bool((fbad == -1).all().item()), "crc32block check failed on freshly framed shards"
+    assert torch.equal(unframed.view(nst, total, S), batch[:, :, :S]), "crc32block round trip differs"
+    blk_bytes = nsh * (S + flen)  # read the payload and write the frames, or the reverse
+    del framed, unframed
 
     data_bytes = K_DATA * S * nst
     launch_bytes = (K_DATA + M_PARITY) * S * nst  # algorithmic bytes per launch (read 12S + write 4S)
@@ -310,6 +329,10 @@ def main():
         "verify_roofline_frac": round(launch_bytes / (verify_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
         "encode_crc_data_GBps": round(data_bytes / (crc_ms * 1e-3) / 1e9, 1),
         "encode_crc_roofline_frac": round(launch_bytes / (crc_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+        "crc32block_encode_data_GBps": round(nsh * S / (blk_enc_ms * 1e-3) / 1e9, 1),
+        "crc32block_encode_roofline_frac": round(blk_bytes / (blk_enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+        "crc32block_decode_data_GBps": round(nsh * S / (blk_dec_ms * 1e-3) / 1e9, 1),
+        "crc32block_decode_roofline_frac": round(blk_bytes / (blk_dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
         "cpu_baseline": cpu,
     }
     print(json.dumps(out), flush=True)

@@ -21,7 +21,7 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from ._shards import _is_torch, _nbytes, _ptr, stream_ptr
+from ._shards import _is_torch, _nbytes, _ptr, ptr_array, stream_ptr
 
 DefaultBlockSize = 64 * 1024  # defaultCrc32BlockSize, block.go:22-24
 
@@ -98,3 +98,21 @@ def Decode(src, size: int, from_: int = 0, to: int | None = None, block_len: int
         raise e
     _lib.check(st)
     return dst
+
+
+def encode_batch(srcs, dsts, size: int, block_len: int = DefaultBlockSize, shard_crcs_ptr=None, stream=None):
+    """cfsec_crc32block_encode_batch: frame n device payloads of `size` bytes (pointer lists) into
+    n framed buffers; shard_crcs_ptr (device, n uint32) receives each payload's ChecksumIEEE.
+    Asynchronous on `stream`."""
+    _lib.check(_lib.lib().cfsec_crc32block_encode_batch(ptr_array(srcs), ptr_array(dsts), len(srcs), int(size),
+                                                        int(block_len), shard_crcs_ptr, stream_ptr(stream)))
+
+
+def decode_batch(srcs, dsts, size: int, bad_ptr: int, from_: int = 0, to: int | None = None,
+                 block_len: int = DefaultBlockSize, stream=None):
+    """cfsec_crc32block_decode_batch: check and unframe payload [from_, to) of n framed device
+    objects; bad_ptr (device, n uint32) receives per object the first bad block or 0xFFFFFFFF."""
+    to = size if to is None else int(to)
+    _lib.check(_lib.lib().cfsec_crc32block_decode_batch(ptr_array(srcs), ptr_array(dsts) if dsts else None,
+                                                        len(srcs), int(size), int(block_len), int(from_), to,
+                                                        bad_ptr, stream_ptr(stream)))

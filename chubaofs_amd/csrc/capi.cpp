@@ -126,8 +126,9 @@ int crc32block_call(bool encode, const uint8_t* src, int64_t size, int64_t block
     if (st == CFSEC_OK) st = cfsec::hip_status(hipMemsetAsync(ws->dflags + 1, 0, 4, s), "hipMemsetAsync");
     cfsec::Crc32BlockJob j;
     j.encode = encode;
-    j.in = din;
-    j.out = dout;
+    j.n = 1;
+    j.in = &din;
+    j.out = &dout;
     j.size = size;
     j.block_len = block_len;
     j.from = from;
@@ -143,7 +144,7 @@ int crc32block_call(bool encode, const uint8_t* src, int64_t size, int64_t block
     const int sync = cfsec::hip_status(hipStreamSynchronize(s), "hipStreamSynchronize");
     if (st == CFSEC_OK) st = sync;
     if (st == CFSEC_OK) {
-      if (encode && shard_crc) *shard_crc = ws->hflags[1] ^ cfsec::crc32_shift_ones((size_t)size);
+      if (encode && shard_crc) *shard_crc = ws->hflags[1];
       if (!encode && ws->hflags[0] != 0xFFFFFFFFu) {
         if (bad_block) *bad_block = b0 + (int64_t)ws->hflags[0];
         st = CFSEC_ERR_MISMATCHED_CRC;
@@ -430,6 +431,53 @@ int cfsec_crc32block_encode(const uint8_t* src, int64_t size, int64_t block_len,
 int cfsec_crc32block_decode(const uint8_t* src, int64_t size, int64_t block_len, int64_t from, int64_t to,
                             uint8_t* dst, int64_t* bad_block, int mem, int device, void* stream) {
   return crc32block_call(false, src, size, block_len, from, to, dst, nullptr, bad_block, mem, device, stream);
+}
+
+int cfsec_crc32block_encode_batch(const uint8_t* const* srcs, uint8_t* const* dsts, int n, int64_t size,
+                                  int64_t block_len, uint32_t* shard_crcs, void* stream) {
+  if (!cfsec::crc32block_valid_len(block_len)) return CFSEC_ERR_INVALID_BLOCK;
+  if (n < 0 || size < 0 || (n > 0 && (!srcs || !dsts))) return CFSEC_ERR_INVALID_ARG;
+  return guarded([&] {
+    hipStream_t s = as_stream(stream);
+    int st = CFSEC_OK;
+    if (shard_crcs && n > 0)
+      st = cfsec::hip_status(hipMemsetAsync(shard_crcs, 0, 4 * (size_t)n, s), "hipMemsetAsync");
+    cfsec::Crc32BlockJob j;
+    j.encode = true;
+    j.n = n;
+    j.in = srcs;
+    j.out = dsts;
+    j.size = size;
+    j.block_len = block_len;
+    j.whole = shard_crcs;
+    if (st == CFSEC_OK) st = cfsec::hip_status(cfsec::launch_crc32block(j, s), "launch_crc32block");
+    return st;
+  });
+}
+
+int cfsec_crc32block_decode_batch(const uint8_t* const* srcs, uint8_t* const* dsts, int n, int64_t size,
+                                  int64_t block_len, int64_t from, int64_t to, uint32_t* bad, void* stream) {
+  if (!cfsec::crc32block_valid_len(block_len)) return CFSEC_ERR_INVALID_BLOCK;
+  if (n < 0 || size < 0 || from < 0 || from > to || to > size || (n > 0 && (!srcs || !bad)) ||
+      (n > 0 && to > from && !dsts))
+    return CFSEC_ERR_INVALID_ARG;
+  return guarded([&] {
+    hipStream_t s = as_stream(stream);
+    int st = CFSEC_OK;
+    if (n > 0) st = cfsec::hip_status(hipMemsetAsync(bad, 0xFF, 4 * (size_t)n, s), "hipMemsetAsync");
+    cfsec::Crc32BlockJob j;
+    j.encode = false;
+    j.n = n;
+    j.in = srcs;
+    j.out = dsts;
+    j.size = size;
+    j.block_len = block_len;
+    j.from = from;
+    j.to = to;
+    j.bad = bad;
+    if (st == CFSEC_OK) st = cfsec::hip_status(cfsec::launch_crc32block(j, s), "launch_crc32block");
+    return st;
+  });
 }
 
 }  // extern "C"

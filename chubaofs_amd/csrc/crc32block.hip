@@ -7,8 +7,10 @@
 // whole shard on the way (core/storage/datafile.go:345-373) -- and checks the frames of the range
 // it reads back (datafile.go:406-426 -> Decoder.Reader, decode.go:122-146).
 //
-// One kernel does both directions: workgroup w owns block b0 + w, streams its payload in 4 KiB
-// tiles (thread j: the 16-byte piece j of each tile, the next tile's piece in flight), folds every
+// One kernel does both directions over a batch of equally sized objects (grid y): workgroup (w, y)
+// owns block b0 + w of object y, streams its payload in 4 KiB tiles cut at 16-byte boundaries of
+// the destination (thread j: the 16-byte piece j of each tile, the next tile's piece in flight;
+// loads may be unaligned, stores are aligned), folds every
 // piece into a Horner register with the slice-by-8 LDS tables of the shard CRC kernels (gf_crc.hpp:
 // R <- f(shift(R, 4080), piece)), and copies the piece to its destination.  After the last tile a
 // per-thread basis moves R to the tile end, the workgroup XOR-reduces, and one multiply by
@@ -16,7 +18,8 @@
 // (zero-preset) CRC of the payload; XOR-ing shift(~0, plen) ^ ~0 makes it ChecksumIEEE.  Encode
 // writes that in front of the block; decode compares it with the stored word and atomicMin's the
 // block index into `bad`.  The whole-object checksum is the XOR of every block's raw CRC moved to
-// the object end, x^(8 * bytes after the block) -- computed per block from a table of x^(8P 2^i).
+// the object end, x^(8 * bytes after the block) -- computed per block from a table of x^(8P 2^i) --
+// with shift(~0, size) ^ ~0 folded in by the last block, so the accumulated word is ChecksumIEEE.
 // Every payload byte is read once and written once.
 #include <algorithm>
 
@@ -24,115 +27,178 @@
 #include "kernels.hpp"
 
 namespace cfsec {
-namespace {
+namespace blk {
 
 using crcdev::kTabWords;
 using crcdev::kTile;
 using dev::u32x4;
 
+constexpr int kSlots = 96;  // objects per launch
+constexpr int kRing = 4;    // tiles in flight per thread
+
 struct __attribute__((aligned(16))) BlockArgs {
-  const uint8_t* in;  // payload of launch block w at in + w*in_stride + in_off
-  uint8_t* out;       // its payload byte o at out + w*out_stride + out_off + o, if lo <= b*P + o < hi
+  const uint8_t* in[kSlots];  // object y: payload of launch block w at in[y] + w*in_stride + in_off
+  uint8_t* out[kSlots];       // its payload byte o at out[y] + w*out_stride + out_off + o, if lo <= b*P + o < hi
   const uint32_t* tabs;
-  uint32_t* bad;      // decode: smallest mismatching launch block index
-  uint32_t* whole;    // encode, optional: raw CRC of the whole object, atomicXor-accumulated
+  uint32_t* bad;      // decode: [object] smallest mismatching launch block index
+  uint32_t* whole;    // encode, optional: [object] raw CRC of the whole object, atomicXor-accumulated
   int64_t in_stride, in_off, out_stride, out_off;
   uint64_t size, lo, hi;  // payload size of the object; copied payload range
   uint64_t b0, nblk;      // first block of the launch; blocks in the object
+  uint32_t nb, items;     // blocks per object in the launch; nb * objects
   uint32_t P;             // payload bytes of a full block
   uint32_t encode;        // 1: write the checksum at out + w*out_stride; 0: check in + w*in_stride
-  uint32_t gconst[2], fin[2];  // [full block, last block]
+  uint32_t gconst[2][16];      // [full block, last block][h]: x^(8(plen + h - tiles*4096))
+  uint32_t fin[2];             // [full block, last block]: shift(~0, plen) ^ ~0
   uint32_t xlast;              // x^(8 * payload of the last block)
+  uint32_t xlen[2];            // x^(8 plen): [full block, last block]
+  uint32_t ipw;                // items per workgroup
+  uint32_t whole_fin;          // shift(~0, size) ^ ~0
   uint32_t xpow2[40];          // x^(8 P 2^i) for 2^i <= nblk
 };
 
-__device__ __forceinline__ void load_piece(const uint8_t* p, uint32_t plen, uint32_t off, uint32_t (&d)[4]) {
+// Bytes [lo, hi) of the 16 at p, zero elsewhere.
+__device__ __forceinline__ u32x4 ld_range(const uint8_t* p, uint32_t lo, uint32_t hi) {
+  uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (uint32_t i = 0; i < 16; ++i)
+    if (i >= lo && i < hi) w[i >> 2] |= (uint32_t)p[i] << (8 * (i & 3));
+  return u32x4{w[0], w[1], w[2], w[3]};
+}
+
+// Piece p of a block: the 16 payload positions 16p - h .. 16p - h + 15, i.e. one 16-byte-aligned
+// chunk of the destination (h = destination misalignment of payload byte 0), so every full store
+// is aligned; positions outside [0, plen) read as zero (leading zeros leave a zero-preset CRC
+// unchanged, trailing ones are taken out by gconst).
+__device__ __forceinline__ void load_piece(const uint8_t* src, uint32_t plen, uint32_t h, uint32_t p,
+                                           uint32_t (&d)[4]) {
+  const int64_t first = (int64_t)16 * p - h;  // payload index of byte 0 of the piece
   u32x4 v{0u, 0u, 0u, 0u};
-  if (off + dev::kLaneBytes <= plen)
-    v = dev::ld16<true>(p + off);
-  else if (off < plen)
-    v = dev::ld_tail(p + off, plen - off);  // zero padding past the payload end
+  if (first >= 0 && first + 16 <= plen)
+    v = dev::ld16<true>(src + first);
+  else if (first < (int64_t)plen)
+    v = ld_range(src + first, first < 0 ? (uint32_t)-first : 0u, (uint32_t)min<int64_t>(16, plen - first));
   d[0] = v.x, d[1] = v.y, d[2] = v.z, d[3] = v.w;
 }
 
+// STORE / CRC / EPI off, SRCALIGN on: measurement variants for tools/blk_probe.hip (the product
+// runs STORE, CRC and EPI on, pieces aligned to the destination).
+template <bool STORE = true, bool CRC = true, bool EPI = true, bool SRCALIGN = false, bool NTS = true>
 __global__ __launch_bounds__(256) void crc32block_kernel(const BlockArgs a) {
   __shared__ uint32_t ct[kTabWords];
   __shared__ uint32_t red[4];
   for (int i = threadIdx.x; i < kTabWords; i += 256) ct[i] = a.tabs[i];
+  // this thread's x^(8*16*(255 - j)): moves its Horner register from its piece to the tile end
+  // (column x^0 of its basis, gf_crc.hip host_tables)
+  const uint32_t kj = a.tabs[kTabWords + threadIdx.x * 32 + 31];
   __syncthreads();
-  const uint32_t w = blockIdx.x;
-  const uint64_t b = a.b0 + w;
-  const uint64_t q0 = b * a.P;  // payload coordinate of the block's first byte
-  const uint32_t plen = (uint32_t)min<uint64_t>(a.P, a.size - q0);
-  const int last = plen != a.P ? 1 : 0;
-  const uint8_t* src = a.in + (int64_t)w * a.in_stride + a.in_off;
-  const int64_t dbase = (int64_t)w * a.out_stride + a.out_off;  // out offset of payload byte 0
-  const uint32_t tiles = (plen + kTile - 1) / kTile;
-  const uint32_t lanepos = threadIdx.x * dev::kLaneBytes;
-  uint32_t R = 0, cur[4], nxt[4];
-  load_piece(src, plen, lanepos, cur);
-  for (uint32_t t = 0; t < tiles; ++t) {
-    const uint32_t o = t * kTile + lanepos;
-    if (t + 1 < tiles) load_piece(src, plen, o + kTile, nxt);
-    R = crcdev::crc_step(ct, R, cur);
-    if (o < plen) {
-      const uint64_t q = q0 + o;
-      const uint32_t n = min<uint32_t>(dev::kLaneBytes, plen - o);
-      if (n == dev::kLaneBytes && q >= a.lo && q + n <= a.hi) {
-        dev::st16<true>(a.out + dbase + o, u32x4{cur[0], cur[1], cur[2], cur[3]});
-      } else {
-        for (uint32_t j = 0; j < n; ++j)
-          if (q + j >= a.lo && q + j < a.hi) a.out[dbase + o + j] = (uint8_t)(cur[j >> 2] >> (8 * (j & 3)));
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) cur[i] = nxt[i];
-  }
-  const u32x4* basis = reinterpret_cast<const u32x4*>(a.tabs + kTabWords + threadIdx.x * 32);
-  uint32_t v = 0;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const u32x4 bv = basis[q];
-    v ^= (0u - ((R >> (4 * q)) & 1u)) & bv.x;
-    v ^= (0u - ((R >> (4 * q + 1)) & 1u)) & bv.y;
-    v ^= (0u - ((R >> (4 * q + 2)) & 1u)) & bv.z;
-    v ^= (0u - ((R >> (4 * q + 3)) & 1u)) & bv.w;
-  }
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) v ^= (uint32_t)__shfl_xor((int)v, d);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t raw = crcdev::mulmod(a.gconst[last], red[0] ^ red[1] ^ red[2] ^ red[3]);
-    const uint32_t crc = raw ^ a.fin[last];
-    if (a.encode) {
-      uint8_t* h = a.out + (int64_t)w * a.out_stride;
-      for (int j = 0; j < 4; ++j) h[j] = (uint8_t)(crc >> (8 * j));
-      if (a.whole) {
-        // bytes after block b: none for the last block, else the last block's payload plus
-        // nblk - 2 - b full blocks
-        uint32_t s = raw;
-        if (b + 1 < a.nblk) {
-          s = crcdev::mulmod(s, a.xlast);
-          uint64_t e = a.nblk - 2 - b;
-          for (int i = 0; e; e >>= 1, ++i)
-            if (e & 1) s = crcdev::mulmod(s, a.xpow2[i]);
-        }
-        atomicXor(a.whole, s);
-      }
+  // work items (launch block w, object y), y-major; a workgroup takes a run of consecutive ones,
+  // so the table load above is paid once per workgroup and the whole-object checksum is a Horner
+  // sum over the run (acc <- acc * x^(8 plen) ^ raw) moved to the object end once per run
+  const uint32_t it0 = blockIdx.x * a.ipw, it1 = min(it0 + a.ipw, a.items);
+  uint32_t acc = 0, run_y = 0xFFFFFFFFu, run_end = 0;  // thread 0: the run's raw CRC, object, next block
+  const auto flush = [&]() {
+    if (threadIdx.x != 0 || !a.whole || run_y == 0xFFFFFFFFu) return;
+    uint32_t s = acc;
+    if (run_end == a.nblk) {
+      s ^= a.whole_fin;  // the run ends the object: fold in the conditioning once per object
     } else {
-      const uint8_t* h = a.in + (int64_t)w * a.in_stride;
-      const uint32_t stored = h[0] | (uint32_t)h[1] << 8 | (uint32_t)h[2] << 16 | (uint32_t)h[3] << 24;
-      if (stored != crc) atomicMin(a.bad, w);
+      // bytes after the run: nblk - 1 - run_end full blocks, then the last block's payload
+      s = crcdev::mulmod(s, a.xlast);
+      uint64_t e = a.nblk - 1 - run_end;
+      for (int i = 0; e; e >>= 1, ++i)
+        if (e & 1) s = crcdev::mulmod(s, a.xpow2[i]);
     }
+    atomicXor(a.whole + run_y, s);
+  };
+  for (uint32_t it = it0; it < it1; ++it) {
+    const uint32_t y = it / a.nb, w = it - y * a.nb;
+    if (y != run_y) {
+      flush();
+      acc = 0;
+      run_y = y;
+    }
+    const uint8_t* const in = a.in[y];
+    uint8_t* const out = a.out[y];
+    const uint64_t b = a.b0 + w;
+    const uint64_t q0 = b * a.P;  // payload coordinate of the block's first byte
+    const uint32_t plen = (uint32_t)min<uint64_t>(a.P, a.size - q0);
+    const int last = plen != a.P ? 1 : 0;
+    const uint8_t* src = in + (int64_t)w * a.in_stride + a.in_off;
+    const int64_t dbase = (int64_t)w * a.out_stride + a.out_off;  // out offset of payload byte 0
+    const uint32_t h = SRCALIGN ? (uint32_t)((uintptr_t)src & 15u) : (uint32_t)(((uintptr_t)out + (uint64_t)dbase) & 15u);
+    const uint32_t tiles = (plen + h + kTile - 1) / kTile;
+    // kRing tiles' pieces in flight per thread, in a ring of registers named at compile time (the
+    // tile loop is unrolled by kRing): moving a register that an outstanding load targets would
+    // make the wave wait for that load, which is what a rotating prefetch buffer does
+    uint32_t R = 0, ring[kRing][4];
+#pragma unroll
+    for (int k = 0; k < kRing; ++k)
+      if (k < (int)tiles) load_piece(src, plen, h, threadIdx.x + 256 * k, ring[k]);
+    for (uint32_t t0 = 0; t0 < tiles; t0 += kRing) {
+#pragma unroll
+      for (int k = 0; k < kRing; ++k) {
+        const uint32_t t = t0 + k;
+        if (t < tiles) {
+          uint32_t (&cur)[4] = ring[k];
+          const uint32_t p = t * 256 + threadIdx.x;
+          if constexpr (CRC) R = crcdev::crc_step(ct, R, cur);
+          else R ^= cur[0] ^ cur[1] ^ cur[2] ^ cur[3];
+          const int64_t first = (int64_t)16 * p - h;
+          if (STORE && first < (int64_t)plen) {
+            const int64_t q = (int64_t)q0 + first;  // payload coordinate of the piece's byte 0
+            uint8_t* dp = out + (dbase + first);    // 16-byte aligned
+            if (first >= 0 && first + 16 <= plen && q >= (int64_t)a.lo && q + 16 <= (int64_t)a.hi) {
+              dev::st16<NTS>(dp, u32x4{cur[0], cur[1], cur[2], cur[3]});
+            } else {
+              for (int j = 0; j < 16; ++j)
+                if (first + j >= 0 && first + j < plen && q + j >= (int64_t)a.lo && q + j < (int64_t)a.hi)
+                  dp[j] = (uint8_t)(cur[j >> 2] >> (8 * (j & 3)));
+            }
+          }
+          if (t + kRing < tiles) load_piece(src, plen, h, p + 256 * kRing, cur);
+        }
+      }
+    }
+    if constexpr (!EPI) {
+      if (R == 0x12345678u) a.bad[0] = R;  // keep the loads live
+      run_y = 0xFFFFFFFFu;
+      continue;
+    }
+    uint32_t v = crcdev::mulmod(kj, R);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v ^= (uint32_t)__shfl_xor((int)v, d);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint32_t raw = crcdev::mulmod(a.gconst[last][h], red[0] ^ red[1] ^ red[2] ^ red[3]);
+      const uint32_t crc = raw ^ a.fin[last];
+      if (a.encode) {
+        uint8_t* hdr = out + (int64_t)w * a.out_stride;
+        for (int j = 0; j < 4; ++j) hdr[j] = (uint8_t)(crc >> (8 * j));
+        if (a.whole) acc = crcdev::mulmod(acc, a.xlen[last]) ^ raw;
+        run_end = (uint32_t)b + 1;
+      } else {
+        const uint8_t* hdr = in + (int64_t)w * a.in_stride;
+        const uint32_t stored = hdr[0] | (uint32_t)hdr[1] << 8 | (uint32_t)hdr[2] << 16 | (uint32_t)hdr[3] << 24;
+        if (stored != crc) atomicMin(a.bad + y, w);
+      }
+    }
+    __syncthreads();  // red[] is reused by the next item
   }
+  flush();
 }
 
-}  // namespace
+}  // namespace blk
+
+using blk::BlockArgs;
+using blk::kSlots;
 
 bool crc32block_valid_len(int64_t block_len) { return block_len > 0 && block_len % 4096 == 0; }
 
-hipError_t launch_crc32block(const Crc32BlockJob& j, hipStream_t stream) {
+namespace blk {
+template <bool STORE, bool CRC, bool EPI = true, bool SRCALIGN = false, bool ONE = true, bool NTS = true>
+hipError_t launch(const Crc32BlockJob& j, hipStream_t stream) {
   if (!crc32block_valid_len(j.block_len) || j.size < 0 || j.block_len > 0xFFFFFFFFll) return hipErrorInvalidValue;
   const int64_t P = j.block_len - 4;
   const int64_t nblk = (j.size + P - 1) / P;
@@ -159,12 +225,9 @@ hipError_t launch_crc32block(const Crc32BlockJob& j, hipStream_t stream) {
     a.in_stride = j.block_len, a.in_off = 4;
     a.out_stride = P, a.out_off = b0 * P - j.from;
   }
-  if (nb <= 0) return hipSuccess;
-  if (nb > 0x7FFFFFFF || !j.in || (!j.out && (j.encode || j.to > j.from)) || (!j.encode && !j.bad))
+  if (nb <= 0 || j.n == 0) return hipSuccess;
+  if (nb > 0xFFFFFFFFll / kSlots || j.n < 0 || !j.in || (!j.out && (j.encode || j.to > j.from)) || (!j.encode && !j.bad))
     return hipErrorInvalidValue;
-  // decode: j.in is the framed object; the launch starts at block b0
-  a.in = j.encode ? j.in : j.in + b0 * j.block_len;
-  a.out = j.out;
   a.bad = j.bad;
   a.whole = j.encode ? j.whole : nullptr;
   a.b0 = (uint64_t)b0;
@@ -172,14 +235,42 @@ hipError_t launch_crc32block(const Crc32BlockJob& j, hipStream_t stream) {
   if (e != hipSuccess) return e;
   const int64_t plens[2] = {P, j.size - (nblk - 1) * P};
   for (int i = 0; i < 2; ++i) {
-    const int64_t tiles = (plens[i] + kTile - 1) / kTile;
-    a.gconst[i] = crc_xpow(8 * (plens[i] - tiles * kTile));
+    for (int h = 0; h < 16; ++h) {
+      const int64_t tiles = (plens[i] + h + kTile - 1) / kTile;
+      a.gconst[i][h] = crc_xpow(8 * (plens[i] + h - tiles * kTile));
+    }
     a.fin[i] = crc32_shift_ones((size_t)plens[i]);
   }
   a.xlast = crc_xpow(8 * plens[1]);
+  a.xlen[0] = crc_xpow(8 * plens[0]);
+  a.xlen[1] = a.xlast;
+  a.whole_fin = crc32_shift_ones((size_t)j.size);
   for (int i = 0; i < 40 && (int64_t(1) << i) <= nblk; ++i) a.xpow2[i] = crc_xpow(8 * P * (int64_t(1) << i));
-  hipLaunchKernelGGL(crc32block_kernel, dim3((unsigned)nb), dim3(256), 0, stream, a);
-  return hipGetLastError();
+  for (int y0 = 0; y0 < j.n; y0 += kSlots) {
+    const int ny = std::min(kSlots, j.n - y0);
+    for (int y = 0; y < ny; ++y) {
+      if (!j.in[y0 + y] || ((!j.out || !j.out[y0 + y]) && (j.encode || j.to > j.from))) return hipErrorInvalidValue;
+      // decode: in[] are the framed objects; the launch starts at block b0
+      a.in[y] = j.encode ? j.in[y0 + y] : j.in[y0 + y] + b0 * j.block_len;
+      a.out[y] = j.out ? j.out[y0 + y] : nullptr;
+    }
+    a.nb = (uint32_t)nb;
+    a.items = (uint32_t)(nb * ny);
+    // one block per workgroup measured best (tools/blk_probe.hip, profiles/r01/crc32block_probe.txt:
+    // runs of ~5 blocks per workgroup, sharing one table load, were 5-10 % slower)
+    a.ipw = ONE ? 1u : (a.items + 2047) / 2048;
+    const unsigned grid = (a.items + a.ipw - 1) / a.ipw;
+    hipLaunchKernelGGL((crc32block_kernel<STORE, CRC, EPI, SRCALIGN, NTS>), dim3(grid), dim3(256), 0, stream, a);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if (a.bad) a.bad += ny;
+    if (a.whole) a.whole += ny;
+  }
+  return hipSuccess;
 }
+
+}  // namespace blk
+
+hipError_t launch_crc32block(const Crc32BlockJob& j, hipStream_t stream) { return blk::launch<true, true>(j, stream); }
 
 }  // namespace cfsec

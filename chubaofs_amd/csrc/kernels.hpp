@@ -65,15 +65,17 @@ uint32_t crc32_shift_ones(size_t len);
 // followed by the payload.  Device pointers.
 struct Crc32BlockJob {
   bool encode = true;
-  const uint8_t* in = nullptr;  // encode: the payload; decode: the framed object
-  uint8_t* out = nullptr;       // encode: the framed object (EncodeSize bytes); decode: to - from bytes
-  int64_t size = 0;             // payload bytes of the object
-  int64_t block_len = 0;        // positive multiple of 4096
-  int64_t from = 0, to = 0;     // decode: payload range (Decoder.Reader(from, to))
-  uint32_t* bad = nullptr;      // decode: device word preset to ~0; receives the smallest mismatching
-                                // block index relative to block from / (block_len - 4)
-  uint32_t* whole = nullptr;    // encode, optional: device word preset to 0; receives the raw
-                                // (zero-preset) CRC of the whole payload
+  int n = 1;                           // objects, all of the same payload size
+  const uint8_t* const* in = nullptr;  // host array [n]: encode: payloads; decode: framed objects
+  uint8_t* const* out = nullptr;       // host array [n]: encode: framed objects (EncodeSize bytes);
+                                       // decode: to - from bytes each
+  int64_t size = 0;                    // payload bytes of each object
+  int64_t block_len = 0;               // positive multiple of 4096
+  int64_t from = 0, to = 0;            // decode: payload range (Decoder.Reader(from, to))
+  uint32_t* bad = nullptr;    // decode: device words [n] preset to ~0; receive the smallest mismatching
+                              // block index relative to block from / (block_len - 4)
+  uint32_t* whole = nullptr;  // encode, optional: device words [n] preset to 0; receive
+                              // crc32.ChecksumIEEE of each whole payload
 };
 bool crc32block_valid_len(int64_t block_len);  // util.go:34-36
 hipError_t launch_crc32block(const Crc32BlockJob& job, hipStream_t stream);

@@ -202,6 +202,15 @@ int cfsec_crc32block_encode(const uint8_t* src, int64_t size, int64_t block_len,
  * otherwise. */
 int cfsec_crc32block_decode(const uint8_t* src, int64_t size, int64_t block_len, int64_t from, int64_t to,
                             uint8_t* dst, int64_t* bad_block, int mem, int device, void* stream);
+/* Batch forms on device memory, asynchronous on `stream` (NULL = the null stream): n objects of one
+ * payload size -- the shards of a stripe batch (blobnode puts and repairs).  encode: shard_crcs
+ * (device, n words, may be NULL) receives each payload's crc32.ChecksumIEEE.  decode: checks and
+ * unframes payload range [from, to) of each object; bad (device, n words) receives per object the
+ * index of the first mismatching block counted from block from / (block_len - 4), or 0xFFFFFFFF. */
+int cfsec_crc32block_encode_batch(const uint8_t* const* srcs, uint8_t* const* dsts, int n, int64_t size,
+                                  int64_t block_len, uint32_t* shard_crcs, void* stream);
+int cfsec_crc32block_decode_batch(const uint8_t* const* srcs, uint8_t* const* dsts, int n, int64_t size,
+                                  int64_t block_len, int64_t from, int64_t to, uint32_t* bad, void* stream);
 
 #ifdef __cplusplus
 }

@@ -133,3 +133,31 @@ def test_large_roundtrip_and_shard_crc(C):
     assert np.array_equal(framed.cpu().numpy(), O.crc32block_encode(h))
     back = C.Decode(framed, size)
     assert torch.equal(back, d)
+
+
+@pytest.mark.parametrize("n,size", [(1, 1), (3, 64 * K - 4), (16, 349526), (130, 4097)])
+def test_batch_encode_decode(C, n, size):
+    """cfsec_crc32block_{encode,decode}_batch: n objects of one size (> 96 spans launches)."""
+    framed_len = C.EncodeSize(size)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(n * 1000 + size)
+    src = torch.randint(0, 256, (n, size), generator=g, device="cuda", dtype=torch.uint8)
+    dst = torch.full((n, framed_len), 0xEE, dtype=torch.uint8, device="cuda")
+    crcs = torch.full((n,), 7, dtype=torch.int32, device="cuda")
+    C.encode_batch([src[i].data_ptr() for i in range(n)], [dst[i].data_ptr() for i in range(n)], size,
+                   shard_crcs_ptr=crcs.data_ptr())
+    h, f = src.cpu().numpy(), dst.cpu().numpy()
+    words = crcs.cpu().numpy().view(np.uint32)
+    for i in range(n):
+        assert np.array_equal(f[i], O.crc32block_encode(h[i])), i
+        assert int(words[i]) == zlib.crc32(h[i].tobytes()) & 0xFFFFFFFF, i
+    # corrupt object n-1's last block, then decode everything back
+    dst[n - 1, framed_len - 1] ^= 1
+    back = torch.zeros_like(src)
+    bad = torch.zeros(n, dtype=torch.int32, device="cuda")
+    C.decode_batch([dst[i].data_ptr() for i in range(n)], [back[i].data_ptr() for i in range(n)], size,
+                   bad.data_ptr())
+    b = bad.cpu().numpy().view(np.uint32)
+    nblk = (size + 64 * K - 5) // (64 * K - 4)
+    assert list(b[:-1]) == [0xFFFFFFFF] * (n - 1) and int(b[-1]) == nblk - 1
+    assert torch.equal(back[:-1], src[:-1])

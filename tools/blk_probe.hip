@@ -1,0 +1,110 @@
+// blk_probe.hip -- where the crc32block framing kernel's time goes (dev tool): the shipped kernel
+// against its CRC-only and copy-only variants and the standalone shard CRC, on blobnode's write
+// batch (16 shards x 8 EC12P4 stripes of S = 5,592,406 bytes, 64 KiB blocks).
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../chubaofs_amd/csrc blk_probe.hip \
+//         -L../chubaofs_amd -lcfsec -Wl,-rpath,'$ORIGIN/../chubaofs_amd' -o blk_probe
+#include <algorithm>
+#include <cstdio>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "../chubaofs_amd/csrc/crc32block.hip"
+
+#define CK(x)                                                                          \
+  do {                                                                                 \
+    hipError_t e_ = (x);                                                               \
+    if (e_ != hipSuccess) {                                                            \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      exit(1);                                                                         \
+    }                                                                                  \
+  } while (0)
+
+__global__ void fill(uint32_t* p, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    uint64_t z = (uint64_t)i * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    p[i] = (uint32_t)(z ^ (z >> 31));
+  }
+}
+
+// flat copy of n16 16-byte chunks with the source / destination offset by SOFF / DOFF bytes
+template <int SOFF, int DOFF>
+__global__ __launch_bounds__(256) void kcopy(const uint8_t* s, uint8_t* d, size_t n16) {
+  for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256)
+    cfsec::dev::st16<true>(d + DOFF + 16 * i, cfsec::dev::ld16<true>(s + SOFF + 16 * i));
+}
+
+int main(int argc, char** argv) {
+  const int64_t S = argc > 1 ? atoll(argv[1]) : 5592406;
+  const int n = argc > 2 ? atoi(argv[2]) : 128;
+  const int64_t L = argc > 3 ? atoll(argv[3]) : 65536, flen = S + 4 * ((S + L - 5) / (L - 4));
+  const int64_t pitch = (S + 255) / 256 * 256, fpitch = (flen + 255) / 256 * 256;
+  uint8_t *pay, *frm;
+  uint32_t* words;
+  CK(hipMalloc(&pay, pitch * n));
+  CK(hipMalloc(&frm, fpitch * n));
+  CK(hipMalloc(&words, 4 * 4096));
+  fill<<<2048, 256>>>((uint32_t*)pay, pitch * n / 4);
+  std::vector<const uint8_t*> in(n);
+  std::vector<uint8_t*> out(n);
+  for (int i = 0; i < n; ++i) in[i] = pay + i * pitch, out[i] = frm + i * fpitch;
+  cfsec::Crc32BlockJob j;
+  j.n = n;
+  j.in = in.data();
+  j.out = out.data();
+  j.size = S;
+  j.block_len = L;
+  j.whole = words;
+  struct V {
+    std::string name;
+    std::function<void()> f;
+    double bytes;
+  };
+  const double pb = double(S) * n;
+  std::vector<V> vs = {
+      {"shipped (crc + store)", [&] { CK((cfsec::blk::launch<true, true>(j, 0))); }, 2 * pb},
+      {"crc only (no store)", [&] { CK((cfsec::blk::launch<false, true>(j, 0))); }, pb},
+      {"copy only (no crc)", [&] { CK((cfsec::blk::launch<true, false>(j, 0))); }, 2 * pb},
+      {"copy, src-aligned", [&] { CK((cfsec::blk::launch<true, false, true, true>(j, 0))); }, 2 * pb},
+      {"copy, no epilogue", [&] { CK((cfsec::blk::launch<true, false, false>(j, 0))); }, 2 * pb},
+      {"copy, runs of blocks", [&] { CK((cfsec::blk::launch<true, false, true, false, false>(j, 0))); }, 2 * pb},
+      {"crc, no epilogue", [&] { CK((cfsec::blk::launch<false, true, false>(j, 0))); }, pb},
+      {"crc+store, runs", [&] { CK((cfsec::blk::launch<true, true, true, false, false>(j, 0))); }, 2 * pb},
+      {"copy, no epi, plain st", [&] { CK((cfsec::blk::launch<true, false, false, false, true, false>(j, 0))); }, 2 * pb},
+      {"copy, no epi, runs, pl", [&] { CK((cfsec::blk::launch<true, false, false, false, false, false>(j, 0))); }, 2 * pb},
+      {"crc+st, plain st", [&] { CK((cfsec::blk::launch<true, true, true, false, true, false>(j, 0))); }, 2 * pb},
+      {"crc+st, no epi, plain", [&] { CK((cfsec::blk::launch<true, true, false, false, true, false>(j, 0))); }, 2 * pb},
+      {"shipped, no shard crc", [&] { cfsec::Crc32BlockJob j2 = j; j2.whole = nullptr; CK((cfsec::blk::launch<true, true>(j2, 0))); }, 2 * pb},
+      {"flat copy aligned", [&] { kcopy<0, 0><<<4096, 256>>>(pay, frm, (size_t)(pb / 16) - 1); }, 2 * pb},
+      {"flat copy src+4", [&] { kcopy<4, 0><<<4096, 256>>>(pay, frm, (size_t)(pb / 16) - 1); }, 2 * pb},
+      {"flat copy dst+4", [&] { kcopy<0, 4><<<4096, 256>>>(pay, frm, (size_t)(pb / 16) - 1); }, 2 * pb},
+      {"flat copy both+4", [&] { kcopy<4, 4><<<4096, 256>>>(pay, frm, (size_t)(pb / 16) - 1); }, 2 * pb},
+      {"standalone shard crc", [&] { CK(cfsec::launch_crc32(in.data(), S, n, words, 0)); }, pb},
+  };
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int i = 0; i < 100; ++i) vs[0].f();
+  std::vector<std::vector<float>> t(vs.size());
+  for (int r = 0; r < 15; ++r)
+    for (size_t v = 0; v < vs.size(); ++v) {
+      vs[v].f();
+      CK(hipEventRecord(e0, 0));
+      for (int i = 0; i < 10; ++i) vs[v].f();
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      t[v].push_back(ms / 10);
+    }
+  printf("S=%lld shards=%d block=%lld  payload %.1f MB\n", (long long)S, n, (long long)L, pb / 1e6);
+  for (size_t v = 0; v < vs.size(); ++v) {
+    std::sort(t[v].begin(), t[v].end());
+    const double ms = t[v][t[v].size() / 2];
+    printf("%-24s median %8.1f us  payload %7.1f GB/s  HBM %6.1f%% of 8 TB/s\n", vs[v].name.c_str(), ms * 1e3,
+           pb / (ms * 1e-3) / 1e9, 100 * vs[v].bytes / (ms * 1e-3) / 8e12);
+  }
+  return 0;
+}
