@@ -305,3 +305,68 @@ func (e *Engine) ReconstructSome(shards [][]byte, required []bool) error {
 func (e *Engine) Update(shards [][]byte, newDatashards [][]byte) error {
 	return reedsolomon.ErrNotSupported
 }
+
+// ---- crc32block framing (blobstore/common/crc32block) ----
+
+// ErrMismatchedCrc / ErrInvalidBlock mirror crc32block's sentinels (common/crc32block/util.go:29-30);
+// a shim dropped into crc32block returns that package's own values instead.
+var (
+	ErrMismatchedCrc = errors.New("crc32block: mismatched checksum")
+	ErrInvalidBlock  = errors.New("crc32block: invalid block buffer")
+)
+
+// BlockEncode frames payload in blockLen-byte crc32block blocks (crc32block.Encoder.Encode,
+// encode.go:48-58) on the GPU and returns the framed bytes together with crc32.ChecksumIEEE of the
+// whole payload -- the shard checksum blobnode's datafile.Write takes on the way
+// (core/storage/datafile.go:345-373) -- from the same single pass.
+func BlockEncode(payload []byte, blockLen int64) ([]byte, uint32, error) {
+	total := int64(C.cfsec_crc32block_encode_size(C.int64_t(len(payload)), C.int64_t(blockLen)))
+	if total < 0 {
+		return nil, 0, ErrInvalidBlock
+	}
+	out := make([]byte, total)
+	if len(payload) == 0 {
+		return out, 0, nil
+	}
+	var pin runtime.Pinner
+	pin.Pin(&payload[0])
+	pin.Pin(&out[0])
+	defer pin.Unpin()
+	var crc C.uint32_t
+	st := C.cfsec_crc32block_encode((*C.uint8_t)(unsafe.Pointer(&payload[0])), C.int64_t(len(payload)),
+		C.int64_t(blockLen), (*C.uint8_t)(unsafe.Pointer(&out[0])), &crc, C.CFSEC_MEM_HOST, -1, nil)
+	if st == C.CFSEC_ERR_INVALID_BLOCK {
+		return nil, 0, ErrInvalidBlock
+	}
+	return out, uint32(crc), toError(st)
+}
+
+// BlockDecode returns payload bytes [from, to) of a framed object whose payload is size bytes,
+// checking every block the range touches (crc32block.Decoder.Reader, decode.go:122-146).
+func BlockDecode(framed []byte, size, from, to, blockLen int64) ([]byte, error) {
+	if from < 0 || from > to || to > size {
+		return nil, errInvalidArg
+	}
+	out := make([]byte, to-from)
+	var pin runtime.Pinner
+	defer pin.Unpin()
+	var src, dst *C.uint8_t
+	if len(framed) > 0 {
+		pin.Pin(&framed[0])
+		src = (*C.uint8_t)(unsafe.Pointer(&framed[0]))
+	}
+	if len(out) > 0 {
+		pin.Pin(&out[0])
+		dst = (*C.uint8_t)(unsafe.Pointer(&out[0]))
+	}
+	var bad C.int64_t
+	switch st := C.cfsec_crc32block_decode(src, C.int64_t(size), C.int64_t(blockLen), C.int64_t(from),
+		C.int64_t(to), dst, &bad, C.CFSEC_MEM_HOST, -1, nil); st {
+	case C.CFSEC_ERR_MISMATCHED_CRC:
+		return nil, ErrMismatchedCrc
+	case C.CFSEC_ERR_INVALID_BLOCK:
+		return nil, ErrInvalidBlock
+	default:
+		return out, toError(st)
+	}
+}
