@@ -127,6 +127,14 @@ def lib():
             raise ImportError(
                 f"{LIB_PATH} is missing: the HIP engine is not built "
                 "(run `python -c 'import __graft_entry__ as g; g.build()'`); there is no CPU fallback")
+        # One HIP runtime per process: PyTorch ships its own libamdhip64.so.7 / libhsa-runtime64.so.1
+        # under the same SONAMEs as /opt/rocm's, and whichever loads first serves both.  Load
+        # torch's first when torch is installed -- with /opt/rocm's loaded first, torch finds no
+        # device (seen on MI355X); the engine runs on either runtime.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         for name, (args, res) in SIGNATURES.items():
             fn = getattr(L, name)
