@@ -1,5 +1,6 @@
 // gf_crc.hip -- host side of the fused matvec + shard CRC32 kernels (device code: gf_crc.hpp).
 #include <algorithm>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <vector>
@@ -156,8 +157,9 @@ hipError_t launch_matvec_crc(const MatVecJob& job, uint32_t* crc, int crc_stride
   const int64_t sstride = affine_stride(job);
   const int per = sstride ? job.nstripes : crcdev::kPtrSlots / (k + m);
   const int stripes_per_launch = std::min(per, 65535);
-  // ~2048 workgroups per launch (8 per CU) while each keeps >= 1 tile; at most kMaxGroups per stripe
-  const uint32_t want = std::max<uint32_t>(1, 2048u / (uint32_t)std::min(job.nstripes, stripes_per_launch));
+  // ~1024 workgroups per launch: each folds ~11 tiles per row before its per-thread basis
+  // epilogue (16 rows x 32 columns); 512 / 2048 / 4096 were 3-7 % slower (profiles/r01/crc_wgs_sweep.txt)
+  const uint32_t want = std::max<uint32_t>(1, 1024u / (uint32_t)std::min(job.nstripes, stripes_per_launch));
   uint32_t groups = std::min<uint32_t>({tiles, want, (uint32_t)crcdev::kMaxGroups});
   const uint32_t tpw = (tiles + groups - 1) / groups;
   groups = (tiles + tpw - 1) / tpw;
