@@ -35,7 +35,7 @@ BLOB = 64 << 20
 S_DEFAULT = (BLOB + K_DATA - 1) // K_DATA  # 5,592,406 (common/ec/buf.go:77-81)
 ERASED = [0, 1, 2, 3]
 HBM_PEAK_GBPS = 8000.0  # MI355X spec (MI355X_MICROARCH.md)
-KERNEL = "gf_dy_kernel<12, 4, 4, (cfsec::MatVecMode)0>"  # both step kernels: 12 -> 4 rows, 4x4-dyadic matrices
+KERNEL = "gf_dy_kernel<12, 4, 4, (cfsec::MatVecMode)0, 0>"  # both step kernels: 12 -> 4 rows, 4x4-dyadic matrices
 
 
 def parse():
@@ -354,7 +354,7 @@ def main():
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
             "traffic": None if traffic is None else int(traffic),
-            "kernel": "gf_dy_kernel<12, 4, 4, kStore> (encode and reconstruct launches: both matrices are 4x4-dyadic)",
+            "kernel": "gf_dy_kernel<12, 4, 4, kStore, 0> (encode and reconstruct launches: both matrices are 4x4-dyadic)",
             "algorithmic_bytes_per_launch": launch_bytes,
             "avg_launch_ms": round(avg_ms, 4),
             "launch_timing": ("HIP event pair on the launch stream around the timed region / launches"
