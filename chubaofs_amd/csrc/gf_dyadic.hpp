@@ -104,7 +104,7 @@ __device__ __forceinline__ uint32_t x3(uint32_t a, uint32_t b, uint32_t c) {
 
 // B = 2, all row blocks of one column block: tq/t2p point at (rb=0, cb) slot 0; row blocks are
 // kb*NC slots apart.
-template <int MB>
+template <int MB, bool PIN = true>
 __device__ __forceinline__ void dy_col2(uint32_t (&acc)[2 * MB][4], const uint32_t (&x0)[4],
                                         const uint32_t (&x1)[4], const u32x4* tq, const uint32_t* t2p,
                                         int stride) {
@@ -132,7 +132,7 @@ __device__ __forceinline__ void dy_col2(uint32_t (&acc)[2 * MB][4], const uint32
 }
 
 // B = 4, all row blocks of one column block.
-template <int MB>
+template <int MB, bool PIN = true>
 __device__ __forceinline__ void dy_col4(uint32_t (&acc)[4 * MB][4], const uint32_t (&x0)[4],
                                         const uint32_t (&x1)[4], const uint32_t (&x2)[4],
                                         const uint32_t (&x3v)[4], const u32x4* tq, const uint32_t* t2p,
@@ -159,8 +159,10 @@ __device__ __forceinline__ void dy_col4(uint32_t (&acc)[4 * MB][4], const uint32
       lookups(q[5], t[5], ss, p);  // (h2^h3) s
 #pragma unroll
       for (int w = 0; w < 4; ++w) ps2[w] = x3(p.a[w], p.b[w], p.c[w]);
-      asm volatile("" : "+v"(ps[0]), "+v"(ps[1]), "+v"(ps[2]), "+v"(ps[3]), "+v"(ps2[0]), "+v"(ps2[1]), "+v"(ps2[2]), "+v"(ps2[3]));
-      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (PIN) {
+        asm volatile("" : "+v"(ps[0]), "+v"(ps[1]), "+v"(ps[2]), "+v"(ps[3]), "+v"(ps2[0]), "+v"(ps2[1]), "+v"(ps2[2]), "+v"(ps2[3]));
+        __builtin_amdgcn_sched_barrier(0);
+      }
       Prod py, p6, p7;
       selectors(x3v, sy);
       selectors(v, sv);
@@ -174,8 +176,10 @@ __device__ __forceinline__ void dy_col4(uint32_t (&acc)[4 * MB][4], const uint32
         c1[w] = x3(p7.a[w], p7.b[w], p7.c[w]) ^ qy;
       }
     }
-    asm volatile("" : "+v"(c0[0]), "+v"(c0[1]), "+v"(c0[2]), "+v"(c0[3]), "+v"(c1[0]), "+v"(c1[1]), "+v"(c1[2]), "+v"(c1[3]));
-    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (PIN) {
+      asm volatile("" : "+v"(c0[0]), "+v"(c0[1]), "+v"(c0[2]), "+v"(c0[3]), "+v"(c1[0]), "+v"(c1[1]), "+v"(c1[2]), "+v"(c1[3]));
+      __builtin_amdgcn_sched_barrier(0);
+    }
     selectors(u, su);
     // one output at a time: out_j ^= h_j u ^ (shared s term) ^ (shared x3/v term)
 #pragma unroll
@@ -188,9 +192,11 @@ __device__ __forceinline__ void dy_col4(uint32_t (&acc)[4 * MB][4], const uint32
 #pragma unroll
       for (int w = 0; w < 4; ++w)
         acc[4 * rb + j][w] = x3(x3(acc[4 * rb + j][w], p.a[w], p.b[w]), x3(p.c[w], sh[w], cc[w]), 0u);
-      asm volatile("" : "+v"(acc[4 * rb + j][0]), "+v"(acc[4 * rb + j][1]), "+v"(acc[4 * rb + j][2]),
-                   "+v"(acc[4 * rb + j][3]));
-      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (PIN) {
+        asm volatile("" : "+v"(acc[4 * rb + j][0]), "+v"(acc[4 * rb + j][1]), "+v"(acc[4 * rb + j][2]),
+                     "+v"(acc[4 * rb + j][3]));
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
   }
 }
@@ -214,7 +220,8 @@ struct DyShape {
 // dyadic global rows + 2 local rows); grid (tiles, stripes), DyShape threads; wave w handles
 // column chunk w / OS and row blocks (w % OS) * RBW .. +RBW (plain rows: single-wave shapes only),
 // one 16-byte chunk per lane per row, column blocks loaded one block ahead.
-template <int K, int M, int B, MatVecMode MODE, bool NTS = true, bool NTL = true, int RBW_ = 64, int E = 0>
+template <int K, int M, int B, MatVecMode MODE, bool NTS = true, bool NTL = true, int RBW_ = 64, int E = 0,
+          bool PIN = true>
 __device__ __forceinline__ void matvec_dy(const GfArgs& a) {
   constexpr int MD = M - E;
   static_assert(K % B == 0 && MD % B == 0 && (B == 2 || B == 4), "dyadic shape");
@@ -257,9 +264,15 @@ __device__ __forceinline__ void matvec_dy(const GfArgs& a) {
 #pragma unroll
     for (int w = 0; w < 4; ++w) acc[r][w] = 0u;
   const auto pin = [&]() {
+    if constexpr (PIN) {
 #pragma unroll
-    for (int r = 0; r < MA; ++r)
-      asm volatile("" : "+v"(acc[r][0]), "+v"(acc[r][1]), "+v"(acc[r][2]), "+v"(acc[r][3]));
+      for (int r = 0; r < MA; ++r)
+        asm volatile("" : "+v"(acc[r][0]), "+v"(acc[r][1]), "+v"(acc[r][2]), "+v"(acc[r][3]));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  const auto sb = [&]() {
+    if constexpr (PIN) __builtin_amdgcn_sched_barrier(0);
   };
   const bool full = (uint64_t)off + kLaneBytes <= a.len;
   const size_t rem = off < a.len ? (size_t)(a.len - off) : 0;
@@ -282,15 +295,14 @@ __device__ __forceinline__ void matvec_dy(const GfArgs& a) {
       if (cb + 1 < KB)
 #pragma unroll
         for (int c = 0; c < B; ++c) load((cb + 1) * B + c);
-      __builtin_amdgcn_sched_barrier(0);
+      sb();
       const int c0 = cb * B;
       auto& dacc = reinterpret_cast<uint32_t(&)[MW][4]>(acc);
       if constexpr (B == 2)
-        dy_col2<RBW>(dacc, x[c0], x[c0 + 1], tq + cb * NC, tt + cb * NC, KB * NC);
+        dy_col2<RBW, PIN>(dacc, x[c0], x[c0 + 1], tq + cb * NC, tt + cb * NC, KB * NC);
       else
-        dy_col4<RBW>(dacc, x[c0], x[c0 + 1], x[c0 + 2], x[c0 + 3], tq + cb * NC, tt + cb * NC, KB * NC);
+        dy_col4<RBW, PIN>(dacc, x[c0], x[c0 + 1], x[c0 + 2], x[c0 + 3], tq + cb * NC, tt + cb * NC, KB * NC);
       pin();
-      __builtin_amdgcn_sched_barrier(0);
       if constexpr (E > 0) {
         auto& eacc = reinterpret_cast<uint32_t(&)[E][4]>(acc[MW]);
 #pragma unroll
@@ -298,7 +310,6 @@ __device__ __forceinline__ void matvec_dy(const GfArgs& a) {
           mac_pair_k<E>(eacc, x[c], x[c + 1], tab01 + ND + c * E, tab2 + ND + c * E, tab01 + ND + (c + 1) * E,
                         tab2 + ND + (c + 1) * E);
           pin();
-          __builtin_amdgcn_sched_barrier(0);
         }
       }
     }

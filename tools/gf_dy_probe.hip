@@ -32,6 +32,12 @@ __global__ __launch_bounds__((dev::DyShape<M, B, RBW>::kThreadsPerWg)) void kdy(
   dev::matvec_dy<K, M, B, MatVecMode::kStore, true, true, RBW>(a);
 }
 
+// free scheduling: no accumulator pins / sched barriers (the compiler may hoist every load)
+template <int K, int M, int B, bool NTS, bool NTL>
+__global__ __launch_bounds__((dev::DyShape<M, B>::kThreadsPerWg)) void kdyf(const GfArgs a) {
+  dev::matvec_dy<K, M, B, MatVecMode::kStore, NTS, NTL, 64, 0, false>(a);
+}
+
 __global__ void fill(uint32_t* p, size_t n) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     uint64_t z = (uint64_t)i * 0x9E3779B97F4A7C15ull;
@@ -60,6 +66,12 @@ template <int K, int M, int B, int RBW>
 V mk(const char* n) {
   using Sh = dev::DyShape<M, B, RBW>;
   return V{n, kdy<K, M, B, RBW>, Sh::kThreadsPerWg, Sh::kTileBytes};
+}
+
+template <int K, int M, int B, bool NTS = true, bool NTL = true>
+V mkf(const char* n) {
+  using Sh = dev::DyShape<M, B>;
+  return V{n, kdyf<K, M, B, NTS, NTL>, Sh::kThreadsPerWg, Sh::kTileBytes};
 }
 
 template <int K, int M, int B>
@@ -150,13 +162,11 @@ void run(size_t S, int nst, std::vector<V> vs) {
 }
 
 int main() {
-  run<16, 20, 4>(262144, 64, {mk<16, 20, 4, 1>("dy4 OS5"), mkp<16, 20, 1>("plain OS1"), mkp<16, 20, 4>("plain OS4")});
-  run<16, 22, 4>(262144, 64, {mkp<16, 22, 1>("plain OS1"), mkp<16, 22, 4>("plain OS4")});
-  run<16, 4, 4>(1048576, 16, {mkp<16, 4, 1>("plain OS1")});
-  run<16, 12, 4>(262144, 64, {mkp<16, 12, 1>("plain OS1"), mk<16, 12, 4, 3>("dy4 OS1")});
-  run<6, 6, 2>(699051, 32, {mkp<6, 6, 1>("plain OS1"), mk<6, 6, 2, 3>("dy2 OS1")});
-  run<6, 10, 2>(699051, 32, {mkp<6, 10, 1>("plain OS1"), mkp<6, 10, 2>("plain OS2")});
-  run<6, 12, 2>(699051, 32, {mkp<6, 12, 1>("plain OS1"), mk<6, 12, 2, 6>("dy2 OS1")});
-  run<12, 4, 4>(5592406, 8, {mkp<12, 4, 1>("plain OS1")});
+  run<12, 4, 4>(5592406, 8, {mkf<12, 4, 4>("dy4 free"), mkf<12, 4, 4, false, true>("dy4 free plainS"),
+                             mkf<12, 4, 4, true, false>("dy4 free plainL"), mk<12, 4, 4, 1>("dy4 pinned")});
+  run<16, 4, 4>(1048576, 16, {mkf<16, 4, 4>("dy4 free"), mk<16, 4, 4, 1>("dy4 pinned")});
+  run<16, 20, 4>(262144, 64, {mkf<16, 20, 4>("dy4 free"), mk<16, 20, 4, 5>("dy4 pinned")});
+  run<6, 6, 2>(699051, 32, {mkf<6, 6, 2>("dy2 free"), mk<6, 6, 2, 3>("dy2 pinned")});
+  run<12, 4, 4>(5592406, 8, {mkf<12, 4, 4>("dy4 free (2)"), mk<12, 4, 4, 1>("dy4 pinned (2)")});
   return 0;
 }
