@@ -1,0 +1,33 @@
+// gf_dy16.hip -- kernels for 16-input matrices opening with a 16x16 dyadic block (EC16P20 encode);
+// see gf_dyadic16.hpp.  The EC16P20L2 fused encode (the same 20 rows + 2 local rows) needed 256
+// VGPRs (1 wave/SIMD) in this form and stays on the 4x4-dyadic kernel with plain rows.
+#include "gf_dyadic16.hpp"
+#include "gf_launch.hpp"
+
+namespace cfsec {
+
+template <int M, int R4, int E, MatVecMode MODE>
+__global__ __launch_bounds__(256) void gf_dy16_kernel(const dev::GfArgs a) {
+  dev::matvec_dy16<M, R4, E, MODE>(a);
+}
+
+namespace {
+template <int M, int R4, int E>
+hipError_t launch_one(MatVecMode mode, const dev::GfArgs& a, unsigned ns, hipStream_t st) {
+  const unsigned tiles = (unsigned)((a.len + 4095) / 4096);
+  if (mode == MatVecMode::kVerify)
+    hipLaunchKernelGGL((gf_dy16_kernel<M, R4, E, MatVecMode::kVerify>), dim3(tiles, ns), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((gf_dy16_kernel<M, R4, E, MatVecMode::kStore>), dim3(tiles, ns), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+}  // namespace
+
+hipError_t launch_dy16(int m, MatVecMode mode, const dev::GfArgs& a, unsigned ns, hipStream_t st) {
+  switch (m) {
+    case 20: return launch_one<20, 1, 0>(mode, a, ns, st);  // EC16P20 global parity
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace cfsec

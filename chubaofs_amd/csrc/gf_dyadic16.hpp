@@ -1,0 +1,213 @@
+// gf_dyadic16.hpp -- GF(2^8) products for 16-input matrices whose first 16 rows form one 16x16
+// dyadic block: the EC16P20 parity (KRS buildMatrix(16, 36) rows 16..31 over data 0..15; parity
+// points 16..31 are the coset 16 + {0..15} of the additive subgroup {0..15}, see gf_dyadic.hpp),
+// followed by 4x4-dyadic row blocks (rows 32..35) and, for the fused EC16P20L2 encode, 2 plain
+// local rows.
+//
+// A dyadic block M[i][j] = h[i ^ j] of size 2n is [[A, B], [B, A]] with A, B dyadic of size n, and
+//   [A B; B A] [X; Y] = [A S + C Y ; B S + C Y],   S = X + Y,  C = A + B
+// so a 16x16 block costs 3 products of 8x8 blocks, each 3 products of 4x4 blocks: 9 leaf 4x4
+// products of 9 GF multiplies (dy_col4) = 81 multiplies for 256 coefficients, against 16 x 9 = 144
+// when the block is cut into 4x4 dyadic blocks.  The leaves' first rows are XOR combinations of h
+// (dy16_coef); the arithmetic is exact, so the bytes equal the plain product.
+#pragma once
+#include "gf_dyadic.hpp"
+
+namespace cfsec {
+namespace dev {
+
+// Leaf l = 3 * l1 + l2 of the 16x16 block with first row h[0..15]: l1 picks the 8x8 block
+// (0: A = h[0..7], 1: C = A + B, 2: B = h[8..15]), l2 the 4x4 block of that (0: its first half,
+// 1: the sum of its halves, 2: its second half); returns derived coefficient q of the leaf.
+__device__ __forceinline__ uint32_t dy16_coef(const uint8_t* h, int leaf, int q) {
+  const int l1 = leaf / 3, l2 = leaf % 3;
+  uint8_t x8[8], g[4];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x8[j] = l1 == 0 ? h[j] : l1 == 1 ? (uint8_t)(h[j] ^ h[j + 8]) : h[j + 8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) g[j] = l2 == 0 ? x8[j] : l2 == 1 ? (uint8_t)(x8[j] ^ x8[j + 4]) : x8[j + 4];
+  return dy_coef<4>(g, q);
+}
+
+constexpr int kDy16Leaves = 81;  // 9 leaves x 9 derived coefficients
+
+// Table slots: [0, 81) the leaves; then R4 row blocks x 4 column blocks x 9 of the 4x4 rows; then
+// K * E plain-row coefficients (slot c * E + e).
+template <int R4, int E>
+__device__ __forceinline__ void build_dy16_tables(const uint8_t* coef, u32x4* tab01, uint32_t* tab2) {
+  constexpr int K = 16, N4 = R4 * 4 * 9;
+  for (int i = threadIdx.x; i < kDy16Leaves + N4 + K * E; i += (int)blockDim.x) {
+    uint32_t cf = 0;
+    if (i < kDy16Leaves) {
+      cf = dy16_coef(coef, i / 9, i % 9);
+    } else if (i < kDy16Leaves + N4) {
+      const int j = i - kDy16Leaves, q = j % 9, blk = j / 9, cb = blk % 4, rb = blk / 4;
+      cf = dy_coef<4>(coef + (16 + 4 * rb) * K + 4 * cb, q);
+    } else if constexpr (E > 0) {
+      const int j = i - kDy16Leaves - N4, c = j / E, e = j % E;
+      cf = coef[(16 + 4 * R4 + e) * K + c];
+    }
+    coef_tables(cf, tab01[i], tab2[i]);
+  }
+}
+
+using Vec = uint32_t[4];
+using Vec4 = uint32_t[4][4];
+
+__device__ __forceinline__ Vec4& v4(uint32_t (&a)[4], int = 0) { return reinterpret_cast<Vec4&>(a); }
+
+// acc (4 rows) ^= leaf * [v[0..3]]
+template <bool PIN>
+__device__ __forceinline__ void leaf4(Vec4& acc, Vec4& v, const u32x4* tab01, const uint32_t* tab2, int leaf) {
+  dy_col4<1, PIN>(acc, v[0], v[1], v[2], v[3], tab01 + leaf * 9, tab2 + leaf * 9, 0);
+}
+
+template <bool PIN>
+__device__ __forceinline__ void xor_into(Vec4& dst, const Vec4& src) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int w = 0; w < 4; ++w) dst[r][w] ^= src[r][w];
+}
+
+// Kernel body: 16 inputs, M = 16 + 4 R4 + E outputs; 256-thread workgroups, each lane one 16-byte
+// chunk of every row (tile 4 KiB), grid (tiles, stripes).  Rows: acc[0..15] the 16x16 block,
+// acc[16..16+4R4) the 4x4 row blocks, then the E plain rows.
+template <int M, int R4, int E, MatVecMode MODE, bool PIN = true>
+__device__ __forceinline__ void matvec_dy16(const GfArgs& a) {
+  constexpr int K = 16, N4 = R4 * 4 * 9;
+  static_assert(M == 16 + 4 * R4 + E, "dyadic-16 shape");
+  constexpr bool kVer = MODE == MatVecMode::kVerify;
+  __shared__ u32x4 tab01[kDy16Leaves + N4 + K * E];
+  __shared__ uint32_t tab2[kDy16Leaves + N4 + K * E];
+  build_dy16_tables<R4, E>(a.coef, tab01, tab2);
+  __syncthreads();
+
+  const uint32_t stripe = blockIdx.y, tile = blockIdx.x;
+  const size_t ts = a.sstride ? 0 : (size_t)stripe;
+  const int64_t sbase = (int64_t)stripe * a.sstride;
+  const uint32_t off = tile * (uint32_t)(256 * kLaneBytes) + (uint32_t)threadIdx.x * kLaneBytes;
+  const uint8_t* row[K + M];
+#pragma unroll
+  for (int c = 0; c < K; ++c) row[c] = a.ptr[ts * K + c] + sbase;
+#pragma unroll
+  for (int r = 0; r < M; ++r) row[K + r] = a.ptr[(size_t)a.tab * K + ts * M + r] + sbase;
+  __builtin_amdgcn_sched_barrier(0);
+
+  const bool full = (uint64_t)off + kLaneBytes <= a.len;
+  const size_t rem = off < a.len ? (size_t)(a.len - off) : 0;
+  uint32_t diff = 0;
+  if (full || rem) {
+    uint32_t acc[M][4];
+#pragma unroll
+    for (int r = 0; r < M; ++r)
+#pragma unroll
+      for (int w = 0; w < 4; ++w) acc[r][w] = 0u;
+    uint32_t x[K][4];
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+      const u32x4 v = full ? ld16<true>(row[c] + off) : ld_tail(row[c] + off, rem);
+      x[c][0] = v.x, x[c][1] = v.y, x[c][2] = v.z, x[c][3] = v.w;
+    }
+    const auto sb = [&]() {
+      if constexpr (PIN) __builtin_amdgcn_sched_barrier(0);
+    };
+    // store (or compare) output row r as soon as it is final, so its registers are free for the
+    // 16x16 block's temporaries
+    const auto put = [&](int r) {
+      uint8_t* p = const_cast<uint8_t*>(row[K + r]) + off;
+      const u32x4 v = u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
+      if constexpr (kVer) {
+        const u32x4 d = v ^ (full ? ld16<true>(p) : ld_tail(p, rem));
+        diff |= d.x | d.y | d.z | d.w;
+      } else if (full) {
+        st16<true>(p, v);
+      } else {
+        st_tail(p, v, rem);
+      }
+    };
+    sb();
+    // rows after the 16x16 block: 4x4 dyadic blocks and plain rows, on the original inputs
+    if constexpr (R4 > 0) {
+      const u32x4* tq = tab01 + kDy16Leaves;
+      const uint32_t* tt = tab2 + kDy16Leaves;
+      auto& racc = reinterpret_cast<uint32_t(&)[4 * R4][4]>(acc[16]);
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) {
+        dy_col4<R4, PIN>(racc, x[4 * cb], x[4 * cb + 1], x[4 * cb + 2], x[4 * cb + 3], tq + cb * 9, tt + cb * 9, 4 * 9);
+        sb();
+      }
+#pragma unroll
+      for (int r = 16; r < 16 + 4 * R4; ++r) put(r);
+      sb();
+    }
+    if constexpr (E > 0) {
+      auto& eacc = reinterpret_cast<uint32_t(&)[E][4]>(acc[16 + 4 * R4]);
+      constexpr int ND = kDy16Leaves + N4;
+#pragma unroll
+      for (int c = 0; c < K; c += 2) {
+        mac_pair_k<E>(eacc, x[c], x[c + 1], tab01 + ND + c * E, tab2 + ND + c * E, tab01 + ND + (c + 1) * E,
+                      tab2 + ND + (c + 1) * E);
+        sb();
+      }
+#pragma unroll
+      for (int r = 16 + 4 * R4; r < M; ++r) put(r);
+      sb();
+    }
+    // the 16x16 block: S = X + Y into x[0..7]
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int w = 0; w < 4; ++w) x[j][w] ^= x[j + 8][w];
+    // rows 8..15 = C Y, C = A + B (leaves 3..5): the 8x8 recursion on Y, rows 8..15 start at zero
+    leaf4<PIN>(v4(acc[12]), v4(x[12]), tab01, tab2, 4);  // C_c Y_hi
+#pragma unroll
+    for (int r = 8; r < 12; ++r)
+#pragma unroll
+      for (int w = 0; w < 4; ++w) acc[r][w] = acc[r + 4][w];
+#pragma unroll
+    for (int j = 8; j < 12; ++j)
+#pragma unroll
+      for (int w = 0; w < 4; ++w) x[j][w] ^= x[j + 4][w];  // Y_lo + Y_hi (Y is dead after this)
+    leaf4<PIN>(v4(acc[8]), v4(x[8]), tab01, tab2, 3);    // C_a
+    leaf4<PIN>(v4(acc[12]), v4(x[8]), tab01, tab2, 5);   // C_b
+    // rows 0..7 = C Y as well, then += A S; rows 8..15 += B S
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+      for (int w = 0; w < 4; ++w) acc[r][w] = acc[r + 8][w];
+    {
+      uint32_t tmp[4][4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int w = 0; w < 4; ++w) tmp[r][w] = 0u;
+      leaf4<PIN>(tmp, v4(x[4]), tab01, tab2, 1);  // A_c S_hi
+      xor_into<PIN>(v4(acc[0]), tmp);
+      xor_into<PIN>(v4(acc[4]), tmp);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int w = 0; w < 4; ++w) tmp[r][w] = 0u;
+      leaf4<PIN>(tmp, v4(x[4]), tab01, tab2, 7);  // B_c S_hi
+      xor_into<PIN>(v4(acc[8]), tmp);
+      xor_into<PIN>(v4(acc[12]), tmp);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int w = 0; w < 4; ++w) x[j][w] ^= x[j + 4][w];  // S_lo + S_hi, shared by A and B
+    leaf4<PIN>(v4(acc[0]), v4(x[0]), tab01, tab2, 0);   // A_a
+    leaf4<PIN>(v4(acc[4]), v4(x[0]), tab01, tab2, 2);   // A_b
+    leaf4<PIN>(v4(acc[8]), v4(x[0]), tab01, tab2, 6);   // B_a
+    leaf4<PIN>(v4(acc[12]), v4(x[0]), tab01, tab2, 8);  // B_b
+#pragma unroll
+    for (int r = 0; r < 16; ++r) put(r);
+  }
+  if constexpr (kVer) {
+    if (diff) atomicOr(a.flags + stripe, 1u);
+  }
+}
+
+}  // namespace dev
+}  // namespace cfsec

@@ -142,11 +142,13 @@ hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
       // matrices of 4x4 / 2x2 dyadic blocks (encode of every code mode but the LRC local stripes,
       // coset-aligned reconstructs such as EC12P4's worst case) take the reduced-product kernel
       DyPlan dy{0, 0};
+      bool dy16 = false;
       if (fixed && r0 == 0 && mc == job.m) {
         std::vector<uint8_t> sub((size_t)mc * kc);
         for (int r = 0; r < mc; ++r)
           for (int c = 0; c < kc; ++c) sub[(size_t)r * kc + c] = job.coef[(size_t)r * job.k + c];
-        dy = dyadic_plan(sub.data(), mc, kc);
+        dy16 = dyadic16_plan(sub.data(), mc, kc);
+        if (!dy16) dy = dyadic_plan(sub.data(), mc, kc);
       }
       const size_t tile = fixed ? size_t(256) * dev::kLaneBytes
                                 : size_t(threads / sh.OS) * dev::kLaneBytes * (verify ? kVerifyW : kStoreW);
@@ -181,6 +183,11 @@ hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
         }
         const dim3 grid((unsigned)(tiles * ns));
         hipError_t e;
+        if (fixed && dy16) {
+          e = launch_dy16(mc, mode, a, (unsigned)ns, stream);
+          if (e != hipSuccess) return e;
+          continue;
+        }
         if (fixed && dy.B) {
           e = kc == 6    ? launch_dy<6>(mc, dy.B, dy.E, mode, a, (unsigned)ns, stream)
               : kc == 12 ? launch_dy<12>(mc, dy.B, dy.E, mode, a, (unsigned)ns, stream)

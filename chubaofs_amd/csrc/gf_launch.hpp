@@ -91,6 +91,22 @@ inline DyPlan dyadic_plan(const uint8_t* coef, int m, int k) {
   return {0, 0};
 }
 
+// 16-input matrices whose first 16 rows form one 16x16 dyadic block, then one 4x4-dyadic row
+// block (gf_dyadic16.hpp; m = 20: EC16P20).
+hipError_t launch_dy16(int m, MatVecMode mode, const dev::GfArgs& a, unsigned ns, hipStream_t st);
+
+inline bool dyadic16_plan(const uint8_t* coef, int m, int k) {
+  if (k != 16 || m != 20) return false;
+  for (int i = 0; i < 16; ++i)
+    for (int j = 0; j < 16; ++j)
+      if (coef[(size_t)i * 16 + j] != coef[i ^ j]) return false;
+  for (int c0 = 0; c0 < 16; c0 += 4)
+    for (int i = 0; i < 4; ++i)
+      for (int j = 0; j < 4; ++j)
+        if (coef[(size_t)(16 + i) * 16 + c0 + j] != coef[(size_t)16 * 16 + c0 + (i ^ j)]) return false;
+  return true;
+}
+
 #define CFSEC_EXTERN_K(K)                                                                         \
   extern template hipError_t launch_k<K, MatVecMode::kStore, fixed_max_m(K)>(int, const dev::GfArgs&, \
                                                                             dim3, hipStream_t);     \
