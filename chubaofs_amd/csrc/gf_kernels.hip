@@ -26,11 +26,14 @@
 // launch free of device allocations and host->device copies (safe under
 // concurrent callers and hipGraph capture).
 //
-// Two kernel families:
-//   fixed-K (gf_fixed.hpp, k in {6, 8, 12, 16, 18}: every CubeFS code mode and local stripe):
-//                256-thread workgroups, 1 chunk per lane, rows pipelined 2 ahead with the issue
-//                order pinned (tools/gf_pipe.hip: +6% over the runtime-k loop on EC12P4, at
-//                the trivial-arithmetic ceiling of the same access pattern)
+// Kernel families, first match wins:
+//   16x16-dyadic (gf_dyadic16.hpp): EC16P20's 20 parity rows
+//   dyadic-block (gf_dyadic.hpp): 4x4 / 2x2 dyadic matrices (code-mode encodes, coset-aligned
+//                repairs, fused LRC encodes with 2 plain rows)
+//   fixed-K (gf_fixed.hpp, every code-mode input count k in {3,4,6,7,8,10,12,15,16,18}, m up to
+//                fixed_max_m(k)): 256-thread workgroups, 1 chunk per lane, all outputs in one
+//                wave, rows pipelined 2 ahead with the issue order pinned (tools/gf_pipe.hip:
+//                +6% over the runtime-k loop on EC12P4)
 //   runtime-k (any other k, or k > 32 chunked with accumulate): policies from
 //                tools/gf_variants.hip -- store/accum 256-thread, 1 chunk per lane, one row at a
 //                time; verify 128-thread, 2 chunks per lane, rows loaded in pairs

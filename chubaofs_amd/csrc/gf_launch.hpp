@@ -1,5 +1,5 @@
 // gf_launch.hpp -- launcher internals shared by gf_kernels.hip and the fixed-K translation
-// units gf_k{6,8,12,16,18}.hip (one TU per input count so the instantiations build in parallel).
+// units gf_k<K>.hip (one TU per input count so the instantiations build in parallel).
 #pragma once
 #include <hip/hip_runtime.h>
 
