@@ -360,9 +360,16 @@ def main():
             "launch_timing": ("HIP event pair on the launch stream around the timed region / launches"
                               + (" (graph replay)" if graph is not None else "")),
             "traffic_note": pmc_note if traffic is None else "rocprofv3 (2*FETCH_SIZE + WRITE_SIZE)*1024, per launch",
+            "cache_note": ("the step alternates encode and reconstruct over the same stripes: each reads the "
+                           "4 rows the other just wrote (4*S*stripes = 179 MB, under the 256 MB Infinity Cache), "
+                           "and with sc1 output stores part of that is served from the cache; the same kernels "
+                           "repeated back to back on one operation (no reuse) give encode_roofline_frac / "
+                           "reconstruct_roofline_frac"),
         },
         "encode_data_GBps": round(data_bytes / (enc_ms * 1e-3) / 1e9, 1),
+        "encode_roofline_frac": round(launch_bytes / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
         "reconstruct_data_GBps": round(data_bytes / (rec_ms * 1e-3) / 1e9, 1),
+        "reconstruct_roofline_frac": round(launch_bytes / (rec_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
         "verify_data_GBps": round(data_bytes / (verify_ms * 1e-3) / 1e9, 1),
         "verify_roofline_frac": round(launch_bytes / (verify_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
         "encode_crc_data_GBps": round(data_bytes / (crc_ms * 1e-3) / 1e9, 1),

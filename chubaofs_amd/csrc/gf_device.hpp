@@ -68,6 +68,28 @@ __device__ __forceinline__ void st16(uint8_t* p, u32x4 v) {
   else *reinterpret_cast<u32x4_ua*>(p) = v;
 }
 
+// 16-byte vector store with explicit gfx950 cache-policy bits (measurement variants; SP = 0: none,
+// 1: nt, 2: sc1, 3: sc0 sc1, 4: nt sc1, 5: nt sc0 sc1, 6: sc0).
+template <int SP>
+__device__ __forceinline__ void st16_pol(uint8_t* p, u32x4 v) {
+  if constexpr (SP == 0) asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(p), "v"(v) : "memory");
+  else if constexpr (SP == 1) asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(p), "v"(v) : "memory");
+  else if constexpr (SP == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+  else if constexpr (SP == 3) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+  else if constexpr (SP == 4) asm volatile("global_store_dwordx4 %0, %1, off nt sc1" ::"v"(p), "v"(v) : "memory");
+  else if constexpr (SP == 5) asm volatile("global_store_dwordx4 %0, %1, off nt sc0 sc1" ::"v"(p), "v"(v) : "memory");
+  else asm volatile("global_store_dwordx4 %0, %1, off sc0" ::"v"(p), "v"(v) : "memory");
+}
+
+// Output-row store of the fixed-K and dyadic kernels: the streaming policy is sc1 (EC12P4 dyadic
+// kernel, profiles/r01/store_policy_probe.txt: sc1 / sc0 sc1 1-2 % faster than nt, plain and sc0
+// 2-3 % slower).
+template <bool NTS>
+__device__ __forceinline__ void st16_out(uint8_t* p, u32x4 v) {
+  if constexpr (NTS) st16_pol<2>(p, v);
+  else st16<false>(p, v);
+}
+
 // Bytes [0, rem) of a 16-byte chunk, zero above (the tail of a shard).
 __device__ __forceinline__ u32x4 ld_tail(const uint8_t* p, size_t rem) {
   uint32_t w[4] = {0u, 0u, 0u, 0u};
@@ -372,7 +394,7 @@ __device__ __forceinline__ void lane_tile_k(int m, const u32x4* tab01, const uin
         uint8_t* p = out[og + r] + sbase + loff;
         u32x4 v = u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
         if constexpr (MODE == MatVecMode::kAccum) v ^= ld16<NTL>(p);
-        st16<NTS>(p, v);
+        st16_out<NTS>(p, v);
       }
     }
   }

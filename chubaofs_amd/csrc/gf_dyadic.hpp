@@ -221,7 +221,7 @@ struct DyShape {
 // column chunk w / OS and row blocks (w % OS) * RBW .. +RBW (plain rows: single-wave shapes only),
 // one 16-byte chunk per lane per row, column blocks loaded one block ahead.
 template <int K, int M, int B, MatVecMode MODE, bool NTS = true, bool NTL = true, int RBW_ = 64, int E = 0,
-          bool PIN = true>
+          bool PIN = true, int SP = -1>
 __device__ __forceinline__ void matvec_dy(const GfArgs& a) {
   constexpr int MD = M - E;
   static_assert(K % B == 0 && MD % B == 0 && (B == 2 || B == 4), "dyadic shape");
@@ -322,7 +322,8 @@ __device__ __forceinline__ void matvec_dy(const GfArgs& a) {
         const u32x4 d = v ^ (full ? ld16<true>(p) : ld_tail(p, rem));
         diff |= d.x | d.y | d.z | d.w;
       } else if (full) {
-        st16<NTS>(p, v);
+        if constexpr (SP >= 0) st16_pol<SP>(p, v);  // probe variants
+        else st16_out<NTS>(p, v);
       } else {
         st_tail(p, v, rem);
       }

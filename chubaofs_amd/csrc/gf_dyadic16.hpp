@@ -121,7 +121,7 @@ __device__ __forceinline__ void matvec_dy16(const GfArgs& a) {
         const u32x4 d = v ^ (full ? ld16<true>(p) : ld_tail(p, rem));
         diff |= d.x | d.y | d.z | d.w;
       } else if (full) {
-        st16<true>(p, v);
+        st16_out<true>(p, v);
       } else {
         st_tail(p, v, rem);
       }

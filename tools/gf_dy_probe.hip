@@ -33,6 +33,11 @@ __global__ __launch_bounds__((dev::DyShape<M, B, RBW>::kThreadsPerWg)) void kdy(
 }
 
 // free scheduling: no accumulator pins / sched barriers (the compiler may hoist every load)
+template <int K, int M, int B, int SP>
+__global__ __launch_bounds__((dev::DyShape<M, B>::kThreadsPerWg)) void kdysp(const GfArgs a) {
+  dev::matvec_dy<K, M, B, MatVecMode::kStore, true, true, 64, 0, true, SP>(a);
+}
+
 template <int K, int M, int B, bool NTS, bool NTL>
 __global__ __launch_bounds__((dev::DyShape<M, B>::kThreadsPerWg)) void kdyf(const GfArgs a) {
   dev::matvec_dy<K, M, B, MatVecMode::kStore, NTS, NTL, 64, 0, false>(a);
@@ -66,6 +71,12 @@ template <int K, int M, int B, int RBW>
 V mk(const char* n) {
   using Sh = dev::DyShape<M, B, RBW>;
   return V{n, kdy<K, M, B, RBW>, Sh::kThreadsPerWg, Sh::kTileBytes};
+}
+
+template <int K, int M, int B, int SP>
+V mksp(const char* n) {
+  using Sh = dev::DyShape<M, B>;
+  return V{n, kdysp<K, M, B, SP>, Sh::kThreadsPerWg, Sh::kTileBytes};
 }
 
 template <int K, int M, int B, bool NTS = true, bool NTL = true>
@@ -162,11 +173,10 @@ void run(size_t S, int nst, std::vector<V> vs) {
 }
 
 int main() {
-  run<12, 4, 4>(5592406, 8, {mkf<12, 4, 4>("dy4 free"), mkf<12, 4, 4, false, true>("dy4 free plainS"),
-                             mkf<12, 4, 4, true, false>("dy4 free plainL"), mk<12, 4, 4, 1>("dy4 pinned")});
-  run<16, 4, 4>(1048576, 16, {mkf<16, 4, 4>("dy4 free"), mk<16, 4, 4, 1>("dy4 pinned")});
-  run<16, 20, 4>(262144, 64, {mkf<16, 20, 4>("dy4 free"), mk<16, 20, 4, 5>("dy4 pinned")});
-  run<6, 6, 2>(699051, 32, {mkf<6, 6, 2>("dy2 free"), mk<6, 6, 2, 3>("dy2 pinned")});
-  run<12, 4, 4>(5592406, 8, {mkf<12, 4, 4>("dy4 free (2)"), mk<12, 4, 4, 1>("dy4 pinned (2)")});
+  run<12, 4, 4>(5592406, 8, {mksp<12, 4, 4, 0>("st plain"), mksp<12, 4, 4, 1>("st nt"), mksp<12, 4, 4, 2>("st sc1"),
+                             mksp<12, 4, 4, 3>("st sc0 sc1"), mksp<12, 4, 4, 4>("st nt sc1"),
+                             mksp<12, 4, 4, 5>("st nt sc0 sc1"), mksp<12, 4, 4, 6>("st sc0")});
+  run<12, 4, 4>(5592406, 8, {mksp<12, 4, 4, 1>("st nt (2)"), mksp<12, 4, 4, 3>("st sc0 sc1 (2)"),
+                             mksp<12, 4, 4, 2>("st sc1 (2)")});
   return 0;
 }
