@@ -81,6 +81,15 @@ __device__ __forceinline__ void st16_pol(uint8_t* p, u32x4 v) {
   else asm volatile("global_store_dwordx4 %0, %1, off sc0" ::"v"(p), "v"(v) : "memory");
 }
 
+// 16-byte load at base + off through a raw buffer descriptor with explicit cache-policy bits
+// (measurement variants; aux: 1 = sc0, 2 = nt, 16 = sc1).
+template <int LP>
+__device__ __forceinline__ u32x4 ld16_pol(const uint8_t* base, uint32_t off) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), (short)0, -1, 0x00020000);
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, LP);
+  return u32x4{v[0], v[1], v[2], v[3]};
+}
+
 // Output-row store of the fixed-K and dyadic kernels: the streaming policy is sc1 (EC12P4 dyadic
 // kernel, profiles/r01/store_policy_probe.txt: sc1 / sc0 sc1 1-2 % faster than nt, plain and sc0
 // 2-3 % slower).

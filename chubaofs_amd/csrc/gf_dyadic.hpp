@@ -221,7 +221,7 @@ struct DyShape {
 // column chunk w / OS and row blocks (w % OS) * RBW .. +RBW (plain rows: single-wave shapes only),
 // one 16-byte chunk per lane per row, column blocks loaded one block ahead.
 template <int K, int M, int B, MatVecMode MODE, bool NTS = true, bool NTL = true, int RBW_ = 64, int E = 0,
-          bool PIN = true, int SP = -1>
+          bool PIN = true, int SP = -1, int LP = -1>
 __device__ __forceinline__ void matvec_dy(const GfArgs& a) {
   constexpr int MD = M - E;
   static_assert(K % B == 0 && MD % B == 0 && (B == 2 || B == 4), "dyadic shape");
@@ -280,7 +280,9 @@ __device__ __forceinline__ void matvec_dy(const GfArgs& a) {
   if (full || rem) {
     uint32_t x[K][4];
     const auto load = [&](int c) {
-      const u32x4 v = full ? ld16<NTL>(row[c] + off) : ld_tail(row[c] + off, rem);
+      u32x4 v;
+      if constexpr (LP >= 0) v = full ? ld16_pol<LP>(row[c], off) : ld_tail(row[c] + off, rem);  // probes
+      else v = full ? ld16<NTL>(row[c] + off) : ld_tail(row[c] + off, rem);
       x[c][0] = v.x;
       x[c][1] = v.y;
       x[c][2] = v.z;

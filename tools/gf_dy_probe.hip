@@ -33,9 +33,9 @@ __global__ __launch_bounds__((dev::DyShape<M, B, RBW>::kThreadsPerWg)) void kdy(
 }
 
 // free scheduling: no accumulator pins / sched barriers (the compiler may hoist every load)
-template <int K, int M, int B, int SP>
+template <int K, int M, int B, int SP, int LP = -1>
 __global__ __launch_bounds__((dev::DyShape<M, B>::kThreadsPerWg)) void kdysp(const GfArgs a) {
-  dev::matvec_dy<K, M, B, MatVecMode::kStore, true, true, 64, 0, true, SP>(a);
+  dev::matvec_dy<K, M, B, MatVecMode::kStore, true, true, 64, 0, true, SP, LP>(a);
 }
 
 template <int K, int M, int B, bool NTS, bool NTL>
@@ -73,10 +73,10 @@ V mk(const char* n) {
   return V{n, kdy<K, M, B, RBW>, Sh::kThreadsPerWg, Sh::kTileBytes};
 }
 
-template <int K, int M, int B, int SP>
+template <int K, int M, int B, int SP, int LP = -1>
 V mksp(const char* n) {
   using Sh = dev::DyShape<M, B>;
-  return V{n, kdysp<K, M, B, SP>, Sh::kThreadsPerWg, Sh::kTileBytes};
+  return V{n, kdysp<K, M, B, SP, LP>, Sh::kThreadsPerWg, Sh::kTileBytes};
 }
 
 template <int K, int M, int B, bool NTS = true, bool NTL = true>
@@ -173,10 +173,12 @@ void run(size_t S, int nst, std::vector<V> vs) {
 }
 
 int main() {
-  run<12, 4, 4>(5592406, 8, {mksp<12, 4, 4, 0>("st plain"), mksp<12, 4, 4, 1>("st nt"), mksp<12, 4, 4, 2>("st sc1"),
-                             mksp<12, 4, 4, 3>("st sc0 sc1"), mksp<12, 4, 4, 4>("st nt sc1"),
-                             mksp<12, 4, 4, 5>("st nt sc0 sc1"), mksp<12, 4, 4, 6>("st sc0")});
-  run<12, 4, 4>(5592406, 8, {mksp<12, 4, 4, 1>("st nt (2)"), mksp<12, 4, 4, 3>("st sc0 sc1 (2)"),
-                             mksp<12, 4, 4, 2>("st sc1 (2)")});
+  // stores sc1 (SP 2) throughout; loads: builtin nt, then buffer loads with aux bits
+  run<12, 4, 4>(5592406, 8, {mksp<12, 4, 4, 2>("ld nt (builtin)"), mksp<12, 4, 4, 2, 2>("ld buf nt"),
+                             mksp<12, 4, 4, 2, 0>("ld buf plain"), mksp<12, 4, 4, 2, 16>("ld buf sc1"),
+                             mksp<12, 4, 4, 2, 18>("ld buf nt sc1"), mksp<12, 4, 4, 2, 1>("ld buf sc0"),
+                             mksp<12, 4, 4, 2, 17>("ld buf sc0 sc1"), mksp<12, 4, 4, 2, 19>("ld buf nt sc0 sc1")});
+  run<12, 4, 4>(5592406, 8, {mksp<12, 4, 4, 2>("ld nt (builtin) (2)"), mksp<12, 4, 4, 2, 2>("ld buf nt (2)"),
+                             mksp<12, 4, 4, 2, 16>("ld buf sc1 (2)"), mksp<12, 4, 4, 2, 18>("ld buf nt sc1 (2)")});
   return 0;
 }
