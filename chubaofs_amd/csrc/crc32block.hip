@@ -149,7 +149,7 @@ __global__ __launch_bounds__(256) void crc32block_kernel(const BlockArgs a) {
             const int64_t q = (int64_t)q0 + first;  // payload coordinate of the piece's byte 0
             uint8_t* dp = out + (dbase + first);    // 16-byte aligned
             if (first >= 0 && first + 16 <= plen && q >= (int64_t)a.lo && q + 16 <= (int64_t)a.hi) {
-              dev::st16<NTS>(dp, u32x4{cur[0], cur[1], cur[2], cur[3]});
+              dev::st16_out<NTS>(dp, u32x4{cur[0], cur[1], cur[2], cur[3]});
             } else {
               for (int j = 0; j < 16; ++j)
                 if (first + j >= 0 && first + j < plen && q + j >= (int64_t)a.lo && q + j < (int64_t)a.hi)

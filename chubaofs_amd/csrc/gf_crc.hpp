@@ -126,7 +126,7 @@ __device__ __forceinline__ void crc_tile(uint64_t len, const u32x4* tab01, const
     }
 #pragma unroll
     for (int r = 0; r < M; ++r)
-      dev::st16<true>(const_cast<uint8_t*>(row[K + r]) + off, u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]});
+      dev::st16_out<true>(const_cast<uint8_t*>(row[K + r]) + off, u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]});
   } else {
     const size_t rem = off < len ? (size_t)(len - off) : 0;
     for (int c = 0; c < K; ++c) {
