@@ -6,7 +6,7 @@
 // Same algebra and work split as the fused kernel, without the product: a workgroup owns `tpw`
 // consecutive 4 KiB tiles of one shard, thread j a 16-byte piece of each (coalesced 16-B loads,
 // the next tile's piece in flight while this one is folded), Horner R <- f(shift(R, 4080), piece)
-// with slice-by-8 LDS tables, a per-thread basis multiply to the tile end, a workgroup XOR
+// with the conflict-free nibble tables (gf_crc.hpp crc_step_nib), a per-thread basis multiply to the tile end, a workgroup XOR
 // reduction and one multiply by x^(8(S - e)) to the shard end, then atomicXor into the shard's
 // word.  `fin` (crc32_shift_ones(S), or 0 for the raw word) is folded in by workgroup 0.
 #include <algorithm>
@@ -50,9 +50,9 @@ __device__ __forceinline__ void piece(const uint8_t* p, uint64_t len, uint32_t o
 }
 
 __global__ __launch_bounds__(256) void crc32_horner_kernel(const CrcArgs a) {
-  __shared__ uint32_t ct[kTabWords];
+  __shared__ uint32_t ct[crcdev::kNibTabWords];
   __shared__ uint32_t red[4];
-  for (int i = threadIdx.x; i < kTabWords; i += 256) ct[i] = a.tabs[i];
+  for (int i = threadIdx.x; i < crcdev::kNibTabWords; i += 256) ct[i] = a.tabs[crcdev::kByteTabWords + i];
   __syncthreads();
   const uint32_t g = blockIdx.x, sh = blockIdx.y;
   const uint8_t* p = a.sstride ? a.ptr[0] + (int64_t)sh * a.sstride : a.ptr[sh];
@@ -62,7 +62,7 @@ __global__ __launch_bounds__(256) void crc32_horner_kernel(const CrcArgs a) {
   piece(p, a.len, t0 * kTile + lanepos, cur);
   for (uint32_t t = t0; t < t1; ++t) {
     if (t + 1 < t1) piece(p, a.len, (t + 1) * kTile + lanepos, nxt);
-    R = crcdev::crc_step(ct, R, cur);
+    R = crcdev::crc_step_nib(ct, R, cur);
 #pragma unroll
     for (int w = 0; w < 4; ++w) cur[w] = nxt[w];
   }

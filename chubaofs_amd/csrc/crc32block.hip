@@ -85,9 +85,9 @@ __device__ __forceinline__ void load_piece(const uint8_t* src, uint32_t plen, ui
 // runs STORE, CRC and EPI on, pieces aligned to the destination).
 template <bool STORE = true, bool CRC = true, bool EPI = true, bool SRCALIGN = false, bool NTS = true>
 __global__ __launch_bounds__(256) void crc32block_kernel(const BlockArgs a) {
-  __shared__ uint32_t ct[kTabWords];
+  __shared__ uint32_t ct[crcdev::kNibTabWords];
   __shared__ uint32_t red[4];
-  for (int i = threadIdx.x; i < kTabWords; i += 256) ct[i] = a.tabs[i];
+  for (int i = threadIdx.x; i < crcdev::kNibTabWords; i += 256) ct[i] = a.tabs[crcdev::kByteTabWords + i];
   // this thread's x^(8*16*(255 - j)): moves its Horner register from its piece to the tile end
   // (column x^0 of its basis, gf_crc.hip host_tables)
   const uint32_t kj = a.tabs[kTabWords + threadIdx.x * 32 + 31];
@@ -142,7 +142,7 @@ __global__ __launch_bounds__(256) void crc32block_kernel(const BlockArgs a) {
         if (t < tiles) {
           uint32_t (&cur)[4] = ring[k];
           const uint32_t p = t * 256 + threadIdx.x;
-          if constexpr (CRC) R = crcdev::crc_step(ct, R, cur);
+          if constexpr (CRC) R = crcdev::crc_step_nib(ct, R, cur);
           else R ^= cur[0] ^ cur[1] ^ cur[2] ^ cur[3];
           const int64_t first = (int64_t)16 * p - h;
           if (STORE && first < (int64_t)plen) {

@@ -61,6 +61,21 @@ std::vector<uint32_t> host_tables() {
   const uint32_t k4080 = xpow(8 * 4080);
   for (int q = 0; q < 4; ++q)  // Hq[b] = shift(b << 8q, 4080)
     for (uint32_t b = 0; b < 256; ++b) t[(8 + q) * 256 + b] = mulmod(k4080, b << (8 * q));
+  uint32_t* nt = t.data() + crcdev::kByteTabWords;
+  const uint32_t k4096 = xpow(8 * 4096);
+  for (int p = 0; p < 32; ++p)  // Np[n] = f(0, 16-byte piece with nibble p = n, the rest 0)
+    for (uint32_t n = 0; n < 16; ++n) {
+      uint8_t piece[16] = {};
+      piece[p / 2] = (uint8_t)(n << (4 * (p & 1)));
+      uint32_t c = 0;
+      for (uint8_t b : piece) {
+        c ^= b;
+        for (int i = 0; i < 8; ++i) c = (c & 1u) ? (c >> 1) ^ crcdev::kPoly : c >> 1;
+      }
+      nt[p * 16 + n] = c;
+    }
+  for (int q = 0; q < 8; ++q)  // Hq[n] = shift(n << 4q, 4096)
+    for (uint32_t n = 0; n < 16; ++n) nt[(32 + q) * 16 + n] = mulmod(k4096, n << (4 * q));
   for (int j = 0; j < 256; ++j) {  // basis of shift(., 16*(255-j)) for thread j
     const uint32_t kj = xpow(8LL * 16 * (255 - j));
     for (int i = 0; i < 32; ++i) t[crcdev::kTabWords + j * 32 + i] = mulmod(kj, 1u << i);

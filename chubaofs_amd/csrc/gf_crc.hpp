@@ -36,7 +36,9 @@ using dev::u32x4;
 constexpr uint32_t kPoly = 0xEDB88320u;
 constexpr int kTile = 4096;            // bytes per row per tile: 256 threads x 16 B
 constexpr int kMaxK = 18, kMaxM = 6, kPtrSlots = 96, kMaxGroups = 384;
-constexpr int kTabWords = 12 * 256;    // T0..T7: slice-by-8;  H0..H3: shift by 4080 bytes
+constexpr int kByteTabWords = 12 * 256;  // T0..T7: slice-by-8;  H0..H3: shift by 4080 bytes
+constexpr int kNibTabWords = 40 * 16;    // N0..N31: nibbles of a 16-B piece;  H0..H7: register nibbles
+constexpr int kTabWords = kByteTabWords + kNibTabWords;  // device table block, the basis follows
 constexpr int kBasisWords = 256 * 32;  // thread j: the 32 columns of shift(., 16*(255-j))
 
 struct __attribute__((aligned(16))) GfCrcArgs {
@@ -54,6 +56,13 @@ struct __attribute__((aligned(16))) GfCrcArgs {
 };
 static_assert(sizeof(GfCrcArgs) <= 3584, "kernel argument block must stay below 4 KiB");
 
+// Two equivalent Horner steps R <- f(shift(R, 4080), d) over a thread's next 16-byte piece d,
+// which sits 4080 bytes after its previous one.  The byte-table step costs 20 LDS reads and ~40
+// VALU; its random byte indices into 256-word tables conflict (~2.6 LDS cycles per read per lane
+// group).  The nibble-table step costs 40 conflict-free reads and ~75 VALU.  Kernels whose VALU
+// is already busy with the GF product (gf_crc_kernel) take the byte step; the CRC-only kernels
+// (crc32.hip, crc32block.hip) take the nibble step (profiles/r01/crc_nibble_ab.txt).
+
 // f(r, 8 bytes w0|w1): slice-by-8 with ct[n*256 + b] = f(0, b followed by n zero bytes).
 __device__ __forceinline__ uint32_t slice8(const uint32_t* ct, uint32_t r, uint32_t w0, uint32_t w1) {
   w0 ^= r;
@@ -62,11 +71,49 @@ __device__ __forceinline__ uint32_t slice8(const uint32_t* ct, uint32_t r, uint3
          ct[1 * 256 + ((w1 >> 16) & 0xFF)] ^ ct[w1 >> 24];
 }
 
-// R <- f(shift(R, 4080), d): the next piece of this thread sits 4080 bytes after the last one.
+// Byte tables ct (kByteTabWords): four lookups shift R, then slice-by-8 twice.
 __device__ __forceinline__ uint32_t crc_step(const uint32_t* ct, uint32_t r, const uint32_t (&d)[4]) {
   const uint32_t s = ct[8 * 256 + (r & 0xFF)] ^ ct[9 * 256 + ((r >> 8) & 0xFF)] ^
                      ct[10 * 256 + ((r >> 16) & 0xFF)] ^ ct[11 * 256 + (r >> 24)];
   return slice8(ct, slice8(ct, s, d[0], d[1]), d[2], d[3]);
+}
+
+// Nibble tables nt (kNibTabWords): f(shift(R, 4080), d) = shift(R, 4096) ^ f(0, d), both
+// GF(2)-linear, as the XOR of 40 words: N_p[n] = f(0, the piece with nibble p = n, all else 0)
+// for the 32 nibbles of d, H_q[n] = shift(n << 4q, 4096) for the 8 nibbles of R.  A 16-word
+// table lies in 16 distinct banks of ds_read_b32's 32, so lanes either hit distinct banks or
+// broadcast one word: no conflicts.  The 40 reads are independent (R is not folded into the
+// data first), so the Horner chain through R is one LDS round per piece.
+__device__ __forceinline__ uint32_t nib_word(const uint32_t* t, uint32_t scaled) {
+  return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(t) + scaled);
+}
+
+__device__ __forceinline__ uint32_t crc_step_nib(const uint32_t* nt, uint32_t r, const uint32_t (&d)[4]) {
+  const uint32_t v[5] = {d[0], d[1], d[2], d[3], r};
+  uint32_t t[40];
+#pragma unroll
+  for (int w = 0; w < 5; ++w) {
+    // byte j of lo / hi = 4 x (low / high nibble of byte j): one byte extract per address.  The
+    // empty asm keeps the compiler from re-forming each address as its own shift + mask.
+    uint32_t lo = (v[w] << 2) & 0x3C3C3C3Cu, hi = (v[w] >> 2) & 0x3C3C3C3Cu;
+    asm volatile("" : "+v"(lo), "+v"(hi));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      t[8 * w + 2 * j] = nib_word(nt + (8 * w + 2 * j) * 16, (lo >> (8 * j)) & 0xFFu);
+      t[8 * w + 2 * j + 1] = nib_word(nt + (8 * w + 2 * j + 1) * 16, (hi >> (8 * j)) & 0xFFu);
+    }
+  }
+  // three-input XORs (v_bitop3_b32): 40 -> 1 in 20 instructions
+  uint32_t u[14];
+#pragma unroll
+  for (int i = 0; i < 13; ++i) u[i] = __builtin_amdgcn_bitop3_b32(t[3 * i], t[3 * i + 1], t[3 * i + 2], 0x96);
+  u[13] = t[39];
+  const uint32_t a0 = __builtin_amdgcn_bitop3_b32(u[0], u[1], u[2], 0x96);
+  const uint32_t a1 = __builtin_amdgcn_bitop3_b32(u[3], u[4], u[5], 0x96);
+  const uint32_t a2 = __builtin_amdgcn_bitop3_b32(u[6], u[7], u[8], 0x96);
+  const uint32_t a3 = __builtin_amdgcn_bitop3_b32(u[9], u[10], u[11], 0x96);
+  const uint32_t a4 = __builtin_amdgcn_bitop3_b32(u[12], u[13], a0, 0x96);
+  return __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(a1, a2, a3, 0x96), a4, 0u, 0x96);
 }
 
 // a * b mod P (reflected: bit 31 = x^0)
@@ -157,10 +204,10 @@ __global__ __launch_bounds__(256) void gf_crc_kernel(const GfCrcArgs a) {
   constexpr int NR = (CIN ? K : 0) + M;  // checksummed rows
   __shared__ u32x4 tab01[K * M];
   __shared__ uint32_t tab2[K * M];
-  __shared__ uint32_t ct[kTabWords];
+  __shared__ uint32_t ct[kByteTabWords];
   __shared__ uint32_t red[4][NR];
   dev::build_tables<M>(K, M, a.coef, tab01, tab2);
-  for (int i = threadIdx.x; i < kTabWords; i += 256) ct[i] = a.tabs[i];
+  for (int i = threadIdx.x; i < kByteTabWords; i += 256) ct[i] = a.tabs[i];
   __syncthreads();
 
   const uint32_t g = blockIdx.x, stripe = blockIdx.y;
