@@ -48,21 +48,19 @@ uint32_t xpow(int64_t e) {
 
 std::vector<uint32_t> host_tables() {
   std::vector<uint32_t> t(crcdev::kTabWords + crcdev::kBasisWords);
-  for (uint32_t b = 0; b < 256; ++b) {  // T0: the byte-at-a-time table of hash/crc32
-    uint32_t c = b;
-    for (int i = 0; i < 8; ++i) c = (c & 1u) ? (c >> 1) ^ crcdev::kPoly : c >> 1;
-    t[b] = c;
-  }
-  for (int n = 1; n < 8; ++n)  // Tn[b] = f(0, b followed by n zero bytes)
-    for (int b = 0; b < 256; ++b) {
-      const uint32_t v = t[(n - 1) * 256 + b];
-      t[n * 256 + b] = (v >> 8) ^ t[v & 0xFF];
-    }
-  const uint32_t k4080 = xpow(8 * 4080);
-  for (int q = 0; q < 4; ++q)  // Hq[b] = shift(b << 8q, 4080)
-    for (uint32_t b = 0; b < 256; ++b) t[(8 + q) * 256 + b] = mulmod(k4080, b << (8 * q));
-  uint32_t* nt = t.data() + crcdev::kByteTabWords;
   const uint32_t k4096 = xpow(8 * 4096);
+  for (int j = 0; j < 16; ++j)  // Fj[b] = f(0, 16-byte piece with byte j = b, the rest 0)
+    for (uint32_t b = 0; b < 256; ++b) {
+      uint32_t c = 0;
+      for (int i = 0; i < 16; ++i) {
+        c ^= i == j ? b : 0u;
+        for (int q = 0; q < 8; ++q) c = (c & 1u) ? (c >> 1) ^ crcdev::kPoly : c >> 1;
+      }
+      t[j * 256 + b] = c;
+    }
+  for (int q = 0; q < 4; ++q)  // Gq[b] = shift(b << 8q, 4096)
+    for (uint32_t b = 0; b < 256; ++b) t[(16 + q) * 256 + b] = mulmod(k4096, b << (8 * q));
+  uint32_t* nt = t.data() + crcdev::kByteTabWords;
   for (int p = 0; p < 32; ++p)  // Np[n] = f(0, 16-byte piece with nibble p = n, the rest 0)
     for (uint32_t n = 0; n < 16; ++n) {
       uint8_t piece[16] = {};

@@ -15,7 +15,7 @@
 // Work split.  A workgroup owns `tpw` consecutive 4 KiB tiles of one stripe; thread j holds
 // bytes [16j, 16j+16) of every row of each tile (the fixed-K GF tile of gf_device.hpp).  Per
 // checksummed row it keeps a Horner register over its pieces, R <- f(shift(R, 4080), piece):
-// four byte lookups for the shift, then slice-by-8 twice -- 20 LDS lookups per 16 bytes.  After
+// 20 independent byte-table lookups per 16 bytes (crc_step below).  After
 // its last tile the thread moves R from its piece end to the tile end e (x^(8*16*(255-j)), a
 // 32-column GF(2) basis read once from global memory), the 256 threads XOR-reduce, and one
 // multiply by x^(8(S - e)) moves the sum to the shard end (a host constant per workgroup;
@@ -36,7 +36,7 @@ using dev::u32x4;
 constexpr uint32_t kPoly = 0xEDB88320u;
 constexpr int kTile = 4096;            // bytes per row per tile: 256 threads x 16 B
 constexpr int kMaxK = 18, kMaxM = 6, kPtrSlots = 96, kMaxGroups = 384;
-constexpr int kByteTabWords = 12 * 256;  // T0..T7: slice-by-8;  H0..H3: shift by 4080 bytes
+constexpr int kByteTabWords = 20 * 256;  // F0..F15: bytes of a 16-B piece;  G0..G3: register bytes
 constexpr int kNibTabWords = 40 * 16;    // N0..N31: nibbles of a 16-B piece;  H0..H7: register nibbles
 constexpr int kTabWords = kByteTabWords + kNibTabWords;  // device table block, the basis follows
 constexpr int kBasisWords = 256 * 32;  // thread j: the 32 columns of shift(., 16*(255-j))
@@ -57,25 +57,29 @@ struct __attribute__((aligned(16))) GfCrcArgs {
 static_assert(sizeof(GfCrcArgs) <= 3584, "kernel argument block must stay below 4 KiB");
 
 // Two equivalent Horner steps R <- f(shift(R, 4080), d) over a thread's next 16-byte piece d,
-// which sits 4080 bytes after its previous one.  The byte-table step costs 20 LDS reads and ~40
+// which sits 4080 bytes after its previous one.  The byte-table step costs 20 LDS reads and ~30
 // VALU; its random byte indices into 256-word tables conflict (~2.6 LDS cycles per read per lane
-// group).  The nibble-table step costs 40 conflict-free reads and ~75 VALU.  Kernels whose VALU
+// group).  The nibble-table step costs 40 conflict-free reads and ~80 VALU.  Kernels whose VALU
 // is already busy with the GF product (gf_crc_kernel) take the byte step; the CRC-only kernels
-// (crc32.hip, crc32block.hip) take the nibble step (profiles/r01/crc_nibble_ab.txt).
+// (crc32.hip, crc32block.hip) take the nibble step (profiles/r01/crc_nibble_ab.txt: also the
+// earlier slice-by-8 byte step, whose three dependent LDS rounds per piece cost 1-8 %).
 
-// f(r, 8 bytes w0|w1): slice-by-8 with ct[n*256 + b] = f(0, b followed by n zero bytes).
-__device__ __forceinline__ uint32_t slice8(const uint32_t* ct, uint32_t r, uint32_t w0, uint32_t w1) {
-  w0 ^= r;
-  return ct[7 * 256 + (w0 & 0xFF)] ^ ct[6 * 256 + ((w0 >> 8) & 0xFF)] ^ ct[5 * 256 + ((w0 >> 16) & 0xFF)] ^
-         ct[4 * 256 + (w0 >> 24)] ^ ct[3 * 256 + (w1 & 0xFF)] ^ ct[2 * 256 + ((w1 >> 8) & 0xFF)] ^
-         ct[1 * 256 + ((w1 >> 16) & 0xFF)] ^ ct[w1 >> 24];
-}
-
-// Byte tables ct (kByteTabWords): four lookups shift R, then slice-by-8 twice.
+// Byte tables ct (kByteTabWords): f(shift(R, 4080), d) = shift(R, 4096) ^ f(0, d) as the XOR of
+// 20 independent words, F_j[b] = f(0, the piece with byte j = b, all else 0) and
+// G_q[b] = shift(b << 8q, 4096): one LDS round per piece instead of three dependent ones.
 __device__ __forceinline__ uint32_t crc_step(const uint32_t* ct, uint32_t r, const uint32_t (&d)[4]) {
-  const uint32_t s = ct[8 * 256 + (r & 0xFF)] ^ ct[9 * 256 + ((r >> 8) & 0xFF)] ^
-                     ct[10 * 256 + ((r >> 16) & 0xFF)] ^ ct[11 * 256 + (r >> 24)];
-  return slice8(ct, slice8(ct, s, d[0], d[1]), d[2], d[3]);
+  const uint32_t v[5] = {d[0], d[1], d[2], d[3], r};
+  uint32_t t[20];
+#pragma unroll
+  for (int w = 0; w < 5; ++w)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) t[4 * w + j] = ct[(4 * w + j) * 256 + ((v[w] >> (8 * j)) & 0xFFu)];
+  uint32_t u[7];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) u[i] = __builtin_amdgcn_bitop3_b32(t[3 * i], t[3 * i + 1], t[3 * i + 2], 0x96);
+  u[6] = t[18] ^ t[19];
+  return __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(u[0], u[1], u[2], 0x96),
+                                     __builtin_amdgcn_bitop3_b32(u[3], u[4], u[5], 0x96), u[6], 0x96);
 }
 
 // Nibble tables nt (kNibTabWords): f(shift(R, 4080), d) = shift(R, 4096) ^ f(0, d), both
