@@ -11,8 +11,8 @@
 // owns block b0 + w of object y, streams its payload in 4 KiB tiles cut at 16-byte boundaries of
 // the destination (thread j: the 16-byte piece j of each tile, the next tile's piece in flight;
 // loads may be unaligned, stores are aligned), folds every
-// piece into a Horner register with the slice-by-8 LDS tables of the shard CRC kernels (gf_crc.hpp:
-// R <- f(shift(R, 4080), piece)), and copies the piece to its destination.  After the last tile a
+// piece into a Horner register with the nibble LDS tables of the shard CRC kernels (gf_crc.hpp
+// crc_step_nib: R <- f(shift(R, 4080), piece)), and copies the piece to its destination.  After the last tile a
 // per-thread basis moves R to the tile end, the workgroup XOR-reduces, and one multiply by
 // x^(8(plen - tiles*4096)) (a negative power: the zero padding of the last tile) gives the raw
 // (zero-preset) CRC of the payload; XOR-ing shift(~0, plen) ^ ~0 makes it ChecksumIEEE.  Encode
@@ -35,6 +35,7 @@ using dev::u32x4;
 
 constexpr int kSlots = 96;  // objects per launch
 constexpr int kRing = 4;    // tiles in flight per thread
+constexpr int kAfter = 320;  // objects of up to 320 blocks (20 MiB at 64 KiB) move a run's CRC in one multiply
 
 struct __attribute__((aligned(16))) BlockArgs {
   const uint8_t* in[kSlots];  // object y: payload of launch block w at in[y] + w*in_stride + in_off
@@ -55,7 +56,10 @@ struct __attribute__((aligned(16))) BlockArgs {
   uint32_t ipw;                // items per workgroup
   uint32_t whole_fin;          // shift(~0, size) ^ ~0
   uint32_t xpow2[40];          // x^(8 P 2^i) for 2^i <= nblk
+  uint32_t nafter;             // entries of xafter (0: nblk too large, use xlast and xpow2)
+  uint32_t xafter[kAfter];     // [r]: x^(8 * payload bytes after block r - 1), 1 <= r < nblk
 };
+static_assert(sizeof(BlockArgs) <= 3584, "kernel argument block must stay below 4 KiB");
 
 // Bytes [lo, hi) of the 16 at p, zero elsewhere.
 __device__ __forceinline__ u32x4 ld_range(const uint8_t* p, uint32_t lo, uint32_t hi) {
@@ -102,6 +106,8 @@ __global__ __launch_bounds__(256) void crc32block_kernel(const BlockArgs a) {
     uint32_t s = acc;
     if (run_end == a.nblk) {
       s ^= a.whole_fin;  // the run ends the object: fold in the conditioning once per object
+    } else if (run_end < a.nafter) {
+      s = crcdev::mulmod(s, a.xafter[run_end]);  // one multiply: thread 0's work is serial
     } else {
       // bytes after the run: nblk - 1 - run_end full blocks, then the last block's payload
       s = crcdev::mulmod(s, a.xlast);
@@ -176,7 +182,7 @@ __global__ __launch_bounds__(256) void crc32block_kernel(const BlockArgs a) {
       if (a.encode) {
         uint8_t* hdr = out + (int64_t)w * a.out_stride;
         for (int j = 0; j < 4; ++j) hdr[j] = (uint8_t)(crc >> (8 * j));
-        if (a.whole) acc = crcdev::mulmod(acc, a.xlen[last]) ^ raw;
+        if (a.whole) acc = (acc ? crcdev::mulmod(acc, a.xlen[last]) : 0u) ^ raw;  // first block of a run: acc = 0
         run_end = (uint32_t)b + 1;
       } else {
         const uint8_t* hdr = in + (int64_t)w * a.in_stride;
@@ -246,6 +252,15 @@ hipError_t launch(const Crc32BlockJob& j, hipStream_t stream) {
   a.xlen[1] = a.xlast;
   a.whole_fin = crc32_shift_ones((size_t)j.size);
   for (int i = 0; i < 40 && (int64_t(1) << i) <= nblk; ++i) a.xpow2[i] = crc_xpow(8 * P * (int64_t(1) << i));
+  if (nblk <= kAfter) {
+    a.nafter = (uint32_t)nblk;
+    const uint32_t xp = crc_xpow(8 * P);
+    uint32_t v = a.xlast;  // after block nblk - 2: the last block's payload
+    for (int64_t r = nblk - 1; r >= 1; --r) {
+      a.xafter[r] = v;
+      v = crc_mulmod(v, xp);
+    }
+  }
   for (int y0 = 0; y0 < j.n; y0 += kSlots) {
     const int ny = std::min(kSlots, j.n - y0);
     for (int y = 0; y < ny; ++y) {

@@ -109,6 +109,7 @@ hipError_t crc_device_tables(const uint32_t** out) {
 }
 
 uint32_t crc_xpow(int64_t e) { return xpow(e); }
+uint32_t crc_mulmod(uint32_t a, uint32_t b) { return mulmod(a, b); }
 
 namespace {
 

@@ -283,6 +283,7 @@ hipError_t launch_crc_k(int m, const GfCrcArgs& a, dim3 grid, hipStream_t st) {
 // per device; x^e mod P for any integer e (negative: powers of x^-1).
 hipError_t crc_device_tables(const uint32_t** out);
 uint32_t crc_xpow(int64_t e);
+uint32_t crc_mulmod(uint32_t a, uint32_t b);  // a * b mod P
 
 namespace crcdev {
 
