@@ -93,8 +93,9 @@ __global__ __launch_bounds__(256) void crc32block_kernel(const BlockArgs a) {
   __shared__ uint32_t red[4];
   for (int i = threadIdx.x; i < crcdev::kNibTabWords; i += 256) ct[i] = a.tabs[crcdev::kByteTabWords + i];
   // this thread's x^(8*16*(255 - j)): moves its Horner register from its piece to the tile end
-  // (column x^0 of its basis, gf_crc.hip host_tables)
-  const uint32_t kj = a.tabs[kTabWords + threadIdx.x * 32 + 31];
+  // (gf_crc.hip host_tables; one coalesced word per thread -- reading column x^0 of the
+  // per-thread basis instead, 128 B apart, cost one L2 request per thread per block)
+  const uint32_t kj = a.tabs[kTabWords + crcdev::kBasisWords + threadIdx.x];
   __syncthreads();
   // work items (launch block w, object y), y-major; a workgroup takes a run of consecutive ones,
   // so the table load above is paid once per workgroup and the whole-object checksum is a Horner

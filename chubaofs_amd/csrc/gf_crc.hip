@@ -47,7 +47,7 @@ uint32_t xpow(int64_t e) {
 }
 
 std::vector<uint32_t> host_tables() {
-  std::vector<uint32_t> t(crcdev::kTabWords + crcdev::kBasisWords);
+  std::vector<uint32_t> t(crcdev::kTabWords + crcdev::kBasisWords + crcdev::kShiftWords);
   const uint32_t k4096 = xpow(8 * 4096);
   for (int j = 0; j < 16; ++j)  // Fj[b] = f(0, 16-byte piece with byte j = b, the rest 0)
     for (uint32_t b = 0; b < 256; ++b) {
@@ -77,6 +77,7 @@ std::vector<uint32_t> host_tables() {
   for (int j = 0; j < 256; ++j) {  // basis of shift(., 16*(255-j)) for thread j
     const uint32_t kj = xpow(8LL * 16 * (255 - j));
     for (int i = 0; i < 32; ++i) t[crcdev::kTabWords + j * 32 + i] = mulmod(kj, 1u << i);
+    t[crcdev::kTabWords + crcdev::kBasisWords + j] = kj;
   }
   return t;
 }

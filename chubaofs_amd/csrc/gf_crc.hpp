@@ -40,6 +40,7 @@ constexpr int kByteTabWords = 20 * 256;  // F0..F15: bytes of a 16-B piece;  G0.
 constexpr int kNibTabWords = 40 * 16;    // N0..N31: nibbles of a 16-B piece;  H0..H7: register nibbles
 constexpr int kTabWords = kByteTabWords + kNibTabWords;  // device table block, the basis follows
 constexpr int kBasisWords = 256 * 32;  // thread j: the 32 columns of shift(., 16*(255-j))
+constexpr int kShiftWords = 256;  // after the basis: [j] = x^(8*16*(255-j)), its column x^0 (coalesced)
 
 struct __attribute__((aligned(16))) GfCrcArgs {
   uint64_t len;
@@ -47,7 +48,7 @@ struct __attribute__((aligned(16))) GfCrcArgs {
   int64_t sstride;       // affine batch: byte distance between stripes (0: explicit table)
   uint32_t tab, fin;     // stripes held in ptr[]; shift(~0, len) ^ ~0
   uint32_t* crc;         // [stripe][crc_stride] checksum words, zeroed by the launcher
-  const uint32_t* tabs;  // device: kTabWords + kBasisWords
+  const uint32_t* tabs;  // device: kTabWords + kBasisWords + kShiftWords
   uint32_t crc_stride, pad0;
   uint8_t slot[kMaxK + kMaxM];  // checksum word of kernel row i (inputs 0..k-1, outputs k..)
   uint8_t coef[kMaxM * kMaxK];
@@ -279,7 +280,7 @@ hipError_t launch_crc_k(int m, const GfCrcArgs& a, dim3 grid, hipStream_t st) {
 
 }  // namespace crcdev
 
-// gf_crc.hip: the lookup tables (kTabWords + kBasisWords) on the current device, uploaded once
+// gf_crc.hip: the lookup tables (kTabWords + kBasisWords + kShiftWords) on the current device, uploaded once
 // per device; x^e mod P for any integer e (negative: powers of x^-1).
 hipError_t crc_device_tables(const uint32_t** out);
 uint32_t crc_xpow(int64_t e);
