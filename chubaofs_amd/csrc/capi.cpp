@@ -440,6 +440,8 @@ int cfsec_crc32block_encode_batch(const uint8_t* const* srcs, uint8_t* const* ds
   return guarded([&] {
     hipStream_t s = as_stream(stream);
     int st = CFSEC_OK;
+    if (shard_crcs && n > 0)
+      st = cfsec::hip_status(hipMemsetAsync(shard_crcs, 0, 4 * (size_t)n, s), "hipMemsetAsync");
     cfsec::Crc32BlockJob j;
     j.encode = true;
     j.n = n;
@@ -448,11 +450,7 @@ int cfsec_crc32block_encode_batch(const uint8_t* const* srcs, uint8_t* const* ds
     j.size = size;
     j.block_len = block_len;
     j.whole = shard_crcs;
-    // with checksums: scratch words one cache line apart, gathered into shard_crcs (overwritten)
-    if (shard_crcs && n > 0)
-      st = cfsec::hip_status(cfsec::launch_crc32block_batch_whole(j, s), "launch_crc32block_batch_whole");
-    else
-      st = cfsec::hip_status(cfsec::launch_crc32block(j, s), "launch_crc32block");
+    if (st == CFSEC_OK) st = cfsec::hip_status(cfsec::launch_crc32block(j, s), "launch_crc32block");
     return st;
   });
 }

@@ -55,7 +55,6 @@ struct __attribute__((aligned(16))) BlockArgs {
   uint32_t xlen[2];            // x^(8 plen): [full block, last block]
   uint32_t ipw;                // items per workgroup
   uint32_t whole_fin;          // shift(~0, size) ^ ~0
-  uint32_t whole_stride;       // words between objects in `whole`
   uint32_t xpow2[40];          // x^(8 P 2^i) for 2^i <= nblk
   uint32_t nafter;             // entries of xafter (0: nblk too large, use xlast and xpow2)
   uint32_t xafter[kAfter];     // [r]: x^(8 * payload bytes after block r - 1), 1 <= r < nblk
@@ -117,7 +116,7 @@ __global__ __launch_bounds__(256) void crc32block_kernel(const BlockArgs a) {
       for (int i = 0; e; e >>= 1, ++i)
         if (e & 1) s = crcdev::mulmod(s, a.xpow2[i]);
     }
-    atomicXor(a.whole + (size_t)run_y * a.whole_stride, s);
+    atomicXor(a.whole + run_y, s);
   };
   for (uint32_t it = it0; it < it1; ++it) {
     const uint32_t y = it / a.nb, w = it - y * a.nb;
@@ -238,8 +237,6 @@ hipError_t launch(const Crc32BlockJob& j, hipStream_t stream) {
     return hipErrorInvalidValue;
   a.bad = j.bad;
   a.whole = j.encode ? j.whole : nullptr;
-  if (j.whole_stride < 1) return hipErrorInvalidValue;
-  a.whole_stride = (uint32_t)j.whole_stride;
   a.b0 = (uint64_t)b0;
   hipError_t e = crc_device_tables(&a.tabs);
   if (e != hipSuccess) return e;
@@ -283,7 +280,7 @@ hipError_t launch(const Crc32BlockJob& j, hipStream_t stream) {
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (a.bad) a.bad += ny;
-    if (a.whole) a.whole += (size_t)ny * a.whole_stride;
+    if (a.whole) a.whole += ny;
   }
   return hipSuccess;
 }
@@ -291,38 +288,5 @@ hipError_t launch(const Crc32BlockJob& j, hipStream_t stream) {
 }  // namespace blk
 
 hipError_t launch_crc32block(const Crc32BlockJob& j, hipStream_t stream) { return blk::launch<true, true>(j, stream); }
-
-namespace blk {
-__global__ __launch_bounds__(256) void gather_whole(const uint32_t* __restrict__ src, uint32_t stride,
-                                                    uint32_t* __restrict__ dst, int n) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < n) dst[i] = src[(size_t)i * stride];
-}
-}  // namespace blk
-
-// Batch encode whose whole-object checksums land in j.whole (n contiguous words, overwritten).
-// Every block XORs its term into its object's word with a device-scope atomic; with the words
-// packed 32 to a 128-byte line, the atomics of all resident workgroups queue on one or two lines
-// (profiles/r01/crc32block_probe.txt: 353 us vs 330 without the checksum), so they go to a
-// stream-ordered scratch with one line per object and a small gather moves them out.
-hipError_t launch_crc32block_batch_whole(const Crc32BlockJob& j, hipStream_t stream) {
-  constexpr int kPad = 32;  // words per object in the scratch: one 128-byte line
-  if (!j.whole || j.n <= 0 || !j.encode) return hipErrorInvalidValue;
-  uint32_t* scratch = nullptr;
-  hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&scratch), sizeof(uint32_t) * kPad * (size_t)j.n, stream);
-  if (e != hipSuccess) return e;
-  e = hipMemsetAsync(scratch, 0, sizeof(uint32_t) * kPad * (size_t)j.n, stream);
-  Crc32BlockJob jp = j;
-  jp.whole = scratch;
-  jp.whole_stride = kPad;
-  if (e == hipSuccess) e = blk::launch<true, true>(jp, stream);
-  if (e == hipSuccess) {
-    hipLaunchKernelGGL(blk::gather_whole, dim3((j.n + 255) / 256), dim3(256), 0, stream, scratch, (uint32_t)kPad,
-                       j.whole, j.n);
-    e = hipGetLastError();
-  }
-  const hipError_t f = hipFreeAsync(scratch, stream);
-  return e != hipSuccess ? e : f;
-}
 
 }  // namespace cfsec

@@ -76,10 +76,8 @@ struct Crc32BlockJob {
                               // block index relative to block from / (block_len - 4)
   uint32_t* whole = nullptr;  // encode, optional: device words [n] preset to 0; receive
                               // crc32.ChecksumIEEE of each whole payload
-  int whole_stride = 1;       // words between consecutive objects' entries of `whole`
 };
 bool crc32block_valid_len(int64_t block_len);  // util.go:34-36
 hipError_t launch_crc32block(const Crc32BlockJob& job, hipStream_t stream);
-hipError_t launch_crc32block_batch_whole(const Crc32BlockJob& job, hipStream_t stream);  // encode, whole != null
 
 }  // namespace cfsec

@@ -76,8 +76,6 @@ int main(int argc, char** argv) {
       {"copy, no epi, runs, pl", [&] { CK((cfsec::blk::launch<true, false, false, false, false, false>(j, 0))); }, 2 * pb},
       {"crc+st, plain st", [&] { CK((cfsec::blk::launch<true, true, true, false, true, false>(j, 0))); }, 2 * pb},
       {"crc+st, no epi, plain", [&] { CK((cfsec::blk::launch<true, true, false, false, true, false>(j, 0))); }, 2 * pb},
-      {"shipped, whole stride 32", [&] { cfsec::Crc32BlockJob j2 = j; j2.whole_stride = 32; CK((cfsec::blk::launch<true, true>(j2, 0))); }, 2 * pb},
-      {"batch_whole (scratch)", [&] { CK((cfsec::launch_crc32block_batch_whole(j, 0))); }, 2 * pb},
       {"shipped, no shard crc", [&] { cfsec::Crc32BlockJob j2 = j; j2.whole = nullptr; CK((cfsec::blk::launch<true, true>(j2, 0))); }, 2 * pb},
       {"flat copy aligned", [&] { kcopy<0, 0><<<4096, 256>>>(pay, frm, (size_t)(pb / 16) - 1); }, 2 * pb},
       {"flat copy src+4", [&] { kcopy<4, 0><<<4096, 256>>>(pay, frm, (size_t)(pb / 16) - 1); }, 2 * pb},
