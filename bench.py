@@ -305,8 +305,9 @@ def main():
     from chubaofs_amd import crc32block
     nsh = nst * total
     flen = crc32block.EncodeSize(S)
-    framed = torch.empty((nsh, flen), dtype=torch.uint8, device=dev)
-    unframed = torch.empty((nsh, S), dtype=torch.uint8, device=dev)
+    # one 256-byte-aligned row per framed shard / unframed shard, like the stripes' rows
+    framed = torch.empty((nsh, (flen + 255) // 256 * 256), dtype=torch.uint8, device=dev)
+    unframed = torch.empty((nsh, pitch), dtype=torch.uint8, device=dev)
     fptrs = (ctypes.c_void_p * nsh)(*[framed[i].data_ptr() for i in range(nsh)])
     uptrs = (ctypes.c_void_p * nsh)(*[unframed[i].data_ptr() for i in range(nsh)])
     fcrc = torch.zeros(nsh, dtype=torch.int32, device=dev)
@@ -315,7 +316,7 @@ def main():
                                                        stream=stream), n_op)
     blk_dec_ms = timed(lambda: crc32block.decode_batch(fptrs, uptrs, S, fbad.data_ptr(), stream=stream), n_op)
     assert bool((fbad == -1).all().item()), "crc32block check failed on freshly framed shards"
-    assert torch.equal(unframed.view(nst, total, S), batch[:, :, :S]), "crc32block round trip differs"
+    assert torch.equal(unframed[:, :S].reshape(nst, total, S), batch[:, :, :S]), "crc32block round trip differs"
     blk_bytes = nsh * (S + flen)  # read the payload and write the frames, or the reverse
     del framed, unframed
 
