@@ -140,9 +140,12 @@ Status DeviceContext::acquire(size_t bytes, size_t nflags, Workspace** out) {
     return hip_status(hipErrorInvalidDevice, "hipSetDevice");
   }
   Status st = CFSEC_OK;
-  if (!ws->stream) st = hip_status(hipStreamCreateWithFlags(&ws->stream, hipStreamNonBlocking), "hipStreamCreate");
+  // Blocking streams: a call without a caller stream is ordered after the work already queued
+  // on the legacy default stream (PyTorch's default stream), e.g. the kernel that produced its
+  // device input.  Non-blocking streams let such a call read its input before it was written.
+  if (!ws->stream) st = hip_status(hipStreamCreateWithFlags(&ws->stream, hipStreamDefault), "hipStreamCreate");
   if (st == CFSEC_OK && !ws->stream2)
-    st = hip_status(hipStreamCreateWithFlags(&ws->stream2, hipStreamNonBlocking), "hipStreamCreate");
+    st = hip_status(hipStreamCreateWithFlags(&ws->stream2, hipStreamDefault), "hipStreamCreate");
   if (st == CFSEC_OK && !ws->ev)
     st = hip_status(hipEventCreateWithFlags(&ws->ev, hipEventDisableTiming), "hipEventCreate");
   if (st == CFSEC_OK && ws->cap < bytes) {

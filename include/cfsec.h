@@ -24,8 +24,9 @@
  * Memory.  mem = CFSEC_MEM_HOST: plain host memory; the engine stages through HBM
  * and returns after the results are back in host memory.  mem = CFSEC_MEM_DEVICE:
  * pointers are HBM device pointers on the engine's device; the call is enqueued on
- * `stream` (hipStream_t, NULL = an engine-owned stream) and returns after it
- * completes.  *_batch entry points never synchronise: they enqueue on `stream`.
+ * `stream` (hipStream_t, NULL = an engine-owned blocking stream, ordered after the
+ * work already queued on the legacy default stream) and returns after it completes.
+ * *_batch entry points never synchronise: they enqueue on `stream`.
  *
  * Threading.  Every handle is safe for concurrent calls from many threads (the
  * reference shares one encoder across goroutines, encoder.go:90,115-116).
