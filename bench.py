@@ -1,17 +1,33 @@
 #!/usr/bin/env python3
 """bench.py -- EC12P4 encode + 4-erasure reconstruct throughput on MI355X.
 
-Workload (BASELINE.json configs[1]/[2], one GPU): a batch of `--stripes` EC12P4
-stripes of 64 MiB blobs (shard size S = ceil(64 MiB / 12) = 5,592,406 B), resident
-in HBM with a 256-B shard pitch.  One step = one pass of the hot path over the batch:
+Workload (BASELINE.json configs[1]/[2], per GPU): batches of `--stripes` EC12P4 stripes of 64 MiB
+blobs (shard size S = ceil(64 MiB / 12) = 5,592,406 B), resident in HBM with a 256-B shard pitch.
+One step = one pass of the hot path over one batch of each operation:
   1. Encode       (cfsec_rs_encode_batch):      read 12*S, write 4*S per stripe
   2. Reconstruct  erased {0,1,2,3}, the worst-case dense decode
                   (cfsec_rs_reconstruct_batch): read 12*S, write 4*S per stripe
-value = data bytes through the engine per second = 2 * 12 * S * stripes * n_gpus / step
-time (each operation counts its stripe's 12*S data bytes once).  Multi-GPU: each rank
-codes its own stripes (weak scaling, no collective on the data path).
+value = data bytes through the engine per second = 2 * 12 * S * stripes * n_gpus / step time
+(each operation counts its stripe's 12*S data bytes once).  Multi-GPU: each rank codes its own
+stripes (weak scaling, no collective on the data path).
+
+No cache reuse between launches: the GPU holds three batches (3 x 716 MB) and step i encodes batch
+i % 3 and reconstructs batch (i + 2) % 3, so between two launches over the same batch at least
+1.4 GB of other traffic passes through the 256 MB Infinity Cache -- every launch reads its inputs
+from HBM (round 1 alternated the two operations on ONE batch, and each re-read the 179 MB the other
+had just written).
+
+Correctness gate (fails a kernel that writes nothing or wrong bytes inside the timed region):
+before the timed region, every batch's rows that its first timed operation writes are zeroed
+(parity before an encode, rows 0-3 before a reconstruct); after it, every row must equal the
+golden codeword (data from the seeded generator, parity from the first encode, which the CPU leg
+checks against the klauspost-strategy CPU port on stripe 0).
 
     python bench.py [--gpus N --steps K --warmup W]
+
+--gpus N > 1 without a torch.distributed environment re-launches this script under
+`python -m torch.distributed.run --nproc-per-node N` as a child process (before this process
+touches a GPU) and exits with its status.
 """
 from __future__ import annotations
 
@@ -22,6 +38,7 @@ import glob
 import json
 import os
 import shutil
+import socket
 import subprocess
 import sys
 import tempfile
@@ -34,7 +51,9 @@ K_DATA, M_PARITY = 12, 4
 BLOB = 64 << 20
 S_DEFAULT = (BLOB + K_DATA - 1) // K_DATA  # 5,592,406 (common/ec/buf.go:77-81)
 ERASED = [0, 1, 2, 3]
+NBATCH = 3  # batches rotated through the step (no Infinity-Cache reuse between launches)
 HBM_PEAK_GBPS = 8000.0  # MI355X spec (MI355X_MICROARCH.md)
+CPU_SHARE = 16  # host CPUs leased with one GPU on the bench pool
 KERNEL = "gf_dy_kernel<12, 4, 4, (cfsec::MatVecMode)0, 0>"  # both step kernels: 12 -> 4 rows, 4x4-dyadic matrices
 
 
@@ -43,15 +62,31 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--stripes", type=int, default=8, help="stripes per GPU per step")
+    p.add_argument("--stripes", type=int, default=8, help="stripes per batch (per GPU per operation)")
     p.add_argument("--shard-size", type=int, default=S_DEFAULT)
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
+    p.add_argument("--op-seconds", type=float, default=0.6, help="device time per isolated-operation figure")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-pmc", action="store_true")
+    p.add_argument("--no-extra", action="store_true", help="skip the secondary per-operation figures")
     p.add_argument("--graph", action="store_true", help="replay each step as a captured HIP graph")
-    p.add_argument("--settle-ms", type=float, default=400.0, help="untimed load before warmup (clock ramp)")
+    p.add_argument("--settle-ms", type=float, default=1000.0, help="untimed load before warmup (clock ramp)")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args()
+
+
+# ----------------------------------------------------------------- multi-rank launch
+def spawn_ranks(args) -> int:
+    """Run this script as N rank processes under torch.distributed.run (a child process: this
+    process never touched a GPU) and return its exit status."""
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
 # ----------------------------------------------------------------- PMC traffic
@@ -92,18 +127,37 @@ def pmc_traffic(args):
 
 
 # ----------------------------------------------------------------- CPU baseline
-def cpu_baseline(S, seconds):
-    """klauspost-strategy restatement (oracle/cpu_simd.c) on the host: the same EC12P4 encode +
-    4-erasure reconstruct of one stripe, repeated for ~`seconds`, with the reference's per-call
-    worker cap (4 with GFNI, else 8; KRS/reedsolomon.go:551-557)."""
+def host_cpu_share():
+    """CPUs this process may use: the affinity mask, capped by a cgroup v2 CPU quota if one is set
+    (the GPU box shows the whole machine in os.cpu_count() but leases a share of it)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        pass
+    usable = min(aff, quota) if quota else aff
+    # the GPU pool leases 16 host CPUs per GPU (its rules: size worker pools to that share, whatever
+    # os.cpu_count() or the affinity mask show)
+    return {"os_cpu_count": os.cpu_count(), "affinity": aff, "cgroup_quota": quota, "lease_share": CPU_SHARE,
+            "usable": min(usable, CPU_SHARE)}
+
+
+def cpu_baseline(S, seconds, stripe0_host, parity0_gpu):
+    """klauspost-strategy restatement (oracle/cpu_simd.c) on the host: EC12P4 encode + 4-erasure
+    reconstruct of stripe 0 of the GPU's batch 0, repeated for ~`seconds`, with the reference's
+    per-call worker cap (4 with GFNI, else 8; KRS/reedsolomon.go:551-557).  Its parity is also the
+    check of the GPU's golden parity for that stripe (the bench's correctness gate)."""
     import numpy as np
 
     from oracle import oracle as O
 
     feats = O.simd_features()
     threads = 4 if feats["gfni"] else 8
-    rng = np.random.default_rng(0xCF5EC000)
-    data = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(K_DATA)]
+    data = [np.ascontiguousarray(stripe0_host[i]) for i in range(K_DATA)]
     parity = [np.zeros(S, np.uint8) for _ in range(M_PARITY)]
     full = O.build_matrix(K_DATA, K_DATA + M_PARITY)
     prow = full[K_DATA:]
@@ -113,6 +167,7 @@ def cpu_baseline(S, seconds):
     survivors = data[4:] + parity
     rebuilt = [np.zeros(S, np.uint8) for _ in range(4)]
     O.simd_code(prow, data, parity, threads)  # warm
+    parity_ok = all(np.array_equal(parity[r], parity0_gpu[r]) for r in range(M_PARITY))
     ops, t0 = 0, time.perf_counter()
     kind = 0
     while True:
@@ -125,29 +180,30 @@ def cpu_baseline(S, seconds):
     for i in range(4):
         assert np.array_equal(rebuilt[i], data[i]), "CPU baseline reconstruct mismatch"
     value = 2 * K_DATA * S * ops / dt / 1e9
-    saturated = cpu_saturated(S, prow, drows, max(2.0, seconds / 2))
+    share = host_cpu_share()
+    saturated = cpu_saturated(S, prow, drows, max(2.0, seconds / 2), share["usable"])
     return {
         "value": round(value, 3), "unit": "GB/s", "cores": threads, "kind": "port",
         "sample": (f"EC12P4 encode + erase{{0,1,2,3}} reconstruct of one S={S} stripe x{ops} "
                    f"({dt:.1f}s), klauspost v1.11.7 strategy restated in C "
                    f"({'AVX2 10x4+2x4 tiles' if kind == 1 else 'GFNI tiles'}), {threads} worker threads"),
-        "host_cpus": os.cpu_count(),
+        "host_cpus": share,
         "features": feats,
         "saturated": saturated,
-    }
+    }, parity_ok
 
 
-def cpu_saturated(S, prow, drows, seconds):
-    """BASELINE.md's second CPU mode: `callers` concurrent single-threaded callers, each coding its
-    own EC12P4 stripe (encode + the {0,1,2,3} reconstruct), for ~`seconds`.  callers = the host's
-    CPUs, capped at 16 (the GPU box's CPU share)."""
+def cpu_saturated(S, prow, drows, seconds, callers):
+    """BASELINE.md's second CPU mode: one single-threaded caller per usable host CPU (affinity
+    mask, capped by the cgroup quota and the pool's 16-CPU lease share), each coding its own EC12P4
+    stripe (encode + the {0,1,2,3} reconstruct), for ~`seconds`."""
     import threading
 
     import numpy as np
 
     from oracle import oracle as O
 
-    callers = max(1, min(16, os.cpu_count() or 1))
+    callers = max(1, int(callers))
     done = [0] * callers
     stop = time.perf_counter() + seconds
 
@@ -176,9 +232,13 @@ def cpu_saturated(S, prow, drows, seconds):
 # ----------------------------------------------------------------- GPU
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ and not args.pmc_child:
+        sys.exit(spawn_ranks(args))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if not args.pmc_child and world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     S, nst = args.shard_size, args.stripes
 
     traffic, pmc_note = None, "skipped"
@@ -194,23 +254,46 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
+        assert dist.get_world_size() == args.gpus
 
     total = K_DATA + M_PARITY
     pitch = (S + 255) // 256 * 256
-    batch = torch.zeros((nst, total, pitch), dtype=torch.uint8, device=dev)
-    for s in range(nst):  # seeded synthetic data, one generator per stripe
-        g = torch.Generator(device=dev)
-        g.manual_seed(0xCF5EC000 + rank * nst + s)
-        batch[s, :K_DATA, :S] = torch.randint(0, 256, (K_DATA, S), generator=g, device=dev, dtype=torch.uint8)
-    base = batch.data_ptr()
-    ptrs = [base + (s * total + i) * pitch for s in range(nst) for i in range(total)]
-    ptrs = (ctypes.c_void_p * len(ptrs))(*ptrs)  # marshalled once, reused by every launch
+    batch = torch.zeros((NBATCH, nst, total, pitch), dtype=torch.uint8, device=dev)
+    for b in range(NBATCH):
+        for s in range(nst):  # seeded synthetic data, one generator per stripe
+            g = torch.Generator(device=dev)
+            g.manual_seed(0xCF5EC000 + (rank * NBATCH + b) * nst + s)
+            batch[b, s, :K_DATA, :S] = torch.randint(0, 256, (K_DATA, S), generator=g, device=dev,
+                                                     dtype=torch.uint8)
+    ptrs = []
+    for b in range(NBATCH):
+        base = batch[b].data_ptr()
+        p = [base + (s * total + i) * pitch for s in range(nst) for i in range(total)]
+        ptrs.append((ctypes.c_void_p * len(p))(*p))  # marshalled once, reused by every launch
     enc = reedsolomon.New(K_DATA, M_PARITY, device=local_rank)
     stream = torch.cuda.Stream(device=dev)
+    launches = [0]  # launches of the step kernel so far (one per batch call: affine 8-stripe batch)
+
+    def encode(b):
+        enc.encode_batch(ptrs[b], S, nst, stream=stream)
+        launches[0] += 1
+
+    def reconstruct(b):
+        enc.reconstruct_batch(ptrs[b], S, nst, ERASED, stream=stream)
+        launches[0] += 1
+
+    step_no = [0]
 
     def step():
-        enc.encode_batch(ptrs, S, nst, stream=stream)
-        enc.reconstruct_batch(ptrs, S, nst, ERASED, stream=stream)
+        i = step_no[0]
+        encode(i % NBATCH)
+        reconstruct((i + 2) % NBATCH)
+        step_no[0] += 1
+
+    with torch.cuda.stream(stream):
+        for b in range(NBATCH):
+            encode(b)  # the golden parity
+    torch.cuda.synchronize()
 
     if args.pmc_child:
         for _ in range(args.warmup + args.steps):
@@ -218,67 +301,66 @@ def main():
         torch.cuda.synchronize()
         return
 
-    step()  # plans the reconstruct (inversion cache) before any timing or capture
+    golden = batch[:, :, :, :S].clone()
+    reconstruct(0)  # plans the reconstruct (inversion cache) before any timing or capture
     torch.cuda.synchronize()
     graph = None
     if args.graph:
-        # optional: one step (two launches) captured into a HIP graph and replayed
+        # optional: the three steps of one rotation captured into a HIP graph
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph, stream=stream):
-            step()
+            for _ in range(NBATCH):
+                step()
         torch.cuda.synchronize()
+        assert args.steps % NBATCH == 0, "--graph replays whole rotations: --steps must be a multiple of 3"
 
-    def run_step():
+    def run_steps(n):
         if graph is None:
-            step()
+            for _ in range(n):
+                step()
         else:
             with torch.cuda.stream(stream):
-                graph.replay()
+                for _ in range(n // NBATCH):
+                    graph.replay()
+                    launches[0] += 2 * NBATCH
+            step_no[0] += n
 
-    def timed(fn, n):
-        """Mean ms per call of fn over n back-to-back calls, one event pair on the launch
-        stream: a timestamp between launches opens idle gaps in the queue (measured
-        6-20 us on MI355X) that slow the next kernel, so per-launch events would time the
-        harness, not the kernel."""
-        t_s = time.perf_counter()
-        while time.perf_counter() - t_s < 0.1:  # settle after the host-side checks' idle gap
-            for _ in range(10):
-                fn()
-            torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        for _ in range(n):
-            fn()
-        e1.record(stream)
-        torch.cuda.synchronize()
-        return e0.elapsed_time(e1) / n
-
-    # Settle: after idle the first ~100-200 launches run up to 10 % slower while the clocks
-    # ramp (measured with tools/bench_env.py), so the device is loaded with the step for
-    # --settle-ms before the W warmup steps.  Nothing from this phase is timed or counted.
+    # Settle: after idle the first ~100-200 launches run up to 10 % slower while the clocks ramp
+    # (tools/bench_env.py), so the device runs the step for --settle-ms before the W warmup steps.
     t_settle = time.perf_counter()
     while time.perf_counter() - t_settle < args.settle_ms / 1e3:
-        for _ in range(10):
-            run_step()
+        run_steps(NBATCH * 4)
         torch.cuda.synchronize()
-    for _ in range(args.warmup):
-        run_step()
+    run_steps(args.warmup)
     torch.cuda.synchronize()
-    golden = batch[:, :, :S].clone()
 
+    # gate: zero what each batch's first timed operation writes
+    first = {}
+    for j in range(args.steps):
+        i = step_no[0] + j
+        first.setdefault(i % NBATCH, "encode")
+        first.setdefault((i + 2) % NBATCH, "reconstruct")
+    for b, op in first.items():
+        if op == "encode":
+            batch[b, :, K_DATA:, :].zero_()
+        else:
+            batch[b, :, ERASED[0]:ERASED[-1] + 1, :].zero_()  # a view: rows 0..3
+    torch.cuda.synchronize()
+
+    timed_first = launches[0]
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     ev0.record(stream)
-    for _ in range(args.steps):
-        run_step()
+    run_steps(args.steps)
     ev1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
+    timed_last = launches[0]
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -286,44 +368,19 @@ def main():
     # both step kernels are gf_dy_kernel<12, 4, 4, kStore> moving the same algorithmic bytes
     avg_ms = ev0.elapsed_time(ev1) / (2 * args.steps)
 
-    # correctness gate: the stripes are unchanged codewords after K reconstructs
-    assert torch.equal(batch[:, :, :S], golden), "batch changed across reconstruct passes"
-    # per-operation rates (outside the timed region)
-    n_op = max(args.steps, 10)
-    enc_ms = timed(lambda: enc.encode_batch(ptrs, S, nst, stream=stream), n_op)
-    rec_ms = timed(lambda: enc.reconstruct_batch(ptrs, S, nst, ERASED, stream=stream), n_op)
-    flags = torch.zeros(nst, dtype=torch.int32, device=dev)
-    verify_ms = timed(lambda: enc.verify_batch(ptrs, S, nst, flags.data_ptr(), stream=stream), n_op)
-    assert int(flags.sum().item()) == 0, "Verify failed after the timed region"
-    # Encode + crc32.ChecksumIEEE of all 16 shards (access/stream_put.go:249-253), fused into the
-    # coding kernel: same algorithmic bytes as the encode
-    crcs = torch.zeros(nst * total, dtype=torch.int32, device=dev)
-    crc_ms = timed(lambda: enc.encode_crc_batch(ptrs, S, nst, crcs.data_ptr(), stream=stream), n_op)
-    # Blobnode's write path frames each shard in 64 KiB crc32block blocks and takes the shard's
-    # checksum on the way (core/storage/datafile.go:345-373); its read path checks and unframes them
-    # (datafile.go:406-426).  All 16 shards of every stripe in one framing / one checking launch.
-    from chubaofs_amd import crc32block
-    nsh = nst * total
-    flen = crc32block.EncodeSize(S)
-    # one 256-byte-aligned row per framed shard / unframed shard, like the stripes' rows
-    framed = torch.empty((nsh, (flen + 255) // 256 * 256), dtype=torch.uint8, device=dev)
-    unframed = torch.empty((nsh, pitch), dtype=torch.uint8, device=dev)
-    fptrs = (ctypes.c_void_p * nsh)(*[framed[i].data_ptr() for i in range(nsh)])
-    uptrs = (ctypes.c_void_p * nsh)(*[unframed[i].data_ptr() for i in range(nsh)])
-    fcrc = torch.zeros(nsh, dtype=torch.int32, device=dev)
-    fbad = torch.zeros(nsh, dtype=torch.int32, device=dev)
-    blk_enc_ms = timed(lambda: crc32block.encode_batch(ptrs, fptrs, S, shard_crcs_ptr=fcrc.data_ptr(),
-                                                       stream=stream), n_op)
-    blk_dec_ms = timed(lambda: crc32block.decode_batch(fptrs, uptrs, S, fbad.data_ptr(), stream=stream), n_op)
-    assert bool((fbad == -1).all().item()), "crc32block check failed on freshly framed shards"
-    assert torch.equal(unframed[:, :S].reshape(nst, total, S), batch[:, :, :S]), "crc32block round trip differs"
-    blk_bytes = nsh * (S + flen)  # read the payload and write the frames, or the reverse
-    del framed, unframed
+    # correctness gate: every row the timed launches wrote is the golden codeword again
+    for b in range(NBATCH):
+        assert torch.equal(batch[b, :, :, :S], golden[b]), f"batch {b} differs from the golden codeword after the timed steps"
+    gate = {"zeroed_before_timed": {str(b): op for b, op in sorted(first.items())}, "rows_equal_golden": True}
 
     data_bytes = K_DATA * S * nst
     launch_bytes = (K_DATA + M_PARITY) * S * nst  # algorithmic bytes per launch (read 12S + write 4S)
     achieved = launch_bytes / (avg_ms * 1e-3) / 1e9
     value = 2 * data_bytes * world * args.steps / elapsed / 1e9
+
+    extra = {}
+    if not args.no_extra:
+        extra = secondary(args, torch, enc, batch, ptrs, stream, S, nst, pitch, dev, launch_bytes, data_bytes)
 
     if rank != 0:
         if world > 1:
@@ -331,7 +388,10 @@ def main():
         return
     cpu = None
     if world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(S, args.cpu_seconds)
+        stripe0 = golden[0, 0].cpu().numpy()
+        cpu, parity_ok = cpu_baseline(S, args.cpu_seconds, stripe0[:K_DATA], stripe0[K_DATA:])
+        assert parity_ok, "GPU golden parity of stripe 0 differs from the CPU port's"
+        gate["stripe0_parity_equals_cpu_port"] = True
     out = {
         "metric": "EC12P4 encode + 4-erasure reconstruct data GB/s",
         "value": round(value, 2),
@@ -347,8 +407,9 @@ def main():
         "data": "synthetic: seeded uniform bytes (torch Generator seed 0xCF5EC000 + stripe), HBM-resident",
         "config": {
             "workload": "EC12P4 Encode then Reconstruct(erased {0,1,2,3}) of 64 MiB-blob stripes",
-            "code_mode": "EC12P4", "shard_size": S, "shard_pitch": pitch, "stripes_per_gpu": nst,
-            "erased": ERASED, "parallelism": f"stripes sharded over {world} GPU(s), no collective",
+            "code_mode": "EC12P4", "shard_size": S, "shard_pitch": pitch, "stripes_per_batch": nst,
+            "batches_rotated": NBATCH, "erased": ERASED,
+            "parallelism": f"stripes sharded over {world} GPU(s), no collective",
             "value_def": "2 * 12 * S * stripes * n_gpus / step time (encode and reconstruct each count the stripe's data once)",
         },
         "roofline": {
@@ -360,30 +421,95 @@ def main():
             "avg_launch_ms": round(avg_ms, 4),
             "launch_timing": ("HIP event pair on the launch stream around the timed region / launches"
                               + (" (graph replay)" if graph is not None else "")),
+            "timed_dispatches": [timed_first, timed_last],
+            "timed_dispatches_note": ("0-based indices [first, last) of the timed launches among this process's "
+                                      "launches of `kernel`, in dispatch order (tools/timed_region_stats.py)"),
             "traffic_note": pmc_note if traffic is None else "rocprofv3 (2*FETCH_SIZE + WRITE_SIZE)*1024, per launch",
-            "cache_note": ("the step alternates encode and reconstruct over the same stripes: each reads the "
-                           "4 rows the other just wrote (4*S*stripes = 179 MB, under the 256 MB Infinity Cache), "
-                           "and with sc1 output stores part of that is served from the cache; the same kernels "
-                           "repeated back to back on one operation (no reuse) give encode_roofline_frac / "
-                           "reconstruct_roofline_frac"),
+            "cache_note": ("3 batches rotated (step i: encode i%3, reconstruct (i+2)%3): >= 1.4 GB of other traffic "
+                           "between two launches over the same batch, so the 256 MB Infinity Cache serves no reuse"),
         },
-        "encode_data_GBps": round(data_bytes / (enc_ms * 1e-3) / 1e9, 1),
-        "encode_roofline_frac": round(launch_bytes / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
-        "reconstruct_data_GBps": round(data_bytes / (rec_ms * 1e-3) / 1e9, 1),
-        "reconstruct_roofline_frac": round(launch_bytes / (rec_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
-        "verify_data_GBps": round(data_bytes / (verify_ms * 1e-3) / 1e9, 1),
-        "verify_roofline_frac": round(launch_bytes / (verify_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
-        "encode_crc_data_GBps": round(data_bytes / (crc_ms * 1e-3) / 1e9, 1),
-        "encode_crc_roofline_frac": round(launch_bytes / (crc_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
-        "crc32block_encode_data_GBps": round(nsh * S / (blk_enc_ms * 1e-3) / 1e9, 1),
-        "crc32block_encode_roofline_frac": round(blk_bytes / (blk_enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
-        "crc32block_decode_data_GBps": round(nsh * S / (blk_dec_ms * 1e-3) / 1e9, 1),
-        "crc32block_decode_roofline_frac": round(blk_bytes / (blk_dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+        "gate": gate,
         "cpu_baseline": cpu,
     }
+    out.update(extra)
     print(json.dumps(out), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+def secondary(args, torch, enc, batch, ptrs, stream, S, nst, pitch, dev, launch_bytes, data_bytes):
+    """Per-operation figures outside the timed region: each operation repeated for ~op_seconds of
+    device time, rotating over the batches like the step (no cache reuse)."""
+
+    def timed(fn):
+        for i in range(6):  # settle after the idle gap of the host-side checks; estimate
+            fn(i % NBATCH)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for i in range(6):
+            fn(i % NBATCH)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        est = max(e0.elapsed_time(e1) / 6, 1e-3)
+        n = max(args.steps, int(args.op_seconds * 1e3 / est))
+        e0.record(stream)
+        for i in range(n):
+            fn(i % NBATCH)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / n
+
+    rate = lambda nbytes, ms: round(nbytes / (ms * 1e-3) / 1e9, 1)
+    frac = lambda nbytes, ms: round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+    out = {}
+    enc_ms = timed(lambda b: enc.encode_batch(ptrs[b], S, nst, stream=stream))
+    rec_ms = timed(lambda b: enc.reconstruct_batch(ptrs[b], S, nst, ERASED, stream=stream))
+    flags = torch.zeros(nst, dtype=torch.int32, device=dev)
+    verify_ms = timed(lambda b: enc.verify_batch(ptrs[b], S, nst, flags.data_ptr(), stream=stream))
+    assert int(flags.sum().item()) == 0, "Verify failed after the timed region"
+    # Encode + crc32.ChecksumIEEE of all 16 shards (access/stream_put.go:249-253), fused into the
+    # coding kernel: same algorithmic bytes as the encode
+    total = K_DATA + M_PARITY
+    crcs = torch.zeros(nst * total, dtype=torch.int32, device=dev)
+    crc_ms = timed(lambda b: enc.encode_crc_batch(ptrs[b], S, nst, crcs.data_ptr(), stream=stream))
+    out.update({
+        "encode_data_GBps": rate(data_bytes, enc_ms), "encode_roofline_frac": frac(launch_bytes, enc_ms),
+        "reconstruct_data_GBps": rate(data_bytes, rec_ms), "reconstruct_roofline_frac": frac(launch_bytes, rec_ms),
+        "verify_data_GBps": rate(data_bytes, verify_ms), "verify_roofline_frac": frac(launch_bytes, verify_ms),
+        "encode_crc_data_GBps": rate(data_bytes, crc_ms), "encode_crc_roofline_frac": frac(launch_bytes, crc_ms),
+    })
+    # Blobnode's write path frames each shard in 64 KiB crc32block blocks and takes the shard's
+    # checksum on the way (core/storage/datafile.go:345-373); its read path checks and unframes them
+    # (datafile.go:406-426).  All 16 shards of every stripe of a batch in one framing / checking launch.
+    from chubaofs_amd import crc32block
+    nsh = nst * total
+    flen = crc32block.EncodeSize(S)
+    fpitch = (flen + 255) // 256 * 256
+    framed = torch.empty((NBATCH, nsh, fpitch), dtype=torch.uint8, device=dev)
+    unframed = torch.empty((NBATCH, nsh, pitch), dtype=torch.uint8, device=dev)
+    fptrs = [(ctypes.c_void_p * nsh)(*[framed[b, i].data_ptr() for i in range(nsh)]) for b in range(NBATCH)]
+    uptrs = [(ctypes.c_void_p * nsh)(*[unframed[b, i].data_ptr() for i in range(nsh)]) for b in range(NBATCH)]
+    fcrc = torch.zeros(nsh, dtype=torch.int32, device=dev)
+    fbad = torch.zeros(nsh, dtype=torch.int32, device=dev)
+    blk_enc_ms = timed(lambda b: crc32block.encode_batch(ptrs[b], fptrs[b], S, shard_crcs_ptr=fcrc.data_ptr(),
+                                                         stream=stream))
+    blk_dec_ms = timed(lambda b: crc32block.decode_batch(fptrs[b], uptrs[b], S, fbad.data_ptr(), stream=stream,
+                                                         src_len=fpitch))
+    assert bool((fbad == -1).all().item()), "crc32block check failed on freshly framed shards"
+    for b in range(NBATCH):
+        assert torch.equal(unframed[b, :, :S].reshape(nst, total, S), batch[b, :, :, :S]), "crc32block round trip differs"
+    blk_bytes = nsh * (S + flen)  # read the payload and write the frames, or the reverse
+    out.update({
+        "crc32block_encode_data_GBps": rate(nsh * S, blk_enc_ms),
+        "crc32block_encode_roofline_frac": frac(blk_bytes, blk_enc_ms),
+        "crc32block_decode_data_GBps": rate(nsh * S, blk_dec_ms),
+        "crc32block_decode_roofline_frac": frac(blk_bytes, blk_dec_ms),
+        "secondary_note": ("each operation repeated for ~op_seconds of device time over the rotated batches, "
+                           "HIP events on the launch stream; roofline fractions use the same algorithmic bytes"),
+    })
+    del framed, unframed
+    return out
 
 
 if __name__ == "__main__":

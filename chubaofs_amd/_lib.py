@@ -110,11 +110,11 @@ SIGNATURES = {
     "cfsec_crc32block_encode_size": ([ctypes.c_int64, ctypes.c_int64], ctypes.c_int64),
     "cfsec_crc32block_decode_size": ([ctypes.c_int64, ctypes.c_int64], ctypes.c_int64),
     "cfsec_crc32block_encode": ([_V, ctypes.c_int64, ctypes.c_int64, _V, _P(ctypes.c_uint32), _I, _I, _V], _I),
-    "cfsec_crc32block_decode": ([_V, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _V,
-                                 _P(ctypes.c_int64), _I, _I, _V], _I),
+    "cfsec_crc32block_decode": ([_V, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                 ctypes.c_int64, _V, _P(ctypes.c_int64), _I, _I, _V], _I),
     "cfsec_crc32block_encode_batch": ([_V, _V, _I, ctypes.c_int64, ctypes.c_int64, _V, _V], _I),
-    "cfsec_crc32block_decode_batch": ([_V, _V, _I, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
-                                       ctypes.c_int64, _V, _V], _I),
+    "cfsec_crc32block_decode_batch": ([_V, ctypes.c_int64, _V, _I, ctypes.c_int64, ctypes.c_int64,
+                                       ctypes.c_int64, ctypes.c_int64, _V, _V], _I),
 }
 
 _LIB = None

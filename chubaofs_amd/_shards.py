@@ -106,9 +106,25 @@ def shard_size(shards) -> int:
     return 0
 
 
-def stream_ptr(stream):
+def stream_ptr(stream, like=None, device=None):
+    """The hipStream_t to pass for `stream`.  None means the caller's current PyTorch stream on the
+    device the call runs on (the device of the torch buffer `like`, else `device`): a call must be
+    ordered after the kernel that produced its input, and PyTorch's side streams are non-blocking,
+    so the C ABI's NULL (ordered after the legacy default stream only) would race with them."""
     if stream is None:
-        return None
+        import sys
+        torch = sys.modules.get("torch")
+        if torch is None:
+            return None
+        if like is not None and _is_torch(like) and like.is_cuda:
+            dev = like.device
+        elif device is not None and device >= 0:
+            dev = torch.device("cuda", device)
+        else:
+            return None
+        if not torch.cuda.is_initialized():
+            return None  # nothing can be queued on a stream yet
+        return torch.cuda.current_stream(dev).cuda_stream or None
     if isinstance(stream, int):
         return stream
     return stream.cuda_stream  # torch.cuda.Stream

@@ -68,12 +68,12 @@ def Encode(src, size: int | None = None, block_len: int = DefaultBlockSize, dst=
     mem, dev = _mem_of(src)
     if dst is None:
         dst = _empty_like(src, total)
-    elif _nbytes(dst) < total or _mem_of(dst)[0] != mem:
-        raise _lib.ErrInvalidArg("ErrInvalidArg: dst too small or in another memory space")
+    elif _nbytes(dst) < total or _mem_of(dst) != (mem, dev):
+        raise _lib.ErrInvalidArg("ErrInvalidArg: dst too small or in another memory space / on another device")
     crc = ctypes.c_uint32(0)
     _lib.check(_lib.lib().cfsec_crc32block_encode(_ptr(src) if size else None, size, block_len,
                                                   _ptr(dst) if total else None, ctypes.byref(crc), mem, dev,
-                                                  stream_ptr(stream)))
+                                                  stream_ptr(stream, src)))
     return dst, int(crc.value)
 
 
@@ -86,12 +86,14 @@ def Decode(src, size: int, from_: int = 0, to: int | None = None, block_len: int
     n = to - from_
     if dst is None:
         dst = _empty_like(src, max(n, 0))
-    elif n > 0 and (_nbytes(dst) < n or _mem_of(dst)[0] != mem):
-        raise _lib.ErrInvalidArg("ErrInvalidArg: dst too small or in another memory space")
+    elif n > 0 and (_nbytes(dst) < n or _mem_of(dst) != (mem, dev)):
+        raise _lib.ErrInvalidArg("ErrInvalidArg: dst too small or in another memory space / on another device")
     bad = ctypes.c_int64(-1)
-    st = _lib.lib().cfsec_crc32block_decode(_ptr(src) if _nbytes(src) else None, int(size), int(block_len),
-                                           int(from_), int(to), _ptr(dst) if n > 0 else None, ctypes.byref(bad),
-                                           mem, dev, stream_ptr(stream))
+    # the framed length bounds every read: a short object is ErrShortData (the reference's
+    # SectionReader: io.ErrUnexpectedEOF), never a read past the buffer
+    st = _lib.lib().cfsec_crc32block_decode(_ptr(src) if _nbytes(src) else None, _nbytes(src), int(size),
+                                           int(block_len), int(from_), int(to), _ptr(dst) if n > 0 else None,
+                                           ctypes.byref(bad), mem, dev, stream_ptr(stream, src))
     if st == _lib.ErrMismatchedCrc.status:
         e = _lib.ErrMismatchedCrc(f"ErrMismatchedCrc: block {bad.value}")
         e.block = int(bad.value)
@@ -100,19 +102,29 @@ def Decode(src, size: int, from_: int = 0, to: int | None = None, block_len: int
     return dst
 
 
-def encode_batch(srcs, dsts, size: int, block_len: int = DefaultBlockSize, shard_crcs_ptr=None, stream=None):
+def encode_batch(srcs, dsts, size: int, block_len: int = DefaultBlockSize, shard_crcs_ptr=None, stream=None,
+                 device: int = -1):
     """cfsec_crc32block_encode_batch: frame n device payloads of `size` bytes (pointer lists) into
     n framed buffers; shard_crcs_ptr (device, n uint32) receives each payload's ChecksumIEEE.
     Asynchronous on `stream`."""
     _lib.check(_lib.lib().cfsec_crc32block_encode_batch(ptr_array(srcs), ptr_array(dsts), len(srcs), int(size),
-                                                        int(block_len), shard_crcs_ptr, stream_ptr(stream)))
+                                                        int(block_len), shard_crcs_ptr, _batch_stream(stream, device)))
+
+
+def _batch_stream(stream, device):
+    if stream is None:
+        from .reedsolomon import _current_device
+        return stream_ptr(None, device=device if device >= 0 else _current_device())
+    return stream_ptr(stream)
 
 
 def decode_batch(srcs, dsts, size: int, bad_ptr: int, from_: int = 0, to: int | None = None,
-                 block_len: int = DefaultBlockSize, stream=None):
+                 block_len: int = DefaultBlockSize, stream=None, src_len: int | None = None, device: int = -1):
     """cfsec_crc32block_decode_batch: check and unframe payload [from_, to) of n framed device
-    objects; bad_ptr (device, n uint32) receives per object the first bad block or 0xFFFFFFFF."""
+    objects of at least src_len bytes each (default: EncodeSize(size)); bad_ptr (device, n uint32)
+    receives per object the first bad block or 0xFFFFFFFF."""
     to = size if to is None else int(to)
-    _lib.check(_lib.lib().cfsec_crc32block_decode_batch(ptr_array(srcs), ptr_array(dsts) if dsts else None,
+    src_len = EncodeSize(size, block_len) if src_len is None else int(src_len)
+    _lib.check(_lib.lib().cfsec_crc32block_decode_batch(ptr_array(srcs), src_len, ptr_array(dsts) if dsts else None,
                                                         len(srcs), int(size), int(block_len), int(from_), to,
-                                                        bad_ptr, stream_ptr(stream)))
+                                                        bad_ptr, _batch_stream(stream, device)))

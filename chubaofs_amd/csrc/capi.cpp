@@ -70,8 +70,9 @@ int64_t crc32block_framed(int64_t size, int64_t block_len) {
 
 // Encoder.Encode / Decoder.Reader through launch_crc32block: device pointers in place, page-locked
 // host buffers in place (device aliases), other host memory staged through the workspace.
-int crc32block_call(bool encode, const uint8_t* src, int64_t size, int64_t block_len, int64_t from, int64_t to,
-                    uint8_t* dst, uint32_t* shard_crc, int64_t* bad_block, int mem, int device, void* stream) {
+int crc32block_call(bool encode, const uint8_t* src, int64_t src_len, int64_t size, int64_t block_len, int64_t from,
+                    int64_t to, uint8_t* dst, uint32_t* shard_crc, int64_t* bad_block, int mem, int device,
+                    void* stream) {
   if (!cfsec::crc32block_valid_len(block_len)) return CFSEC_ERR_INVALID_BLOCK;
   if (size < 0 || (mem != CFSEC_MEM_HOST && mem != CFSEC_MEM_DEVICE)) return CFSEC_ERR_INVALID_ARG;
   if (!encode && (from < 0 || from > to || to > size)) return CFSEC_ERR_INVALID_ARG;
@@ -90,6 +91,13 @@ int crc32block_call(bool encode, const uint8_t* src, int64_t size, int64_t block
   const int64_t in_bytes = encode ? size : f1 - f0;
   const int64_t out_bytes = encode ? framed : to - from;
   if (!src || (!dst && out_bytes > 0)) return CFSEC_ERR_INVALID_ARG;
+  // Decoder.Reader reads the touched blocks through an io.SectionReader: a framed object that ends
+  // before them is io.ErrUnexpectedEOF there (decode.go:94-97, 126-130), ErrShortData here --
+  // checked before any copy or launch, so nothing reads past the caller's buffer.
+  if (!encode && src_len < f1) {
+    cfsec::set_last_error("crc32block decode: framed source shorter than the blocks the range touches");
+    return CFSEC_ERR_SHORT_DATA;
+  }
   return guarded([&] {
     if (device < 0 && hipGetDevice(&device) != hipSuccess) return (int)CFSEC_ERR_DEVICE;
     cfsec::DeviceContext* ctx = cfsec::DeviceContext::get(device);
@@ -98,6 +106,7 @@ int crc32block_call(bool encode, const uint8_t* src, int64_t size, int64_t block
       return (int)CFSEC_ERR_DEVICE;
     }
     cfsec::DeviceGuard g(device);
+    if (!g.ok()) return cfsec::hip_status(hipErrorInvalidDevice, "hipSetDevice");
     const uint8_t* din = src;
     uint8_t* dout = dst;
     bool stage = false;
@@ -115,7 +124,8 @@ int crc32block_call(bool encode, const uint8_t* src, int64_t size, int64_t block
     int st = ctx->acquire(stage ? (size_t)(in_bytes + out_bytes) : 0, 2, &ws);
     if (st != CFSEC_OK) return st;
     hipStream_t s = stream ? as_stream(stream) : ws->stream;
-    if (stage) {
+    if (!stream && !stage) st = ctx->order_after_default(ws);
+    if (st == CFSEC_OK && stage) {
       st = cfsec::hip_status(hipMemcpyAsync(ws->dbuf, src + (encode ? 0 : f0), (size_t)in_bytes, hipMemcpyHostToDevice, s),
                              "hipMemcpyAsync H2D");
       // the launch addresses the framed object from its start; the staged copy begins at block b0
@@ -394,11 +404,14 @@ int cfsec_crc32_ieee_batch(uint8_t* const* ptrs, size_t shard_size, int n, uint3
       return (int)CFSEC_ERR_DEVICE;
     }
     cfsec::DeviceGuard g(device);
+    if (!g.ok()) return cfsec::hip_status(hipErrorInvalidDevice, "hipSetDevice");
     cfsec::DeviceContext::Workspace* ws = nullptr;
     int st = ctx->acquire(0, (size_t)n, &ws);
     if (st != CFSEC_OK) return st;
     hipStream_t s = stream ? as_stream(stream) : ws->stream;
-    st = cfsec::hip_status(cfsec::launch_crc32(ptrs, shard_size, n, ws->dflags, s), "launch_crc32");
+    if (!stream) st = ctx->order_after_default(ws);
+    if (st == CFSEC_OK)
+      st = cfsec::hip_status(cfsec::launch_crc32(ptrs, shard_size, n, ws->dflags, s), "launch_crc32");
     if (st == CFSEC_OK)
       st = cfsec::hip_status(hipMemcpyAsync(ws->hflags, ws->dflags, 4 * (size_t)n, hipMemcpyDeviceToHost, s),
                              "hipMemcpyAsync D2H");
@@ -425,12 +438,13 @@ int64_t cfsec_crc32block_decode_size(int64_t total, int64_t block_len) {
 
 int cfsec_crc32block_encode(const uint8_t* src, int64_t size, int64_t block_len, uint8_t* dst,
                             uint32_t* shard_crc, int mem, int device, void* stream) {
-  return crc32block_call(true, src, size, block_len, 0, size, dst, shard_crc, nullptr, mem, device, stream);
+  return crc32block_call(true, src, size, size, block_len, 0, size, dst, shard_crc, nullptr, mem, device, stream);
 }
 
-int cfsec_crc32block_decode(const uint8_t* src, int64_t size, int64_t block_len, int64_t from, int64_t to,
-                            uint8_t* dst, int64_t* bad_block, int mem, int device, void* stream) {
-  return crc32block_call(false, src, size, block_len, from, to, dst, nullptr, bad_block, mem, device, stream);
+int cfsec_crc32block_decode(const uint8_t* src, int64_t src_len, int64_t size, int64_t block_len, int64_t from,
+                            int64_t to, uint8_t* dst, int64_t* bad_block, int mem, int device, void* stream) {
+  return crc32block_call(false, src, src_len, size, block_len, from, to, dst, nullptr, bad_block, mem, device,
+                         stream);
 }
 
 int cfsec_crc32block_encode_batch(const uint8_t* const* srcs, uint8_t* const* dsts, int n, int64_t size,
@@ -455,12 +469,22 @@ int cfsec_crc32block_encode_batch(const uint8_t* const* srcs, uint8_t* const* ds
   });
 }
 
-int cfsec_crc32block_decode_batch(const uint8_t* const* srcs, uint8_t* const* dsts, int n, int64_t size,
-                                  int64_t block_len, int64_t from, int64_t to, uint32_t* bad, void* stream) {
+int cfsec_crc32block_decode_batch(const uint8_t* const* srcs, int64_t src_len, uint8_t* const* dsts, int n,
+                                  int64_t size, int64_t block_len, int64_t from, int64_t to, uint32_t* bad,
+                                  void* stream) {
   if (!cfsec::crc32block_valid_len(block_len)) return CFSEC_ERR_INVALID_BLOCK;
   if (n < 0 || size < 0 || from < 0 || from > to || to > size || (n > 0 && (!srcs || !bad)) ||
       (n > 0 && to > from && !dsts))
     return CFSEC_ERR_INVALID_ARG;
+  {  // the framed end of the last block the range touches must lie inside every source object
+    const int64_t P = block_len - 4, b0 = from / P;
+    const int64_t b1 = from < to ? (to - 1) / P : (from % P ? b0 : b0 - 1);
+    const int64_t f1 = std::min(crc32block_framed(size, block_len), (b1 + 1) * block_len);
+    if (b1 >= b0 && src_len < f1) {
+      cfsec::set_last_error("crc32block decode: framed source shorter than the blocks the range touches");
+      return CFSEC_ERR_SHORT_DATA;
+    }
+  }
   return guarded([&] {
     hipStream_t s = as_stream(stream);
     int st = CFSEC_OK;

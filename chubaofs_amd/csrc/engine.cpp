@@ -140,14 +140,16 @@ Status DeviceContext::acquire(size_t bytes, size_t nflags, Workspace** out) {
     return hip_status(hipErrorInvalidDevice, "hipSetDevice");
   }
   Status st = CFSEC_OK;
-  // Blocking streams: a call without a caller stream is ordered after the work already queued
-  // on the legacy default stream (PyTorch's default stream), e.g. the kernel that produced its
-  // device input.  Non-blocking streams let such a call read its input before it was written.
-  if (!ws->stream) st = hip_status(hipStreamCreateWithFlags(&ws->stream, hipStreamDefault), "hipStreamCreate");
+  // Non-blocking streams: work on them does not wait for (or hold up) the legacy default stream,
+  // so concurrent callers overlap.  A device-memory call without a caller stream orders itself
+  // after the default stream explicitly (order_after_default).
+  if (!ws->stream) st = hip_status(hipStreamCreateWithFlags(&ws->stream, hipStreamNonBlocking), "hipStreamCreate");
   if (st == CFSEC_OK && !ws->stream2)
-    st = hip_status(hipStreamCreateWithFlags(&ws->stream2, hipStreamDefault), "hipStreamCreate");
+    st = hip_status(hipStreamCreateWithFlags(&ws->stream2, hipStreamNonBlocking), "hipStreamCreate");
   if (st == CFSEC_OK && !ws->ev)
     st = hip_status(hipEventCreateWithFlags(&ws->ev, hipEventDisableTiming), "hipEventCreate");
+  if (st == CFSEC_OK && !ws->ev_in)
+    st = hip_status(hipEventCreateWithFlags(&ws->ev_in, hipEventDisableTiming), "hipEventCreate");
   if (st == CFSEC_OK && ws->cap < bytes) {
     if (ws->dbuf) (void)hipFree(ws->dbuf);
     ws->dbuf = nullptr;
@@ -174,6 +176,14 @@ Status DeviceContext::acquire(size_t bytes, size_t nflags, Workspace** out) {
   }
   *out = ws;
   return CFSEC_OK;
+}
+
+Status DeviceContext::order_after_default(Workspace* ws) {
+  // An event recorded on the legacy null stream completes after everything queued before it on
+  // that stream and on every blocking stream of the device.
+  Status st = hip_status(hipEventRecord(ws->ev_in, nullptr), "hipEventRecord(null stream)");
+  if (st == CFSEC_OK) st = hip_status(hipStreamWaitEvent(ws->stream, ws->ev_in, 0), "hipStreamWaitEvent");
+  return st;
 }
 
 void DeviceContext::release(Workspace* ws) {
@@ -299,6 +309,7 @@ Status RSEngine::run(const Matrix& rows, const std::vector<cfsec_shard*>& ins,
   Status st = ctx_->acquire(staging, 1, &ws);
   if (st != CFSEC_OK) return st;
   hipStream_t s = (host || !stream) ? ws->stream : stream;
+  if (!host && !stream) st = ctx_->order_after_default(ws);
 
   std::vector<const uint8_t*> din(nin);
   std::vector<uint8_t*> dout(nout);
@@ -505,6 +516,7 @@ Status RSEngine::encode_crc(cfsec_shard* shards, int n, int mem, hipStream_t str
   st = ctx_->acquire(staged ? slot * n : 0, (size_t)n, &ws);
   if (st != CFSEC_OK) return st;
   hipStream_t s = (mem == CFSEC_MEM_HOST || !stream) ? ws->stream : stream;
+  if (!staged && !stream) st = ctx_->order_after_default(ws);
   if (staged)
     for (int i = 0; i < n; ++i) {
       dptr[i] = ws->dbuf + slot * i;
@@ -695,6 +707,7 @@ Status RSEngine::encode_batch(uint8_t* const* ptrs, size_t S, int nstripes, hipS
     for (int r = 0; r < m_; ++r) out[size_t(s) * m_ + r] = ptrs[size_t(s) * total() + k_ + r];
   }
   DeviceGuard g(ctx_->device());
+  if (!g.ok()) return hip_status(hipErrorInvalidDevice, "hipSetDevice");
   MatVecJob job;
   job.k = k_;
   job.m = m_;
@@ -719,6 +732,7 @@ Status RSEngine::verify_batch(uint8_t* const* ptrs, size_t S, int nstripes, uint
     for (int r = 0; r < m_; ++r) out[size_t(s) * m_ + r] = ptrs[size_t(s) * total() + k_ + r];
   }
   DeviceGuard g(ctx_->device());
+  if (!g.ok()) return hip_status(hipErrorInvalidDevice, "hipSetDevice");
   MatVecJob job;
   job.k = k_;
   job.m = m_;
@@ -760,6 +774,7 @@ Status RSEngine::reconstruct_batch(uint8_t* const* ptrs, size_t S, int nstripes,
     for (int r = 0; r < nout; ++r) out[size_t(s) * nout + r] = ptrs[size_t(s) * total() + plan.outputs[r]];
   }
   DeviceGuard g(ctx_->device());
+  if (!g.ok()) return hip_status(hipErrorInvalidDevice, "hipSetDevice");
   MatVecJob job;
   job.k = k_;
   job.m = nout;
@@ -800,6 +815,7 @@ Status RSEngine::encode_crc_batch(uint8_t* const* ptrs, size_t S, int nstripes, 
   if (!ptrs || !crcs || nstripes < 0) return CFSEC_ERR_INVALID_ARG;
   if (nstripes == 0) return CFSEC_OK;
   DeviceGuard g(ctx_->device());
+  if (!g.ok()) return hip_status(hipErrorInvalidDevice, "hipSetDevice");
   if (m_ == 0 || S == 0) {
     Status st = hip_status(hipMemsetAsync(crcs, 0, 4 * (size_t)total() * nstripes, stream), "hipMemsetAsync");
     if (st != CFSEC_OK || S == 0) return st;
@@ -839,6 +855,7 @@ Status RSEngine::reconstruct_crc_batch(uint8_t* const* ptrs, size_t S, int nstri
   for (int i = 0; i < total(); ++i) np += present[i] ? 1 : 0;
   if (np < k_ && nstripes > 0) return CFSEC_ERR_TOO_FEW_SHARDS;
   DeviceGuard g(ctx_->device());
+  if (!g.ok()) return hip_status(hipErrorInvalidDevice, "hipSetDevice");
   if (nstripes == 0) return CFSEC_OK;
   ReconPlan plan;
   if (np < total()) {

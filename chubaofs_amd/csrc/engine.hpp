@@ -44,7 +44,14 @@ class DeviceContext {
     hipStream_t stream = nullptr;
     hipStream_t stream2 = nullptr;  // second lane of the chunked host pipeline
     hipEvent_t ev = nullptr;        // orders stream2 after work enqueued on stream
+    hipEvent_t ev_in = nullptr;     // orders stream after the legacy default stream (no caller stream)
   };
+  // Order ws->stream after the work already queued on the legacy default stream (and, by that
+  // stream's semantics, on every blocking stream of the device): a device-memory call made
+  // without a caller stream must not read its input before the kernel that produced it ran.
+  // The workspace streams themselves are non-blocking, so concurrent callers do not serialise
+  // on each other's null-stream work.
+  Status order_after_default(Workspace* ws);
   // Check out a workspace with at least `bytes` of staging and `nflags` flag words.
   Status acquire(size_t bytes, size_t nflags, Workspace** out);
   void release(Workspace* ws);

@@ -62,14 +62,14 @@ class Encoder:
     # -- coding --
     def Encode(self, shards, stream=None) -> None:
         m = Marshal(shards, fill_size=shard_size(shards))
-        st = self._L.cfsec_ec_encode(self._h, m.ptr(), m.n, m.mem, stream_ptr(stream))
+        st = self._L.cfsec_ec_encode(self._h, m.ptr(), m.n, m.mem, stream_ptr(stream, m.like))
         m.writeback()
         _lib.check(st)
 
     def _recon(self, fn, shards, badIdx, stream):
         m = Marshal(shards, fill_size=shard_size(shards))
         bad = (ctypes.c_int * max(len(badIdx), 1))(*badIdx)
-        st = fn(self._h, m.ptr(), m.n, bad, len(badIdx), m.mem, stream_ptr(stream))
+        st = fn(self._h, m.ptr(), m.n, bad, len(badIdx), m.mem, stream_ptr(stream, m.like))
         m.writeback()
         _lib.check(st)
 
@@ -82,7 +82,7 @@ class Encoder:
     def Verify(self, shards, stream=None) -> bool:
         m = Marshal(shards)
         ok = ctypes.c_int(0)
-        _lib.check(self._L.cfsec_ec_verify(self._h, m.ptr(), m.n, m.mem, stream_ptr(stream), ctypes.byref(ok)))
+        _lib.check(self._L.cfsec_ec_verify(self._h, m.ptr(), m.n, m.mem, stream_ptr(stream, m.like), ctypes.byref(ok)))
         return bool(ok.value)
 
     # -- slice bookkeeping (host) --

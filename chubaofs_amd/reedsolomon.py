@@ -28,6 +28,7 @@ class ReedSolomon:
         self.data_shards = data_shards
         self.parity_shards = parity_shards
         self.total_shards = data_shards + parity_shards
+        self.device = device if device >= 0 else _current_device()
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -38,25 +39,25 @@ class ReedSolomon:
     # -- KRS Encoder methods used by CubeFS --
     def Encode(self, shards, stream=None) -> None:
         m = Marshal(shards)
-        _lib.check(self._L.cfsec_rs_encode(self._h, m.ptr(), m.n, m.mem, stream_ptr(stream)))
+        _lib.check(self._L.cfsec_rs_encode(self._h, m.ptr(), m.n, m.mem, stream_ptr(stream, m.like)))
 
     def EncodeCRC(self, shards, stream=None):
         """Encode + crc32.ChecksumIEEE of every shard, fused (cfsec_rs_encode_crc); returns the
         n checksums (what access computes per shard after Encode, stream_put.go:249-253)."""
         m = Marshal(shards)
         out = (ctypes.c_uint32 * max(m.n, 1))()
-        _lib.check(self._L.cfsec_rs_encode_crc(self._h, m.ptr(), m.n, m.mem, stream_ptr(stream), out))
+        _lib.check(self._L.cfsec_rs_encode_crc(self._h, m.ptr(), m.n, m.mem, stream_ptr(stream, m.like), out))
         return [int(out[i]) for i in range(m.n)]
 
     def Verify(self, shards, stream=None) -> bool:
         m = Marshal(shards)
         ok = ctypes.c_int(0)
-        _lib.check(self._L.cfsec_rs_verify(self._h, m.ptr(), m.n, m.mem, stream_ptr(stream), ctypes.byref(ok)))
+        _lib.check(self._L.cfsec_rs_verify(self._h, m.ptr(), m.n, m.mem, stream_ptr(stream, m.like), ctypes.byref(ok)))
         return bool(ok.value)
 
     def _reconstruct(self, fn, shards, stream):
         m = Marshal(shards, fill_size=shard_size(shards))
-        st = fn(self._h, m.ptr(), m.n, m.mem, stream_ptr(stream))
+        st = fn(self._h, m.ptr(), m.n, m.mem, stream_ptr(stream, m.like))
         m.writeback()
         _lib.check(st)
 
@@ -117,23 +118,23 @@ class ReedSolomon:
 
     def encode_batch(self, ptrs, shard_len: int, nstripes: int, stream=None) -> None:
         _lib.check(self._L.cfsec_rs_encode_batch(self._h, ptr_array(ptrs), shard_len, nstripes,
-                                                 stream_ptr(stream)))
+                                                 stream_ptr(stream, device=self.device)))
 
     def verify_batch(self, ptrs, shard_len: int, nstripes: int, flags_ptr: int, stream=None) -> None:
         _lib.check(self._L.cfsec_rs_verify_batch(self._h, ptr_array(ptrs), shard_len, nstripes,
-                                                 flags_ptr, stream_ptr(stream)))
+                                                 flags_ptr, stream_ptr(stream, device=self.device)))
 
     def reconstruct_batch(self, ptrs, shard_len: int, nstripes: int, erased, data_only=False,
                           stream=None) -> None:
         er = (ctypes.c_int * max(len(erased), 1))(*erased)
         _lib.check(self._L.cfsec_rs_reconstruct_batch(self._h, ptr_array(ptrs), shard_len, nstripes, er,
-                                                      len(erased), int(data_only), stream_ptr(stream)))
+                                                      len(erased), int(data_only), stream_ptr(stream, device=self.device)))
 
     def encode_crc_batch(self, ptrs, shard_len: int, nstripes: int, crcs_ptr: int, stream=None) -> None:
         """encode_batch + crc32.ChecksumIEEE of every shard into the device uint32 array at
         crcs_ptr, [stripe][shard] (access/stream_put.go:249-253), fused where supported."""
         _lib.check(self._L.cfsec_rs_encode_crc_batch(self._h, ptr_array(ptrs), shard_len, nstripes, crcs_ptr,
-                                                     stream_ptr(stream)))
+                                                     stream_ptr(stream, device=self.device)))
 
     def reconstruct_crc_batch(self, ptrs, shard_len: int, nstripes: int, erased, crcs_ptr: int,
                               data_only=False, stream=None) -> None:
@@ -142,7 +143,16 @@ class ReedSolomon:
         er = (ctypes.c_int * max(len(erased), 1))(*erased)
         _lib.check(self._L.cfsec_rs_reconstruct_crc_batch(self._h, ptr_array(ptrs), shard_len, nstripes, er,
                                                           len(erased), int(data_only), crcs_ptr,
-                                                          stream_ptr(stream)))
+                                                          stream_ptr(stream, device=self.device)))
+
+
+def _current_device() -> int:
+    """The HIP device a handle created with device=-1 binds to (the calling thread's current one)."""
+    import sys
+    torch = sys.modules.get("torch")
+    if torch is not None and torch.cuda.is_initialized():
+        return torch.cuda.current_device()
+    return 0
 
 
 def New(data_shards: int, parity_shards: int, device: int = -1) -> ReedSolomon:
@@ -154,6 +164,7 @@ def crc32_ieee_batch(ptrs, shard_len: int, device: int = -1, stream=None):
     """crc32.ChecksumIEEE of each device shard (list of device pointers)."""
     L = _lib.lib()
     out = (ctypes.c_uint32 * max(len(ptrs), 1))()
+    dev = device if device >= 0 else _current_device()
     _lib.check(L.cfsec_crc32_ieee_batch(ptr_array(ptrs), shard_len, len(ptrs), out, device,
-                                        stream_ptr(stream)))
+                                        stream_ptr(stream, device=dev)))
     return [int(out[i]) for i in range(len(ptrs))]

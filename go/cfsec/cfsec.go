@@ -360,12 +360,16 @@ func BlockDecode(framed []byte, size, from, to, blockLen int64) ([]byte, error) 
 		dst = (*C.uint8_t)(unsafe.Pointer(&out[0]))
 	}
 	var bad C.int64_t
-	switch st := C.cfsec_crc32block_decode(src, C.int64_t(size), C.int64_t(blockLen), C.int64_t(from),
-		C.int64_t(to), dst, &bad, C.CFSEC_MEM_HOST, -1, nil); st {
+	switch st := C.cfsec_crc32block_decode(src, C.int64_t(len(framed)), C.int64_t(size), C.int64_t(blockLen),
+		C.int64_t(from), C.int64_t(to), dst, &bad, C.CFSEC_MEM_HOST, -1, nil); st {
 	case C.CFSEC_ERR_MISMATCHED_CRC:
 		return nil, ErrMismatchedCrc
 	case C.CFSEC_ERR_INVALID_BLOCK:
 		return nil, ErrInvalidBlock
+	case C.CFSEC_ERR_SHORT_DATA:
+		// the framed object ends before the blocks the range touches: what the reference's
+		// SectionReader reports (decode.go:94-97, 126-130)
+		return nil, io.ErrUnexpectedEOF
 	default:
 		return out, toError(st)
 	}

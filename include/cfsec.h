@@ -24,8 +24,11 @@
  * Memory.  mem = CFSEC_MEM_HOST: plain host memory; the engine stages through HBM
  * and returns after the results are back in host memory.  mem = CFSEC_MEM_DEVICE:
  * pointers are HBM device pointers on the engine's device; the call is enqueued on
- * `stream` (hipStream_t, NULL = an engine-owned blocking stream, ordered after the
- * work already queued on the legacy default stream) and returns after it completes.
+ * `stream` (hipStream_t) and returns after it completes.  stream = NULL: the call runs on an
+ * engine-owned non-blocking stream that first waits for an event recorded on the legacy default
+ * stream, i.e. it is ordered after everything already queued on the default stream and on every
+ * blocking stream of the device, but not after work on other non-blocking streams (PyTorch's
+ * side streams are non-blocking: pass the producer's stream explicitly).
  * *_batch entry points never synchronise: they enqueue on `stream`.
  *
  * Threading.  Every handle is safe for concurrent calls from many threads (the
@@ -196,22 +199,26 @@ int64_t cfsec_crc32block_decode_size(int64_t total, int64_t block_len);
 int cfsec_crc32block_encode(const uint8_t* src, int64_t size, int64_t block_len, uint8_t* dst,
                             uint32_t* shard_crc, int mem, int device, void* stream);
 /* Decoder.Reader(from, to) (decode.go:122-146; blobnode datafile.go:406-426): check the blocks of
- * the framed object src (payload size `size`) that hold payload bytes [from, to) -- and the block
- * holding `from` when from == to is not block-aligned, as the reference's skip does -- and copy
- * those bytes to dst (to - from bytes; may be NULL when from == to).  CFSEC_ERR_MISMATCHED_CRC when a
- * checked block's checksum differs; *bad_block (may be NULL) = index of the first such block, -1
- * otherwise. */
-int cfsec_crc32block_decode(const uint8_t* src, int64_t size, int64_t block_len, int64_t from, int64_t to,
-                            uint8_t* dst, int64_t* bad_block, int mem, int device, void* stream);
+ * the framed object src (src_len bytes readable; payload size `size`) that hold payload bytes
+ * [from, to) -- and the block holding `from` when from == to is not block-aligned, as the
+ * reference's skip does -- and copy those bytes to dst (to - from bytes; may be NULL when
+ * from == to).  CFSEC_ERR_SHORT_DATA, before anything is read, when src_len ends before the last
+ * touched block (the reference's SectionReader gives io.ErrUnexpectedEOF).
+ * CFSEC_ERR_MISMATCHED_CRC when a checked block's checksum differs; *bad_block (may be NULL) =
+ * index of the first such block, -1 otherwise. */
+int cfsec_crc32block_decode(const uint8_t* src, int64_t src_len, int64_t size, int64_t block_len, int64_t from,
+                            int64_t to, uint8_t* dst, int64_t* bad_block, int mem, int device, void* stream);
 /* Batch forms on device memory, asynchronous on `stream` (NULL = the null stream): n objects of one
- * payload size -- the shards of a stripe batch (blobnode puts and repairs).  encode: shard_crcs
+ * payload size -- the shards of a stripe batch (blobnode puts and repairs); decode: every source
+ * object has at least src_len readable bytes (CFSEC_ERR_SHORT_DATA otherwise, as above).  encode: shard_crcs
  * (device, n words, may be NULL) receives each payload's crc32.ChecksumIEEE.  decode: checks and
  * unframes payload range [from, to) of each object; bad (device, n words) receives per object the
  * index of the first mismatching block counted from block from / (block_len - 4), or 0xFFFFFFFF. */
 int cfsec_crc32block_encode_batch(const uint8_t* const* srcs, uint8_t* const* dsts, int n, int64_t size,
                                   int64_t block_len, uint32_t* shard_crcs, void* stream);
-int cfsec_crc32block_decode_batch(const uint8_t* const* srcs, uint8_t* const* dsts, int n, int64_t size,
-                                  int64_t block_len, int64_t from, int64_t to, uint32_t* bad, void* stream);
+int cfsec_crc32block_decode_batch(const uint8_t* const* srcs, int64_t src_len, uint8_t* const* dsts, int n,
+                                  int64_t size, int64_t block_len, int64_t from, int64_t to, uint32_t* bad,
+                                  void* stream);
 
 #ifdef __cplusplus
 }

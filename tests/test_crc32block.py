@@ -89,3 +89,30 @@ def test_oracle_decode_detects_corruption():
     assert O.crc32block_decode(f, FSIZE, 0, 10)[1] == -1          # block 0 only
     assert O.crc32block_decode(f, FSIZE, 0, 64 * K)[1] == 1       # reaches block 1
     assert O.crc32block_decode(f, FSIZE, 64 * K + 4, 64 * K + 4)[1] == 1  # from == to skips into block 1
+
+
+@pytest.mark.parametrize("lo,hi", [(0, FSIZE), (64 * K + 4, FSIZE), (FSIZE - 1, FSIZE), (64 * K, 64 * K), (0, 10)])
+def test_decode_short_source_is_short_data(lo, hi):
+    """A framed object that ends before the last block [lo, hi) touches is refused before anything
+    is read or copied (the reference's SectionReader gives io.ErrUnexpectedEOF, decode.go:94-97,
+    126-130): host call, no device needed -- the check runs first."""
+    from chubaofs_amd import _lib
+    from chubaofs_amd import crc32block as C
+    d = np.random.default_rng(9).integers(0, 256, FSIZE, dtype=np.uint8)
+    f = O.crc32block_encode(d)
+    P = 64 * K - 4
+    last = (hi - 1) // P if lo < hi else lo // P  # from == to inside a block checks that block
+    end = min(f.size, (last + 1) * 64 * K)       # framed end of the last touched block
+    with pytest.raises(_lib.ErrShortData):
+        C.Decode(np.ascontiguousarray(f[:end - 1]), FSIZE, lo, hi)
+
+
+def test_decode_batch_short_source_is_short_data():
+    from chubaofs_amd import _lib
+    from chubaofs_amd import crc32block as C
+    size = 3 * (64 * K - 4) + 10
+    fake = [0x1000, 0x2000]  # never dereferenced: the length check comes first
+    with pytest.raises(_lib.ErrShortData):
+        C.decode_batch(fake, fake, size, 0x3000, src_len=C.EncodeSize(size) - 1)
+    with pytest.raises(_lib.ErrShortData):  # only block 0 is touched, and it is cut
+        C.decode_batch(fake, fake, size, 0x3000, 0, 10, src_len=64 * K - 1)
