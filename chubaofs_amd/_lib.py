@@ -96,6 +96,10 @@ SIGNATURES = {
     "cfsec_rs_encode_crc": ([_V, P_SHARD, _I, _I, _V, _V], _I),
     "cfsec_rs_encode_crc_batch": ([_V, _V, _S, _I, _V, _V], _I),
     "cfsec_rs_reconstruct_crc_batch": ([_V, _V, _S, _I, _V, _I, _I, _V, _V], _I),
+    "cfsec_rs_set_devices": ([_V, _V, _I], _I),
+    "cfsec_rs_encode_stripes": ([_V, P_SHARD, _I, _I, _V], _I),
+    "cfsec_rs_verify_stripes": ([_V, P_SHARD, _I, _I, _V], _I),
+    "cfsec_rs_reconstruct_stripes": ([_V, P_SHARD, _I, _I, _I, _V], _I),
     "cfsec_codemode_tactic": ([_I, _P(TacticC)], _I),
     "cfsec_ec_new": ([_P(TacticC), _I, _I, _I, _P(_V)], _I),
     "cfsec_ec_free": ([_V], None),
@@ -104,6 +108,8 @@ SIGNATURES = {
     "cfsec_ec_reconstruct_data": ([_V, P_SHARD, _I, _V, _I, _I, _V], _I),
     "cfsec_ec_verify": ([_V, P_SHARD, _I, _I, _V, _P(_I)], _I),
     "cfsec_ec_shards_in_idc": ([_V, _I, _V, _I, _P(_I)], _I),
+    "cfsec_ec_set_devices": ([_V, _V, _I], _I),
+    "cfsec_ec_reconstruct_batch": ([_V, P_SHARD, _I, _I, _V, _V, _I, _I, _V], _I),
     "cfsec_crc32_ieee_batch": ([_V, _S, _I, _V, _I, _V], _I),
     "cfsec_host_alloc": ([_S, _P(_V)], _I),
     "cfsec_host_free": ([_V], _I),

@@ -136,3 +136,34 @@ def ptr_array(ptrs):
     if isinstance(ptrs, ctypes.Array):
         return ptrs
     return (ctypes.c_void_p * len(ptrs))(*[int(p) for p in ptrs])
+
+
+class BatchMarshal:
+    """A list of stripes (each a list of shards, as Marshal takes) as one cfsec_shard array of
+    nstripes * n entries, stripe-major; missing shards get fresh buffers of their stripe's size."""
+
+    def __init__(self, stripes, n, fill=False):
+        self.parts = []
+        self.n = n
+        self.mem = None
+        for st in stripes:
+            if len(st) != n:
+                raise ValueError(f"every stripe needs {n} shards")
+            m = Marshal(st, fill_size=shard_size(st) if fill else None)
+            if self.mem is None:
+                self.mem = m.mem
+            elif m.mem != self.mem and any(_nbytes(x) for x in st):
+                raise TypeError("mixing host and device stripes in one batch")
+            self.parts.append(m)
+        if self.mem is None:
+            self.mem = _lib.MEM_HOST
+        self.arr = (_lib.Shard * max(len(stripes) * n, 1))()
+        for s, m in enumerate(self.parts):
+            for i in range(n):
+                self.arr[s * n + i] = m.arr[i]
+
+    def writeback(self):
+        for s, m in enumerate(self.parts):
+            for i in range(self.n):
+                m.arr[i] = self.arr[s * self.n + i]
+            m.writeback()

@@ -1,0 +1,606 @@
+// batch.cpp -- heterogeneous stripe batches over one or more GPUs (see engine.hpp).
+//
+// The reference codes one stripe per call: access puts encode one blob at a time
+// (access/stream_put.go:104-143, up to 4 in flight per request) and blobnode repairs a tasklet bid
+// by bid, each bid with its own shard size and its own missing set, Reconstruct then Verify
+// (blobnode/work_shard_recover.go:708-771).  Here a whole batch is one call: stripes with the same
+// erasure pattern share one decode plan and run in the same launches (per-stripe lengths in the
+// kernel arguments), Reconstruct + Verify is one pass (the stored rows and the compared rows come
+// out of one product over the first k present shards), and the stripes are spread over the
+// handle's devices, each with its own streams and staging.
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <thread>
+
+#include "engine.hpp"
+
+namespace cfsec {
+namespace {
+
+constexpr size_t kSlot = 256;                      // staging rows start on 256-B boundaries
+constexpr size_t kLaneBudget = size_t(256) << 20;  // staging bytes per lane of a pageable batch
+
+size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+// The HIP device that owns device memory p, or -1.
+int device_of(const void* p) {
+  hipPointerAttribute_t attr;
+  if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  if (attr.type != hipMemoryTypeDevice) return -1;
+  return attr.device;
+}
+
+// KRS/reedsolomon.go:1314-1339 checkShards / shardSize (as engine.cpp's).
+Status stripe_size(const cfsec_shard* shards, int n, bool nilok, size_t* size) {
+  size_t s = 0;
+  for (int i = 0; i < n; ++i)
+    if (shards[i].len != 0) {
+      s = shards[i].len;
+      break;
+    }
+  if (s == 0) return CFSEC_ERR_SHARD_NO_DATA;
+  for (int i = 0; i < n; ++i)
+    if (shards[i].len != s && (shards[i].len != 0 || !nilok)) return CFSEC_ERR_SHARD_SIZE;
+  *size = s;
+  return CFSEC_OK;
+}
+
+// Rows of one device launch group: stripes sharing a plan.
+struct Group {
+  const StripePlan* plan = nullptr;
+  std::vector<StripeTask*> tasks;
+  std::vector<const uint8_t*> in;  // [tasks * k]
+  std::vector<uint8_t*> out;       // [tasks * m]
+  std::vector<uint64_t> lens;
+  int flag0 = 0;                   // first flag word
+};
+
+// Enqueue one group: the mixed store/compare product, split into a store and a compare launch
+// when the rows exceed one launch.
+hipError_t launch_group(const Group& g, uint32_t* dflags, hipStream_t s) {
+  MatVecJob job;
+  job.k = (int)g.plan->in.size();
+  job.m = (int)g.plan->out.size();
+  job.coef = g.plan->rows.v.data();
+  job.nstripes = (int)g.tasks.size();
+  job.in = g.in.data();
+  job.out = g.out.data();
+  job.lens = g.lens.data();
+  job.flags = dflags + g.flag0;
+  job.mode = MatVecMode::kStoreVerify;
+  job.nstore = g.plan->nstore;
+  if (job.m <= kLaunchMaxRows || job.nstore == 0 || job.nstore == job.m) return launch_matvec(job, s);
+  // store rows [0, nstore) then compare rows [nstore, m): two jobs over row subsets
+  const int k = job.k, m = job.m, ns = job.nstripes, nst = job.nstore;
+  std::vector<uint8_t*> o1((size_t)ns * nst), o2((size_t)ns * (m - nst));
+  for (int t = 0; t < ns; ++t) {
+    for (int r = 0; r < nst; ++r) o1[(size_t)t * nst + r] = g.out[(size_t)t * m + r];
+    for (int r = nst; r < m; ++r) o2[(size_t)t * (m - nst) + r - nst] = g.out[(size_t)t * m + r];
+  }
+  MatVecJob a = job, b = job;
+  a.m = nst;
+  a.out = o1.data();
+  a.mode = MatVecMode::kStore;
+  b.m = m - nst;
+  b.coef = g.plan->rows.v.data() + (size_t)nst * k;
+  b.out = o2.data();
+  b.mode = MatVecMode::kVerify;
+  hipError_t e = launch_matvec(a, s);
+  return e != hipSuccess ? e : launch_matvec(b, s);
+}
+
+// Group tasks by plan (first appearance order) and give each group consecutive flag words from
+// *next_flag; row pointers from ptr(task, shard index).
+template <class Ptr>
+std::vector<Group> make_groups(const std::vector<StripeTask*>& tasks, int* next_flag, Ptr ptr) {
+  std::vector<Group> groups;
+  std::map<const StripePlan*, size_t> index;
+  for (StripeTask* t : tasks) {
+    auto it = index.find(t->plan);
+    if (it == index.end()) {
+      it = index.emplace(t->plan, groups.size()).first;
+      groups.emplace_back();
+      groups.back().plan = t->plan;
+    }
+    groups[it->second].tasks.push_back(t);
+  }
+  for (Group& g : groups) {
+    g.flag0 = *next_flag;
+    for (size_t i = 0; i < g.tasks.size(); ++i) {
+      StripeTask* t = g.tasks[i];
+      for (int c : g.plan->in) g.in.push_back(ptr(t, c));
+      for (int o : g.plan->out) g.out.push_back(const_cast<uint8_t*>(ptr(t, o)));
+      g.lens.push_back(t->len);
+    }
+    *next_flag += (int)g.tasks.size();
+  }
+  return groups;
+}
+
+}  // namespace
+
+Status RSEngine::set_devices(const int* devices, int n) {
+  if (!devices || n <= 0) return CFSEC_ERR_INVALID_ARG;
+  std::vector<DeviceContext*> v;
+  for (int i = 0; i < n; ++i) {
+    DeviceContext* c = DeviceContext::get(devices[i]);
+    if (!c) {
+      set_last_error("set_devices: device " + std::to_string(devices[i]) + " does not exist");
+      return CFSEC_ERR_DEVICE;
+    }
+    if (std::find(v.begin(), v.end(), c) != v.end()) return CFSEC_ERR_INVALID_ARG;
+    v.push_back(c);
+  }
+  devs_ = std::move(v);
+  return CFSEC_OK;
+}
+
+Status RSEngine::plan_stripe(const std::vector<bool>& present, bool verify, StripePlan* plan) {
+  // KRS/reedsolomon.go:1453-1501: the first k present rows in index order, decode matrix from the
+  // inversion cache (key: the invalid rows met before the k-th valid one).
+  std::vector<int> invalid;
+  plan->in.clear();
+  for (int row = 0; row < total() && (int)plan->in.size() < k_; ++row) {
+    if (present[row]) plan->in.push_back(row);
+    else invalid.push_back(row);
+  }
+  if ((int)plan->in.size() < k_) return CFSEC_ERR_TOO_FEW_SHARDS;
+  Matrix dec;
+  if (!tree_.get(invalid, &dec)) {
+    Matrix sub(k_, k_);
+    for (int r = 0; r < k_; ++r)
+      for (int c = 0; c < k_; ++c) sub.at(r, c) = mat_.at(plan->in[r], c);
+    if (!mat_invert(sub, dec)) return CFSEC_ERR_SINGULAR;
+    tree_.put(invalid, dec);
+  }
+  // Stored rows: missing data = dec rows (:1508-1524); missing parity = parity x data, the same
+  // linear map over the k inputs as parity_row x dec (:1537-1550).  Compared rows (Verify,
+  // :1287-1301, after the reconstruct): every present parity shard outside the k inputs against
+  // parity_row x dec.  That is the whole of Verify: present data shards are always among the k
+  // inputs (they come first), so the data after the reconstruct is exactly dec x inputs, and a
+  // parity shard that is an input or was just rebuilt equals its row by construction.
+  plan->out.clear();
+  for (int i = 0; i < k_; ++i)
+    if (!present[i]) plan->out.push_back(i);
+  for (int i = k_; i < total(); ++i)
+    if (!present[i]) plan->out.push_back(i);
+  plan->nstore = (int)plan->out.size();
+  if (verify)
+    for (int i = k_; i < total(); ++i)
+      if (present[i] && std::find(plan->in.begin(), plan->in.end(), i) == plan->in.end()) plan->out.push_back(i);
+  plan->rows = Matrix((int)plan->out.size(), k_);
+  const GF& gf = GF::get();
+  for (size_t o = 0; o < plan->out.size(); ++o) {
+    const int idx = plan->out[o];
+    uint8_t* dst = plan->rows.row((int)o);
+    if (idx < k_) {
+      std::memcpy(dst, dec.row(idx), k_);
+    } else {
+      const uint8_t* p = parity_.row(idx - k_);
+      for (int c = 0; c < k_; ++c) {
+        uint8_t v = 0;
+        for (int j = 0; j < k_; ++j) v ^= gf.mul(p[j], dec.at(j, c));
+        dst[c] = v;
+      }
+    }
+  }
+  return CFSEC_OK;
+}
+
+Status RSEngine::encode_stripes(cfsec_shard* const* stripes, int nst, int mem, int* status) {
+  if (!stripes || !status || nst < 0) return CFSEC_ERR_INVALID_ARG;
+  StripePlan plan;
+  for (int i = 0; i < k_; ++i) plan.in.push_back(i);
+  for (int i = k_; i < total(); ++i) plan.out.push_back(i);
+  plan.nstore = m_;
+  plan.rows = parity_;
+  std::vector<StripeTask> tasks;
+  for (int s = 0; s < nst; ++s) {
+    status[s] = CFSEC_OK;
+    size_t S = 0;
+    Status st = stripes[s] ? stripe_size(stripes[s], total(), false, &S) : CFSEC_ERR_INVALID_ARG;
+    for (int i = 0; i < total() && st == CFSEC_OK; ++i)
+      if (!stripes[s][i].data) st = CFSEC_ERR_INVALID_ARG;
+    if (st != CFSEC_OK) {
+      status[s] = st;
+      continue;
+    }
+    if (m_ > 0) tasks.push_back(StripeTask{stripes[s], &plan, S, &status[s], 0});
+  }
+  return run_stripes(tasks, mem);
+}
+
+Status RSEngine::verify_stripes(cfsec_shard* const* stripes, int nst, int mem, int* status) {
+  if (!stripes || !status || nst < 0) return CFSEC_ERR_INVALID_ARG;
+  StripePlan plan;
+  for (int i = 0; i < k_; ++i) plan.in.push_back(i);
+  for (int i = k_; i < total(); ++i) plan.out.push_back(i);
+  plan.nstore = 0;
+  plan.rows = parity_;
+  std::vector<StripeTask> tasks;
+  for (int s = 0; s < nst; ++s) {
+    status[s] = CFSEC_OK;
+    size_t S = 0;
+    Status st = stripes[s] ? stripe_size(stripes[s], total(), false, &S) : CFSEC_ERR_INVALID_ARG;
+    for (int i = 0; i < total() && st == CFSEC_OK; ++i)
+      if (!stripes[s][i].data) st = CFSEC_ERR_INVALID_ARG;
+    if (st != CFSEC_OK) {
+      status[s] = st;
+      continue;
+    }
+    if (m_ > 0) tasks.push_back(StripeTask{stripes[s], &plan, S, &status[s], 0});
+  }
+  return run_stripes(tasks, mem);
+}
+
+Status RSEngine::reconstruct_stripes(cfsec_shard* const* stripes, int nst, int mem, bool verify, int* status) {
+  if (!stripes || !status || nst < 0) return CFSEC_ERR_INVALID_ARG;
+  std::map<std::vector<bool>, std::unique_ptr<StripePlan>> plans;
+  std::vector<StripeTask> tasks;
+  for (int s = 0; s < nst; ++s) {
+    status[s] = CFSEC_OK;
+    cfsec_shard* sh = stripes[s];
+    size_t S = 0;
+    Status st = sh ? stripe_size(sh, total(), true, &S) : CFSEC_ERR_INVALID_ARG;
+    if (st != CFSEC_OK) {
+      status[s] = st;
+      continue;
+    }
+    std::vector<bool> present(total());
+    int np = 0;
+    for (int i = 0; i < total(); ++i) {
+      present[i] = sh[i].len != 0;
+      np += present[i] ? 1 : 0;
+    }
+    if (np < k_) {
+      status[s] = CFSEC_ERR_TOO_FEW_SHARDS;
+      continue;
+    }
+    if (np == total() && (!verify || m_ == 0)) continue;  // Reconstruct of a full stripe is a no-op
+    auto& plan = plans[present];
+    if (!plan) {
+      plan.reset(new StripePlan());
+      st = plan_stripe(present, verify, plan.get());
+      if (st != CFSEC_OK) {
+        plan.reset();
+        plans.erase(present);
+        status[s] = st;
+        continue;
+      }
+    }
+    for (int r = 0; r < plan->nstore && st == CFSEC_OK; ++r)
+      if (!sh[plan->out[r]].data || sh[plan->out[r]].cap < S) st = CFSEC_ERR_INVALID_ARG;
+    for (int c : plan->in)
+      if (!sh[c].data) st = CFSEC_ERR_INVALID_ARG;
+    if (st != CFSEC_OK) {
+      set_last_error("reconstruct batch: stripe " + std::to_string(s) + " has a missing shard with cap < shard size");
+      status[s] = st;
+      continue;
+    }
+    // KRS/reedsolomon.go:1514-1518: shards[i] = shards[i][0:S]
+    for (int r = 0; r < plan->nstore; ++r) sh[plan->out[r]].len = S;
+    if (!plan->out.empty()) tasks.push_back(StripeTask{sh, plan.get(), S, &status[s], 0});
+  }
+  return run_stripes(tasks, mem);
+}
+
+Status RSEngine::run_stripes(std::vector<StripeTask>& tasks, int mem) {
+  if (tasks.empty()) return CFSEC_OK;
+  if (devs_.empty()) {
+    set_last_error("no HIP device available to the cfsec engine");
+    return CFSEC_ERR_DEVICE;
+  }
+  if (mem != CFSEC_MEM_HOST && mem != CFSEC_MEM_DEVICE) return CFSEC_ERR_INVALID_ARG;
+  const int nd = (int)devs_.size();
+  if (mem == CFSEC_MEM_DEVICE) {
+    // device memory runs where it lives
+    for (auto& t : tasks) {
+      const int d = device_of(t.shards[t.plan->in[0]].data);
+      int idx = -1;
+      for (int i = 0; i < nd; ++i)
+        if (devs_[i]->device() == d) idx = i;
+      if (idx < 0) {
+        set_last_error("stripe batch: device memory on device " + std::to_string(d) +
+                       ", which is not one of the handle's devices");
+        return CFSEC_ERR_INVALID_ARG;
+      }
+      t.dev = idx;
+    }
+  } else {
+    // host memory: contiguous runs of stripes, balanced by the bytes each moves
+    double total = 0;
+    for (auto& t : tasks) total += double(t.len) * double(t.plan->in.size() + t.plan->out.size());
+    double acc = 0;
+    for (auto& t : tasks) {
+      const double b = double(t.len) * double(t.plan->in.size() + t.plan->out.size());
+      t.dev = std::min(nd - 1, (int)((acc + b / 2) * nd / std::max(total, 1.0)));
+      acc += b;
+    }
+  }
+  std::vector<std::vector<StripeTask*>> per(nd);
+  for (auto& t : tasks) per[t.dev].push_back(&t);
+  std::vector<Status> st(nd, CFSEC_OK);
+  std::vector<std::string> err(nd);
+  std::vector<std::thread> threads;
+  for (int d = 1; d < nd; ++d)
+    if (!per[d].empty())
+      threads.emplace_back([&, d] {
+        st[d] = run_device(per[d], mem, devs_[d]);
+        if (st[d] != CFSEC_OK) err[d] = last_error_cstr();
+      });
+  if (!per[0].empty()) st[0] = run_device(per[0], mem, devs_[0]);
+  for (auto& th : threads) th.join();
+  for (int d = 1; d < nd; ++d)
+    if (st[d] != CFSEC_OK && st[0] == CFSEC_OK) {
+      set_last_error(err[d]);
+      return st[d];
+    }
+  return st[0];
+}
+
+Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceContext* ctx) {
+  DeviceGuard g(ctx->device());
+  if (!g.ok()) return hip_status(hipErrorInvalidDevice, "hipSetDevice");
+  const int n = (int)tasks.size();
+  // which stripes the GPU addresses in place (device memory, or page-locked host memory on every
+  // row the product touches) and which go through staging (pageable host memory)
+  std::vector<StripeTask*> direct, staged;
+  std::map<std::pair<const StripeTask*, int>, uint8_t*> alias;
+  for (StripeTask* t : tasks) {
+    bool in_place = true;
+    if (mem == CFSEC_MEM_HOST) {
+      for (int c : t->plan->in) {
+        uint8_t* d = nullptr;
+        in_place = in_place && device_alias(t->shards[c].data, &d);
+        alias[{t, c}] = d;
+      }
+      for (int o : t->plan->out) {
+        uint8_t* d = nullptr;
+        in_place = in_place && device_alias(t->shards[o].data, &d);
+        alias[{t, o}] = d;
+      }
+    }
+    (in_place ? direct : staged).push_back(t);
+  }
+  // staging lanes: each holds whole stripes, at least the largest one
+  size_t lane_bytes = 0;
+  for (StripeTask* t : staged) {
+    const size_t b = align_up(t->len, kSlot) * (t->plan->in.size() + t->plan->out.size());
+    lane_bytes = std::max(lane_bytes, b);
+  }
+  size_t staged_total = 0;
+  for (StripeTask* t : staged) staged_total += align_up(t->len, kSlot) * (t->plan->in.size() + t->plan->out.size());
+  if (!staged.empty()) lane_bytes = std::max(lane_bytes, std::min(kLaneBudget, staged_total));
+  const int nlanes = staged_total > lane_bytes ? 2 : 1;
+  DeviceContext::Workspace* ws = nullptr;
+  Status st = ctx->acquire(lane_bytes * nlanes, (size_t)n, &ws);
+  if (st != CFSEC_OK) return st;
+  hipStream_t lane[2] = {ws->stream, ws->stream2};
+  if (mem == CFSEC_MEM_DEVICE) st = ctx->order_after_default(ws);
+  if (st == CFSEC_OK) st = hip_status(hipMemsetAsync(ws->dflags, 0, 4 * (size_t)n, lane[0]), "hipMemsetAsync");
+  if (st == CFSEC_OK && nlanes > 1) {
+    st = hip_status(hipEventRecord(ws->ev, lane[0]), "hipEventRecord");
+    if (st == CFSEC_OK) st = hip_status(hipStreamWaitEvent(lane[1], ws->ev, 0), "hipStreamWaitEvent");
+  }
+  int next_flag = 0;
+  std::vector<std::pair<StripeTask*, int>> flags;  // (task, flag word)
+  const auto record = [&](const std::vector<Group>& groups) {
+    for (const Group& gr : groups)
+      for (size_t i = 0; i < gr.tasks.size(); ++i) flags.emplace_back(gr.tasks[i], gr.flag0 + (int)i);
+  };
+  // in-place stripes: one set of launches on lane 0
+  if (st == CFSEC_OK && !direct.empty()) {
+    std::vector<Group> groups = make_groups(direct, &next_flag, [&](const StripeTask* t, int idx) {
+      return mem == CFSEC_MEM_DEVICE ? (const uint8_t*)t->shards[idx].data : (const uint8_t*)alias[{t, idx}];
+    });
+    for (const Group& gr : groups)
+      if (st == CFSEC_OK) st = hip_status(launch_group(gr, ws->dflags, lane[0]), "launch_matvec(batch)");
+    record(groups);
+  }
+  // staged stripes: chunks of whole stripes alternating over the two lanes; each lane copies its
+  // chunk in, runs it and copies the stored rows back while the other lane's chunk moves
+  size_t i0 = 0;
+  for (int chunk = 0; st == CFSEC_OK && i0 < staged.size(); ++chunk) {
+    const int l = chunk % nlanes;
+    hipStream_t s = lane[l];
+    uint8_t* base = ws->dbuf + lane_bytes * l;
+    size_t used = 0, i1 = i0;
+    std::map<std::pair<const StripeTask*, int>, uint8_t*> slot;
+    while (i1 < staged.size()) {
+      StripeTask* t = staged[i1];
+      const size_t sl = align_up(t->len, kSlot);
+      const size_t need = sl * (t->plan->in.size() + t->plan->out.size());
+      if (i1 > i0 && used + need > lane_bytes) break;
+      for (int c : t->plan->in) {
+        slot[{t, c}] = base + used;
+        used += sl;
+      }
+      for (int o : t->plan->out) {
+        slot[{t, o}] = base + used;
+        used += sl;
+      }
+      ++i1;
+    }
+    std::vector<StripeTask*> part(staged.begin() + i0, staged.begin() + i1);
+    for (StripeTask* t : part) {
+      for (int c : t->plan->in)
+        if (st == CFSEC_OK)
+          st = hip_status(hipMemcpyAsync(slot[{t, c}], t->shards[c].data, t->len, hipMemcpyHostToDevice, s),
+                          "hipMemcpyAsync H2D");
+      for (size_t r = t->plan->nstore; r < t->plan->out.size(); ++r)
+        if (st == CFSEC_OK) {
+          const int o = t->plan->out[r];
+          st = hip_status(hipMemcpyAsync(slot[{t, o}], t->shards[o].data, t->len, hipMemcpyHostToDevice, s),
+                          "hipMemcpyAsync H2D");
+        }
+    }
+    std::vector<Group> groups =
+        make_groups(part, &next_flag, [&](const StripeTask* t, int idx) { return (const uint8_t*)slot[{t, idx}]; });
+    for (const Group& gr : groups)
+      if (st == CFSEC_OK) st = hip_status(launch_group(gr, ws->dflags, s), "launch_matvec(batch)");
+    record(groups);
+    for (StripeTask* t : part)
+      for (int r = 0; r < t->plan->nstore && st == CFSEC_OK; ++r) {
+        const int o = t->plan->out[r];
+        st = hip_status(hipMemcpyAsync(t->shards[o].data, slot[{t, o}], t->len, hipMemcpyDeviceToHost, s),
+                        "hipMemcpyAsync D2H");
+      }
+    i0 = i1;
+  }
+  if (st == CFSEC_OK && nlanes > 1) {
+    st = hip_status(hipEventRecord(ws->ev, lane[1]), "hipEventRecord");
+    if (st == CFSEC_OK) st = hip_status(hipStreamWaitEvent(lane[0], ws->ev, 0), "hipStreamWaitEvent");
+  }
+  if (st == CFSEC_OK)
+    st = hip_status(hipMemcpyAsync(ws->hflags, ws->dflags, 4 * (size_t)n, hipMemcpyDeviceToHost, lane[0]),
+                    "hipMemcpyAsync D2H");
+  for (int l = 0; l < nlanes; ++l) {
+    const Status sync = hip_status(hipStreamSynchronize(lane[l]), "hipStreamSynchronize");
+    if (st == CFSEC_OK) st = sync;
+  }
+  if (st == CFSEC_OK)
+    for (auto& f : flags)
+      if (ws->hflags[f.second] != 0 && *f.first->status == CFSEC_OK) *f.first->status = CFSEC_ERR_VERIFY;
+  ctx->release(ws);
+  return st;
+}
+
+}  // namespace cfsec
+
+// ---------------------------------------------------------------- ec.Encoder batches
+
+namespace cfsec {
+
+Status ECEncoder::set_devices(const int* devices, int n) { return engine_->set_devices(devices, n); }
+
+Status LrcEncoder::set_devices(const int* devices, int n) {
+  Status st = engine_->set_devices(devices, n);
+  return st != CFSEC_OK ? st : local_->set_devices(devices, n);
+}
+
+Status ECEncoder::reconstruct_batch(cfsec_shard* shards, int n, int nbids, const int* bad, const int* bad_off,
+                                    int mem, bool verify, int* status) {
+  // encoder.go:139-144 per bid (initBadShards, engine Reconstruct), then encoder.go:133-137 (Verify)
+  if (!shards || !status || !bad_off || nbids < 0) return CFSEC_ERR_INVALID_ARG;
+  Slot slot(pool_.get());
+  std::vector<cfsec_shard*> stripes;
+  std::vector<int> pos;
+  for (int b = 0; b < nbids; ++b) {
+    status[b] = CFSEC_OK;
+    cfsec_shard* sh = shards + (size_t)b * n;
+    if (n != engine_->total()) {
+      status[b] = CFSEC_ERR_TOO_FEW_SHARDS;  // reedsolomon.go:1408-1410
+      continue;
+    }
+    const Status st = init_bad_shards(sh, n, std::vector<int>(bad + bad_off[b], bad + bad_off[b + 1]));
+    if (st != CFSEC_OK) {
+      status[b] = st;
+      continue;
+    }
+    stripes.push_back(sh);
+    pos.push_back(b);
+  }
+  std::vector<int> st(stripes.size());
+  const Status rc = engine_->reconstruct_stripes(stripes.data(), (int)stripes.size(), mem, verify, st.data());
+  for (size_t i = 0; i < pos.size(); ++i) status[pos[i]] = st[i];
+  return rc;
+}
+
+Status LrcEncoder::reconstruct_batch(cfsec_shard* shards, int n, int nbids, const int* bad, const int* bad_off,
+                                     int mem, bool verify, int* status) {
+  // lrcencoder.go:133-186 per bid, then lrcencoder.go:89-131 (Verify): a local stripe (n = its size)
+  // is the local engine alone; a whole stripe is the global engine over its first N+M shards, then
+  // each AZ's local engine over that AZ's local stripe -- two batched passes, in that order, as
+  // the reference runs them.
+  if (!shards || !status || !bad_off || nbids < 0) return CFSEC_ERR_INVALID_ARG;
+  const int N = t_.n, M = t_.m, L = t_.l, AZ = t_.az_count;
+  const int lsz = (N + M + L) / AZ;
+  Slot slot(pool_.get());
+  std::vector<cfsec_shard*> stripes;
+  std::vector<int> pos;
+  for (int b = 0; b < nbids; ++b) {
+    status[b] = CFSEC_OK;
+    cfsec_shard* sh = shards + (size_t)b * n;
+    if (n != lsz && n != N + M + L) {
+      status[b] = CFSEC_ERR_INVALID_SHARDS;
+      continue;
+    }
+    Status st = fill_full_shards(sh, n);
+    std::vector<int> global_bad;
+    for (int i = bad_off[b]; i < bad_off[b + 1]; ++i)
+      if (bad[i] < N + M) global_bad.push_back(bad[i]);
+    if (st == CFSEC_OK) st = init_bad_shards(sh, n, global_bad);
+    if (st != CFSEC_OK) {
+      status[b] = st;
+      continue;
+    }
+    stripes.push_back(sh);
+    pos.push_back(b);
+  }
+  if (n == lsz) {  // local stripes: local engine only (lrcencoder.go:93-99, 147-152)
+    std::vector<int> st(stripes.size());
+    const Status rc = local_->reconstruct_stripes(stripes.data(), (int)stripes.size(), mem, verify, st.data());
+    for (size_t i = 0; i < pos.size(); ++i) status[pos[i]] = st[i];
+    return rc;
+  }
+  // pass 1: global Reconstruct (+ global Verify) over shards [0, N+M)
+  std::vector<int> st1(stripes.size());
+  Status rc = engine_->reconstruct_stripes(stripes.data(), (int)stripes.size(), mem, verify, st1.data());
+  if (rc != CFSEC_OK) return rc;
+  // pass 2: every AZ's local stripe (copied headers, lrcencoder.go:236-243): local Reconstruct of
+  // its bad local shards (index remap lrcencoder.go:161-171) (+ local Verify)
+  std::vector<std::vector<cfsec_shard>> views;
+  std::vector<size_t> owner;
+  views.reserve(stripes.size() * AZ);
+  for (size_t i = 0; i < stripes.size(); ++i) {
+    if (st1[i] != CFSEC_OK && st1[i] != CFSEC_ERR_VERIFY) continue;  // Reconstruct failed: no local pass
+    cfsec_shard* sh = stripes[i];
+    const int b = pos[i];
+    std::map<int, std::vector<int>> local_bad;
+    for (int j = bad_off[b]; j < bad_off[b + 1]; ++j)
+      if (bad[j] >= N + M) {
+        const int idc = (bad[j] - N - M) * AZ / L;
+        local_bad[idc].push_back(bad[j] - N - M - L / AZ * idc + (N + M) / AZ);
+      }
+    for (int a = 0; a < AZ; ++a) {
+      const bool has_bad = local_bad.count(a) != 0;
+      if (!has_bad && !verify) continue;
+      std::vector<cfsec_shard> ls;
+      for (int g : shards_in_idc(a)) ls.push_back(sh[g]);
+      if (has_bad) {
+        const Status s = init_bad_shards(ls.data(), (int)ls.size(), local_bad[a]);
+        if (s != CFSEC_OK) {
+          st1[i] = s;
+          break;
+        }
+      }
+      views.push_back(std::move(ls));
+      owner.push_back(i);
+    }
+  }
+  std::vector<cfsec_shard*> lp;
+  for (auto& v : views) lp.push_back(v.data());
+  std::vector<int> st2(lp.size());
+  rc = local_->reconstruct_stripes(lp.data(), (int)lp.size(), mem, verify, st2.data());
+  // per bid: a Reconstruct error (global, then local) wins over a failed Verify
+  std::vector<int> local_err(stripes.size(), CFSEC_OK);
+  for (size_t v = 0; v < lp.size(); ++v) {
+    int& e = local_err[owner[v]];
+    if (st2[v] != CFSEC_OK && (e == CFSEC_OK || (e == CFSEC_ERR_VERIFY && st2[v] != CFSEC_ERR_VERIFY))) e = st2[v];
+  }
+  for (size_t i = 0; i < stripes.size(); ++i) {
+    int s = st1[i];
+    if (s == CFSEC_OK || s == CFSEC_ERR_VERIFY) {
+      if (local_err[i] != CFSEC_OK && local_err[i] != CFSEC_ERR_VERIFY) s = local_err[i];
+      else if (s == CFSEC_OK) s = local_err[i];
+    }
+    status[pos[i]] = s;
+  }
+  return rc;
+}
+
+}  // namespace cfsec

@@ -309,6 +309,46 @@ int cfsec_rs_reconstruct_crc_batch(cfsec_rs* h, uint8_t* const* ptrs, size_t sha
   });
 }
 
+// ---------------- stripe batches ----------------
+
+int cfsec_rs_set_devices(cfsec_rs* h, const int* devices, int ndev) {
+  if (!h) return CFSEC_ERR_INVALID_ARG;
+  return guarded([&] { return h->e->set_devices(devices, ndev); });
+}
+
+namespace {
+std::vector<cfsec_shard*> stripe_views(cfsec_shard* shards, int nstripes, int total) {
+  std::vector<cfsec_shard*> v((size_t)std::max(nstripes, 0));
+  for (int s = 0; s < nstripes; ++s) v[s] = shards + (size_t)s * total;
+  return v;
+}
+}  // namespace
+
+int cfsec_rs_encode_stripes(cfsec_rs* h, cfsec_shard* shards, int nstripes, int mem, int* status) {
+  if (!h || nstripes < 0 || (nstripes > 0 && (!shards || !status))) return CFSEC_ERR_INVALID_ARG;
+  return guarded([&] {
+    auto v = stripe_views(shards, nstripes, h->e->total());
+    return h->e->encode_stripes(v.data(), nstripes, mem, status);
+  });
+}
+
+int cfsec_rs_verify_stripes(cfsec_rs* h, cfsec_shard* shards, int nstripes, int mem, int* status) {
+  if (!h || nstripes < 0 || (nstripes > 0 && (!shards || !status))) return CFSEC_ERR_INVALID_ARG;
+  return guarded([&] {
+    auto v = stripe_views(shards, nstripes, h->e->total());
+    return h->e->verify_stripes(v.data(), nstripes, mem, status);
+  });
+}
+
+int cfsec_rs_reconstruct_stripes(cfsec_rs* h, cfsec_shard* shards, int nstripes, int verify, int mem,
+                                 int* status) {
+  if (!h || nstripes < 0 || (nstripes > 0 && (!shards || !status))) return CFSEC_ERR_INVALID_ARG;
+  return guarded([&] {
+    auto v = stripe_views(shards, nstripes, h->e->total());
+    return h->e->reconstruct_stripes(v.data(), nstripes, mem, verify != 0, status);
+  });
+}
+
 // ---------------- ec.Encoder ----------------
 
 int cfsec_codemode_tactic(int codemode, cfsec_tactic* t) {
@@ -364,6 +404,19 @@ int cfsec_ec_verify(cfsec_ec* h, cfsec_shard* shards, int n, int mem, void* stre
     *ok = b ? 1 : 0;
     return st;
   });
+}
+
+int cfsec_ec_set_devices(cfsec_ec* h, const int* devices, int ndev) {
+  if (!h) return CFSEC_ERR_INVALID_ARG;
+  return guarded([&] { return h->e->set_devices(devices, ndev); });
+}
+
+int cfsec_ec_reconstruct_batch(cfsec_ec* h, cfsec_shard* shards, int n, int nbids, const int* bad_idx,
+                               const int* bad_off, int verify, int mem, int* status) {
+  if (!h || nbids < 0 || n <= 0 || (nbids > 0 && (!shards || !status || !bad_off))) return CFSEC_ERR_INVALID_ARG;
+  for (int b = 0; b < nbids; ++b)
+    if (bad_off[b + 1] < bad_off[b] || (bad_off[b + 1] > bad_off[b] && !bad_idx)) return CFSEC_ERR_INVALID_ARG;
+  return guarded([&] { return h->e->reconstruct_batch(shards, n, nbids, bad_idx, bad_off, mem, verify != 0, status); });
 }
 
 int cfsec_ec_shards_in_idc(const cfsec_ec* h, int idx, int* out, int out_cap, int* count) {

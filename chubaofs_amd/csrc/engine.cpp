@@ -34,6 +34,8 @@ size_t first_size(const cfsec_shard* shards, int n) {
   return 0;
 }
 
+}  // namespace
+
 // ec.fillFullShards (encoder.go:199-210).  Go allocates when cap is short; across the
 // C ABI the caller must hand in buffers with enough capacity.
 Status fill_full_shards(cfsec_shard* shards, int n) {
@@ -60,6 +62,8 @@ Status init_bad_shards(cfsec_shard* shards, int n, const std::vector<int>& bad) 
   }
   return CFSEC_OK;
 }
+
+namespace {
 
 // codemode.Tactic.IsValid (codemode.go:267-271).
 bool tactic_valid(const cfsec_tactic& t) {
@@ -234,6 +238,7 @@ Status RSEngine::create(int k, int m, int device, std::unique_ptr<RSEngine>* out
   // A missing device is reported by the first call that needs it (CFSEC_ERR_DEVICE); the
   // host-only methods (matrix, Split, Join) work without one.
   e->ctx_ = device >= 0 ? DeviceContext::get(device) : nullptr;
+  if (e->ctx_) e->devs_.push_back(e->ctx_);
   *out = std::move(e);
   return CFSEC_OK;
 }

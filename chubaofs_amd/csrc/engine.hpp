@@ -24,6 +24,10 @@ namespace cfsec {
 using Status = int;  // cfsec_status
 
 void set_last_error(const std::string& msg);
+const char* last_error_cstr();
+// ec.initBadShards (encoder.go:182-188) / ec.fillFullShards (encoder.go:199-210), engine.cpp.
+Status init_bad_shards(cfsec_shard* shards, int n, const std::vector<int>& bad);
+Status fill_full_shards(cfsec_shard* shards, int n);
 Status hip_status(hipError_t e, const char* what);
 // The device address of page-locked host memory (hipHostMalloc / cfsec_host_alloc); false for
 // pageable memory.
@@ -95,6 +99,25 @@ struct ReconPlan {
   Matrix rows;               // outputs.size() x k, over the shards in `valid`
 };
 
+// The product one stripe of a heterogeneous batch needs (batch.cpp): rows x shards[in]; rows
+// [0, nstore) are written to shards[out[0 .. nstore)), the rest compared with shards[out[nstore ..)]
+// (a mismatch raises the stripe's flag).  Shared by every stripe with the same erasure pattern.
+struct StripePlan {
+  std::vector<int> in;
+  std::vector<int> out;
+  int nstore = 0;
+  Matrix rows;  // out.size() x in.size()
+};
+
+// One stripe of a batch call: its shard vector, the plan, its length, its result.
+struct StripeTask {
+  cfsec_shard* shards = nullptr;
+  const StripePlan* plan = nullptr;
+  size_t len = 0;
+  int* status = nullptr;        // set to CFSEC_ERR_VERIFY when a compared row mismatches
+  int dev = 0;                  // index into the engine's device list
+};
+
 class RSEngine {
  public:
   static Status create(int k, int m, int device, std::unique_ptr<RSEngine>* out);
@@ -128,6 +151,26 @@ class RSEngine {
   // Plan the rows of a reconstruct given which shards are present.
   Status plan_reconstruct(const std::vector<bool>& present, bool data_only, ReconPlan* plan);
 
+  // ---- heterogeneous stripe batches (batch.cpp) ----
+  // The devices batch entry points spread stripes over (the handle's own device first).
+  Status set_devices(const int* devices, int n);
+  int ndevices() const { return (int)devs_.size(); }
+  // `stripes` holds nst pointers to shard vectors of total() entries; each stripe has its own
+  // shard size and missing set.  Per-stripe results go to status[]; the return value reports only
+  // failures of the call itself (device errors, bad arguments).
+  //   encode:              Encode(shards)                         (KRS/reedsolomon.go:609-625)
+  //   verify:              Verify(shards): OK, or CFSEC_ERR_VERIFY when it returns false
+  //   reconstruct(verify): Reconstruct(shards) [then Verify(shards)], the blobnode repair step
+  //                        (blobnode/work_shard_recover.go:751-760), in one fused pass
+  Status encode_stripes(cfsec_shard* const* stripes, int nst, int mem, int* status);
+  Status verify_stripes(cfsec_shard* const* stripes, int nst, int mem, int* status);
+  Status reconstruct_stripes(cfsec_shard* const* stripes, int nst, int mem, bool verify, int* status);
+  // Run the tasks' products (device memory, pinned host memory in place, pageable host memory
+  // through double-buffered staging), tasks partitioned over the devices.
+  Status run_stripes(std::vector<StripeTask>& tasks, int mem);
+  // Plan of a Reconstruct (+ Verify) over the present shards.
+  Status plan_stripe(const std::vector<bool>& present, bool verify, StripePlan* plan);
+
   // Generic "outputs = rows x inputs" over caller shards (host or device memory).
   // mode kVerify: *ok set; outputs are read, not written.
   Status run(const Matrix& rows, const std::vector<cfsec_shard*>& ins,
@@ -150,6 +193,8 @@ class RSEngine {
   Matrix parity_;  // m x k (r.parity, KRS/reedsolomon.go:568-571)
   InversionCache tree_;
   DeviceContext* ctx_ = nullptr;
+  std::vector<DeviceContext*> devs_;  // batch devices, ctx_ first
+  Status run_device(std::vector<StripeTask*>& tasks, int mem, DeviceContext* ctx);
 };
 
 // Counting semaphore (util/limit/count.NewBlockingCount, encoder.go:90).
@@ -186,6 +231,14 @@ class ECEncoder {
   virtual Status verify(cfsec_shard* shards, int n, int mem, hipStream_t s, bool* ok);
   virtual std::vector<int> shards_in_idc(int idx) const;
   const cfsec_tactic& tactic() const { return t_; }
+  // Devices the batch entry points spread bids over (batch.cpp).
+  virtual Status set_devices(const int* devices, int n);
+  // blobnode's repair step over a batch of bids (work_shard_recover.go:708-771): for bid b, the
+  // n shards at shards[b*n ..], Reconstruct(shards_b, bad_b) then Verify(shards_b), where bad_b =
+  // bad[bad_off[b] .. bad_off[b+1]); status[b] = the Reconstruct error, CFSEC_ERR_VERIFY when Verify
+  // returns false, or CFSEC_OK.  verify = false: Reconstruct only.
+  virtual Status reconstruct_batch(cfsec_shard* shards, int n, int nbids, const int* bad, const int* bad_off,
+                                   int mem, bool verify, int* status);
 
  protected:
   struct Slot {
@@ -208,6 +261,9 @@ class LrcEncoder : public ECEncoder {
                           hipStream_t s) override;
   Status verify(cfsec_shard* shards, int n, int mem, hipStream_t s, bool* ok) override;
   std::vector<int> shards_in_idc(int idx) const override;
+  Status set_devices(const int* devices, int n) override;
+  Status reconstruct_batch(cfsec_shard* shards, int n, int nbids, const int* bad, const int* bad_off, int mem,
+                           bool verify, int* status) override;
 
  private:
   friend class ECEncoder;

@@ -29,7 +29,8 @@ namespace dev {
 
 constexpr int kMaxK = 32;       // inputs per launch
 constexpr int kMaxM = 32;       // outputs per launch
-constexpr int kPtrSlots = 300;  // shard pointers per launch
+constexpr int kPtrSlots = 288;  // shard pointers per launch
+constexpr int kLenSlots = 32;   // per-stripe lengths per launch (heterogeneous batches)
 constexpr int kThreads = 256;
 constexpr int kLaneBytes = 16;
 
@@ -37,16 +38,34 @@ constexpr int kLaneBytes = 16;
 //   explicit table (sstride == 0): ptr[s*k + j] (inputs), ptr[tab*k + s*m + r] (outputs)
 //   affine batch   (sstride != 0): ptr[j] + s*sstride, table holds stripe 0 only (tab == 1),
 //                                  so one launch covers any number of stripes.
+// Stripe lengths: every stripe is `len` bytes, or (varlen != 0, explicit table only) stripe s is
+// slen[s] bytes and `len` is the longest (it sizes the grid; tiles past a stripe's end exit).
 struct __attribute__((aligned(16))) GfArgs {
   uint64_t len;
   uint32_t k, m, nstripes, tiles_per_stripe;  // tiles_per_stripe: in units of the kernel's tile
   uint32_t* flags;
   int64_t sstride;                 // byte distance between consecutive stripes (affine batch)
-  uint32_t tab, pad0;              // stripes held in ptr[]
+  uint32_t tab;                    // stripes held in ptr[]
+  uint16_t nstore;                 // kStoreVerify: outputs [0, nstore) are stored, [nstore, m) compared
+  uint16_t varlen;                 // nonzero: per-stripe lengths in slen[]
   uint8_t coef[kMaxM * kMaxK];    // m x k, row stride k
+  uint32_t slen[kLenSlots];
   const uint8_t* ptr[kPtrSlots];  // [tab*k inputs][tab*m outputs]
 };
 static_assert(sizeof(GfArgs) <= 3584, "kernel argument block must stay below 4 KiB");
+
+// Bytes in stripe s of the launch.
+__device__ __forceinline__ uint64_t stripe_len(const GfArgs& a, uint32_t s) {
+  return a.varlen ? (uint64_t)a.slen[s] : a.len;
+}
+
+// Output row r of the launch is compared, not stored.
+template <MatVecMode MODE>
+__device__ __forceinline__ bool row_compared(const GfArgs& a, int r) {
+  if constexpr (MODE == MatVecMode::kVerify) return true;
+  else if constexpr (MODE == MatVecMode::kStoreVerify) return r >= (int)a.nstore;
+  else return false;
+}
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef u32x4 u32x4_ua __attribute__((aligned(1)));  // shard rows may start at any byte
@@ -189,7 +208,7 @@ __device__ __forceinline__ void finish(const GfArgs& a, u32x4 (&acc)[M], uint8_t
   for (int r = 0; r < M; ++r) {
     if (og + r < m) {
       uint8_t* p = out[og + r] + off;
-      if constexpr (MODE == MatVecMode::kVerify) {
+      if (row_compared<MODE>(a, og + r)) {
         const u32x4 d = acc[r] ^ ld16<NTL>(p);
         diff |= d.x | d.y | d.z | d.w;
       } else {
@@ -216,7 +235,7 @@ __device__ __forceinline__ void lane_tail(const GfArgs& a, const u32x4* tab01, c
   for (int r = 0; r < M; ++r) {
     if (og + r < m) {
       uint8_t* p = out[og + r] + off;
-      if constexpr (MODE == MatVecMode::kVerify) {
+      if (row_compared<MODE>(a, og + r)) {
         const u32x4 d = acc[r] ^ ld_tail(p, rem);
         diff |= d.x | d.y | d.z | d.w;
       } else {
@@ -326,12 +345,15 @@ __device__ __forceinline__ void mac_pair_k(uint32_t (&acc)[M][4], const uint32_t
 // (empty asm) behind a sched_barrier, and the row pointers (uniform: SGPR bases, 32-bit lane
 // offsets) are loaded once up front.  tools/gf_pipe.hip measured the effect.
 template <int K, int M, int MT, MatVecMode MODE, int D, bool NTL, bool NTS, bool PAIR = true>
-__device__ __forceinline__ void lane_tile_k(int m, const u32x4* tab01, const uint32_t* tab2,
+__device__ __forceinline__ void lane_tile_k(int m, int nstore, const u32x4* tab01, const uint32_t* tab2,
                                             const uint8_t* const* in, uint8_t* const* out, int og,
                                             int64_t sbase, uint32_t loff, uint32_t& diff) {
   static_assert(D >= 2, "the fixed-K tile consumes input rows in pairs, a pair ahead");
   constexpr bool kVer = MODE == MatVecMode::kVerify;
-  constexpr int R = K + (kVer ? M : 0);  // rows loaded
+  constexpr bool kMix = MODE == MatVecMode::kStoreVerify;  // rows < nstore stored, the rest compared
+  if constexpr (kVer) nstore = 0;
+  else if constexpr (!kMix) nstore = m;
+  constexpr int R = K + (kVer || kMix ? M : 0);  // rows loaded
   const uint8_t* row[R];
 #pragma unroll
   for (int c = 0; c < K; ++c) row[c] = in[c] + sbase;
@@ -346,7 +368,7 @@ __device__ __forceinline__ void lane_tile_k(int m, const u32x4* tab01, const uin
     for (int w = 0; w < 4; ++w) acc[r][w] = 0u;
   uint32_t x[R][4];
   const auto load = [&](int c) {
-    if (c >= K && og + (c - K) >= m) return;  // verify padding row
+    if (c >= K && (og + (c - K) >= m || og + (c - K) < nstore)) return;  // padding / stored row
     const u32x4 v = ld16<NTL>(row[c] + loff);
     x[c][0] = v.x;
     x[c][1] = v.y;
@@ -390,7 +412,7 @@ __device__ __forceinline__ void lane_tile_k(int m, const u32x4* tab01, const uin
   for (int c = K; c < R; ++c) {
     if (c + D < R) load(c + D);
     __builtin_amdgcn_sched_barrier(0);
-    if (og + (c - K) < m) {
+    if (og + (c - K) < m && og + (c - K) >= nstore) {
       const int r = c - K;
       diff |= (acc[r][0] ^ x[c][0]) | (acc[r][1] ^ x[c][1]) | (acc[r][2] ^ x[c][2]) | (acc[r][3] ^ x[c][3]);
     }
@@ -399,7 +421,7 @@ __device__ __forceinline__ void lane_tile_k(int m, const u32x4* tab01, const uin
   if constexpr (!kVer) {
 #pragma unroll
     for (int r = 0; r < M; ++r) {
-      if (og + r < m) {
+      if (og + r < m && og + r < nstore) {
         uint8_t* p = out[og + r] + sbase + loff;
         u32x4 v = u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
         if constexpr (MODE == MatVecMode::kAccum) v ^= ld16<NTL>(p);
@@ -433,14 +455,16 @@ __device__ __forceinline__ void matvec_k(const GfArgs& a) {
   const uint8_t* const* in = a.ptr + tstripe * K;
   uint8_t* const* out = const_cast<uint8_t* const*>(a.ptr + (size_t)a.tab * K + tstripe * a.m);
   const uint32_t off = tile * kTile + (uint32_t)(cw * 64 + lane) * kLaneBytes;
+  const uint64_t len = stripe_len(a, stripe);
   uint32_t diff = 0;
   if (og < (int)a.m) {
-    if ((uint64_t)off + kLaneBytes <= a.len)
-      lane_tile_k<K, M, MT, MODE, D, NTL, NTS, PAIR>((int)a.m, tab01, tab2, in, out, og, sbase, off, diff);
-    else if (off < a.len)
-      lane_tail<M, MT, MODE>(a, tab01, tab2, in, out, og, (size_t)sbase + off, a.len - off, diff);
+    if ((uint64_t)off + kLaneBytes <= len)
+      lane_tile_k<K, M, MT, MODE, D, NTL, NTS, PAIR>((int)a.m, (int)a.nstore, tab01, tab2, in, out, og, sbase, off,
+                                                     diff);
+    else if (off < len)
+      lane_tail<M, MT, MODE>(a, tab01, tab2, in, out, og, (size_t)sbase + off, len - off, diff);
   }
-  if constexpr (MODE == MatVecMode::kVerify) {
+  if constexpr (MODE == MatVecMode::kVerify || MODE == MatVecMode::kStoreVerify) {
     if (diff) atomicOr(a.flags + stripe, 1u);
   }
 }
@@ -482,21 +506,22 @@ __device__ __forceinline__ void matvec(const GfArgs& a) {
     const uint8_t* const* in = a.ptr + tstripe * a.k;
     uint8_t* const* out = const_cast<uint8_t* const*>(a.ptr + (size_t)a.tab * a.k + tstripe * a.m);
     const size_t off = tile * kTile + lane_off;  // byte offset inside the shard
+    const uint64_t len = stripe_len(a, (uint32_t)stripe);
     if (og < (int)a.m) {  // waves whose output rows are all padding have nothing to do
-      if (off + (W - 1) * kStep + kLaneBytes <= a.len) {
+      if (off + (W - 1) * kStep + kLaneBytes <= len) {
         lane_tile<M, MT, MODE, W, G, NTL, NTS>(a, tab01, tab2, in, out, og, soff + off, kStep, diff);
       } else {
 #pragma unroll
         for (int w = 0; w < W; ++w) {
           const size_t o = off + w * kStep;
-          if (o + kLaneBytes <= a.len)
+          if (o + kLaneBytes <= len)
             lane_tile<M, MT, MODE, 1, G, NTL, NTS>(a, tab01, tab2, in, out, og, soff + o, kStep, diff);
-          else if (o < a.len)
-            lane_tail<M, MT, MODE>(a, tab01, tab2, in, out, og, soff + o, a.len - o, diff);
+          else if (o < len)
+            lane_tail<M, MT, MODE>(a, tab01, tab2, in, out, og, soff + o, len - o, diff);
         }
       }
     }
-    if constexpr (MODE == MatVecMode::kVerify) {
+    if constexpr (MODE == MatVecMode::kVerify || MODE == MatVecMode::kStoreVerify) {
       if (diff) {
         atomicOr(a.flags + stripe, 1u);
         diff = 0;

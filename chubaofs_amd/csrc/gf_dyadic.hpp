@@ -274,8 +274,9 @@ __device__ __forceinline__ void matvec_dy(const GfArgs& a) {
   const auto sb = [&]() {
     if constexpr (PIN) __builtin_amdgcn_sched_barrier(0);
   };
-  const bool full = (uint64_t)off + kLaneBytes <= a.len;
-  const size_t rem = off < a.len ? (size_t)(a.len - off) : 0;
+  const uint64_t slen = stripe_len(a, stripe);
+  const bool full = (uint64_t)off + kLaneBytes <= slen;
+  const size_t rem = off < slen ? (size_t)(slen - off) : 0;
   uint32_t diff = 0;
   if (full || rem) {
     uint32_t x[K][4];

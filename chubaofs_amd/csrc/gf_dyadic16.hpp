@@ -94,8 +94,9 @@ __device__ __forceinline__ void matvec_dy16(const GfArgs& a) {
   for (int r = 0; r < M; ++r) row[K + r] = a.ptr[(size_t)a.tab * K + ts * M + r] + sbase;
   __builtin_amdgcn_sched_barrier(0);
 
-  const bool full = (uint64_t)off + kLaneBytes <= a.len;
-  const size_t rem = off < a.len ? (size_t)(a.len - off) : 0;
+  const uint64_t slen = stripe_len(a, stripe);
+  const bool full = (uint64_t)off + kLaneBytes <= slen;
+  const size_t rem = off < slen ? (size_t)(slen - off) : 0;
   uint32_t diff = 0;
   if (full || rem) {
     uint32_t acc[M][4];

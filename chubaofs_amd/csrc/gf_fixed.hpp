@@ -36,4 +36,6 @@ hipError_t launch_k(int m, const dev::GfArgs& a, dim3 grid, hipStream_t st) {
                                                                      hipStream_t);                  \
   template hipError_t launch_k<K, MatVecMode::kVerify, fixed_max_m(K)>(int, const dev::GfArgs&, dim3, \
                                                                       hipStream_t);                 \
+  template hipError_t launch_k<K, MatVecMode::kStoreVerify, fixed_max_m(K)>(int, const dev::GfArgs&,   \
+                                                                           dim3, hipStream_t);      \
   }

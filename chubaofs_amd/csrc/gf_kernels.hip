@@ -58,7 +58,7 @@ constexpr int kVerifyW = 2;
 template <int M, int OS, MatVecMode MODE>
 __global__ __launch_bounds__(256) void gf_matvec_kernel(const GfArgs a) {
   constexpr int G = OS > 1 ? CFSEC_SPLIT_G : 1;
-  if constexpr (MODE == MatVecMode::kVerify)
+  if constexpr (MODE == MatVecMode::kVerify || MODE == MatVecMode::kStoreVerify)
     dev::matvec<M, MODE, kVerifyW, 2, false, true, true, false, false, OS>(a);
   else
     dev::matvec<M, MODE, kStoreW, G, false, true, true, false, false, OS>(a);
@@ -102,7 +102,7 @@ hipError_t launch_mode(Shape sh, const GfArgs& a, dim3 grid, int threads, hipStr
 // batch (e.g. stripes carved from one pitched HBM buffer) runs as a single launch whatever its
 // stripe count; anything else is carried as an explicit pointer table, kPtrSlots per launch.
 int64_t affine_stride(const MatVecJob& job, int c0, int kc, int r0, int mc) {
-  if (job.nstripes < 2) return 0;
+  if (job.nstripes < 2 || job.lens) return 0;
   const auto addr = [](const void* p) { return (int64_t)(uintptr_t)p; };
   const int64_t ss = addr(job.in[job.k + c0]) - addr(job.in[c0]);
   if (ss == 0) return 0;
@@ -123,30 +123,44 @@ hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
   using dev::kPtrSlots;
   if (job.k <= 0 || job.m < 0 || job.nstripes < 0 || !job.coef || !job.in || !job.out)
     return hipErrorInvalidValue;
-  if (job.m == 0 || job.nstripes == 0 || job.len == 0) return hipSuccess;
-  if (job.mode == MatVecMode::kVerify && (job.k > kMaxK || !job.flags)) return hipErrorInvalidValue;
+  MatVecMode jmode = job.mode;
+  if (jmode == MatVecMode::kStoreVerify) {
+    if (job.nstore < 0 || job.nstore > job.m) return hipErrorInvalidValue;
+    if (job.nstore == job.m) jmode = MatVecMode::kStore;
+    else if (job.nstore == 0) jmode = MatVecMode::kVerify;
+    else if (job.m > kMaxM) return hipErrorInvalidValue;  // the stored/compared split lives in one launch
+  }
+  uint64_t maxlen = job.len;
+  if (job.lens) {
+    maxlen = 0;
+    for (int s = 0; s < job.nstripes; ++s) maxlen = std::max<uint64_t>(maxlen, job.lens[s]);
+    if (maxlen > 0xFFFFFFFFull) return hipErrorInvalidValue;  // slen[] is 32-bit
+  }
+  if (job.m == 0 || job.nstripes == 0 || maxlen == 0) return hipSuccess;
+  if ((jmode == MatVecMode::kVerify || jmode == MatVecMode::kStoreVerify) && (job.k > kMaxK || !job.flags))
+    return hipErrorInvalidValue;
 
   GfArgs a;
   for (int r0 = 0; r0 < job.m; r0 += kMaxM) {
     const int mc = std::min(kMaxM, job.m - r0);
     for (int c0 = 0; c0 < job.k; c0 += kMaxK) {
       const int kc = std::min(kMaxK, job.k - c0);
-      MatVecMode mode = job.mode;
+      MatVecMode mode = jmode;
       if (mode == MatVecMode::kStore && c0 > 0) mode = MatVecMode::kAccum;
-      const bool verify = mode == MatVecMode::kVerify;
+      const bool verify = mode == MatVecMode::kVerify || mode == MatVecMode::kStoreVerify;
       const Shape sh = choose(mc);
       // the code-mode input counts take the fixed-K pipelined kernels (256 threads, one wave per
       // column chunk holding every output, 1 chunk per lane); anything else the runtime-k
       // kernel, whose verify policy is 128-thread workgroups with 2 chunks per lane unless the
       // outputs are split over waves
       const bool fixed = fixed_k(kc) && kc == job.k && mc <= fixed_max_m(kc) && mode != MatVecMode::kAccum &&
-                         job.len <= 0xFFFFFFFFull - 4096;  // 32-bit lane offsets
+                         maxlen <= 0xFFFFFFFFull - 4096;  // 32-bit lane offsets
       const int threads = (!fixed && verify && sh.OS == 1) ? 128 : 256;
       // matrices of 4x4 / 2x2 dyadic blocks (encode of every code mode but the LRC local stripes,
       // coset-aligned reconstructs such as EC12P4's worst case) take the reduced-product kernel
       DyPlan dy{0, 0};
       bool dy16 = false;
-      if (fixed && r0 == 0 && mc == job.m) {
+      if (fixed && r0 == 0 && mc == job.m && mode != MatVecMode::kStoreVerify) {
         std::vector<uint8_t> sub((size_t)mc * kc);
         for (int r = 0; r < mc; ++r)
           for (int c = 0; c < kc; ++c) sub[(size_t)r * kc + c] = job.coef[(size_t)r * job.k + c];
@@ -155,10 +169,11 @@ hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
       }
       const size_t tile = fixed ? size_t(256) * dev::kLaneBytes
                                 : size_t(threads / sh.OS) * dev::kLaneBytes * (verify ? kVerifyW : kStoreW);
-      const size_t tiles = (job.len + tile - 1) / tile;
       const int per_stripe = kc + mc;
       const int64_t sstride = affine_stride(job, c0, kc, r0, mc);
       int stripes_per_launch = sstride ? job.nstripes : kPtrSlots / per_stripe;
+      if (job.lens) stripes_per_launch = std::min(stripes_per_launch, dev::kLenSlots);
+      const size_t tiles = (maxlen + tile - 1) / tile;  // (varlen: per launch below)
       // one launch covers tiles * stripes workgroups: keep that in a 32-bit grid
       stripes_per_launch = (int)std::min<size_t>(stripes_per_launch, std::max<size_t>(1, 0x7fffffffu / tiles));
       if (fixed) stripes_per_launch = std::min(stripes_per_launch, 65535);  // grid.y = stripes
@@ -166,15 +181,26 @@ hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
       for (int s0 = 0; s0 < job.nstripes; s0 += stripes_per_launch) {
         const int ns = std::min(stripes_per_launch, job.nstripes - s0);
         const int tab = sstride ? 1 : ns;  // stripes held in the pointer table
-        a.len = job.len;
+        uint64_t llen = job.len;
+        if (job.lens) {
+          llen = 0;
+          for (int s = 0; s < ns; ++s) {
+            a.slen[s] = (uint32_t)job.lens[s0 + s];
+            llen = std::max<uint64_t>(llen, job.lens[s0 + s]);
+          }
+          if (llen == 0) continue;
+        }
+        const size_t ltiles = (llen + tile - 1) / tile;
+        a.len = llen;
         a.k = (uint32_t)kc;
         a.m = (uint32_t)mc;
         a.nstripes = (uint32_t)ns;
-        a.tiles_per_stripe = (uint32_t)tiles;
+        a.tiles_per_stripe = (uint32_t)ltiles;
         a.flags = job.flags ? job.flags + s0 : nullptr;
         a.sstride = sstride;
         a.tab = (uint32_t)tab;
-        a.pad0 = 0;
+        a.nstore = (uint16_t)(mode == MatVecMode::kStoreVerify ? job.nstore - r0 : 0);
+        a.varlen = job.lens ? 1 : 0;
         for (int r = 0; r < mc; ++r)
           for (int c = 0; c < kc; ++c)
             a.coef[r * kc + c] = job.coef[(size_t)(r0 + r) * job.k + (c0 + c)];
@@ -184,7 +210,7 @@ hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
           for (int r = 0; r < mc; ++r)
             a.ptr[tab * kc + s * mc + r] = job.out[(size_t)(s0 + s) * job.m + r0 + r];
         }
-        const dim3 grid((unsigned)(tiles * ns));
+        const dim3 grid((unsigned)(ltiles * ns));
         hipError_t e;
         if (fixed && dy16) {
           e = launch_dy16(mc, mode, a, (unsigned)ns, stream);
@@ -199,15 +225,19 @@ hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
           continue;
         }
         if (fixed) {
-          const dim3 grid2((unsigned)tiles, (unsigned)ns);
-          e = verify ? launch_fixed<MatVecMode::kVerify>(kc, mc, a, grid2, stream)
-                     : launch_fixed<MatVecMode::kStore>(kc, mc, a, grid2, stream);
+          const dim3 grid2((unsigned)ltiles, (unsigned)ns);
+          e = mode == MatVecMode::kVerify        ? launch_fixed<MatVecMode::kVerify>(kc, mc, a, grid2, stream)
+              : mode == MatVecMode::kStoreVerify ? launch_fixed<MatVecMode::kStoreVerify>(kc, mc, a, grid2, stream)
+                                                 : launch_fixed<MatVecMode::kStore>(kc, mc, a, grid2, stream);
           if (e != hipSuccess) return e;
           continue;
         }
         switch (mode) {
           case MatVecMode::kStore: e = launch_mode<MatVecMode::kStore>(sh, a, grid, threads, stream); break;
           case MatVecMode::kAccum: e = launch_mode<MatVecMode::kAccum>(sh, a, grid, threads, stream); break;
+          case MatVecMode::kStoreVerify:
+            e = launch_mode<MatVecMode::kStoreVerify>(sh, a, grid, threads, stream);
+            break;
           default: e = launch_mode<MatVecMode::kVerify>(sh, a, grid, threads, stream); break;
         }
         if (e != hipSuccess) return e;

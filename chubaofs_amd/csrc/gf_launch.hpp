@@ -111,7 +111,9 @@ inline bool dyadic16_plan(const uint8_t* coef, int m, int k) {
   extern template hipError_t launch_k<K, MatVecMode::kStore, fixed_max_m(K)>(int, const dev::GfArgs&, \
                                                                             dim3, hipStream_t);     \
   extern template hipError_t launch_k<K, MatVecMode::kVerify, fixed_max_m(K)>(int, const dev::GfArgs&, \
-                                                                             dim3, hipStream_t);
+                                                                             dim3, hipStream_t);     \
+  extern template hipError_t launch_k<K, MatVecMode::kStoreVerify, fixed_max_m(K)>(                   \
+      int, const dev::GfArgs&, dim3, hipStream_t);
 CFSEC_EXTERN_K(3)
 CFSEC_EXTERN_K(4)
 CFSEC_EXTERN_K(6)

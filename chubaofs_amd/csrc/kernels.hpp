@@ -16,9 +16,10 @@
 namespace cfsec {
 
 enum class MatVecMode : uint32_t {
-  kStore = 0,   // out = M * in
-  kAccum = 1,   // out ^= M * in     (input chunking when k > kMaxK)
-  kVerify = 2,  // flags[s] |= (out != M * in)
+  kStore = 0,        // out = M * in
+  kAccum = 1,        // out ^= M * in     (input chunking when k > kMaxK)
+  kVerify = 2,       // flags[s] |= (out != M * in)
+  kStoreVerify = 3,  // rows [0, nstore): out = M * in; rows [nstore, m): flags[s] |= (out != M * in)
 };
 
 struct MatVecJob {
@@ -30,8 +31,13 @@ struct MatVecJob {
   const uint8_t* const* in = nullptr;  // host array [nstripes * k] of device pointers
   uint8_t* const* out = nullptr;       // host array [nstripes * m] of device pointers
   MatVecMode mode = MatVecMode::kStore;
-  uint32_t* flags = nullptr;           // device [nstripes], kVerify only
+  uint32_t* flags = nullptr;           // device [nstripes], kVerify / kStoreVerify
+  int nstore = 0;                      // kStoreVerify: stored rows (the first nstore of m)
+  const uint64_t* lens = nullptr;      // host [nstripes] per-stripe lengths (len = 0 then); NULL: all `len`
 };
+
+// Rows one launch carries (dev::kMaxK / dev::kMaxM); kStoreVerify needs m <= kLaunchMaxRows.
+constexpr int kLaunchMaxRows = 32;
 
 // Enqueue the product on `stream`.  Splits into as many launches as the kernel
 // argument block needs (inputs > 32, outputs > 32, or too many pointers).

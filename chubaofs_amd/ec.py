@@ -16,7 +16,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import ErrShortData, ErrInvalidCodeMode, ErrVerify, ErrInvalidShards  # noqa: F401 (re-export)
-from ._shards import Marshal, shard_size, stream_ptr
+from ._shards import BatchMarshal, Marshal, shard_size, stream_ptr
 from .codemode import Tactic
 from .reedsolomon import ReedSolomon
 
@@ -84,6 +84,32 @@ class Encoder:
         ok = ctypes.c_int(0)
         _lib.check(self._L.cfsec_ec_verify(self._h, m.ptr(), m.n, m.mem, stream_ptr(stream, m.like), ctypes.byref(ok)))
         return bool(ok.value)
+
+    # -- batches (blobnode repair loop, work_shard_recover.go:708-771) --
+    def SetDevices(self, devices) -> None:
+        arr = (ctypes.c_int * len(devices))(*devices)
+        _lib.check(self._L.cfsec_ec_set_devices(self._h, arr, len(devices)))
+
+    def ReconstructBatch(self, bids, badIdx, verify: bool = True):
+        """bids: list of shard lists (one per bid, all of one length n); badIdx: one index list per
+        bid.  Per bid Reconstruct(shards, bad) then Verify(shards), one batched call; returns the
+        per-bid status codes (0 ok, ErrVerify.status when Verify is false, else the error)."""
+        if len(bids) != len(badIdx):
+            raise ValueError("one bad-index list per bid")
+        n = len(bids[0]) if bids else 0
+        bm = BatchMarshal(bids, n, fill=True)
+        flat = [i for b in badIdx for i in b]
+        off = [0]
+        for b in badIdx:
+            off.append(off[-1] + len(b))
+        bad = (ctypes.c_int * max(len(flat), 1))(*flat)
+        offs = (ctypes.c_int * len(off))(*off)
+        status = (ctypes.c_int * max(len(bids), 1))()
+        st = self._L.cfsec_ec_reconstruct_batch(self._h, bm.arr, n, len(bids), bad, offs, int(verify), bm.mem,
+                                                status)
+        bm.writeback()
+        _lib.check(st)
+        return [int(status[i]) for i in range(len(bids))]
 
     # -- slice bookkeeping (host) --
     def Split(self, data, length: int | None = None):

@@ -15,7 +15,7 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from ._shards import Marshal, ptr_array, shard_size, stream_ptr
+from ._shards import BatchMarshal, Marshal, ptr_array, shard_size, stream_ptr
 
 
 class ReedSolomon:
@@ -109,6 +109,34 @@ class ReedSolomon:
             dst.write(data)
         else:
             dst.extend(data)
+
+    # -- stripe batches over the handle's devices (cfsec_rs_*_stripes) --
+    def SetDevices(self, devices) -> None:
+        """Spread stripe batches over these HIP devices (default: the handle's own)."""
+        arr = (ctypes.c_int * len(devices))(*devices)
+        _lib.check(self._L.cfsec_rs_set_devices(self._h, arr, len(devices)))
+
+    def _stripes(self, fn, stripes, fill, *extra):
+        bm = BatchMarshal(stripes, self.total_shards, fill=fill)
+        status = (ctypes.c_int * max(len(stripes), 1))()
+        st = fn(self._h, bm.arr, len(stripes), *extra, bm.mem, status)
+        bm.writeback()
+        _lib.check(st)
+        return [int(status[i]) for i in range(len(stripes))]
+
+    def EncodeStripes(self, stripes):
+        """Encode every stripe (each a list of total_shards buffers, sizes may differ per stripe);
+        returns one status code per stripe (0 = ok, else the code Encode would raise)."""
+        return self._stripes(self._L.cfsec_rs_encode_stripes, stripes, False)
+
+    def VerifyStripes(self, stripes):
+        """Per stripe: 0 when Verify holds, ErrVerify.status when it returns false, else the error."""
+        return self._stripes(self._L.cfsec_rs_verify_stripes, stripes, False)
+
+    def ReconstructStripes(self, stripes, verify: bool = True):
+        """Reconstruct (+ Verify) every stripe in one fused pass per stripe; missing entries (None or
+        empty) are replaced in the lists by the rebuilt shards.  Per-stripe status codes."""
+        return self._stripes(self._L.cfsec_rs_reconstruct_stripes, stripes, True, int(verify))
 
     # -- helpers / GPU batch API --
     def matrix(self) -> np.ndarray:

@@ -150,6 +150,37 @@ int cfsec_rs_reconstruct_crc_batch(cfsec_rs* h, uint8_t* const* ptrs, size_t sha
                                    const int* erased, int nerased, int data_only, uint32_t* crcs,
                                    void* stream);
 
+/* ---------------- stripe batches over one or more GPUs ----------------
+ * The reference codes one stripe per call: access encodes blob by blob (access/stream_put.go:104-143,
+ * up to 4 blobs in flight per request) and blobnode repairs a tasklet bid by bid, each bid with
+ * its own shard size and missing set, Reconstruct then Verify (blobnode/work_shard_recover.go:
+ * 708-771).  These entry points take a whole batch: `shards` holds nstripes consecutive shard
+ * vectors of (data+parity) entries each (stripe-major), every stripe with its own shard size and
+ * its own missing shards (len == 0); stripes with one erasure pattern share a decode plan and run
+ * in the same launches.  mem = CFSEC_MEM_HOST: the stripes are split into contiguous runs over the
+ * handle's devices (balanced by bytes), page-locked buffers (cfsec_host_alloc) are coded in place,
+ * pageable ones through double-buffered staging, one host thread and stream pair per device.
+ * mem = CFSEC_MEM_DEVICE: each stripe runs on the device its memory lives on (one of the handle's
+ * devices), after the work queued on that device's legacy default stream.  Synchronous: returns
+ * when every result is in place.  status[s] (nstripes words) receives stripe s's result as the
+ * single-stripe call would return it; the return value reports failures of the call itself
+ * (CFSEC_ERR_DEVICE, CFSEC_ERR_INVALID_ARG). */
+/* Devices batches are spread over (default: the handle's own device).  Call before sharing the
+ * handle between threads. */
+int cfsec_rs_set_devices(cfsec_rs* h, const int* devices, int ndev);
+/* Encode each stripe (KRS/reedsolomon.go:609-625). */
+int cfsec_rs_encode_stripes(cfsec_rs* h, cfsec_shard* shards, int nstripes, int mem, int* status);
+/* Verify each stripe (KRS/reedsolomon.go:770-784): status CFSEC_OK when it holds, CFSEC_ERR_VERIFY
+ * when Verify would return false (no error), another code for Verify's errors. */
+int cfsec_rs_verify_stripes(cfsec_rs* h, cfsec_shard* shards, int nstripes, int mem, int* status);
+/* Reconstruct each stripe (KRS/reedsolomon.go:1377-1552; missing shards need cap >= shard size and
+ * get len = shard size) and, with verify != 0, Verify it afterwards, in one fused pass per stripe:
+ * the kernel reads the first data_shards present shards and every other present parity shard once,
+ * writes the missing ones and compares the rest (status CFSEC_ERR_VERIFY when Verify would return
+ * false).  Bit-exact with the two calls on any input, consistent or not. */
+int cfsec_rs_reconstruct_stripes(cfsec_rs* h, cfsec_shard* shards, int nstripes, int verify, int mem,
+                                 int* status);
+
 /* ---------------- ec.Encoder ---------------- */
 /* Code-mode table (codemode.go:26-79): fill *t for a CodeMode value; CFSEC_ERR_INVALID_CODE_MODE
  * when unknown. */
@@ -164,6 +195,16 @@ int cfsec_ec_reconstruct(cfsec_ec* h, cfsec_shard* shards, int n, const int* bad
 int cfsec_ec_reconstruct_data(cfsec_ec* h, cfsec_shard* shards, int n, const int* bad_idx,
                               int nbad, int mem, void* stream);
 int cfsec_ec_verify(cfsec_ec* h, cfsec_shard* shards, int n, int mem, void* stream, int* ok);
+/* blobnode's repair loop over a tasklet (blobnode/work_shard_recover.go:708-771) in one call: bid b
+ * is the n shards at shards[b*n ..] and its bad indices bad_idx[bad_off[b] .. bad_off[b+1]) (global
+ * stripe indices, or local ones for a local stripe: n = its size); per bid exactly
+ * encoder.Reconstruct(shards_b, bad_b) then, with verify != 0, encoder.Verify(shards_b).  status[b]:
+ * the Reconstruct error, CFSEC_ERR_VERIFY when Verify returns false, or CFSEC_OK.  RS modes run one
+ * fused Reconstruct+Verify pass; LRC modes the global pass then every AZ's local pass
+ * (lrcencoder.go:133-186, 89-131).  Memory and devices as for cfsec_rs_*_stripes. */
+int cfsec_ec_reconstruct_batch(cfsec_ec* h, cfsec_shard* shards, int n, int nbids, const int* bad_idx,
+                               const int* bad_off, int verify, int mem, int* status);
+int cfsec_ec_set_devices(cfsec_ec* h, const int* devices, int ndev);
 /* GetShardsInIdc index map (encoder.go:169-176 / lrcencoder.go:236-243): writes the global
  * shard indices of AZ idx into out (capacity out_cap) and their count into *count. */
 int cfsec_ec_shards_in_idc(const cfsec_ec* h, int idx, int* out, int out_cap, int* count);

@@ -1,0 +1,283 @@
+"""Heterogeneous stripe batches (cfsec_rs_*_stripes, cfsec_ec_reconstruct_batch) on the GPU.
+
+The reference repairs a blobnode tasklet bid by bid (blobnode/work_shard_recover.go:708-771): each
+bid has its own shard size and its own broken shards, and each runs encoder.Reconstruct then
+encoder.Verify.  Here one call does the whole batch; every bid must come out exactly as the two
+reference calls leave it -- bytes from the oracle's two-pass reconstruct (KRS/reedsolomon.go:
+1407-1552, restated in oracle/gf_oracle.c) and the Verify verdict from the oracle's Verify -- on
+consistent stripes and on stripes whose unused parity was corrupted (Verify false).  The bid
+sizes are worker_for_test.go's {1024, 2048, 0, 512, 23, 65, 12} (:79-83) with its genMockBytes
+data (:62-69), plus larger and odd sizes.
+"""
+import random
+
+import numpy as np
+import pytest
+
+from chubaofs_amd import _lib, codemode as cm
+from oracle import oracle as O
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+MOCK_SIZES = [1024, 2048, 0, 512, 23, 65, 12]  # worker_for_test.go:79-83
+RS_MODES = [(6, 6), (12, 4), (15, 12), (16, 20), (10, 4), (3, 3)]
+
+
+def gen_mock_bytes(letter, size):
+    """worker_for_test.go:62-69"""
+    return ((letter + np.arange(size)) & 0xFF).astype(np.uint8)
+
+
+def codeword(k, m, size, bid):
+    sh = [gen_mock_bytes(bid + i, size) for i in range(k)] + [np.zeros(size, np.uint8) for _ in range(m)]
+    assert O.encode(k, m, sh) == 0
+    return sh
+
+
+def reference_repair(k, m, shards, bad, verify=True):
+    """Reconstruct then Verify with the oracle, as the reference's two calls; returns (status,
+    shards after)."""
+    n = k + m
+    work = [s.copy() for s in shards]
+    present = [i not in bad for i in range(n)]
+    S = len(shards[0])
+    if S == 0:
+        return _lib.ErrShardNoData.status, work
+    if sum(present) < k:
+        return _lib.ErrTooFewShards.status, work
+    if not all(present):
+        err, _ = O.reconstruct(k, m, work, present)
+        if err:
+            return err, work
+    if verify:
+        err, ok = O.verify(k, m, work)
+        if err:
+            return err, work
+        if not ok:
+            return _lib.ErrVerify.status, work
+    return 0, work
+
+
+def to_mem(shards, memory):
+    if memory == "device":
+        return [torch.from_numpy(np.ascontiguousarray(s)).cuda() for s in shards]
+    if memory == "pinned":
+        out = []
+        for s in shards:
+            p = _lib.pinned_empty(s.size)
+            p[:] = s
+            out.append(p)
+        return out
+    return [s.copy() for s in shards]
+
+
+def host(x):
+    return x.cpu().numpy() if hasattr(x, "cpu") else np.asarray(x)
+
+
+def mark_missing(stripe, bad, memory):
+    for i in bad:
+        stripe[i] = stripe[i][:0]  # len 0 = missing; the call gives it a fresh buffer
+
+
+@pytest.mark.parametrize("memory", ["host", "pinned", "device"])
+@pytest.mark.parametrize("k,m", RS_MODES)
+def test_reconstruct_stripes_mock_bids(k, m, memory):
+    from chubaofs_amd import reedsolomon
+    enc = reedsolomon.New(k, m, device=0)
+    r = random.Random(k * 100 + m)
+    sizes = MOCK_SIZES + [174763, 4096, 1, 100003]
+    stripes, want, bads = [], [], []
+    for b, size in enumerate(sizes):
+        good = codeword(k, m, size, b + 1)
+        nbad = r.randint(0, m)
+        bad = sorted(r.sample(range(k + m), nbad))
+        src = [s.copy() for s in good]
+        corrupt = b % 3 == 2 and nbad < m and size > 0  # an unused present parity goes bad
+        if corrupt:
+            spare = [i for i in range(k + m) if i not in bad][k:]  # present beyond the first k
+            j = spare[-1]
+            src[j][size // 2] ^= 0x5A
+        stripes.append(to_mem(src, memory))
+        mark_missing(stripes[-1], bad, memory)
+        bads.append(bad)
+        want.append(reference_repair(k, m, src, bad))
+    status = enc.ReconstructStripes(stripes, verify=True)
+    for b, (st, shards) in enumerate(want):
+        assert status[b] == st, (b, sizes[b], bads[b], status[b], st)
+        if st in (0, _lib.ErrVerify.status):
+            got = [host(x) for x in stripes[b]]
+            for i in range(k + m):
+                assert np.array_equal(got[i], shards[i]), (b, sizes[b], bads[b], i)
+
+
+@pytest.mark.parametrize("memory", ["host", "device"])
+def test_reconstruct_stripes_many_patterns_and_launch_splits(memory):
+    """70 stripes (more than one launch's 32 length slots), 9 erasure patterns, varied sizes."""
+    from chubaofs_amd import reedsolomon
+    k, m = 12, 4
+    enc = reedsolomon.New(k, m, device=0)
+    r = random.Random(5)
+    patterns = [sorted(r.sample(range(16), r.randint(1, 4))) for _ in range(9)]
+    stripes, want = [], []
+    for b in range(70):
+        size = r.choice([37, 4096, 4097, 65536 + 3, 300001])
+        good = codeword(k, m, size, b)
+        bad = patterns[b % len(patterns)]
+        stripes.append(to_mem(good, memory))
+        mark_missing(stripes[-1], bad, memory)
+        want.append(good)
+    assert enc.ReconstructStripes(stripes) == [0] * 70
+    for b in range(70):
+        for i in range(16):
+            assert np.array_equal(host(stripes[b][i]), want[b][i]), (b, i)
+
+
+def test_reconstruct_stripes_pageable_two_lanes():
+    """A pageable host batch larger than one staging lane (256 MiB): chunks alternate over the two
+    lanes of the device."""
+    from chubaofs_amd import reedsolomon
+    k, m, S = 12, 4, 1 << 20
+    enc = reedsolomon.New(k, m, device=0)
+    rng = np.random.default_rng(3)
+    base = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)] + [np.zeros(S, np.uint8) for _ in range(m)]
+    assert O.encode(k, m, base) == 0
+    stripes, want = [], []
+    for b in range(24):  # 24 x 16 MiB = 384 MiB of staging
+        good = [np.roll(x, b) for x in base[:k]] + [np.zeros(S, np.uint8) for _ in range(m)]
+        assert enc.EncodeStripes([good]) == [0]
+        want.append([x.copy() for x in good])
+        bad = [b % 16, (b + 5) % 16]
+        mark_missing(good, bad, "host")
+        stripes.append(good)
+    assert enc.ReconstructStripes(stripes) == [0] * 24
+    for b in range(24):
+        for i in range(16):
+            assert np.array_equal(stripes[b][i], want[b][i]), (b, i)
+    assert np.array_equal(want[0][k], base[k])  # the GPU encode of stripe 0 equals the oracle's
+
+
+@pytest.mark.parametrize("memory", ["host", "device"])
+def test_encode_and_verify_stripes(memory):
+    from chubaofs_amd import reedsolomon
+    k, m = 6, 6
+    enc = reedsolomon.New(k, m, device=0)
+    sizes = [1, 15, 16, 17, 2048, 174763, 0, 5]
+    stripes, want = [], []
+    for b, size in enumerate(sizes):
+        good = codeword(k, m, size, b) if size else [np.zeros(0, np.uint8)] * (k + m)
+        src = [x.copy() for x in good[:k]] + [np.full(size, 0xEE, np.uint8) for _ in range(m)]
+        stripes.append(to_mem(src, memory))
+        want.append(good)
+    st = enc.EncodeStripes(stripes)
+    assert st == [0 if s else _lib.ErrShardNoData.status for s in sizes]
+    for b, size in enumerate(sizes):
+        for i in range(k + m):
+            assert np.array_equal(host(stripes[b][i]), want[b][i]), (b, i)
+    stripes[3][k + 2][5] ^= 1
+    vs = enc.VerifyStripes(stripes)
+    assert vs[3] == _lib.ErrVerify.status and vs[6] == _lib.ErrShardNoData.status
+    assert all(v == 0 for i, v in enumerate(vs) if i not in (3, 6))
+
+
+def test_set_devices():
+    from chubaofs_amd import reedsolomon
+    enc = reedsolomon.New(12, 4, device=0)
+    enc.SetDevices([0])
+    with pytest.raises(_lib.ErrInvalidArg):
+        enc.SetDevices([0, 0])
+    with pytest.raises(_lib.ErrDevice):
+        enc.SetDevices([0, 4096])
+    good = codeword(12, 4, 4096, 1)
+    st = [x.copy() for x in good]
+    mark_missing(st, [0, 13], "host")
+    assert enc.ReconstructStripes([st]) == [0]
+    assert all(np.array_equal(a, b) for a, b in zip(st, good))
+
+
+# ------------------------------------------------------------------ ec.Encoder batches
+
+def ec_new(mode):
+    from chubaofs_amd import ec
+    return ec.NewEncoder(ec.Config(CodeMode=cm.GetTactic(mode), EnableVerify=False))
+
+
+def ec_full_codeword(enc, t, size, bid):
+    shards = [gen_mock_bytes(bid + i, size) for i in range(t.N)] + \
+             [np.zeros(size, np.uint8) for _ in range(t.M + t.L)]
+    enc.Encode(shards)
+    return shards
+
+
+def sequential(enc, shards, bad):
+    """The reference loop body: Reconstruct then Verify, with the single-call engine."""
+    work = [s.copy() for s in shards]
+    try:
+        enc.Reconstruct(work, list(bad))
+    except _lib.CfsecError as e:
+        return e.status, work
+    try:
+        ok = enc.Verify(work)
+    except _lib.CfsecError as e:
+        return e.status, work
+    return (0 if ok else _lib.ErrVerify.status), work
+
+
+@pytest.mark.parametrize("memory", ["host", "device"])
+@pytest.mark.parametrize("mode", [cm.EC6P6, cm.EC12P4, cm.EC15P12, cm.EC6P10L2, cm.EC16P20L2, cm.EC4P4L2, cm.EC6P3L3])
+def test_ec_reconstruct_batch_matches_repair_loop(mode, memory):
+    """cfsec_ec_reconstruct_batch over a tasklet == the per-bid Reconstruct + Verify calls (which the
+    single-call GPU tests pin to the oracle), global stripes, with corrupted bids."""
+    t = cm.GetTactic(mode)
+    enc = ec_new(mode)
+    total = t.N + t.M + t.L
+    r = random.Random(mode)
+    bids, bads, want = [], [], []
+    for b, size in enumerate([1024, 2048, 512, 23, 65, 12, 262144, 4097]):
+        good = ec_full_codeword(enc, t, size, b + 1)
+        nbad = r.randint(1, t.M)
+        bad = sorted(r.sample(range(total), nbad))
+        src = [x.copy() for x in good]
+        if b % 3 == 1:  # corrupt a surviving parity (global or local) outside the bad set
+            cand = [i for i in range(t.N, total) if i not in bad]
+            src[cand[-1]][size // 3] ^= 0x81
+        want.append(sequential(enc, src, bad))
+        work = to_mem(src, memory)
+        for i in bad:
+            if memory == "device":
+                work[i].zero_()
+            else:
+                work[i][:] = 0  # a broken shard's buffer, still full length (work_shard_recover.go)
+        bids.append(work)
+        bads.append(bad)
+    status = enc.ReconstructBatch(bids, bads)
+    for b, (st, shards) in enumerate(want):
+        assert status[b] == st, (b, bads[b], status[b], st)
+        if st in (0, _lib.ErrVerify.status):
+            for i in range(total):
+                assert np.array_equal(host(bids[b][i]), shards[i]), (b, bads[b], i)
+
+
+@pytest.mark.parametrize("mode", [cm.EC6P10L2, cm.EC16P20L2])
+def test_ec_reconstruct_batch_local_stripes(mode):
+    """AZ-local repair (lrcencoder.go:147-152): a batch of local stripes (n = local stripe size)."""
+    t = cm.GetTactic(mode)
+    enc = ec_new(mode)
+    ln = (t.N + t.M + t.L) // t.AZCount
+    bids, bads, want = [], [], []
+    for b, size in enumerate([699051, 1024, 23]):
+        good = ec_full_codeword(enc, t, size, b)
+        az = b % t.AZCount
+        idx, _, _ = t.LocalStripeInAZ(az)
+        local = [good[i].copy() for i in idx]
+        bad = [b % ln]
+        want.append(sequential(enc, local, bad))
+        work = [x.copy() for x in local]
+        work[bad[0]][:] = 0
+        bids.append(work)
+        bads.append(bad)
+    assert enc.ReconstructBatch(bids, bads) == [w[0] for w in want]
+    for b, (_, shards) in enumerate(want):
+        for i in range(ln):
+            assert np.array_equal(bids[b][i], shards[i]), (b, i)
