@@ -97,6 +97,7 @@ SIGNATURES = {
     "cfsec_rs_encode_crc_batch": ([_V, _V, _S, _I, _V, _V], _I),
     "cfsec_rs_reconstruct_crc_batch": ([_V, _V, _S, _I, _V, _I, _I, _V, _V], _I),
     "cfsec_rs_set_devices": ([_V, _V, _I], _I),
+    "cfsec_batch_partition": ([_V, _I, _I, _V], _I),
     "cfsec_rs_encode_stripes": ([_V, P_SHARD, _I, _I, _V], _I),
     "cfsec_rs_verify_stripes": ([_V, P_SHARD, _I, _I, _V], _I),
     "cfsec_rs_reconstruct_stripes": ([_V, P_SHARD, _I, _I, _I, _V], _I),
@@ -180,3 +181,13 @@ def pinned_empty(size: int):
     arr = np.frombuffer(buf, dtype=np.uint8)
     buf._cfsec_owner = owner  # the ctypes buffer (referenced by arr.base) holds the owner
     return arr
+
+
+def batch_partition(nbytes, ndev: int):
+    """cfsec_batch_partition: the device index each stripe of a host batch runs on."""
+    import numpy as np
+
+    b = np.ascontiguousarray(np.asarray(nbytes, np.uint64))
+    out = np.zeros(max(len(b), 1), np.int32)
+    check(lib().cfsec_batch_partition(b.ctypes.data if len(b) else None, len(b), ndev, out.ctypes.data))
+    return [int(x) for x in out[:len(b)]]

@@ -123,6 +123,20 @@ std::vector<Group> make_groups(const std::vector<StripeTask*>& tasks, int* next_
 
 }  // namespace
 
+void partition_stripes(const uint64_t* bytes, int n, int ndev, int* dev) {
+  // Stripe i goes to the device whose share of the byte total holds the midpoint of stripe i's
+  // bytes: contiguous, non-decreasing runs whose loads differ by at most one stripe's bytes.
+  long double total = 0;
+  for (int i = 0; i < n; ++i) total += bytes[i];
+  long double acc = 0;
+  for (int i = 0; i < n; ++i) {
+    const long double mid = acc + (long double)bytes[i] / 2;
+    int d = total > 0 ? (int)(mid * ndev / total) : (int)((long double)i * ndev / std::max(n, 1));
+    dev[i] = std::max(0, std::min(ndev - 1, d));
+    acc += bytes[i];
+  }
+}
+
 Status RSEngine::set_devices(const int* devices, int n) {
   if (!devices || n <= 0) return CFSEC_ERR_INVALID_ARG;
   std::vector<DeviceContext*> v;
@@ -312,14 +326,11 @@ Status RSEngine::run_stripes(std::vector<StripeTask>& tasks, int mem) {
     }
   } else {
     // host memory: contiguous runs of stripes, balanced by the bytes each moves
-    double total = 0;
-    for (auto& t : tasks) total += double(t.len) * double(t.plan->in.size() + t.plan->out.size());
-    double acc = 0;
-    for (auto& t : tasks) {
-      const double b = double(t.len) * double(t.plan->in.size() + t.plan->out.size());
-      t.dev = std::min(nd - 1, (int)((acc + b / 2) * nd / std::max(total, 1.0)));
-      acc += b;
-    }
+    std::vector<uint64_t> bytes;
+    for (auto& t : tasks) bytes.push_back(uint64_t(t.len) * (t.plan->in.size() + t.plan->out.size()));
+    std::vector<int> dev(tasks.size());
+    partition_stripes(bytes.data(), (int)bytes.size(), nd, dev.data());
+    for (size_t i = 0; i < tasks.size(); ++i) tasks[i].dev = dev[i];
   }
   std::vector<std::vector<StripeTask*>> per(nd);
   for (auto& t : tasks) per[t.dev].push_back(&t);

@@ -324,6 +324,12 @@ std::vector<cfsec_shard*> stripe_views(cfsec_shard* shards, int nstripes, int to
 }
 }  // namespace
 
+int cfsec_batch_partition(const uint64_t* bytes, int n, int ndev, int* dev) {
+  if (n < 0 || ndev <= 0 || (n > 0 && (!bytes || !dev))) return CFSEC_ERR_INVALID_ARG;
+  cfsec::partition_stripes(bytes, n, ndev, dev);
+  return CFSEC_OK;
+}
+
 int cfsec_rs_encode_stripes(cfsec_rs* h, cfsec_shard* shards, int nstripes, int mem, int* status) {
   if (!h || nstripes < 0 || (nstripes > 0 && (!shards || !status))) return CFSEC_ERR_INVALID_ARG;
   return guarded([&] {

@@ -109,6 +109,10 @@ struct StripePlan {
   Matrix rows;  // out.size() x in.size()
 };
 
+// The device (0 .. ndev-1) each of n stripes of a host-memory batch runs on: contiguous runs
+// balanced by the bytes each stripe moves (cfsec_batch_partition).
+void partition_stripes(const uint64_t* bytes, int n, int ndev, int* dev);
+
 // One stripe of a batch call: its shard vector, the plan, its length, its result.
 struct StripeTask {
   cfsec_shard* shards = nullptr;

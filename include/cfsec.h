@@ -168,6 +168,10 @@ int cfsec_rs_reconstruct_crc_batch(cfsec_rs* h, uint8_t* const* ptrs, size_t sha
 /* Devices batches are spread over (default: the handle's own device).  Call before sharing the
  * handle between threads. */
 int cfsec_rs_set_devices(cfsec_rs* h, const int* devices, int ndev);
+/* The split a host-memory batch uses: stripe i (moving bytes[i] bytes) runs on device index dev[i]
+ * of the handle's list -- contiguous runs, balanced by bytes.  Host only (no device needed); lets a
+ * caller place its staging per device ahead of the call. */
+int cfsec_batch_partition(const uint64_t* bytes, int n, int ndev, int* dev);
 /* Encode each stripe (KRS/reedsolomon.go:609-625). */
 int cfsec_rs_encode_stripes(cfsec_rs* h, cfsec_shard* shards, int nstripes, int mem, int* status);
 /* Verify each stripe (KRS/reedsolomon.go:770-784): status CFSEC_OK when it holds, CFSEC_ERR_VERIFY
