@@ -614,4 +614,77 @@ Status LrcEncoder::reconstruct_batch(cfsec_shard* shards, int n, int nbids, cons
   return rc;
 }
 
+Status ECEncoder::encode_batch(cfsec_shard* shards, int n, int nstripes, int mem, int* status) {
+  // encoder.go:114-131 per stripe: engine Encode, then Verify when EnableVerify
+  if (!shards || !status || nstripes < 0) return CFSEC_ERR_INVALID_ARG;
+  Slot slot(pool_.get());
+  std::vector<cfsec_shard*> stripes;
+  std::vector<int> pos;
+  for (int s = 0; s < nstripes; ++s) {
+    status[s] = CFSEC_OK;
+    if (n != engine_->total()) {
+      status[s] = CFSEC_ERR_TOO_FEW_SHARDS;  // reedsolomon.go:610-612
+      continue;
+    }
+    stripes.push_back(shards + (size_t)s * n);
+    pos.push_back(s);
+  }
+  std::vector<int> st(stripes.size());
+  Status rc = engine_->encode_stripes(stripes.data(), (int)stripes.size(), mem, st.data());
+  if (rc == CFSEC_OK && enable_verify_) {
+    std::vector<cfsec_shard*> ok;
+    std::vector<size_t> okp;
+    for (size_t i = 0; i < stripes.size(); ++i)
+      if (st[i] == CFSEC_OK) ok.push_back(stripes[i]), okp.push_back(i);
+    std::vector<int> vs(ok.size());
+    rc = engine_->verify_stripes(ok.data(), (int)ok.size(), mem, vs.data());
+    for (size_t i = 0; i < ok.size(); ++i) st[okp[i]] = vs[i];  // ErrVerify when Verify is false
+  }
+  for (size_t i = 0; i < pos.size(); ++i) status[pos[i]] = st[i];
+  return rc;
+}
+
+Status LrcEncoder::encode_batch(cfsec_shard* shards, int n, int nstripes, int mem, int* status) {
+  // lrcencoder.go:35-82 per stripe, fused: global parity and every AZ's local parity as one
+  // (M+L) x N product over the data (the same rows LrcEncoder::encode launches); EnableVerify
+  // compares all M+L rows in a second pass (the reference verifies the global and the local stripes)
+  if (!shards || !status || nstripes < 0) return CFSEC_ERR_INVALID_ARG;
+  const int N = t_.n, M = t_.m, L = t_.l;
+  Slot slot(pool_.get());
+  StripePlan plan;
+  for (int i = 0; i < N; ++i) plan.in.push_back(i);
+  for (int i = N; i < N + M + L; ++i) plan.out.push_back(i);
+  plan.nstore = M + L;
+  plan.rows = fused_;
+  std::vector<StripeTask> tasks;
+  for (int s = 0; s < nstripes; ++s) {
+    status[s] = CFSEC_OK;
+    cfsec_shard* sh = shards + (size_t)s * n;
+    if (n != N + M + L) {
+      status[s] = CFSEC_ERR_INVALID_SHARDS;
+      continue;
+    }
+    Status st = fill_full_shards(sh, n);
+    size_t S = 0;
+    if (st == CFSEC_OK) st = stripe_size(sh, n, false, &S);
+    for (int i = 0; i < n && st == CFSEC_OK; ++i)
+      if (!sh[i].data) st = CFSEC_ERR_INVALID_ARG;
+    if (st != CFSEC_OK) {
+      status[s] = st;
+      continue;
+    }
+    tasks.push_back(StripeTask{sh, &plan, S, &status[s], 0});
+  }
+  Status rc = engine_->run_stripes(tasks, mem);
+  if (rc == CFSEC_OK && enable_verify_) {
+    StripePlan vplan = plan;
+    vplan.nstore = 0;
+    std::vector<StripeTask> vt;
+    for (auto& t : tasks)
+      if (*t.status == CFSEC_OK) vt.push_back(StripeTask{t.shards, &vplan, t.len, t.status, 0});
+    rc = engine_->run_stripes(vt, mem);
+  }
+  return rc;
+}
+
 }  // namespace cfsec

@@ -425,6 +425,11 @@ int cfsec_ec_reconstruct_batch(cfsec_ec* h, cfsec_shard* shards, int n, int nbid
   return guarded([&] { return h->e->reconstruct_batch(shards, n, nbids, bad_idx, bad_off, mem, verify != 0, status); });
 }
 
+int cfsec_ec_encode_batch(cfsec_ec* h, cfsec_shard* shards, int n, int nstripes, int mem, int* status) {
+  if (!h || nstripes < 0 || n <= 0 || (nstripes > 0 && (!shards || !status))) return CFSEC_ERR_INVALID_ARG;
+  return guarded([&] { return h->e->encode_batch(shards, n, nstripes, mem, status); });
+}
+
 int cfsec_ec_shards_in_idc(const cfsec_ec* h, int idx, int* out, int out_cap, int* count) {
   if (!h || !count) return CFSEC_ERR_INVALID_ARG;
   const std::vector<int> v = h->e->shards_in_idc(idx);

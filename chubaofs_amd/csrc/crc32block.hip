@@ -196,6 +196,98 @@ __global__ __launch_bounds__(256) void crc32block_kernel(const BlockArgs a) {
   flush();
 }
 
+// The shipped kernel: one 64 KiB block per workgroup (consecutive workgroups take consecutive
+// blocks, so the workgroups in flight sweep one compact region of HBM: runs of blocks per
+// workgroup spread them over hundreds of MiB and measured 18-60 % slower, profiles/r02/
+// blk_probe.txt), with an epilogue that keeps its serial work off the barrier: every wave moves
+// its reduced register to the block end itself (the x^(8*16*(255-j)) and x^(8(plen - tiles*4096))
+// multiplies are linear, so they distribute over the XOR), and in encode also to the object end
+// and into the whole-object word; after one barrier thread 0 only XORs four words and stores or
+// compares the header.
+template <int RING, bool NTS = true>
+__global__ __launch_bounds__(256) void crc32block_block_kernel(const BlockArgs a) {
+  __shared__ uint32_t ct[crcdev::kNibTabWords];
+  __shared__ uint32_t red[8];  // per wave: its share of the block's raw CRC, and of the object's
+  for (int i = threadIdx.x; i < crcdev::kNibTabWords; i += 256) ct[i] = a.tabs[crcdev::kByteTabWords + i];
+  const uint32_t kj = a.tabs[kTabWords + crcdev::kBasisWords + threadIdx.x];
+  __syncthreads();
+  const uint32_t it = blockIdx.x;
+  const uint32_t y = it / a.nb, w = it - y * a.nb;
+  const uint8_t* const in = a.in[y];
+  uint8_t* const out = a.out[y];
+  const uint64_t b = a.b0 + w;
+  const uint64_t q0 = b * a.P;
+  const uint32_t plen = (uint32_t)min<uint64_t>(a.P, a.size - q0);
+  const int last = plen != a.P ? 1 : 0;
+  const uint8_t* src = in + (int64_t)w * a.in_stride + a.in_off;
+  const int64_t dbase = (int64_t)w * a.out_stride + a.out_off;
+  const uint32_t h = (uint32_t)(((uintptr_t)out + (uint64_t)dbase) & 15u);
+  const uint32_t tiles = (plen + h + kTile - 1) / kTile;
+  uint32_t R = 0, ring[RING][4];
+#pragma unroll
+  for (int k = 0; k < RING; ++k)
+    if (k < (int)tiles) load_piece(src, plen, h, threadIdx.x + 256 * k, ring[k]);
+  for (uint32_t t0 = 0; t0 < tiles; t0 += RING) {
+#pragma unroll
+    for (int k = 0; k < RING; ++k) {
+      const uint32_t t = t0 + k;
+      if (t < tiles) {
+        uint32_t (&cur)[4] = ring[k];
+        const uint32_t p = t * 256 + threadIdx.x;
+        R = crcdev::crc_step_nib(ct, R, cur);
+        const int64_t first = (int64_t)16 * p - h;
+        if (first < (int64_t)plen) {
+          const int64_t q = (int64_t)q0 + first;
+          uint8_t* dp = out + (dbase + first);  // 16-byte aligned
+          if (first >= 0 && first + 16 <= plen && q >= (int64_t)a.lo && q + 16 <= (int64_t)a.hi) {
+            dev::st16_out<NTS>(dp, u32x4{cur[0], cur[1], cur[2], cur[3]});
+          } else {
+            for (int j = 0; j < 16; ++j)
+              if (first + j >= 0 && first + j < plen && q + j >= (int64_t)a.lo && q + j < (int64_t)a.hi)
+                dp[j] = (uint8_t)(cur[j >> 2] >> (8 * (j & 3)));
+          }
+        }
+        if (t + RING < tiles) load_piece(src, plen, h, p + 256 * RING, cur);
+      }
+    }
+  }
+  uint32_t v = crcdev::mulmod(kj, R);
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v ^= (uint32_t)__shfl_xor((int)v, d);
+  if ((threadIdx.x & 63) == 0) {
+    const uint32_t raw = crcdev::mulmod(a.gconst[last][h], v);  // this wave's share of the block's raw CRC
+    red[threadIdx.x >> 6] = raw;
+    if (a.encode && a.whole) {
+      uint32_t s = raw;  // the share moved to the object end
+      if (b + 1 < a.nblk) {
+        if (b + 1 < a.nafter) {
+          s = crcdev::mulmod(s, a.xafter[b + 1]);
+        } else {
+          s = crcdev::mulmod(s, a.xlast);
+          uint64_t e = a.nblk - 2 - b;
+          for (int q = 0; e; e >>= 1, ++q)
+            if (e & 1) s = crcdev::mulmod(s, a.xpow2[q]);
+        }
+      }
+      red[4 + (threadIdx.x >> 6)] = s;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t crc = red[0] ^ red[1] ^ red[2] ^ red[3] ^ a.fin[last];
+    if (a.encode) {
+      uint8_t* hdr = out + (int64_t)w * a.out_stride;
+      for (int j = 0; j < 4; ++j) hdr[j] = (uint8_t)(crc >> (8 * j));
+      // one atomic per block (the four waves' shares XOR-ed here: many adders on one word are slow)
+      if (a.whole) atomicXor(a.whole + y, red[4] ^ red[5] ^ red[6] ^ red[7] ^ (b + 1 == a.nblk ? a.whole_fin : 0u));
+    } else {
+      const uint8_t* hdr = in + (int64_t)w * a.in_stride;
+      const uint32_t stored = hdr[0] | (uint32_t)hdr[1] << 8 | (uint32_t)hdr[2] << 16 | (uint32_t)hdr[3] << 24;
+      if (stored != crc) atomicMin(a.bad + y, w);
+    }
+  }
+}
+
 }  // namespace blk
 
 using blk::BlockArgs;
@@ -204,7 +296,8 @@ using blk::kSlots;
 bool crc32block_valid_len(int64_t block_len) { return block_len > 0 && block_len % 4096 == 0; }
 
 namespace blk {
-template <bool STORE, bool CRC, bool EPI = true, bool SRCALIGN = false, bool ONE = true, bool NTS = true>
+template <bool STORE, bool CRC, bool EPI = true, bool SRCALIGN = false, bool ONE = true, bool NTS = true,
+          int RING = kRing, bool FASTEPI = true>
 hipError_t launch(const Crc32BlockJob& j, hipStream_t stream) {
   if (!crc32block_valid_len(j.block_len) || j.size < 0 || j.block_len > 0xFFFFFFFFll) return hipErrorInvalidValue;
   const int64_t P = j.block_len - 4;
@@ -276,7 +369,10 @@ hipError_t launch(const Crc32BlockJob& j, hipStream_t stream) {
     // runs of ~5 blocks per workgroup, sharing one table load, were 5-10 % slower)
     a.ipw = ONE ? 1u : (a.items + 2047) / 2048;
     const unsigned grid = (a.items + a.ipw - 1) / a.ipw;
-    hipLaunchKernelGGL((crc32block_kernel<STORE, CRC, EPI, SRCALIGN, NTS>), dim3(grid), dim3(256), 0, stream, a);
+    if (FASTEPI && ONE && EPI && STORE && CRC)
+      hipLaunchKernelGGL((crc32block_block_kernel<RING, NTS>), dim3(grid), dim3(256), 0, stream, a);
+    else
+      hipLaunchKernelGGL((crc32block_kernel<STORE, CRC, EPI, SRCALIGN, NTS>), dim3(grid), dim3(256), 0, stream, a);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (a.bad) a.bad += ny;

@@ -243,6 +243,9 @@ class ECEncoder {
   // returns false, or CFSEC_OK.  verify = false: Reconstruct only.
   virtual Status reconstruct_batch(cfsec_shard* shards, int n, int nbids, const int* bad, const int* bad_off,
                                    int mem, bool verify, int* status);
+  // Encode over a batch of stripes of n shards each (access puts, stream_put.go:104-143), with
+  // the Config's EnableVerify; status[s] as Encode would return it.
+  virtual Status encode_batch(cfsec_shard* shards, int n, int nstripes, int mem, int* status);
 
  protected:
   struct Slot {
@@ -268,6 +271,7 @@ class LrcEncoder : public ECEncoder {
   Status set_devices(const int* devices, int n) override;
   Status reconstruct_batch(cfsec_shard* shards, int n, int nbids, const int* bad, const int* bad_off, int mem,
                            bool verify, int* status) override;
+  Status encode_batch(cfsec_shard* shards, int n, int nstripes, int mem, int* status) override;
 
  private:
   friend class ECEncoder;

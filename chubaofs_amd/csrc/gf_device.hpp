@@ -109,12 +109,13 @@ __device__ __forceinline__ u32x4 ld16_pol(const uint8_t* base, uint32_t off) {
   return u32x4{v[0], v[1], v[2], v[3]};
 }
 
-// Output-row store of the fixed-K and dyadic kernels: the streaming policy is sc1 (EC12P4 dyadic
-// kernel, profiles/r01/store_policy_probe.txt: sc1 / sc0 sc1 1-2 % faster than nt, plain and sc0
-// 2-3 % slower).
+// Output-row store of the fixed-K and dyadic kernels: non-temporal (nt).  Measured with no
+// Infinity-Cache reuse between launches (tools/rot_probe.hip, profiles/r02/rot_probe.txt): nt
+// 69.1 %, sc1 67.8 %, plain 61.2 % of 8 TB/s on the EC12P4 step kernel.  (Round 1 picked sc1 on a
+// bench that re-read its own outputs, where leaving them in the cache paid.)
 template <bool NTS>
 __device__ __forceinline__ void st16_out(uint8_t* p, u32x4 v) {
-  if constexpr (NTS) st16_pol<2>(p, v);
+  if constexpr (NTS) st16_pol<1>(p, v);
   else st16<false>(p, v);
 }
 

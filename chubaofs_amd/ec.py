@@ -90,6 +90,17 @@ class Encoder:
         arr = (ctypes.c_int * len(devices))(*devices)
         _lib.check(self._L.cfsec_ec_set_devices(self._h, arr, len(devices)))
 
+    def EncodeBatch(self, stripes):
+        """Encode every stripe (each a list of N+M+L shards; sizes may differ per stripe) in one
+        call, EnableVerify included; returns per-stripe status codes."""
+        n = len(stripes[0]) if stripes else 0
+        bm = BatchMarshal(stripes, n, fill=True)
+        status = (ctypes.c_int * max(len(stripes), 1))()
+        st = self._L.cfsec_ec_encode_batch(self._h, bm.arr, n, len(stripes), bm.mem, status)
+        bm.writeback()
+        _lib.check(st)
+        return [int(status[i]) for i in range(len(stripes))]
+
     def ReconstructBatch(self, bids, badIdx, verify: bool = True):
         """bids: list of shard lists (one per bid, all of one length n); badIdx: one index list per
         bid.  Per bid Reconstruct(shards, bad) then Verify(shards), one batched call; returns the

@@ -209,6 +209,11 @@ int cfsec_ec_verify(cfsec_ec* h, cfsec_shard* shards, int n, int mem, void* stre
 int cfsec_ec_reconstruct_batch(cfsec_ec* h, cfsec_shard* shards, int n, int nbids, const int* bad_idx,
                                const int* bad_off, int verify, int mem, int* status);
 int cfsec_ec_set_devices(cfsec_ec* h, const int* devices, int ndev);
+/* access's Put over a batch of blobs (stream_put.go:104-143 encodes them one by one): for stripe s
+ * (the n shards at shards[s*n ..]) exactly encoder.Encode(shards_s), EnableVerify included; LRC
+ * modes as one fused (M+L) x N pass (lrcencoder.go:35-82).  status[s]: Encode's result (CFSEC_ERR_VERIFY
+ * when the enabled Verify fails).  Memory and devices as for cfsec_rs_*_stripes. */
+int cfsec_ec_encode_batch(cfsec_ec* h, cfsec_shard* shards, int n, int nstripes, int mem, int* status);
 /* GetShardsInIdc index map (encoder.go:169-176 / lrcencoder.go:236-243): writes the global
  * shard indices of AZ idx into out (capacity out_cap) and their count into *count. */
 int cfsec_ec_shards_in_idc(const cfsec_ec* h, int idx, int* out, int out_cap, int* count);

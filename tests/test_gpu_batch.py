@@ -281,3 +281,28 @@ def test_ec_reconstruct_batch_local_stripes(mode):
     for b, (_, shards) in enumerate(want):
         for i in range(ln):
             assert np.array_equal(bids[b][i], shards[i]), (b, i)
+
+
+@pytest.mark.parametrize("memory", ["host", "device"])
+@pytest.mark.parametrize("mode", [cm.EC6P6, cm.EC12P4, cm.EC6P10L2, cm.EC16P20L2, cm.EC6P3L3, cm.EC4P4L2])
+@pytest.mark.parametrize("verify", [False, True])
+def test_ec_encode_batch_matches_encode(mode, memory, verify):
+    """cfsec_ec_encode_batch (access puts batched, LRC fused) == per-stripe Encode, whose parity the
+    single-call tests pin to the oracle (global + every AZ's local parity)."""
+    from chubaofs_amd import ec
+    t = cm.GetTactic(mode)
+    enc = ec.NewEncoder(ec.Config(CodeMode=t, EnableVerify=verify))
+    total = t.N + t.M + t.L
+    stripes, want = [], []
+    for b, size in enumerate([1, 23, 2048, 4097, 699051, 65536]):
+        data = [gen_mock_bytes(b * 7 + i, size) for i in range(t.N)]
+        ref = data + [np.zeros(size, np.uint8) for _ in range(total - t.N)]
+        ref = [x.copy() for x in ref]
+        enc.Encode(ref)
+        want.append(ref)
+        src = data + [np.full(size, 0x5A, np.uint8) for _ in range(total - t.N)]
+        stripes.append(to_mem([x.copy() for x in src], memory))
+    assert enc.EncodeBatch(stripes) == [0] * len(stripes)
+    for b in range(len(stripes)):
+        for i in range(total):
+            assert np.array_equal(host(stripes[b][i]), want[b][i]), (b, i)

@@ -41,22 +41,44 @@ int main(int argc, char** argv) {
   const int n = argc > 2 ? atoi(argv[2]) : 128;
   const int64_t L = argc > 3 ? atoll(argv[3]) : 65536, flen = S + 4 * ((S + L - 5) / (L - 4));
   const int64_t pitch = (S + 255) / 256 * 256, fpitch = (flen + 255) / 256 * 256;
-  uint8_t *pay, *frm;
+  // three buffer sets used in rotation: no launch finds its data in the 256 MB Infinity Cache
+  constexpr int NB = 3;
+  uint8_t *pays[NB], *frms[NB];
   uint32_t* words;
-  CK(hipMalloc(&pay, pitch * n));
-  CK(hipMalloc(&frm, fpitch * n));
   CK(hipMalloc(&words, 4 * 4096));
-  fill<<<2048, 256>>>((uint32_t*)pay, pitch * n / 4);
-  std::vector<const uint8_t*> in(n);
-  std::vector<uint8_t*> out(n);
-  for (int i = 0; i < n; ++i) in[i] = pay + i * pitch, out[i] = frm + i * fpitch;
+  std::vector<std::vector<const uint8_t*>> ins(NB, std::vector<const uint8_t*>(n)), fins(NB, std::vector<const uint8_t*>(n));
+  std::vector<std::vector<uint8_t*>> outs(NB, std::vector<uint8_t*>(n)), fouts(NB, std::vector<uint8_t*>(n));
+  for (int b = 0; b < NB; ++b) {
+    CK(hipMalloc(&pays[b], pitch * n));
+    CK(hipMalloc(&frms[b], fpitch * n));
+    fill<<<2048, 256>>>((uint32_t*)pays[b], pitch * n / 4);
+    for (int i = 0; i < n; ++i) {
+      ins[b][i] = pays[b] + i * pitch, outs[b][i] = frms[b] + i * fpitch;
+      fins[b][i] = frms[b] + i * fpitch, fouts[b][i] = pays[b] + i * pitch;
+    }
+  }
+  uint8_t* pay = pays[0];
+  uint8_t* frm = frms[0];
+  int rot = 0;
   cfsec::Crc32BlockJob j;
   j.n = n;
-  j.in = in.data();
-  j.out = out.data();
+  j.in = ins[0].data();
+  j.out = outs[0].data();
   j.size = S;
   j.block_len = L;
   j.whole = words;
+  const auto J = [&](bool enc) {
+    cfsec::Crc32BlockJob k = j;
+    const int b = rot++ % NB;
+    k.encode = enc;
+    k.in = enc ? ins[b].data() : fins[b].data();
+    k.out = enc ? outs[b].data() : fouts[b].data();
+    k.whole = enc ? words : nullptr;
+    k.bad = enc ? nullptr : words;
+    k.from = 0;
+    k.to = S;
+    return k;
+  };
   struct V {
     std::string name;
     std::function<void()> f;
@@ -64,6 +86,13 @@ int main(int argc, char** argv) {
   };
   const double pb = double(S) * n;
   std::vector<V> vs = {
+      {"enc old epilogue", [&] { CK((cfsec::blk::launch<true, true, true, false, true, true, 4, false>(J(true), 0))); }, 2 * pb},
+      {"enc new epi R4", [&] { CK((cfsec::blk::launch<true, true, true, false, true, true, 4, true>(J(true), 0))); }, 2 * pb},
+      {"enc new epi R6", [&] { CK((cfsec::blk::launch<true, true, true, false, true, true, 6, true>(J(true), 0))); }, 2 * pb},
+      {"enc new epi R8", [&] { CK((cfsec::blk::launch<true, true, true, false, true, true, 8, true>(J(true), 0))); }, 2 * pb},
+      {"dec old epilogue", [&] { CK((cfsec::blk::launch<true, true, true, false, true, true, 4, false>(J(false), 0))); }, 2 * pb},
+      {"dec new epi R4", [&] { CK((cfsec::blk::launch<true, true, true, false, true, true, 4, true>(J(false), 0))); }, 2 * pb},
+      {"dec new epi R8", [&] { CK((cfsec::blk::launch<true, true, true, false, true, true, 8, true>(J(false), 0))); }, 2 * pb},
       {"shipped (crc + store)", [&] { CK((cfsec::blk::launch<true, true>(j, 0))); }, 2 * pb},
       {"crc only (no store)", [&] { CK((cfsec::blk::launch<false, true>(j, 0))); }, pb},
       {"copy only (no crc)", [&] { CK((cfsec::blk::launch<true, false>(j, 0))); }, 2 * pb},
@@ -81,8 +110,26 @@ int main(int argc, char** argv) {
       {"flat copy src+4", [&] { kcopy<4, 0><<<4096, 256>>>(pay, frm, (size_t)(pb / 16) - 1); }, 2 * pb},
       {"flat copy dst+4", [&] { kcopy<0, 4><<<4096, 256>>>(pay, frm, (size_t)(pb / 16) - 1); }, 2 * pb},
       {"flat copy both+4", [&] { kcopy<4, 4><<<4096, 256>>>(pay, frm, (size_t)(pb / 16) - 1); }, 2 * pb},
-      {"standalone shard crc", [&] { CK(cfsec::launch_crc32(in.data(), S, n, words, 0)); }, pb},
+      {"standalone shard crc", [&] { CK(cfsec::launch_crc32(ins[0].data(), S, n, words, 0)); }, pb},
   };
+  {  // the run kernel frames and checks exactly like the per-block kernel
+    std::vector<uint8_t> want((size_t)fpitch * n), got((size_t)fpitch * n);
+    std::vector<uint32_t> w1(n), w2(n);
+    cfsec::Crc32BlockJob k = j;
+    k.encode = true;
+    CK(hipMemset(frm, 0, fpitch * n));
+    CK(hipMemset(words, 0, 4 * n));
+    CK((cfsec::blk::launch<true, true, true, false, true, true, 4, false>(k, 0)));
+    CK(hipMemcpy(want.data(), frm, want.size(), hipMemcpyDeviceToHost));
+    CK(hipMemcpy(w1.data(), words, 4 * n, hipMemcpyDeviceToHost));
+    CK(hipMemset(frm, 0, fpitch * n));
+    CK(hipMemset(words, 0, 4 * n));
+    CK((cfsec::blk::launch<true, true, true, false, true, true, 8, true>(k, 0)));
+    CK(hipMemcpy(got.data(), frm, got.size(), hipMemcpyDeviceToHost));
+    CK(hipMemcpy(w2.data(), words, 4 * n, hipMemcpyDeviceToHost));
+    printf("new-epilogue kernel == old kernel: framed %s, whole-shard crc %s\n", want == got ? "yes" : "NO",
+           w1 == w2 ? "yes" : "NO");
+  }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
