@@ -113,9 +113,12 @@ __device__ __forceinline__ u32x4 ld16_pol(const uint8_t* base, uint32_t off) {
 // Infinity-Cache reuse between launches (tools/rot_probe.hip, profiles/r02/rot_probe.txt): nt
 // 69.1 %, sc1 67.8 %, plain 61.2 % of 8 TB/s on the EC12P4 step kernel.  (Round 1 picked sc1 on a
 // bench that re-read its own outputs, where leaving them in the cache paid.)
+#ifndef CFSEC_STORE_POL
+#define CFSEC_STORE_POL 1  // st16_pol policy of the output stores (1 = nt)
+#endif
 template <bool NTS>
 __device__ __forceinline__ void st16_out(uint8_t* p, u32x4 v) {
-  if constexpr (NTS) st16_pol<1>(p, v);
+  if constexpr (NTS) st16_pol<CFSEC_STORE_POL>(p, v);
   else st16<false>(p, v);
 }
 

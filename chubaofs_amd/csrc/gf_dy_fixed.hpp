@@ -6,17 +6,9 @@
 
 namespace cfsec {
 
-// Column blocks loaded ahead: every input up front for up to 8 outputs (EC12P4 105 VGPRs, still 4
-// waves/SIMD: 68.4 -> 68.7 % of 8 TB/s, tools/rot_probe.hip), one block ahead for wider outputs
-// whose accumulators already fill the register file.
-template <int K, int MD, int B>
-constexpr int dy_lookahead() {
-  return MD <= 8 ? K / B : 1;
-}
-
 template <int K, int M, int B, MatVecMode MODE, int E>
 __global__ __launch_bounds__((dev::DyShape<M - E, B>::kThreadsPerWg)) void gf_dy_kernel(const dev::GfArgs a) {
-  dev::matvec_dy<K, M, B, MODE, true, true, 64, E, true, -1, -1, dy_lookahead<K, M - E, B>()>(a);
+  dev::matvec_dy<K, M, B, MODE, true, true, 64, E>(a);
 }
 
 template <int K, int M, int B, MatVecMode MODE, int E>

@@ -215,109 +215,13 @@ struct DyShape {
   static constexpr int kTileBytes = 64 * kLaneBytes * CW;
 };
 
-// One lane's work on NW 16-byte chunks of every row, at byte offsets off[w] (all NW in bounds, or
-// NW == 1 with rem < 16 bytes left at the shard's tail when full = false): column blocks loaded LA
-// blocks ahead of the multiply, products accumulated per chunk, then stored (or compared).
-template <int K, int MW, int E, int B, int KB, int NC, int ND, int LA, int NW, MatVecMode MODE, bool NTS, bool NTL,
-          bool PIN, int SP, int LP>
-__device__ __forceinline__ void dy_chunks(const uint8_t* const* row, const u32x4* tab01, const uint32_t* tab2,
-                                          const u32x4* tq, const uint32_t* tt, int live_rows, const uint32_t (&off)[NW],
-                                          bool full, size_t rem, uint32_t& diff) {
-  constexpr bool kVer = MODE == MatVecMode::kVerify;
-  constexpr int MA = MW + E;  // accumulators: dyadic rows, then plain rows
-  uint32_t acc[NW][MA][4];
-#pragma unroll
-  for (int w = 0; w < NW; ++w)
-#pragma unroll
-    for (int r = 0; r < MA; ++r)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) acc[w][r][q] = 0u;
-  const auto pin = [&]() {
-    if constexpr (PIN) {
-#pragma unroll
-      for (int w = 0; w < NW; ++w)
-#pragma unroll
-        for (int r = 0; r < MA; ++r)
-          asm volatile("" : "+v"(acc[w][r][0]), "+v"(acc[w][r][1]), "+v"(acc[w][r][2]), "+v"(acc[w][r][3]));
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-  const auto sb = [&]() {
-    if constexpr (PIN) __builtin_amdgcn_sched_barrier(0);
-  };
-  uint32_t x[NW][K][4];
-  const auto load = [&](int c) {
-#pragma unroll
-    for (int w = 0; w < NW; ++w) {
-      u32x4 v;
-      if constexpr (LP >= 0) v = full ? ld16_pol<LP>(row[c], off[w]) : ld_tail(row[c] + off[w], rem);  // probes
-      else v = full ? ld16<NTL>(row[c] + off[w]) : ld_tail(row[c] + off[w], rem);
-      x[w][c][0] = v.x;
-      x[w][c][1] = v.y;
-      x[w][c][2] = v.z;
-      x[w][c][3] = v.w;
-    }
-  };
-#pragma unroll
-  for (int cb = 0; cb < LA && cb < KB; ++cb)
-#pragma unroll
-    for (int c = 0; c < B; ++c) load(cb * B + c);
-#pragma unroll
-  for (int cb = 0; cb < KB; ++cb) {
-    if (cb + LA < KB)
-#pragma unroll
-      for (int c = 0; c < B; ++c) load((cb + LA) * B + c);
-    sb();
-    const int c0 = cb * B;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) {
-      auto& dacc = reinterpret_cast<uint32_t(&)[MW][4]>(acc[w]);
-      if constexpr (B == 2)
-        dy_col2<MW / B, PIN>(dacc, x[w][c0], x[w][c0 + 1], tq + cb * NC, tt + cb * NC, KB * NC);
-      else
-        dy_col4<MW / B, PIN>(dacc, x[w][c0], x[w][c0 + 1], x[w][c0 + 2], x[w][c0 + 3], tq + cb * NC, tt + cb * NC,
-                             KB * NC);
-      pin();
-      if constexpr (E > 0) {
-        auto& eacc = reinterpret_cast<uint32_t(&)[E][4]>(acc[w][MW]);
-#pragma unroll
-        for (int c = c0; c < c0 + B; c += 2) {
-          mac_pair_k<E>(eacc, x[w][c], x[w][c + 1], tab01 + ND + c * E, tab2 + ND + c * E, tab01 + ND + (c + 1) * E,
-                        tab2 + ND + (c + 1) * E);
-          pin();
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int w = 0; w < NW; ++w)
-#pragma unroll
-    for (int r = 0; r < MA; ++r) {
-      if (r < MW && r >= live_rows) continue;
-      uint8_t* p = const_cast<uint8_t*>(row[K + r]) + off[w];
-      const u32x4 v = u32x4{acc[w][r][0], acc[w][r][1], acc[w][r][2], acc[w][r][3]};
-      if constexpr (kVer) {
-        const u32x4 d = v ^ (full ? ld16<true>(p) : ld_tail(p, rem));
-        diff |= d.x | d.y | d.z | d.w;
-      } else if (full) {
-        if constexpr (SP >= 0) st16_pol<SP>(p, v);  // probe variants
-        else st16_out<NTS>(p, v);
-      } else {
-        st_tail(p, v, rem);
-      }
-    }
-}
-
 // Kernel body: compile-time K inputs, M outputs of which the first M - E are made of dyadic blocks
 // of B and the last E are plain rows (the local parities of a fused LRC encode: EC16P20L2 is 20
 // dyadic global rows + 2 local rows); grid (tiles, stripes), DyShape threads; wave w handles
-// column chunk w / OS and row blocks (w % OS) * RBW .. +RBW (plain rows: single-wave shapes only).
-// A lane owns W 16-byte chunks of every row, 1 KiB apart inside its wave's run of W KiB (W loads
-// per row in flight together: tools/rot_probe.hip measured the 12-read / 4-write pattern at
-// 71.4 / 72.5 / 73.9 % of 8 TB/s with 1 / 2 / 4 KiB per wave and row, and no gain from walking the
-// same chunks one after the other); column blocks are loaded LA blocks ahead.
+// column chunk w / OS and row blocks (w % OS) * RBW .. +RBW (plain rows: single-wave shapes only),
+// one 16-byte chunk per lane per row, column blocks loaded one block ahead.
 template <int K, int M, int B, MatVecMode MODE, bool NTS = true, bool NTL = true, int RBW_ = 64, int E = 0,
-          bool PIN = true, int SP = -1, int LP = -1, int LA = 1, int W = 1>
+          bool PIN = true, int SP = -1, int LP = -1>
 __device__ __forceinline__ void matvec_dy(const GfArgs& a) {
   constexpr int MD = M - E;
   static_assert(K % B == 0 && MD % B == 0 && (B == 2 || B == 4), "dyadic shape");
@@ -340,8 +244,7 @@ __device__ __forceinline__ void matvec_dy(const GfArgs& a) {
   const uint32_t stripe = blockIdx.y, tile = blockIdx.x;
   const size_t ts = a.sstride ? 0 : (size_t)stripe;
   const int64_t sbase = (int64_t)stripe * a.sstride;
-  constexpr uint32_t kRun = 64 * kLaneBytes;  // one wave's 1 KiB of a row per chunk
-  const uint32_t off0 = tile * (uint32_t)(Sh::kTileBytes * W) + (uint32_t)cw * (kRun * W) + (uint32_t)lane * kLaneBytes;
+  const uint32_t off = tile * (uint32_t)Sh::kTileBytes + (uint32_t)(cw * 64 + lane) * kLaneBytes;
   const uint8_t* row[K + MW + E];
 #pragma unroll
   for (int c = 0; c < K; ++c) row[c] = a.ptr[ts * K + c] + sbase;
@@ -354,26 +257,79 @@ __device__ __forceinline__ void matvec_dy(const GfArgs& a) {
   for (int e = 0; e < E; ++e) row[K + MW + e] = a.ptr[(size_t)a.tab * K + ts * M + MD + e] + sbase;
   __builtin_amdgcn_sched_barrier(0);
 
-  const u32x4* tq = tab01 + rb0 * KB * NC;
-  const uint32_t* tt = tab2 + rb0 * KB * NC;
-  const uint64_t slen = stripe_len(a, stripe);
-  uint32_t diff = 0;
-  if ((uint64_t)off0 + (W - 1) * kRun + kLaneBytes <= slen) {
-    uint32_t off[W];
+  constexpr int MA = MW + E;  // accumulators: dyadic rows, then plain rows
+  uint32_t acc[MA][4];
 #pragma unroll
-    for (int w = 0; w < W; ++w) off[w] = off0 + w * kRun;
-    dy_chunks<K, MW, E, B, KB, NC, ND, LA, W, MODE, NTS, NTL, PIN, SP, LP>(row, tab01, tab2, tq, tt, nrb * B, off,
-                                                                          true, 0, diff);
-  } else {
-    // the shard's last tile: chunk by chunk, the one holding the end byte-granular
-#pragma unroll 1
-    for (int w = 0; w < W; ++w) {
-      const uint32_t o[1] = {off0 + w * kRun};
-      const bool full = (uint64_t)o[0] + kLaneBytes <= slen;
-      const size_t rem = o[0] < slen ? (size_t)(slen - o[0]) : 0;
-      if (full || rem)
-        dy_chunks<K, MW, E, B, KB, NC, ND, LA, 1, MODE, NTS, NTL, PIN, SP, LP>(row, tab01, tab2, tq, tt, nrb * B, o,
-                                                                              full, rem, diff);
+  for (int r = 0; r < MA; ++r)
+#pragma unroll
+    for (int w = 0; w < 4; ++w) acc[r][w] = 0u;
+  const auto pin = [&]() {
+    if constexpr (PIN) {
+#pragma unroll
+      for (int r = 0; r < MA; ++r)
+        asm volatile("" : "+v"(acc[r][0]), "+v"(acc[r][1]), "+v"(acc[r][2]), "+v"(acc[r][3]));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  const auto sb = [&]() {
+    if constexpr (PIN) __builtin_amdgcn_sched_barrier(0);
+  };
+  const uint64_t slen = stripe_len(a, stripe);
+  const bool full = (uint64_t)off + kLaneBytes <= slen;
+  const size_t rem = off < slen ? (size_t)(slen - off) : 0;
+  uint32_t diff = 0;
+  if (full || rem) {
+    uint32_t x[K][4];
+    const auto load = [&](int c) {
+      u32x4 v;
+      if constexpr (LP >= 0) v = full ? ld16_pol<LP>(row[c], off) : ld_tail(row[c] + off, rem);  // probes
+      else v = full ? ld16<NTL>(row[c] + off) : ld_tail(row[c] + off, rem);
+      x[c][0] = v.x;
+      x[c][1] = v.y;
+      x[c][2] = v.z;
+      x[c][3] = v.w;
+    };
+#pragma unroll
+    for (int c = 0; c < B; ++c) load(c);
+    const u32x4* tq = tab01 + rb0 * KB * NC;
+    const uint32_t* tt = tab2 + rb0 * KB * NC;
+#pragma unroll
+    for (int cb = 0; cb < KB; ++cb) {
+      if (cb + 1 < KB)
+#pragma unroll
+        for (int c = 0; c < B; ++c) load((cb + 1) * B + c);
+      sb();
+      const int c0 = cb * B;
+      auto& dacc = reinterpret_cast<uint32_t(&)[MW][4]>(acc);
+      if constexpr (B == 2)
+        dy_col2<RBW, PIN>(dacc, x[c0], x[c0 + 1], tq + cb * NC, tt + cb * NC, KB * NC);
+      else
+        dy_col4<RBW, PIN>(dacc, x[c0], x[c0 + 1], x[c0 + 2], x[c0 + 3], tq + cb * NC, tt + cb * NC, KB * NC);
+      pin();
+      if constexpr (E > 0) {
+        auto& eacc = reinterpret_cast<uint32_t(&)[E][4]>(acc[MW]);
+#pragma unroll
+        for (int c = c0; c < c0 + B; c += 2) {
+          mac_pair_k<E>(eacc, x[c], x[c + 1], tab01 + ND + c * E, tab2 + ND + c * E, tab01 + ND + (c + 1) * E,
+                        tab2 + ND + (c + 1) * E);
+          pin();
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < MA; ++r) {
+      if (r < MW && r >= nrb * B) continue;
+      uint8_t* p = const_cast<uint8_t*>(row[K + r]) + off;
+      const u32x4 v = u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
+      if constexpr (kVer) {
+        const u32x4 d = v ^ (full ? ld16<true>(p) : ld_tail(p, rem));
+        diff |= d.x | d.y | d.z | d.w;
+      } else if (full) {
+        if constexpr (SP >= 0) st16_pol<SP>(p, v);  // probe variants
+        else st16_out<NTS>(p, v);
+      } else {
+        st_tail(p, v, rem);
+      }
     }
   }
   if constexpr (kVer) {

@@ -41,11 +41,6 @@ __global__ __launch_bounds__(256) void kdy(const GfArgs a) {
   dev::matvec_dy<K, M, B, MatVecMode::kStore, true, true, 64, 0, PIN, SP, LP>(a);
 }
 
-template <int SP, int LA, int W>
-__global__ __launch_bounds__(256) void kdyv(const GfArgs a) {
-  dev::matvec_dy<K, M, B, MatVecMode::kStore, true, true, 64, 0, true, SP, -1, LA, W>(a);
-}
-
 // trivial arithmetic, same tiling: out r = in[3r] ^ in[3r+1] ^ in[3r+2]; all 12 loads issued first
 template <int SP>
 __global__ __launch_bounds__(256) void ktriv(const GfArgs a) {
@@ -215,12 +210,6 @@ int main() {
   vs.push_back({"dy st nt", [&](int b) { hipLaunchKernelGGL(kdy<1>, grid, dim3(256), 0, 0, args[b]); }, step_bytes});
   vs.push_back({"dy st sc1", [&](int b) { hipLaunchKernelGGL(kdy<2>, grid, dim3(256), 0, 0, args[b]); }, step_bytes});
   vs.push_back({"dy st nt sc1", [&](int b) { hipLaunchKernelGGL(kdy<4>, grid, dim3(256), 0, 0, args[b]); }, step_bytes});
-  vs.push_back({"dy nt LA2", [&](int b) { hipLaunchKernelGGL((kdyv<1, 2, 1>), grid, dim3(256), 0, 0, args[b]); }, step_bytes});
-  vs.push_back({"dy nt LA3 (all ahead)", [&](int b) { hipLaunchKernelGGL((kdyv<1, 3, 1>), grid, dim3(256), 0, 0, args[b]); }, step_bytes});
-  vs.push_back({"dy nt W2", [&](int b) { hipLaunchKernelGGL((kdyv<1, 1, 2>), dim3((nt1 + 1) / 2, NST), dim3(256), 0, 0, args[b]); }, step_bytes});
-  vs.push_back({"dy nt W2 LA2", [&](int b) { hipLaunchKernelGGL((kdyv<1, 2, 2>), dim3((nt1 + 1) / 2, NST), dim3(256), 0, 0, args[b]); }, step_bytes});
-  vs.push_back({"dy nt W2 LA3", [&](int b) { hipLaunchKernelGGL((kdyv<1, 3, 2>), dim3((nt1 + 1) / 2, NST), dim3(256), 0, 0, args[b]); }, step_bytes});
-  vs.push_back({"dy nt W4", [&](int b) { hipLaunchKernelGGL((kdyv<1, 1, 4>), dim3((nt1 + 3) / 4, NST), dim3(256), 0, 0, args[b]); }, step_bytes});
   vs.push_back({"triv 12r4w st nt", [&](int b) { hipLaunchKernelGGL(ktriv<1>, grid, dim3(256), 0, 0, args[b]); }, step_bytes});
   vs.push_back({"triv 12r4w st sc1", [&](int b) { hipLaunchKernelGGL(ktriv<2>, grid, dim3(256), 0, 0, args[b]); }, step_bytes});
   vs.push_back({"triv W2 (8 KiB/row/wg)", [&](int b) { hipLaunchKernelGGL((ktrivw<2, 0>), dim3((nt1 + 1) / 2, NST), dim3(256), 0, 0, args[b]); }, step_bytes});
