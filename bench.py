@@ -302,6 +302,7 @@ def main():
         return
 
     golden = batch[:, :, :, :S].clone()
+    golden_stripe0 = golden[0, 0].cpu().numpy() if rank == 0 else None
     reconstruct(0)  # plans the reconstruct (inversion cache) before any timing or capture
     torch.cuda.synchronize()
     graph = None
@@ -381,6 +382,9 @@ def main():
     extra = {}
     if not args.no_extra:
         extra = secondary(args, torch, enc, batch, ptrs, stream, S, nst, pitch, dev, launch_bytes, data_bytes)
+        del batch, golden
+        torch.cuda.empty_cache()
+        extra["configs"] = other_configs(args, torch, dev, stream, cpu=(world == 1 and rank == 0 and not args.no_cpu))
 
     if rank != 0:
         if world > 1:
@@ -388,7 +392,7 @@ def main():
         return
     cpu = None
     if world == 1 and not args.no_cpu:
-        stripe0 = golden[0, 0].cpu().numpy()
+        stripe0 = golden_stripe0
         cpu, parity_ok = cpu_baseline(S, args.cpu_seconds, stripe0[:K_DATA], stripe0[K_DATA:])
         assert parity_ok, "GPU golden parity of stripe 0 differs from the CPU port's"
         gate["stripe0_parity_equals_cpu_port"] = True
@@ -509,6 +513,233 @@ def secondary(args, torch, enc, batch, ptrs, stream, S, nst, pitch, dev, launch_
                            "HIP events on the launch stream; roofline fractions use the same algorithmic bytes"),
     })
     del framed, unframed
+    return out
+
+
+# ----------------------------------------------------------------- BASELINE configs 1, 4, 5
+def cpu_rate(fn, seconds):
+    """Calls of fn per second over ~seconds (after one warm call)."""
+    fn()
+    n, t0 = 0, time.perf_counter()
+    while True:
+        fn()
+        n += 1
+        dt = time.perf_counter() - t0
+        if dt >= seconds:
+            return n / dt
+
+
+def api_rate(fn, seconds):
+    """Synchronous calls of fn per second over ~seconds (after two warm calls)."""
+    fn()
+    fn()
+    n, t0 = 0, time.perf_counter()
+    while True:
+        fn()
+        n += 1
+        dt = time.perf_counter() - t0
+        if dt >= seconds:
+            return n / dt
+
+
+def other_configs(args, torch, dev, stream, cpu):
+    """BASELINE.json configs[0], [3] and [4] on this GPU, each with the klauspost-strategy CPU port
+    (oracle/cpu_simd.c, 4 threads per call as the reference with GFNI) timed beside it on the same
+    shapes.  GPU rates: C1 from HIP events around back-to-back launches (device-resident batch);
+    C4 / C5 from the synchronous batch calls a caller makes (cfsec_ec_encode_batch,
+    cfsec_ec_reconstruct_batch on device memory: planning, launches and the final sync included,
+    so their roofline fraction is a lower bound for the kernels)."""
+    import numpy as np
+
+    from chubaofs_amd import _lib, codemode as cm, ec, reedsolomon
+    from chubaofs_amd._shards import BatchMarshal
+
+    out = {}
+    secs = max(0.3, args.op_seconds)
+    cpu_secs = max(1.0, args.cpu_seconds / 5)
+    if cpu:
+        from oracle import oracle as O
+    gfni = cpu and O.simd_features()["gfni"]
+    thr = 4 if gfni else 8
+
+    # ---- C1: EC6P6 encode of 1 MiB blobs, 256 blobs per batch (configs[0])
+    k, m, nb = 6, 6, 256
+    S1 = (1 << 20) + k - 1
+    S1 //= k  # 174,763
+    p1 = (S1 + 255) // 256 * 256
+    b1 = torch.randint(0, 256, (NBATCH, nb, k + m, p1), dtype=torch.uint8, device=dev)
+    r6 = reedsolomon.New(k, m, device=dev.index)
+    pt = [(ctypes.c_void_p * (nb * (k + m)))(*[b1[b].data_ptr() + (s * (k + m) + i) * p1 for s in range(nb)
+                                              for i in range(k + m)]) for b in range(NBATCH)]
+    for b in range(NBATCH):
+        r6.encode_batch(pt[b], S1, nb, stream=stream)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    n = 30
+    e0.record(stream)
+    for i in range(n):
+        r6.encode_batch(pt[i % NBATCH], S1, nb, stream=stream)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / n
+    c1 = {"workload": f"EC6P6 encode, {nb} blobs of 1 MiB (S={S1}), device-resident, one launch",
+          "data_GBps": round(k * S1 * nb / (ms * 1e-3) / 1e9, 1),
+          "roofline_frac": round((k + m) * S1 * nb / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+          "avg_launch_ms": round(ms, 4), "algorithmic_bytes_per_launch": (k + m) * S1 * nb}
+    if cpu:
+        full = O.build_matrix(k, k + m)
+        h = b1[0, 0, :k, :S1].cpu().numpy()
+        data = [np.ascontiguousarray(h[i]) for i in range(k)]
+        par = [np.zeros(S1, np.uint8) for _ in range(m)]
+        rate = cpu_rate(lambda: O.simd_code(full[k:], data, par, thr), cpu_secs)
+        ok = all(np.array_equal(par[r], b1[0, 0, k + r, :S1].cpu().numpy()) for r in range(m))
+        c1["cpu_baseline"] = {"value": round(k * S1 * rate / 1e9, 3), "unit": "GB/s", "cores": thr, "kind": "port",
+                              "sample": f"one 1 MiB blob encoded repeatedly for ~{cpu_secs:.0f}s",
+                              "parity_equals_gpu": bool(ok)}
+    out["C1_EC6P6_1MiB_encode"] = c1
+    del b1, pt
+
+    # ---- C4: EC6P10L2 fused LRC encode + AZ-local repair, 4 MiB blobs (configs[3])
+    t4 = cm.GetTactic(cm.EC6P10L2)
+    N, M, L = t4.N, t4.M, t4.L
+    tot4 = N + M + L
+    S4 = ((4 << 20) + N - 1) // N  # 699,051
+    p4 = (S4 + 255) // 256 * 256
+    nb4 = 48
+    e4 = ec.NewEncoder(ec.Config(CodeMode=t4, EnableVerify=False), device=dev.index)
+    b4 = torch.randint(0, 256, (NBATCH, nb4, tot4, p4), dtype=torch.uint8, device=dev)
+    bms = [BatchMarshal([[b4[b, s, i, :S4] for i in range(tot4)] for s in range(nb4)], tot4) for b in range(NBATCH)]
+    st4 = (ctypes.c_int * nb4)()
+    rot = [0]
+
+    def enc4():
+        bm = bms[rot[0] % NBATCH]
+        rot[0] += 1
+        _lib.check(e4._L.cfsec_ec_encode_batch(e4._h, bm.arr, tot4, nb4, bm.mem, st4))
+
+    rate = api_rate(enc4, secs)
+    assert list(st4) == [0] * nb4
+    c4 = {"workload": f"EC6P10L2 fused LRC encode (global + 2 local parities in one pass), {nb4} blobs of 4 MiB (S={S4})",
+          "encode_data_GBps": round(N * S4 * nb4 * rate / 1e9, 1),
+          "encode_roofline_frac": round((N + M + L) * S4 * nb4 * rate / 1e9 / HBM_PEAK_GBPS, 4)}
+    # AZ-local repair: AZ0's local stripe (8 + 1 shards) per blob, local index 0 lost
+    idx0, _, _ = t4.LocalStripeInAZ(0)
+    lsz = len(idx0)
+    lbm = [BatchMarshal([[b4[b, s, i, :S4] for i in idx0] for s in range(nb4)], lsz) for b in range(NBATCH)]
+    bad = (ctypes.c_int * nb4)(*([0] * nb4))
+    off = (ctypes.c_int * (nb4 + 1))(*range(nb4 + 1))
+
+    def rep4():
+        bm = lbm[rot[0] % NBATCH]
+        rot[0] += 1
+        _lib.check(e4._L.cfsec_ec_reconstruct_batch(e4._h, bm.arr, lsz, nb4, bad, off, 1, bm.mem, st4))
+
+    rate_r = api_rate(rep4, secs)
+    assert list(st4) == [0] * nb4
+    c4.update({"local_repair_data_GBps": round((lsz - 1) * S4 * nb4 * rate_r / 1e9, 1),
+               "local_repair_roofline_frac": round(lsz * S4 * nb4 * rate_r / 1e9 / HBM_PEAK_GBPS, 4),
+               "timing": "synchronous batch calls on device memory (planning + launch + sync)"})
+    if cpu:
+        G = O.build_matrix(N, N + M)
+        Lm = O.build_matrix(lsz - 1, lsz)
+        h = b4[0, 0, :, :S4].cpu().numpy()
+        data = [np.ascontiguousarray(h[i]) for i in range(N)]
+        gpar = [np.zeros(S4, np.uint8) for _ in range(M)]
+        lpar = [np.zeros(S4, np.uint8) for _ in range(L)]
+
+        def cpu_enc4():  # lrcencoder.go:35-82: global Encode, then each AZ's local Encode
+            O.simd_code(G[N:], data, gpar, thr)
+            full = data + gpar
+            for a in range(t4.AZCount):
+                ia, _, _ = t4.LocalStripeInAZ(a)
+                O.simd_code(Lm[lsz - 1:], [full[i] for i in ia[:lsz - 1]], [lpar[a]], thr)
+
+        rate_c = cpu_rate(cpu_enc4, cpu_secs)
+        ok = all(np.array_equal(gpar[r], h[N + r]) for r in range(M)) and \
+            all(np.array_equal(lpar[a], h[N + M + a]) for a in range(L))
+        err, dec = O.invert(Lm[1:lsz])  # local stripe with index 0 lost: survivors 1..8
+        assert err == 0
+        surv = [np.ascontiguousarray(h[i]) for i in idx0[1:]]
+        rebuilt = [np.zeros(S4, np.uint8)]
+        rate_cr = cpu_rate(lambda: O.simd_code(dec[:1], surv, rebuilt, thr), cpu_secs)
+        c4["cpu_baseline"] = {
+            "encode": {"value": round(N * S4 * rate_c / 1e9, 3), "unit": "GB/s", "cores": thr, "kind": "port",
+                       "sample": "one blob: global (6,10) encode + two local (8,1) encodes, repeated",
+                       "parity_equals_gpu": bool(ok)},
+            "local_repair": {"value": round((lsz - 1) * S4 * rate_cr / 1e9, 3), "unit": "GB/s", "cores": thr,
+                             "kind": "port", "sample": "one local stripe: the lost shard rebuilt from 8, repeated",
+                             "equals_original": bool(np.array_equal(rebuilt[0], h[idx0[0]]))}}
+    out["C4_EC6P10L2_lrc_encode_local_repair"] = c4
+    del bms, lbm, b4
+
+    # ---- C5: EC16P20L2 repair tasklet, 64 bids of 4 MiB blobs, erased {0, 1, 16, 17} (configs[4]),
+    # on one GPU: Reconstruct + Verify per bid (blobnode/work_shard_recover.go:751-757)
+    t5 = cm.GetTactic(cm.EC16P20L2)
+    N5, tot5 = t5.N, t5.N + t5.M + t5.L
+    S5 = max(((4 << 20) + N5 - 1) // N5, t5.MinShardSize)  # 262,144
+    p5 = (S5 + 255) // 256 * 256
+    nb5 = 64
+    e5 = ec.NewEncoder(ec.Config(CodeMode=t5, EnableVerify=False), device=dev.index)
+    b5 = torch.randint(0, 256, (NBATCH, nb5, tot5, p5), dtype=torch.uint8, device=dev)
+    bm5 = [BatchMarshal([[b5[b, s, i, :S5] for i in range(tot5)] for s in range(nb5)], tot5) for b in range(NBATCH)]
+    st5 = (ctypes.c_int * nb5)()
+    for b in range(NBATCH):
+        _lib.check(e5._L.cfsec_ec_encode_batch(e5._h, bm5[b].arr, tot5, nb5, bm5[b].mem, st5))
+    torch.cuda.synchronize()
+    er5 = [0, 1, 16, 17]
+    bad5 = (ctypes.c_int * (4 * nb5))(*(er5 * nb5))
+    off5 = (ctypes.c_int * (nb5 + 1))(*range(0, 4 * nb5 + 1, 4))
+
+    def rep5():
+        bm = bm5[rot[0] % NBATCH]
+        rot[0] += 1
+        _lib.check(e5._L.cfsec_ec_reconstruct_batch(e5._h, bm.arr, tot5, nb5, bad5, off5, 1, bm.mem, st5))
+
+    rate5 = api_rate(rep5, secs)
+    assert list(st5) == [0] * nb5
+    # per bid: global pass reads 16 inputs + 16 checked parities, writes 4; local pass reads 2 x 19
+    alg5 = (16 + 16 + 4 + 2 * 19) * S5
+    c5 = {"workload": (f"EC16P20L2 repair tasklet on one GPU: {nb5} bids x S={S5}, erased {{0,1,16,17}}, "
+                       "Reconstruct + Verify per bid in one cfsec_ec_reconstruct_batch (global fused pass + AZ-local pass)"),
+          "data_GBps": round(N5 * S5 * nb5 * rate5 / 1e9, 1),
+          "roofline_frac": round(alg5 * nb5 * rate5 / 1e9 / HBM_PEAK_GBPS, 4),
+          "algorithmic_bytes_per_bid": alg5,
+          "timing": "synchronous batch calls on device memory (planning + launches + sync)",
+          "multi_gpu_note": "the RCCL exchange of survivors spread over 8 GPUs is chubaofs_amd/repair.py (gloo-tested; "
+                            "not run by this 1-GPU bench)"}
+    if cpu:
+        G5 = O.build_matrix(N5, N5 + t5.M)
+        l5 = (N5 + t5.M) // t5.AZCount
+        Lm5 = O.build_matrix(l5, l5 + 1)
+        h = b5[0, 0, :, :S5].cpu().numpy()
+        sh = [np.ascontiguousarray(h[i]) for i in range(tot5)]
+        valid = [i for i in range(N5 + t5.M) if i not in er5][:N5]
+        err, dec = O.invert(G5[valid])
+        assert err == 0
+        outs = [np.zeros(S5, np.uint8) for _ in range(4)]
+        tmp = [np.zeros(S5, np.uint8) for _ in range(t5.M)]
+        ltmp = [np.zeros(S5, np.uint8)]
+        rows_data = dec[[0, 1]]
+        prow = G5[[16, 17]]
+
+        def cpu_rep5():  # Reconstruct (data rows, then parity rows) + Verify (global, then local)
+            ins = [sh[i] for i in valid]
+            O.simd_code(rows_data, ins, outs[:2], thr)
+            O.simd_code(prow, [sh[i] for i in range(N5)], outs[2:], thr)
+            O.simd_code(G5[N5:], [sh[i] for i in range(N5)], tmp, thr)
+            ok = all(np.array_equal(tmp[r], sh[N5 + r]) for r in range(t5.M))
+            for a in range(t5.AZCount):
+                ia, _, _ = t5.LocalStripeInAZ(a)
+                O.simd_code(Lm5[l5:], [sh[i] for i in ia[:l5]], ltmp, thr)
+                ok = ok and np.array_equal(ltmp[0], sh[ia[l5]])
+            return ok
+
+        assert cpu_rep5()
+        rate_c5 = cpu_rate(cpu_rep5, cpu_secs)
+        c5["cpu_baseline"] = {"value": round(N5 * S5 * rate_c5 / 1e9, 3), "unit": "GB/s", "cores": thr, "kind": "port",
+                              "sample": "one bid: reconstruct 2 data + 2 parity rows, global and 2 local verifies, repeated"}
+    out["C5_EC16P20L2_repair_tasklet"] = c5
+    del bm5, b5
     return out
 
 

@@ -310,7 +310,16 @@ Status RSEngine::run_stripes(std::vector<StripeTask>& tasks, int mem) {
   }
   if (mem != CFSEC_MEM_HOST && mem != CFSEC_MEM_DEVICE) return CFSEC_ERR_INVALID_ARG;
   const int nd = (int)devs_.size();
-  if (mem == CFSEC_MEM_DEVICE) {
+  if (mem == CFSEC_MEM_DEVICE && nd == 1) {
+    // one device: the batch's memory must live on it (checked on the first stripe; per-stripe
+    // pointer queries cost ~1 us each)
+    const int d = device_of(tasks[0].shards[tasks[0].plan->in[0]].data);
+    if (d != devs_[0]->device()) {
+      set_last_error("stripe batch: device memory on device " + std::to_string(d) + ", the handle runs on device " +
+                     std::to_string(devs_[0]->device()));
+      return CFSEC_ERR_INVALID_ARG;
+    }
+  } else if (mem == CFSEC_MEM_DEVICE) {
     // device memory runs where it lives
     for (auto& t : tasks) {
       const int d = device_of(t.shards[t.plan->in[0]].data);
