@@ -9,6 +9,7 @@
 // out of one product over the first k present shards), and the stripes are spread over the
 // handle's devices, each with its own streams and staging.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <thread>
@@ -59,18 +60,54 @@ struct Group {
   int flag0 = 0;                   // first flag word
 };
 
-// Enqueue one group: the mixed store/compare product, split into a store and a compare launch
-// when the rows exceed one launch.
+hipError_t launch_group_run(const Group& g, size_t t0, size_t t1, uint32_t* dflags, hipStream_t s);
+
+// Enqueue one group: maximal runs of stripes that sit at one stride from each other (every row)
+// launch as affine batches of any size; the rest as pointer tables.
 hipError_t launch_group(const Group& g, uint32_t* dflags, hipStream_t s) {
+  const size_t k = g.plan->in.size(), m = g.plan->out.size(), nt = g.tasks.size();
+  bool uniform = true;
+  for (uint64_t l : g.lens) uniform = uniform && l == g.lens[0];
+  if (!uniform || nt < 3) return launch_group_run(g, 0, nt, dflags, s);
+  const auto addr = [](const void* p) { return (int64_t)(uintptr_t)p; };
+  const auto stride_ok = [&](size_t t, int64_t d) {  // stripe t+1 = stripe t + d on every row
+    for (size_t c = 0; c < k; ++c)
+      if (addr(g.in[(t + 1) * k + c]) - addr(g.in[t * k + c]) != d) return false;
+    for (size_t r = 0; r < m; ++r)
+      if (addr(g.out[(t + 1) * m + r]) - addr(g.out[t * m + r]) != d) return false;
+    return true;
+  };
+  size_t t0 = 0;
+  while (t0 < nt) {
+    size_t t1 = t0 + 1;
+    if (t1 < nt) {
+      const int64_t d = addr(g.in[t1 * k]) - addr(g.in[t0 * k]);
+      while (t1 < nt && d != 0 && stride_ok(t1 - 1, d)) ++t1;
+    }
+    const hipError_t e = launch_group_run(g, t0, t1, dflags, s);
+    if (e != hipSuccess) return e;
+    t0 = t1;
+  }
+  return hipSuccess;
+}
+
+// Stripes [t0, t1) of a group: the mixed store/compare product, split into a store and a compare
+// launch when the rows exceed one launch.
+hipError_t launch_group_run(const Group& g, size_t t0, size_t t1, uint32_t* dflags, hipStream_t s) {
   MatVecJob job;
   job.k = (int)g.plan->in.size();
   job.m = (int)g.plan->out.size();
   job.coef = g.plan->rows.v.data();
-  job.nstripes = (int)g.tasks.size();
-  job.in = g.in.data();
-  job.out = g.out.data();
-  job.lens = g.lens.data();
-  job.flags = dflags + g.flag0;
+  job.nstripes = (int)(t1 - t0);
+  job.in = g.in.data() + t0 * job.k;
+  job.out = g.out.data() + t0 * job.m;
+  // one length for the run: no per-stripe lengths, so stripes carved from one pitched buffer run
+  // as a single affine launch (any number of stripes) instead of 8-32 per launch
+  bool uniform = true;
+  for (size_t t = t0; t < t1; ++t) uniform = uniform && g.lens[t] == g.lens[t0];
+  job.lens = uniform ? nullptr : g.lens.data() + t0;
+  job.len = g.lens[t0];
+  job.flags = dflags + g.flag0 + t0;
   job.mode = MatVecMode::kStoreVerify;
   job.nstore = g.plan->nstore;
   if (job.m <= kLaunchMaxRows || job.nstore == 0 || job.nstore == job.m) return launch_matvec(job, s);
@@ -78,8 +115,8 @@ hipError_t launch_group(const Group& g, uint32_t* dflags, hipStream_t s) {
   const int k = job.k, m = job.m, ns = job.nstripes, nst = job.nstore;
   std::vector<uint8_t*> o1((size_t)ns * nst), o2((size_t)ns * (m - nst));
   for (int t = 0; t < ns; ++t) {
-    for (int r = 0; r < nst; ++r) o1[(size_t)t * nst + r] = g.out[(size_t)t * m + r];
-    for (int r = nst; r < m; ++r) o2[(size_t)t * (m - nst) + r - nst] = g.out[(size_t)t * m + r];
+    for (int r = 0; r < nst; ++r) o1[(size_t)t * nst + r] = job.out[(size_t)t * m + r];
+    for (int r = nst; r < m; ++r) o2[(size_t)t * (m - nst) + r - nst] = job.out[(size_t)t * m + r];
   }
   MatVecJob a = job, b = job;
   a.m = nst;
@@ -223,7 +260,7 @@ Status RSEngine::encode_stripes(cfsec_shard* const* stripes, int nst, int mem, i
       status[s] = st;
       continue;
     }
-    if (m_ > 0) tasks.push_back(StripeTask{stripes[s], &plan, S, &status[s], 0});
+    if (m_ > 0) tasks.push_back(StripeTask{stripes[s], &plan, S, &status[s], 0, 0, s});
   }
   return run_stripes(tasks, mem);
 }
@@ -246,15 +283,23 @@ Status RSEngine::verify_stripes(cfsec_shard* const* stripes, int nst, int mem, i
       status[s] = st;
       continue;
     }
-    if (m_ > 0) tasks.push_back(StripeTask{stripes[s], &plan, S, &status[s], 0});
+    if (m_ > 0) tasks.push_back(StripeTask{stripes[s], &plan, S, &status[s], 0, 0, s});
   }
   return run_stripes(tasks, mem);
 }
 
 Status RSEngine::reconstruct_stripes(cfsec_shard* const* stripes, int nst, int mem, bool verify, int* status) {
   if (!stripes || !status || nst < 0) return CFSEC_ERR_INVALID_ARG;
-  std::map<std::vector<bool>, std::unique_ptr<StripePlan>> plans;
+  PlanStore store;
   std::vector<StripeTask> tasks;
+  plan_reconstruct_tasks(stripes, nst, verify, status, 0, 0, &store, &tasks);
+  return run_stripes(tasks, mem);
+}
+
+void RSEngine::plan_reconstruct_tasks(cfsec_shard* const* stripes, int nst, bool verify, int* status, int phase,
+                                      int owner0, PlanStore* store, std::vector<StripeTask>* tasks) {
+  StripePlan* vplan = nullptr;  // Verify as an encode-matrix pass (split_verify)
+  std::map<const StripePlan*, StripePlan*> store_only;
   for (int s = 0; s < nst; ++s) {
     status[s] = CFSEC_OK;
     cfsec_shard* sh = stripes[s];
@@ -275,13 +320,13 @@ Status RSEngine::reconstruct_stripes(cfsec_shard* const* stripes, int nst, int m
       continue;
     }
     if (np == total() && (!verify || m_ == 0)) continue;  // Reconstruct of a full stripe is a no-op
-    auto& plan = plans[present];
+    auto& plan = store->by_pattern[present];
     if (!plan) {
       plan.reset(new StripePlan());
       st = plan_stripe(present, verify, plan.get());
       if (st != CFSEC_OK) {
         plan.reset();
-        plans.erase(present);
+        store->by_pattern.erase(present);
         status[s] = st;
         continue;
       }
@@ -297,9 +342,44 @@ Status RSEngine::reconstruct_stripes(cfsec_shard* const* stripes, int nst, int m
     }
     // KRS/reedsolomon.go:1514-1518: shards[i] = shards[i][0:S]
     for (int r = 0; r < plan->nstore; ++r) sh[plan->out[r]].len = S;
-    if (!plan->out.empty()) tasks.push_back(StripeTask{sh, plan.get(), S, &status[s], 0});
+    const StripePlan* use = plan.get();
+    if (split_verify(*plan)) {
+      // Verify as a second pass over the whole stripe with the encoding matrix instead of compared
+      // rows in the reconstruct pass: the compared rows (parity_row x dec over the k inputs) have
+      // no structure, the parity rows over the data do (dyadic kernels)
+      StripePlan*& so = store_only[plan.get()];
+      if (!so) {
+        StripePlan cut = *plan;
+        cut.out.resize(cut.nstore);
+        cut.rows = Matrix(cut.nstore, k_);
+        std::memcpy(cut.rows.v.data(), plan->rows.v.data(), (size_t)cut.nstore * k_);
+        so = store->add(cut);
+      }
+      if (!vplan) {
+        StripePlan v;
+        for (int i = 0; i < k_; ++i) v.in.push_back(i);
+        for (int i = k_; i < total(); ++i) v.out.push_back(i);
+        v.nstore = 0;
+        v.rows = parity_;
+        vplan = store->add(v);
+      }
+      use = so;
+      StripeTask vt{sh, vplan, S, &status[s], 0, phase + 1, owner0 + s};
+      tasks->push_back(vt);
+    }
+    if (!use->out.empty()) tasks->push_back(StripeTask{sh, use, S, &status[s], 0, phase, owner0 + s});
   }
-  return run_stripes(tasks, mem);
+}
+
+bool RSEngine::split_verify(const StripePlan& p) const {
+  const int checks = (int)p.out.size() - p.nstore;
+  if (checks <= 0) return false;
+  static const int mode = [] {
+    const char* e = getenv("CFSEC_VERIFY_SPLIT");
+    return e ? atoi(e) : -1;
+  }();
+  if (mode >= 0) return mode != 0;
+  return false;
 }
 
 Status RSEngine::run_stripes(std::vector<StripeTask>& tasks, int mem) {
@@ -334,12 +414,19 @@ Status RSEngine::run_stripes(std::vector<StripeTask>& tasks, int mem) {
       t.dev = idx;
     }
   } else {
-    // host memory: contiguous runs of stripes, balanced by the bytes each moves
+    // host memory: contiguous runs of batch items, balanced by the bytes each moves; every task of
+    // an item (its phases) on one device, so a later phase reads what an earlier one wrote
+    std::map<int, uint64_t> per_owner;
+    for (auto& t : tasks) per_owner[t.owner] += uint64_t(t.len) * (t.plan->in.size() + t.plan->out.size());
     std::vector<uint64_t> bytes;
-    for (auto& t : tasks) bytes.push_back(uint64_t(t.len) * (t.plan->in.size() + t.plan->out.size()));
-    std::vector<int> dev(tasks.size());
+    std::map<int, int> slot;
+    for (auto& kv : per_owner) {
+      slot[kv.first] = (int)bytes.size();
+      bytes.push_back(kv.second);
+    }
+    std::vector<int> dev(bytes.size());
     partition_stripes(bytes.data(), (int)bytes.size(), nd, dev.data());
-    for (size_t i = 0; i < tasks.size(); ++i) tasks[i].dev = dev[i];
+    for (auto& t : tasks) t.dev = dev[slot[t.owner]];
   }
   std::vector<std::vector<StripeTask*>> per(nd);
   for (auto& t : tasks) per[t.dev].push_back(&t);
@@ -370,7 +457,9 @@ Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceCont
   // row the product touches) and which go through staging (pageable host memory)
   std::vector<StripeTask*> direct, staged;
   std::map<std::pair<const StripeTask*, int>, uint8_t*> alias;
+  int nphase = 1;
   for (StripeTask* t : tasks) {
+    nphase = std::max(nphase, t->phase + 1);
     bool in_place = true;
     if (mem == CFSEC_MEM_HOST) {
       for (int c : t->plan->in) {
@@ -387,94 +476,105 @@ Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceCont
     (in_place ? direct : staged).push_back(t);
   }
   // staging lanes: each holds whole stripes, at least the largest one
-  size_t lane_bytes = 0;
+  size_t lane_bytes = 0, staged_total = 0;
   for (StripeTask* t : staged) {
     const size_t b = align_up(t->len, kSlot) * (t->plan->in.size() + t->plan->out.size());
     lane_bytes = std::max(lane_bytes, b);
+    staged_total += b;
   }
-  size_t staged_total = 0;
-  for (StripeTask* t : staged) staged_total += align_up(t->len, kSlot) * (t->plan->in.size() + t->plan->out.size());
   if (!staged.empty()) lane_bytes = std::max(lane_bytes, std::min(kLaneBudget, staged_total));
-  const int nlanes = staged_total > lane_bytes ? 2 : 1;
+  const int nlanes = staged_total > lane_bytes || nphase > 1 ? 2 : 1;
   DeviceContext::Workspace* ws = nullptr;
   Status st = ctx->acquire(lane_bytes * nlanes, (size_t)n, &ws);
   if (st != CFSEC_OK) return st;
   hipStream_t lane[2] = {ws->stream, ws->stream2};
+  // lane `to` waits for everything queued on lane `from` so far
+  const auto join = [&](int from, int to) {
+    Status e = hip_status(hipEventRecord(ws->ev, lane[from]), "hipEventRecord");
+    if (e == CFSEC_OK) e = hip_status(hipStreamWaitEvent(lane[to], ws->ev, 0), "hipStreamWaitEvent");
+    return e;
+  };
   if (mem == CFSEC_MEM_DEVICE) st = ctx->order_after_default(ws);
   if (st == CFSEC_OK) st = hip_status(hipMemsetAsync(ws->dflags, 0, 4 * (size_t)n, lane[0]), "hipMemsetAsync");
-  if (st == CFSEC_OK && nlanes > 1) {
-    st = hip_status(hipEventRecord(ws->ev, lane[0]), "hipEventRecord");
-    if (st == CFSEC_OK) st = hip_status(hipStreamWaitEvent(lane[1], ws->ev, 0), "hipStreamWaitEvent");
-  }
+  if (st == CFSEC_OK && nlanes > 1) st = join(0, 1);
   int next_flag = 0;
   std::vector<std::pair<StripeTask*, int>> flags;  // (task, flag word)
   const auto record = [&](const std::vector<Group>& groups) {
     for (const Group& gr : groups)
       for (size_t i = 0; i < gr.tasks.size(); ++i) flags.emplace_back(gr.tasks[i], gr.flag0 + (int)i);
   };
-  // in-place stripes: one set of launches on lane 0
-  if (st == CFSEC_OK && !direct.empty()) {
-    std::vector<Group> groups = make_groups(direct, &next_flag, [&](const StripeTask* t, int idx) {
-      return mem == CFSEC_MEM_DEVICE ? (const uint8_t*)t->shards[idx].data : (const uint8_t*)alias[{t, idx}];
-    });
-    for (const Group& gr : groups)
-      if (st == CFSEC_OK) st = hip_status(launch_group(gr, ws->dflags, lane[0]), "launch_matvec(batch)");
-    record(groups);
-  }
-  // staged stripes: chunks of whole stripes alternating over the two lanes; each lane copies its
-  // chunk in, runs it and copies the stored rows back while the other lane's chunk moves
-  size_t i0 = 0;
-  for (int chunk = 0; st == CFSEC_OK && i0 < staged.size(); ++chunk) {
-    const int l = chunk % nlanes;
-    hipStream_t s = lane[l];
-    uint8_t* base = ws->dbuf + lane_bytes * l;
-    size_t used = 0, i1 = i0;
-    std::map<std::pair<const StripeTask*, int>, uint8_t*> slot;
-    while (i1 < staged.size()) {
-      StripeTask* t = staged[i1];
-      const size_t sl = align_up(t->len, kSlot);
-      const size_t need = sl * (t->plan->in.size() + t->plan->out.size());
-      if (i1 > i0 && used + need > lane_bytes) break;
-      for (int c : t->plan->in) {
-        slot[{t, c}] = base + used;
-        used += sl;
-      }
-      for (int o : t->plan->out) {
-        slot[{t, o}] = base + used;
-        used += sl;
-      }
-      ++i1;
+  int chunk = 0;
+  for (int ph = 0; ph < nphase && st == CFSEC_OK; ++ph) {
+    if (ph > 0 && nlanes > 1) {  // a phase starts after everything of the previous one, on both lanes
+      st = join(1, 0);
+      if (st == CFSEC_OK) st = join(0, 1);
     }
-    std::vector<StripeTask*> part(staged.begin() + i0, staged.begin() + i1);
-    for (StripeTask* t : part) {
-      for (int c : t->plan->in)
-        if (st == CFSEC_OK)
-          st = hip_status(hipMemcpyAsync(slot[{t, c}], t->shards[c].data, t->len, hipMemcpyHostToDevice, s),
-                          "hipMemcpyAsync H2D");
-      for (size_t r = t->plan->nstore; r < t->plan->out.size(); ++r)
-        if (st == CFSEC_OK) {
-          const int o = t->plan->out[r];
-          st = hip_status(hipMemcpyAsync(slot[{t, o}], t->shards[o].data, t->len, hipMemcpyHostToDevice, s),
-                          "hipMemcpyAsync H2D");
+    // in-place stripes: one set of launches on lane 0
+    std::vector<StripeTask*> dph, sph;
+    for (StripeTask* t : direct)
+      if (t->phase == ph) dph.push_back(t);
+    for (StripeTask* t : staged)
+      if (t->phase == ph) sph.push_back(t);
+    if (st == CFSEC_OK && !dph.empty()) {
+      std::vector<Group> groups = make_groups(dph, &next_flag, [&](const StripeTask* t, int idx) {
+        return mem == CFSEC_MEM_DEVICE ? (const uint8_t*)t->shards[idx].data : (const uint8_t*)alias[{t, idx}];
+      });
+      for (const Group& gr : groups)
+        if (st == CFSEC_OK) st = hip_status(launch_group(gr, ws->dflags, lane[0]), "launch_matvec(batch)");
+      record(groups);
+    }
+    // staged stripes: chunks of whole stripes alternating over the two lanes; each lane copies its
+    // chunk in, runs it and copies the stored rows back while the other lane's chunk moves
+    size_t i0 = 0;
+    for (; st == CFSEC_OK && i0 < sph.size(); ++chunk) {
+      const int l = chunk % nlanes;
+      hipStream_t s = lane[l];
+      uint8_t* base = ws->dbuf + lane_bytes * l;
+      size_t used = 0, i1 = i0;
+      std::map<std::pair<const StripeTask*, int>, uint8_t*> slot;
+      while (i1 < sph.size()) {
+        StripeTask* t = sph[i1];
+        const size_t sl = align_up(t->len, kSlot);
+        const size_t need = sl * (t->plan->in.size() + t->plan->out.size());
+        if (i1 > i0 && used + need > lane_bytes) break;
+        for (int c : t->plan->in) {
+          slot[{t, c}] = base + used;
+          used += sl;
         }
-    }
-    std::vector<Group> groups =
-        make_groups(part, &next_flag, [&](const StripeTask* t, int idx) { return (const uint8_t*)slot[{t, idx}]; });
-    for (const Group& gr : groups)
-      if (st == CFSEC_OK) st = hip_status(launch_group(gr, ws->dflags, s), "launch_matvec(batch)");
-    record(groups);
-    for (StripeTask* t : part)
-      for (int r = 0; r < t->plan->nstore && st == CFSEC_OK; ++r) {
-        const int o = t->plan->out[r];
-        st = hip_status(hipMemcpyAsync(t->shards[o].data, slot[{t, o}], t->len, hipMemcpyDeviceToHost, s),
-                        "hipMemcpyAsync D2H");
+        for (int o : t->plan->out) {
+          slot[{t, o}] = base + used;
+          used += sl;
+        }
+        ++i1;
       }
-    i0 = i1;
+      std::vector<StripeTask*> part(sph.begin() + i0, sph.begin() + i1);
+      for (StripeTask* t : part) {
+        for (int c : t->plan->in)
+          if (st == CFSEC_OK)
+            st = hip_status(hipMemcpyAsync(slot[{t, c}], t->shards[c].data, t->len, hipMemcpyHostToDevice, s),
+                            "hipMemcpyAsync H2D");
+        for (size_t r = t->plan->nstore; r < t->plan->out.size(); ++r)
+          if (st == CFSEC_OK) {
+            const int o = t->plan->out[r];
+            st = hip_status(hipMemcpyAsync(slot[{t, o}], t->shards[o].data, t->len, hipMemcpyHostToDevice, s),
+                            "hipMemcpyAsync H2D");
+          }
+      }
+      std::vector<Group> groups =
+          make_groups(part, &next_flag, [&](const StripeTask* t, int idx) { return (const uint8_t*)slot[{t, idx}]; });
+      for (const Group& gr : groups)
+        if (st == CFSEC_OK) st = hip_status(launch_group(gr, ws->dflags, s), "launch_matvec(batch)");
+      record(groups);
+      for (StripeTask* t : part)
+        for (int r = 0; r < t->plan->nstore && st == CFSEC_OK; ++r) {
+          const int o = t->plan->out[r];
+          st = hip_status(hipMemcpyAsync(t->shards[o].data, slot[{t, o}], t->len, hipMemcpyDeviceToHost, s),
+                          "hipMemcpyAsync D2H");
+        }
+      i0 = i1;
+    }
   }
-  if (st == CFSEC_OK && nlanes > 1) {
-    st = hip_status(hipEventRecord(ws->ev, lane[1]), "hipEventRecord");
-    if (st == CFSEC_OK) st = hip_status(hipStreamWaitEvent(lane[0], ws->ev, 0), "hipStreamWaitEvent");
-  }
+  if (st == CFSEC_OK && nlanes > 1) st = join(1, 0);
   if (st == CFSEC_OK)
     st = hip_status(hipMemcpyAsync(ws->hflags, ws->dflags, 4 * (size_t)n, hipMemcpyDeviceToHost, lane[0]),
                     "hipMemcpyAsync D2H");
@@ -534,8 +634,8 @@ Status LrcEncoder::reconstruct_batch(cfsec_shard* shards, int n, int nbids, cons
                                      int mem, bool verify, int* status) {
   // lrcencoder.go:133-186 per bid, then lrcencoder.go:89-131 (Verify): a local stripe (n = its size)
   // is the local engine alone; a whole stripe is the global engine over its first N+M shards, then
-  // each AZ's local engine over that AZ's local stripe -- two batched passes, in that order, as
-  // the reference runs them.
+  // each AZ's local engine over that AZ's local stripe -- planned together and run as two phases of
+  // one call (one sync), in that order, as the reference runs them.
   if (!shards || !status || !bad_off || nbids < 0) return CFSEC_ERR_INVALID_ARG;
   const int N = t_.n, M = t_.m, L = t_.l, AZ = t_.az_count;
   const int lsz = (N + M + L) / AZ;
@@ -567,17 +667,22 @@ Status LrcEncoder::reconstruct_batch(cfsec_shard* shards, int n, int nbids, cons
     for (size_t i = 0; i < pos.size(); ++i) status[pos[i]] = st[i];
     return rc;
   }
-  // pass 1: global Reconstruct (+ global Verify) over shards [0, N+M)
+  // phase 0 (1): global Reconstruct (+ global Verify) over shards [0, N+M)
+  PlanStore gstore, lstore;
+  std::vector<StripeTask> tasks;
   std::vector<int> st1(stripes.size());
-  Status rc = engine_->reconstruct_stripes(stripes.data(), (int)stripes.size(), mem, verify, st1.data());
-  if (rc != CFSEC_OK) return rc;
-  // pass 2: every AZ's local stripe (copied headers, lrcencoder.go:236-243): local Reconstruct of
-  // its bad local shards (index remap lrcencoder.go:161-171) (+ local Verify)
-  std::vector<std::vector<cfsec_shard>> views;
-  std::vector<size_t> owner;
-  views.reserve(stripes.size() * AZ);
+  engine_->plan_reconstruct_tasks(stripes.data(), (int)stripes.size(), verify, st1.data(), 0, 0, &gstore, &tasks);
+  int lphase = 1;
+  for (auto& t : tasks) lphase = std::max(lphase, t.phase + 1);
+  // then every AZ's local stripe (copied headers, lrcencoder.go:236-243) with the rebuilt global
+  // shards' lengths already set: local Reconstruct of its bad local shards (index remap
+  // lrcencoder.go:161-171) (+ local Verify)
+  // per AZ, in bid order: an AZ's views of bids carved from one pitched buffer sit at one stride
+  // from each other, so each AZ runs as one affine launch
+  std::vector<std::vector<std::vector<cfsec_shard>>> views(AZ);
+  std::vector<std::vector<size_t>> vowner(AZ);
   for (size_t i = 0; i < stripes.size(); ++i) {
-    if (st1[i] != CFSEC_OK && st1[i] != CFSEC_ERR_VERIFY) continue;  // Reconstruct failed: no local pass
+    if (st1[i] != CFSEC_OK) continue;  // Reconstruct failed: no local pass
     cfsec_shard* sh = stripes[i];
     const int b = pos[i];
     std::map<int, std::vector<int>> local_bad;
@@ -598,14 +703,26 @@ Status LrcEncoder::reconstruct_batch(cfsec_shard* shards, int n, int nbids, cons
           break;
         }
       }
-      views.push_back(std::move(ls));
-      owner.push_back(i);
+      views[a].push_back(std::move(ls));
+      vowner[a].push_back(i);
     }
   }
   std::vector<cfsec_shard*> lp;
-  for (auto& v : views) lp.push_back(v.data());
+  std::vector<size_t> owner;
+  for (int a = 0; a < AZ; ++a)
+    for (size_t v = 0; v < views[a].size(); ++v) {
+      lp.push_back(views[a][v].data());
+      owner.push_back(vowner[a][v]);
+    }
   std::vector<int> st2(lp.size());
-  rc = local_->reconstruct_stripes(lp.data(), (int)lp.size(), mem, verify, st2.data());
+  const size_t first_local = tasks.size();
+  local_->plan_reconstruct_tasks(lp.data(), (int)lp.size(), verify, st2.data(), lphase, 0, &lstore, &tasks);
+  for (size_t t = first_local; t < tasks.size(); ++t) {
+    // owner: the bid (a host batch keeps a bid's passes on one device)
+    const size_t v = (size_t)(tasks[t].status - st2.data());
+    tasks[t].owner = (int)owner[v];
+  }
+  const Status rc = engine_->run_stripes(tasks, mem);
   // per bid: a Reconstruct error (global, then local) wins over a failed Verify
   std::vector<int> local_err(stripes.size(), CFSEC_OK);
   for (size_t v = 0; v < lp.size(); ++v) {
@@ -682,18 +799,20 @@ Status LrcEncoder::encode_batch(cfsec_shard* shards, int n, int nstripes, int me
       status[s] = st;
       continue;
     }
-    tasks.push_back(StripeTask{sh, &plan, S, &status[s], 0});
+    tasks.push_back(StripeTask{sh, &plan, S, &status[s], 0, 0, s});
   }
-  Status rc = engine_->run_stripes(tasks, mem);
-  if (rc == CFSEC_OK && enable_verify_) {
-    StripePlan vplan = plan;
-    vplan.nstore = 0;
-    std::vector<StripeTask> vt;
-    for (auto& t : tasks)
-      if (*t.status == CFSEC_OK) vt.push_back(StripeTask{t.shards, &vplan, t.len, t.status, 0});
-    rc = engine_->run_stripes(vt, mem);
+  StripePlan vplan = plan;
+  vplan.nstore = 0;
+  if (enable_verify_) {  // the Verify pass in the same call, after the encode (phase 1)
+    const size_t ne = tasks.size();
+    for (size_t i = 0; i < ne; ++i) {
+      StripeTask v = tasks[i];
+      v.plan = &vplan;
+      v.phase = 1;
+      tasks.push_back(v);
+    }
   }
-  return rc;
+  return engine_->run_stripes(tasks, mem);
 }
 
 }  // namespace cfsec

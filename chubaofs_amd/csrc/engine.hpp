@@ -120,6 +120,18 @@ struct StripeTask {
   size_t len = 0;
   int* status = nullptr;        // set to CFSEC_ERR_VERIFY when a compared row mismatches
   int dev = 0;                  // index into the engine's device list
+  int phase = 0;                // tasks of phase p run after every task of phase p - 1 (same call)
+  int owner = 0;                // batch item: a host batch keeps an item's tasks on one device
+};
+
+// Plans built for one batch call (stable addresses for the tasks that point at them).
+struct PlanStore {
+  std::map<std::vector<bool>, std::unique_ptr<StripePlan>> by_pattern;
+  std::vector<std::unique_ptr<StripePlan>> other;
+  StripePlan* add(const StripePlan& p) {
+    other.emplace_back(new StripePlan(p));
+    return other.back().get();
+  }
 };
 
 class RSEngine {
@@ -169,11 +181,18 @@ class RSEngine {
   Status encode_stripes(cfsec_shard* const* stripes, int nst, int mem, int* status);
   Status verify_stripes(cfsec_shard* const* stripes, int nst, int mem, int* status);
   Status reconstruct_stripes(cfsec_shard* const* stripes, int nst, int mem, bool verify, int* status);
+  // The planning half of reconstruct_stripes: checks every stripe (errors to status[s]), sets the
+  // rebuilt shards' lengths and appends the tasks (phase `phase`, and phase + 1 for a split Verify)
+  // that run_stripes executes; owner of stripe s = owner0 + s.
+  void plan_reconstruct_tasks(cfsec_shard* const* stripes, int nst, bool verify, int* status, int phase,
+                              int owner0, PlanStore* store, std::vector<StripeTask>* tasks);
   // Run the tasks' products (device memory, pinned host memory in place, pageable host memory
   // through double-buffered staging), tasks partitioned over the devices.
   Status run_stripes(std::vector<StripeTask>& tasks, int mem);
   // Plan of a Reconstruct (+ Verify) over the present shards.
   Status plan_stripe(const std::vector<bool>& present, bool verify, StripePlan* plan);
+  // Run a plan's Verify as a separate encode-matrix pass instead of its compared rows.
+  bool split_verify(const StripePlan& p) const;
 
   // Generic "outputs = rows x inputs" over caller shards (host or device memory).
   // mode kVerify: *ok set; outputs are read, not written.
