@@ -33,9 +33,9 @@ using crcdev::kTabWords;
 using crcdev::kTile;
 using dev::u32x4;
 
-constexpr int kSlots = 96;  // objects per launch
+constexpr int kSlots = 128;  // objects per launch (a whole 8-stripe EC12P4 batch: 128 shards)
 constexpr int kRing = 4;    // tiles in flight per thread
-constexpr int kAfter = 320;  // objects of up to 320 blocks (20 MiB at 64 KiB) move a run's CRC in one multiply
+constexpr int kAfter = 200;  // objects of up to 200 blocks (12.5 MiB at 64 KiB) move a block's CRC in one multiply
 
 struct __attribute__((aligned(16))) BlockArgs {
   const uint8_t* in[kSlots];  // object y: payload of launch block w at in[y] + w*in_stride + in_off
@@ -204,15 +204,19 @@ __global__ __launch_bounds__(256) void crc32block_kernel(const BlockArgs a) {
 // multiplies are linear, so they distribute over the XOR), and in encode also to the object end
 // and into the whole-object word; after one barrier thread 0 only XORs four words and stores or
 // compares the header.
-template <int RING, bool NTS = true>
-__global__ __launch_bounds__(256) void crc32block_block_kernel(const BlockArgs a) {
+// BPW blocks per workgroup (256 threads each, side by side: adjacent blocks, one table load).
+template <int RING, bool NTS = true, int BPW = 1>
+__global__ __launch_bounds__(256 * BPW) void crc32block_block_kernel(const BlockArgs a) {
   __shared__ uint32_t ct[crcdev::kNibTabWords];
-  __shared__ uint32_t red[8];  // per wave: its share of the block's raw CRC, and of the object's
-  for (int i = threadIdx.x; i < crcdev::kNibTabWords; i += 256) ct[i] = a.tabs[crcdev::kByteTabWords + i];
-  const uint32_t kj = a.tabs[kTabWords + crcdev::kBasisWords + threadIdx.x];
+  __shared__ uint32_t redb[BPW][8];  // per wave: its share of the block's raw CRC, and of the object's
+  for (int i = threadIdx.x; i < crcdev::kNibTabWords; i += 256 * BPW) ct[i] = a.tabs[crcdev::kByteTabWords + i];
+  const uint32_t half = threadIdx.x >> 8, tid = threadIdx.x & 255;
+  uint32_t* red = redb[half];
+  const uint32_t kj = a.tabs[kTabWords + crcdev::kBasisWords + tid];
   __syncthreads();
-  const uint32_t it = blockIdx.x;
-  const uint32_t y = it / a.nb, w = it - y * a.nb;
+  const uint32_t it = blockIdx.x * BPW + half;
+  const bool live = it < a.items;
+  const uint32_t y = live ? it / a.nb : 0, w = live ? it - y * a.nb : 0;
   const uint8_t* const in = a.in[y];
   uint8_t* const out = a.out[y];
   const uint64_t b = a.b0 + w;
@@ -222,18 +226,18 @@ __global__ __launch_bounds__(256) void crc32block_block_kernel(const BlockArgs a
   const uint8_t* src = in + (int64_t)w * a.in_stride + a.in_off;
   const int64_t dbase = (int64_t)w * a.out_stride + a.out_off;
   const uint32_t h = (uint32_t)(((uintptr_t)out + (uint64_t)dbase) & 15u);
-  const uint32_t tiles = (plen + h + kTile - 1) / kTile;
+  const uint32_t tiles = live ? (plen + h + kTile - 1) / kTile : 0;
   uint32_t R = 0, ring[RING][4];
 #pragma unroll
   for (int k = 0; k < RING; ++k)
-    if (k < (int)tiles) load_piece(src, plen, h, threadIdx.x + 256 * k, ring[k]);
+    if (k < (int)tiles) load_piece(src, plen, h, tid + 256 * k, ring[k]);
   for (uint32_t t0 = 0; t0 < tiles; t0 += RING) {
 #pragma unroll
     for (int k = 0; k < RING; ++k) {
       const uint32_t t = t0 + k;
       if (t < tiles) {
         uint32_t (&cur)[4] = ring[k];
-        const uint32_t p = t * 256 + threadIdx.x;
+        const uint32_t p = t * 256 + tid;
         R = crcdev::crc_step_nib(ct, R, cur);
         const int64_t first = (int64_t)16 * p - h;
         if (first < (int64_t)plen) {
@@ -254,9 +258,9 @@ __global__ __launch_bounds__(256) void crc32block_block_kernel(const BlockArgs a
   uint32_t v = crcdev::mulmod(kj, R);
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) v ^= (uint32_t)__shfl_xor((int)v, d);
-  if ((threadIdx.x & 63) == 0) {
+  if ((tid & 63) == 0 && live) {
     const uint32_t raw = crcdev::mulmod(a.gconst[last][h], v);  // this wave's share of the block's raw CRC
-    red[threadIdx.x >> 6] = raw;
+    red[tid >> 6] = raw;
     if (a.encode && a.whole) {
       uint32_t s = raw;  // the share moved to the object end
       if (b + 1 < a.nblk) {
@@ -269,11 +273,11 @@ __global__ __launch_bounds__(256) void crc32block_block_kernel(const BlockArgs a
             if (e & 1) s = crcdev::mulmod(s, a.xpow2[q]);
         }
       }
-      red[4 + (threadIdx.x >> 6)] = s;
+      red[4 + (tid >> 6)] = s;
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (tid == 0 && live) {
     const uint32_t crc = red[0] ^ red[1] ^ red[2] ^ red[3] ^ a.fin[last];
     if (a.encode) {
       uint8_t* hdr = out + (int64_t)w * a.out_stride;
@@ -297,7 +301,7 @@ bool crc32block_valid_len(int64_t block_len) { return block_len > 0 && block_len
 
 namespace blk {
 template <bool STORE, bool CRC, bool EPI = true, bool SRCALIGN = false, bool ONE = true, bool NTS = true,
-          int RING = kRing, bool FASTEPI = true>
+          int RING = kRing, bool FASTEPI = true, int BPW = 1>
 hipError_t launch(const Crc32BlockJob& j, hipStream_t stream) {
   if (!crc32block_valid_len(j.block_len) || j.size < 0 || j.block_len > 0xFFFFFFFFll) return hipErrorInvalidValue;
   const int64_t P = j.block_len - 4;
@@ -370,7 +374,8 @@ hipError_t launch(const Crc32BlockJob& j, hipStream_t stream) {
     a.ipw = ONE ? 1u : (a.items + 2047) / 2048;
     const unsigned grid = (a.items + a.ipw - 1) / a.ipw;
     if (FASTEPI && ONE && EPI && STORE && CRC)
-      hipLaunchKernelGGL((crc32block_block_kernel<RING, NTS>), dim3(grid), dim3(256), 0, stream, a);
+      hipLaunchKernelGGL((crc32block_block_kernel<RING, NTS, BPW>), dim3((a.items + BPW - 1) / BPW), dim3(256 * BPW), 0,
+                         stream, a);
     else
       hipLaunchKernelGGL((crc32block_kernel<STORE, CRC, EPI, SRCALIGN, NTS>), dim3(grid), dim3(256), 0, stream, a);
     e = hipGetLastError();

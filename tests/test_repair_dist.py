@@ -96,17 +96,25 @@ def test_plan_first_k_survivors():
         repair.RepairPlan.make(12, 16, [0, 1, 2, 3, 4])
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("strategy", ["columns", "allgather"])
-def test_repair_gpu_single_rank(strategy):
-    """End to end on one GPU (world 1, RCCL): exchange + fused decode vs the oracle."""
-    from chubaofs_amd import reedsolomon
-    from oracle import oracle as O
-    k, m, nb, S_ = 16, 20, 4, 262144 + 7
+@pytest.fixture(scope="module")
+def nccl_world1():
+    """A world-1 RCCL process group for this module, destroyed at its end."""
     if not dist.is_initialized():
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(free_port())
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    yield
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("strategy", ["columns", "allgather"])
+def test_repair_gpu_single_rank(strategy, nccl_world1):
+    """End to end on one GPU (world 1, RCCL): exchange + fused decode vs the oracle."""
+    from chubaofs_amd import reedsolomon
+    from oracle import oracle as O
+    k, m, nb, S_ = 16, 20, 4, 262144 + 7
     rng = np.random.default_rng(5)
     full = []
     for b in range(nb):
@@ -121,3 +129,23 @@ def test_repair_gpu_single_rank(strategy):
     for b in range(nb):
         for q, e in enumerate([0, 1, 16, 17]):
             assert np.array_equal(got[b, q], full[b][e]), (b, e)
+
+
+@pytest.mark.gpu
+def test_repair_gpu_tasklet_64_bids(nccl_world1):
+    """The C5 shape on one GPU: a 64-bid EC16P20 tasklet (S = 262144), erased {0, 1, 16, 17},
+    exchanged over RCCL (world 1) and decoded; every rebuilt row equals the original."""
+    from chubaofs_amd import reedsolomon
+    k, m, nb, S_ = 16, 20, 64, 262144
+    g = torch.Generator(device="cuda")
+    g.manual_seed(64)
+    local = torch.zeros((nb, k + m, S_), dtype=torch.uint8, device="cuda")
+    local[:, :k] = torch.randint(0, 256, (nb, k, S_), generator=g, device="cuda", dtype=torch.uint8)
+    enc = reedsolomon.New(k, m, device=0)
+    enc.encode_batch([local[b, i].data_ptr() for b in range(nb) for i in range(k + m)], S_, nb)
+    torch.cuda.synchronize()
+    want = local[:, [0, 1, 16, 17]].clone()
+    local[:, [0, 1, 16, 17]] = 0
+    out = repair.repair_batch(enc, local, [0, 1, 16, 17], 0, 1, strategy="columns")
+    torch.cuda.synchronize()
+    assert torch.equal(out, want)

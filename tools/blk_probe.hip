@@ -90,6 +90,11 @@ int main(int argc, char** argv) {
       {"enc new epi R4", [&] { CK((cfsec::blk::launch<true, true, true, false, true, true, 4, true>(J(true), 0))); }, 2 * pb},
       {"enc new epi R6", [&] { CK((cfsec::blk::launch<true, true, true, false, true, true, 6, true>(J(true), 0))); }, 2 * pb},
       {"enc new epi R8", [&] { CK((cfsec::blk::launch<true, true, true, false, true, true, 8, true>(J(true), 0))); }, 2 * pb},
+      {"enc 2 blk/wg R4", [&] { CK((cfsec::blk::launch<true, true, true, false, true, true, 4, true, 2>(J(true), 0))); }, 2 * pb},
+      {"enc 2 blk/wg R3", [&] { CK((cfsec::blk::launch<true, true, true, false, true, true, 3, true, 2>(J(true), 0))); }, 2 * pb},
+      {"enc 4 blk/wg R4", [&] { CK((cfsec::blk::launch<true, true, true, false, true, true, 4, true, 4>(J(true), 0))); }, 2 * pb},
+      {"enc new epi R2", [&] { CK((cfsec::blk::launch<true, true, true, false, true, true, 2, true>(J(true), 0))); }, 2 * pb},
+      {"dec 2 blk/wg R4", [&] { CK((cfsec::blk::launch<true, true, true, false, true, true, 4, true, 2>(J(false), 0))); }, 2 * pb},
       {"dec old epilogue", [&] { CK((cfsec::blk::launch<true, true, true, false, true, true, 4, false>(J(false), 0))); }, 2 * pb},
       {"dec new epi R4", [&] { CK((cfsec::blk::launch<true, true, true, false, true, true, 4, true>(J(false), 0))); }, 2 * pb},
       {"dec new epi R8", [&] { CK((cfsec::blk::launch<true, true, true, false, true, true, 8, true>(J(false), 0))); }, 2 * pb},
@@ -124,7 +129,7 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(w1.data(), words, 4 * n, hipMemcpyDeviceToHost));
     CK(hipMemset(frm, 0, fpitch * n));
     CK(hipMemset(words, 0, 4 * n));
-    CK((cfsec::blk::launch<true, true, true, false, true, true, 8, true>(k, 0)));
+    CK((cfsec::blk::launch<true, true, true, false, true, true, 4, true, 2>(k, 0)));
     CK(hipMemcpy(got.data(), frm, got.size(), hipMemcpyDeviceToHost));
     CK(hipMemcpy(w2.data(), words, 4 * n, hipMemcpyDeviceToHost));
     printf("new-epilogue kernel == old kernel: framed %s, whole-shard crc %s\n", want == got ? "yes" : "NO",
