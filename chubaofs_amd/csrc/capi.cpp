@@ -316,6 +316,7 @@ int cfsec_rs_set_devices(cfsec_rs* h, const int* devices, int ndev) {
   return guarded([&] { return h->e->set_devices(devices, ndev); });
 }
 
+extern "C++" {
 namespace {
 std::vector<cfsec_shard*> stripe_views(cfsec_shard* shards, int nstripes, int total) {
   std::vector<cfsec_shard*> v((size_t)std::max(nstripes, 0));
@@ -323,6 +324,7 @@ std::vector<cfsec_shard*> stripe_views(cfsec_shard* shards, int nstripes, int to
   return v;
 }
 }  // namespace
+}
 
 int cfsec_batch_partition(const uint64_t* bytes, int n, int ndev, int* dev) {
   if (n < 0 || ndev <= 0 || (n > 0 && (!bytes || !dev))) return CFSEC_ERR_INVALID_ARG;

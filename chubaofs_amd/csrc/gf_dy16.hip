@@ -1,6 +1,7 @@
-// gf_dy16.hip -- kernels for 16-input matrices opening with a 16x16 dyadic block (EC16P20 encode);
-// see gf_dyadic16.hpp.  The EC16P20L2 fused encode (the same 20 rows + 2 local rows) needed 256
-// VGPRs (1 wave/SIMD) in this form and stays on the 4x4-dyadic kernel with plain rows.
+// gf_dy16.hip -- kernels for 16-input matrices opening with a 16x16 dyadic block (EC16P20 encode
+// and the EC16P20L2 fused encode, the same 20 rows + 2 local rows); see gf_dyadic16.hpp.  The local
+// rows share the 4x4 row block's registers and take one input column at a time (pairs of columns
+// needed 256 VGPRs + AGPRs: 1 wave/SIMD; this form 214-217, 2 waves/SIMD like EC16P20's 178-201).
 #include "gf_dyadic16.hpp"
 #include "gf_launch.hpp"
 
@@ -26,6 +27,7 @@ hipError_t launch_one(MatVecMode mode, const dev::GfArgs& a, unsigned ns, hipStr
 hipError_t launch_dy16(int m, MatVecMode mode, const dev::GfArgs& a, unsigned ns, hipStream_t st) {
   switch (m) {
     case 20: return launch_one<20, 1, 0>(mode, a, ns, st);  // EC16P20 global parity
+    case 22: return launch_one<22, 1, 2>(mode, a, ns, st);  // EC16P20L2 fused: + 2 local rows
     default: return hipErrorInvalidValue;
   }
 }

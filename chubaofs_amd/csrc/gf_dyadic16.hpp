@@ -71,8 +71,9 @@ __device__ __forceinline__ void xor_into(Vec4& dst, const Vec4& src) {
 }
 
 // Kernel body: 16 inputs, M = 16 + 4 R4 + E outputs; 256-thread workgroups, each lane one 16-byte
-// chunk of every row (tile 4 KiB), grid (tiles, stripes).  Rows: acc[0..15] the 16x16 block,
-// acc[16..16+4R4) the 4x4 row blocks, then the E plain rows.
+// chunk of every row (tile 4 KiB), grid (tiles, stripes).  Output rows 16.. (the 4x4 row blocks,
+// then the E plain rows) are computed first, from the original inputs, and stored one group at a
+// time from acc[16..]; then the 16x16 block into acc[0..15].
 template <int M, int R4, int E, MatVecMode MODE, bool PIN = true>
 __device__ __forceinline__ void matvec_dy16(const GfArgs& a) {
   constexpr int K = 16, N4 = R4 * 4 * 9;
@@ -99,9 +100,11 @@ __device__ __forceinline__ void matvec_dy16(const GfArgs& a) {
   const size_t rem = off < slen ? (size_t)(slen - off) : 0;
   uint32_t diff = 0;
   if (full || rem) {
-    uint32_t acc[M][4];
+    // rows 16.. share registers: the 4x4 row blocks, stored, then the plain rows in the same slots
+    constexpr int NA = 16 + (4 * R4 > E ? 4 * R4 : E);
+    uint32_t acc[NA][4];
 #pragma unroll
-    for (int r = 0; r < M; ++r)
+    for (int r = 0; r < NA; ++r)
 #pragma unroll
       for (int w = 0; w < 4; ++w) acc[r][w] = 0u;
     uint32_t x[K][4];
@@ -115,9 +118,9 @@ __device__ __forceinline__ void matvec_dy16(const GfArgs& a) {
     };
     // store (or compare) output row r as soon as it is final, so its registers are free for the
     // 16x16 block's temporaries
-    const auto put = [&](int r) {
+    const auto put = [&](int r, int ai) {
       uint8_t* p = const_cast<uint8_t*>(row[K + r]) + off;
-      const u32x4 v = u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
+      const u32x4 v = u32x4{acc[ai][0], acc[ai][1], acc[ai][2], acc[ai][3]};
       if constexpr (kVer) {
         const u32x4 d = v ^ (full ? ld16<true>(p) : ld_tail(p, rem));
         diff |= d.x | d.y | d.z | d.w;
@@ -139,20 +142,26 @@ __device__ __forceinline__ void matvec_dy16(const GfArgs& a) {
         sb();
       }
 #pragma unroll
-      for (int r = 16; r < 16 + 4 * R4; ++r) put(r);
+      for (int r = 16; r < 16 + 4 * R4; ++r) put(r, r);
       sb();
+#pragma unroll
+      for (int r = 16; r < NA; ++r)
+#pragma unroll
+        for (int w = 0; w < 4; ++w) acc[r][w] = 0u;
     }
     if constexpr (E > 0) {
-      auto& eacc = reinterpret_cast<uint32_t(&)[E][4]>(acc[16 + 4 * R4]);
+      auto& eacc = reinterpret_cast<uint32_t(&)[E][4]>(acc[16]);
       constexpr int ND = kDy16Leaves + N4;
 #pragma unroll
-      for (int c = 0; c < K; c += 2) {
-        mac_pair_k<E>(eacc, x[c], x[c + 1], tab01 + ND + c * E, tab2 + ND + c * E, tab01 + ND + (c + 1) * E,
-                      tab2 + ND + (c + 1) * E);
+      for (int c = 0; c < K; ++c) {
+        mac_row_k<E>(eacc, x[c], tab01 + ND + c * E, tab2 + ND + c * E);
+        if constexpr (PIN)
+#pragma unroll
+          for (int e = 0; e < E; ++e) asm volatile("" : "+v"(eacc[e][0]), "+v"(eacc[e][1]), "+v"(eacc[e][2]), "+v"(eacc[e][3]));
         sb();
       }
 #pragma unroll
-      for (int r = 16 + 4 * R4; r < M; ++r) put(r);
+      for (int e = 0; e < E; ++e) put(16 + 4 * R4 + e, 16 + e);
       sb();
     }
     // the 16x16 block: S = X + Y into x[0..7]
@@ -203,7 +212,7 @@ __device__ __forceinline__ void matvec_dy16(const GfArgs& a) {
     leaf4<PIN>(v4(acc[8]), v4(x[0]), tab01, tab2, 6);   // B_a
     leaf4<PIN>(v4(acc[12]), v4(x[0]), tab01, tab2, 8);  // B_b
 #pragma unroll
-    for (int r = 0; r < 16; ++r) put(r);
+    for (int r = 0; r < 16; ++r) put(r, r);
   }
   if constexpr (kVer) {
     if (diff) atomicOr(a.flags + stripe, 1u);

@@ -92,11 +92,12 @@ inline DyPlan dyadic_plan(const uint8_t* coef, int m, int k) {
 }
 
 // 16-input matrices whose first 16 rows form one 16x16 dyadic block, then one 4x4-dyadic row
-// block (gf_dyadic16.hpp; m = 20: EC16P20).
+// block (gf_dyadic16.hpp; m = 20: EC16P20), then for m = 22 two plain rows (the EC16P20L2 fused
+// encode's local parity).
 hipError_t launch_dy16(int m, MatVecMode mode, const dev::GfArgs& a, unsigned ns, hipStream_t st);
 
 inline bool dyadic16_plan(const uint8_t* coef, int m, int k) {
-  if (k != 16 || m != 20) return false;
+  if (k != 16 || (m != 20 && m != 22)) return false;
   for (int i = 0; i < 16; ++i)
     for (int j = 0; j < 16; ++j)
       if (coef[(size_t)i * 16 + j] != coef[i ^ j]) return false;
