@@ -161,3 +161,25 @@ def test_batch_encode_decode(C, n, size):
     nblk = (size + 64 * K - 5) // (64 * K - 4)
     assert list(b[:-1]) == [0xFFFFFFFF] * (n - 1) and int(b[-1]) == nblk - 1
     assert torch.equal(back[:-1], src[:-1])
+
+
+@pytest.mark.parametrize("doff", [0, 1, 4, 60, 127])
+@pytest.mark.parametrize("block_len", [4096, 64 * K])
+def test_decode_destination_alignment(C, doff, block_len):
+    """Decode writes consecutive blocks' payloads back to back; the 128-byte line across each seam
+    has one writer (crc32block.hip).  Every destination alignment, whole objects and a sub-range:
+    the payload bytes, and no byte written outside [dst, dst + to - from)."""
+    size = 7 * (block_len - 4) + 333
+    d = data(size, doff + block_len)
+    framed = torch.from_numpy(O.crc32block_encode(d, block_len)).cuda()
+    n = 3
+    for lo, hi in [(0, size), (block_len + 3, 5 * (block_len - 4) + 17), (size - 100, size)]:
+        buf = torch.full((n, size + 256), 0xA5, dtype=torch.uint8, device="cuda")
+        bad = torch.zeros(n, dtype=torch.int32, device="cuda")
+        C.decode_batch([framed.data_ptr()] * n, [buf[i].data_ptr() + doff for i in range(n)], size, bad.data_ptr(),
+                       from_=lo, to=hi, block_len=block_len)
+        assert (bad.cpu().numpy().view(np.uint32) == 0xFFFFFFFF).all()
+        h = buf.cpu().numpy()
+        for i in range(n):
+            assert np.array_equal(h[i, doff:doff + hi - lo], d[lo:hi]), (i, lo, hi)
+            assert (h[i, :doff] == 0xA5).all() and (h[i, doff + hi - lo:] == 0xA5).all(), (i, lo, hi)

@@ -43,18 +43,22 @@ int main(int argc, char** argv) {
   const int64_t pitch = (S + 255) / 256 * 256, fpitch = (flen + 255) / 256 * 256;
   // three buffer sets used in rotation: no launch finds its data in the 256 MB Infinity Cache
   constexpr int NB = 3;
-  uint8_t *pays[NB], *frms[NB];
+  uint8_t *pays[NB], *frms[NB], *seams[NB];
+  const int64_t spitch = (S + L - 5) / (L - 4) * L;  // the no-seams probe: destination blocks L apart
   uint32_t* words;
   CK(hipMalloc(&words, 4 * 4096));
   std::vector<std::vector<const uint8_t*>> ins(NB, std::vector<const uint8_t*>(n)), fins(NB, std::vector<const uint8_t*>(n));
-  std::vector<std::vector<uint8_t*>> outs(NB, std::vector<uint8_t*>(n)), fouts(NB, std::vector<uint8_t*>(n));
+  std::vector<std::vector<uint8_t*>> outs(NB, std::vector<uint8_t*>(n)), fouts(NB, std::vector<uint8_t*>(n)),
+      souts(NB, std::vector<uint8_t*>(n));
   for (int b = 0; b < NB; ++b) {
     CK(hipMalloc(&pays[b], pitch * n));
     CK(hipMalloc(&frms[b], fpitch * n));
+    CK(hipMalloc(&seams[b], spitch * n));
     fill<<<2048, 256>>>((uint32_t*)pays[b], pitch * n / 4);
     for (int i = 0; i < n; ++i) {
       ins[b][i] = pays[b] + i * pitch, outs[b][i] = frms[b] + i * fpitch;
       fins[b][i] = frms[b] + i * fpitch, fouts[b][i] = pays[b] + i * pitch;
+      souts[b][i] = seams[b] + i * spitch;
     }
   }
   uint8_t* pay = pays[0];
@@ -79,6 +83,11 @@ int main(int argc, char** argv) {
     k.to = S;
     return k;
   };
+  const auto Jseam = [&]() {  // decode into destination blocks L apart (launch<..., SEAMLESS_PROBE>)
+    cfsec::Crc32BlockJob k = J(false);
+    k.out = souts[(rot - 1) % NB].data();
+    return k;
+  };
   struct V {
     std::string name;
     std::function<void()> f;
@@ -90,15 +99,18 @@ int main(int argc, char** argv) {
       {"enc new epi R4", [&] { CK((cfsec::blk::launch<true, true, true, false, true, true, 4, true>(J(true), 0))); }, 2 * pb},
       {"enc new epi R6", [&] { CK((cfsec::blk::launch<true, true, true, false, true, true, 6, true>(J(true), 0))); }, 2 * pb},
       {"enc new epi R8", [&] { CK((cfsec::blk::launch<true, true, true, false, true, true, 8, true>(J(true), 0))); }, 2 * pb},
-      {"enc 2 blk/wg R4", [&] { CK((cfsec::blk::launch<true, true, true, false, true, true, 4, true, 2>(J(true), 0))); }, 2 * pb},
-      {"enc 2 blk/wg R3", [&] { CK((cfsec::blk::launch<true, true, true, false, true, true, 3, true, 2>(J(true), 0))); }, 2 * pb},
-      {"enc 4 blk/wg R4", [&] { CK((cfsec::blk::launch<true, true, true, false, true, true, 4, true, 4>(J(true), 0))); }, 2 * pb},
+      {"enc stride R4", [&] { CK((cfsec::blk::launch<true, true, true, false, true, true, 4, true, true>(J(true), 0))); }, 2 * pb},
+      {"enc stride R6", [&] { CK((cfsec::blk::launch<true, true, true, false, true, true, 6, true, true>(J(true), 0))); }, 2 * pb},
+      {"enc stride R8", [&] { CK((cfsec::blk::launch<true, true, true, false, true, true, 8, true, true>(J(true), 0))); }, 2 * pb},
       {"enc new epi R2", [&] { CK((cfsec::blk::launch<true, true, true, false, true, true, 2, true>(J(true), 0))); }, 2 * pb},
-      {"dec 2 blk/wg R4", [&] { CK((cfsec::blk::launch<true, true, true, false, true, true, 4, true, 2>(J(false), 0))); }, 2 * pb},
+      {"dec stride R4", [&] { CK((cfsec::blk::launch<true, true, true, false, true, true, 4, true, true>(J(false), 0))); }, 2 * pb},
+      {"dec stride R8", [&] { CK((cfsec::blk::launch<true, true, true, false, true, true, 8, true, true>(J(false), 0))); }, 2 * pb},
+      {"dec stride R8 no seams", [&] { CK((cfsec::blk::launch<true, true, true, false, true, true, 8, true, true, true>(Jseam(), 0))); }, 2 * pb},
       {"dec old epilogue", [&] { CK((cfsec::blk::launch<true, true, true, false, true, true, 4, false>(J(false), 0))); }, 2 * pb},
       {"dec new epi R4", [&] { CK((cfsec::blk::launch<true, true, true, false, true, true, 4, true>(J(false), 0))); }, 2 * pb},
       {"dec new epi R8", [&] { CK((cfsec::blk::launch<true, true, true, false, true, true, 8, true>(J(false), 0))); }, 2 * pb},
-      {"shipped (crc + store)", [&] { CK((cfsec::blk::launch<true, true>(j, 0))); }, 2 * pb},
+      {"shipped enc", [&] { CK(cfsec::launch_crc32block(J(true), 0)); }, 2 * pb},
+      {"shipped dec", [&] { CK(cfsec::launch_crc32block(J(false), 0)); }, 2 * pb},
       {"crc only (no store)", [&] { CK((cfsec::blk::launch<false, true>(j, 0))); }, pb},
       {"copy only (no crc)", [&] { CK((cfsec::blk::launch<true, false>(j, 0))); }, 2 * pb},
       {"copy, src-aligned", [&] { CK((cfsec::blk::launch<true, false, true, true>(j, 0))); }, 2 * pb},
@@ -117,7 +129,7 @@ int main(int argc, char** argv) {
       {"flat copy both+4", [&] { kcopy<4, 4><<<4096, 256>>>(pay, frm, (size_t)(pb / 16) - 1); }, 2 * pb},
       {"standalone shard crc", [&] { CK(cfsec::launch_crc32(ins[0].data(), S, n, words, 0)); }, pb},
   };
-  {  // the run kernel frames and checks exactly like the per-block kernel
+  {  // the grid-stride kernel frames exactly like the old per-block kernel
     std::vector<uint8_t> want((size_t)fpitch * n), got((size_t)fpitch * n);
     std::vector<uint32_t> w1(n), w2(n);
     cfsec::Crc32BlockJob k = j;
@@ -129,10 +141,10 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(w1.data(), words, 4 * n, hipMemcpyDeviceToHost));
     CK(hipMemset(frm, 0, fpitch * n));
     CK(hipMemset(words, 0, 4 * n));
-    CK((cfsec::blk::launch<true, true, true, false, true, true, 4, true, 2>(k, 0)));
+    CK((cfsec::blk::launch<true, true, true, false, true, true, 4, true, true>(k, 0)));
     CK(hipMemcpy(got.data(), frm, got.size(), hipMemcpyDeviceToHost));
     CK(hipMemcpy(w2.data(), words, 4 * n, hipMemcpyDeviceToHost));
-    printf("new-epilogue kernel == old kernel: framed %s, whole-shard crc %s\n", want == got ? "yes" : "NO",
+    printf("stride kernel == old kernel: framed %s, whole-shard crc %s\n", want == got ? "yes" : "NO",
            w1 == w2 ? "yes" : "NO");
   }
   hipEvent_t e0, e1;
