@@ -450,6 +450,8 @@ Status RSEngine::run_stripes(std::vector<StripeTask>& tasks, int mem) {
 }
 
 Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceContext* ctx) {
+  HostTimer whole("  run_device");
+  std::unique_ptr<HostTimer> tm(new HostTimer("    classify + acquire"));
   DeviceGuard g(ctx->device());
   if (!g.ok()) return hip_status(hipErrorInvalidDevice, "hipSetDevice");
   const int n = (int)tasks.size();
@@ -494,8 +496,12 @@ Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceCont
     if (e == CFSEC_OK) e = hip_status(hipStreamWaitEvent(lane[to], ws->ev, 0), "hipStreamWaitEvent");
     return e;
   };
+  // verify flags only where some task compares rows (a batch of pure stores skips the flag memset
+  // and read-back: ~10 us of a synchronous call)
+  bool checks = false;
+  for (StripeTask* t : tasks) checks = checks || t->plan->out.size() > (size_t)t->plan->nstore;
   if (mem == CFSEC_MEM_DEVICE) st = ctx->order_after_default(ws);
-  if (st == CFSEC_OK) st = hip_status(hipMemsetAsync(ws->dflags, 0, 4 * (size_t)n, lane[0]), "hipMemsetAsync");
+  if (st == CFSEC_OK && checks) st = hip_status(hipMemsetAsync(ws->dflags, 0, 4 * (size_t)n, lane[0]), "hipMemsetAsync");
   if (st == CFSEC_OK && nlanes > 1) st = join(0, 1);
   int next_flag = 0;
   std::vector<std::pair<StripeTask*, int>> flags;  // (task, flag word)
@@ -504,6 +510,7 @@ Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceCont
       for (size_t i = 0; i < gr.tasks.size(); ++i) flags.emplace_back(gr.tasks[i], gr.flag0 + (int)i);
   };
   int chunk = 0;
+  tm.reset(new HostTimer("    group + launch"));
   for (int ph = 0; ph < nphase && st == CFSEC_OK; ++ph) {
     if (ph > 0 && nlanes > 1) {  // a phase starts after everything of the previous one, on both lanes
       st = join(1, 0);
@@ -574,15 +581,17 @@ Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceCont
       i0 = i1;
     }
   }
+  tm.reset(new HostTimer("    sync"));
   if (st == CFSEC_OK && nlanes > 1) st = join(1, 0);
-  if (st == CFSEC_OK)
+  if (st == CFSEC_OK && checks)
     st = hip_status(hipMemcpyAsync(ws->hflags, ws->dflags, 4 * (size_t)n, hipMemcpyDeviceToHost, lane[0]),
                     "hipMemcpyAsync D2H");
   for (int l = 0; l < nlanes; ++l) {
     const Status sync = hip_status(hipStreamSynchronize(lane[l]), "hipStreamSynchronize");
     if (st == CFSEC_OK) st = sync;
   }
-  if (st == CFSEC_OK)
+  tm.reset();
+  if (st == CFSEC_OK && checks)
     for (auto& f : flags)
       if (ws->hflags[f.second] != 0 && *f.first->status == CFSEC_OK) *f.first->status = CFSEC_ERR_VERIFY;
   ctx->release(ws);
@@ -637,9 +646,11 @@ Status LrcEncoder::reconstruct_batch(cfsec_shard* shards, int n, int nbids, cons
   // each AZ's local engine over that AZ's local stripe -- planned together and run as two phases of
   // one call (one sync), in that order, as the reference runs them.
   if (!shards || !status || !bad_off || nbids < 0) return CFSEC_ERR_INVALID_ARG;
+  HostTimer whole("lrc reconstruct_batch");
   const int N = t_.n, M = t_.m, L = t_.l, AZ = t_.az_count;
   const int lsz = (N + M + L) / AZ;
   Slot slot(pool_.get());
+  std::unique_ptr<HostTimer> ph(new HostTimer("  init/fill"));
   std::vector<cfsec_shard*> stripes;
   std::vector<int> pos;
   for (int b = 0; b < nbids; ++b) {
@@ -668,12 +679,14 @@ Status LrcEncoder::reconstruct_batch(cfsec_shard* shards, int n, int nbids, cons
     return rc;
   }
   // phase 0 (1): global Reconstruct (+ global Verify) over shards [0, N+M)
+  ph.reset(new HostTimer("  global plan"));
   PlanStore gstore, lstore;
   std::vector<StripeTask> tasks;
   std::vector<int> st1(stripes.size());
   engine_->plan_reconstruct_tasks(stripes.data(), (int)stripes.size(), verify, st1.data(), 0, 0, &gstore, &tasks);
   int lphase = 1;
   for (auto& t : tasks) lphase = std::max(lphase, t.phase + 1);
+  ph.reset(new HostTimer("  local views + plan"));
   // then every AZ's local stripe (copied headers, lrcencoder.go:236-243) with the rebuilt global
   // shards' lengths already set: local Reconstruct of its bad local shards (index remap
   // lrcencoder.go:161-171) (+ local Verify)
@@ -722,6 +735,7 @@ Status LrcEncoder::reconstruct_batch(cfsec_shard* shards, int n, int nbids, cons
     const size_t v = (size_t)(tasks[t].status - st2.data());
     tasks[t].owner = (int)owner[v];
   }
+  ph.reset();
   const Status rc = engine_->run_stripes(tasks, mem);
   // per bid: a Reconstruct error (global, then local) wins over a failed Verify
   std::vector<int> local_err(stripes.size(), CFSEC_OK);

@@ -7,7 +7,10 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -25,6 +28,23 @@ using Status = int;  // cfsec_status
 
 void set_last_error(const std::string& msg);
 const char* last_error_cstr();
+
+// Host-side phase timing of the batch calls, printed to stderr when CFSEC_HOST_TIMING is set
+// (development aid: where a synchronous batch call spends its time besides the kernels).
+struct HostTimer {
+  const char* name;
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  static bool on() {
+    static const bool v = std::getenv("CFSEC_HOST_TIMING") != nullptr;
+    return v;
+  }
+  explicit HostTimer(const char* n) : name(n) {}
+  ~HostTimer() {
+    if (on())
+      std::fprintf(stderr, "cfsec host %-28s %8.1f us\n", name,
+                   std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+  }
+};
 // ec.initBadShards (encoder.go:182-188) / ec.fillFullShards (encoder.go:199-210), engine.cpp.
 Status init_bad_shards(cfsec_shard* shards, int n, const std::vector<int>& bad);
 Status fill_full_shards(cfsec_shard* shards, int n);

@@ -281,12 +281,12 @@ __device__ __forceinline__ void lane_tile(const GfArgs& a, const u32x4* tab01, c
 }
 
 // acc[r][w] ^= coef(c, r) * x[w] on plain dword arrays (the fixed-K tile's form of mac_row).
-template <int M>
-__device__ __forceinline__ void mac_row_k(uint32_t (&acc)[M][4], const uint32_t (&x)[4],
+template <int M, int W = 4>
+__device__ __forceinline__ void mac_row_k(uint32_t (&acc)[M][W], const uint32_t (&x)[W],
                                           const u32x4* __restrict__ tq, const uint32_t* __restrict__ t2p) {
-  uint32_t s0[4], s1[4], s2[4];
+  uint32_t s0[W], s1[W], s2[W];
 #pragma unroll
-  for (int w = 0; w < 4; ++w) {
+  for (int w = 0; w < W; ++w) {
     s0[w] = x[w] & 0x07070707u;
     s1[w] = (x[w] >> 3) & 0x07070707u;
     s2[w] = (x[w] >> 6) & 0x03030303u;
@@ -296,7 +296,7 @@ __device__ __forceinline__ void mac_row_k(uint32_t (&acc)[M][4], const uint32_t 
     const u32x4 q = tq[r];
     const uint32_t t2 = t2p[r];
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
+    for (int w = 0; w < W; ++w) {
       const uint32_t p0 = __builtin_amdgcn_perm(q.y, q.x, s0[w]);
       const uint32_t p1 = __builtin_amdgcn_perm(q.w, q.z, s1[w]);
       const uint32_t p2 = __builtin_amdgcn_perm(0u, t2, s2[w]);

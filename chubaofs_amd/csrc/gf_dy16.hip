@@ -5,29 +5,34 @@
 #include "gf_dyadic16.hpp"
 #include "gf_launch.hpp"
 
+#ifndef CFSEC_DY16_W
+#define CFSEC_DY16_W 2  // dwords per lane: 8-byte lane chunks
+#endif
+
 namespace cfsec {
 
-template <int M, int R4, int E, MatVecMode MODE>
+template <int M, int R4, int E, MatVecMode MODE, int W>
 __global__ __launch_bounds__(256) void gf_dy16_kernel(const dev::GfArgs a) {
-  dev::matvec_dy16<M, R4, E, MODE>(a);
+  dev::matvec_dy16<M, R4, E, MODE, true, W>(a);
 }
 
 namespace {
-template <int M, int R4, int E>
+template <int M, int R4, int E, int W>
 hipError_t launch_one(MatVecMode mode, const dev::GfArgs& a, unsigned ns, hipStream_t st) {
-  const unsigned tiles = (unsigned)((a.len + 4095) / 4096);
+  constexpr uint64_t tile = 256 * 4 * W;
+  const unsigned tiles = (unsigned)((a.len + tile - 1) / tile);
   if (mode == MatVecMode::kVerify)
-    hipLaunchKernelGGL((gf_dy16_kernel<M, R4, E, MatVecMode::kVerify>), dim3(tiles, ns), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((gf_dy16_kernel<M, R4, E, MatVecMode::kVerify, W>), dim3(tiles, ns), dim3(256), 0, st, a);
   else
-    hipLaunchKernelGGL((gf_dy16_kernel<M, R4, E, MatVecMode::kStore>), dim3(tiles, ns), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((gf_dy16_kernel<M, R4, E, MatVecMode::kStore, W>), dim3(tiles, ns), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 }  // namespace
 
 hipError_t launch_dy16(int m, MatVecMode mode, const dev::GfArgs& a, unsigned ns, hipStream_t st) {
   switch (m) {
-    case 20: return launch_one<20, 1, 0>(mode, a, ns, st);  // EC16P20 global parity
-    case 22: return launch_one<22, 1, 2>(mode, a, ns, st);  // EC16P20L2 fused: + 2 local rows
+    case 20: return launch_one<20, 1, 0, CFSEC_DY16_W>(mode, a, ns, st);  // EC16P20 global parity
+    case 22: return launch_one<22, 1, 2, CFSEC_DY16_W>(mode, a, ns, st);  // EC16P20L2 fused: + 2 local rows
     default: return hipErrorInvalidValue;
   }
 }

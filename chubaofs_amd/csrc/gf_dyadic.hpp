@@ -72,13 +72,17 @@ __device__ __forceinline__ void build_dy_tables(const uint8_t* coef, u32x4* tab0
   }
 }
 
-struct Sel {
-  uint32_t s0[4], s1[4], s2[4];
+// v_perm selectors of W dwords per lane (W = 4: 16 bytes, the shipped width; W = 2: 8 bytes)
+template <int W = 4>
+struct SelW {
+  uint32_t s0[W], s1[W], s2[W];
 };
+using Sel = SelW<4>;
 
-__device__ __forceinline__ void selectors(const uint32_t (&x)[4], Sel& s) {
+template <int W>
+__device__ __forceinline__ void selectors(const uint32_t (&x)[W], SelW<W>& s) {
 #pragma unroll
-  for (int w = 0; w < 4; ++w) {
+  for (int w = 0; w < W; ++w) {
     s.s0[w] = x[w] & 0x07070707u;
     s.s1[w] = (x[w] >> 3) & 0x07070707u;
     s.s2[w] = (x[w] >> 6) & 0x03030303u;
@@ -86,12 +90,16 @@ __device__ __forceinline__ void selectors(const uint32_t (&x)[4], Sel& s) {
 }
 
 // The three partial lookups of coefficient q times the multiplicand whose selectors are s.
-struct Prod {
-  uint32_t a[4], b[4], c[4];
+template <int W = 4>
+struct ProdW {
+  uint32_t a[W], b[W], c[W];
 };
-__device__ __forceinline__ void lookups(const u32x4 q, uint32_t t2, const Sel& s, Prod& p) {
+using Prod = ProdW<4>;
+
+template <int W>
+__device__ __forceinline__ void lookups(const u32x4 q, uint32_t t2, const SelW<W>& s, ProdW<W>& p) {
 #pragma unroll
-  for (int w = 0; w < 4; ++w) {
+  for (int w = 0; w < W; ++w) {
     p.a[w] = __builtin_amdgcn_perm(q.y, q.x, s.s0[w]);
     p.b[w] = __builtin_amdgcn_perm(q.w, q.z, s.s1[w]);
     p.c[w] = __builtin_amdgcn_perm(0u, t2, s.s2[w]);
@@ -132,69 +140,71 @@ __device__ __forceinline__ void dy_col2(uint32_t (&acc)[2 * MB][4], const uint32
 }
 
 // B = 4, all row blocks of one column block.
-template <int MB, bool PIN = true>
-__device__ __forceinline__ void dy_col4(uint32_t (&acc)[4 * MB][4], const uint32_t (&x0)[4],
-                                        const uint32_t (&x1)[4], const uint32_t (&x2)[4],
-                                        const uint32_t (&x3v)[4], const u32x4* tq, const uint32_t* t2p,
+template <int MB, bool PIN = true, int W = 4>
+__device__ __forceinline__ void dy_col4(uint32_t (&acc)[4 * MB][W], const uint32_t (&x0)[W],
+                                        const uint32_t (&x1)[W], const uint32_t (&x2)[W],
+                                        const uint32_t (&x3v)[W], const u32x4* tq, const uint32_t* t2p,
                                         int stride) {
-  uint32_t u[4], s[4], v[4];
+  uint32_t u[W], s[W], v[W];
 #pragma unroll
-  for (int w = 0; w < 4; ++w) {
+  for (int w = 0; w < W; ++w) {
     s[w] = x1[w] ^ x3v[w];
     v[w] = x2[w] ^ x3v[w];
     u[w] = x3(x0[w], x2[w], s[w]);  // x0^x1^x2^x3
   }
-  Sel su, ss, sv, sy;
+  SelW<W> su, ss, sv, sy;
 #pragma unroll
   for (int rb = 0; rb < MB; ++rb) {
     const u32x4* q = tq + rb * stride;
     const uint32_t* t = t2p + rb * stride;
-    uint32_t ps[4], ps2[4], c0[4], c1[4];
+    uint32_t ps[W], ps2[W], c0[W], c1[W];
     {
-      Prod p;
+      ProdW<W> p;
       selectors(s, ss);
       lookups(q[2], t[2], ss, p);  // (h0^h1) s
 #pragma unroll
-      for (int w = 0; w < 4; ++w) ps[w] = x3(p.a[w], p.b[w], p.c[w]);
+      for (int w = 0; w < W; ++w) ps[w] = x3(p.a[w], p.b[w], p.c[w]);
       lookups(q[5], t[5], ss, p);  // (h2^h3) s
 #pragma unroll
-      for (int w = 0; w < 4; ++w) ps2[w] = x3(p.a[w], p.b[w], p.c[w]);
+      for (int w = 0; w < W; ++w) ps2[w] = x3(p.a[w], p.b[w], p.c[w]);
       if constexpr (PIN) {
-        asm volatile("" : "+v"(ps[0]), "+v"(ps[1]), "+v"(ps[2]), "+v"(ps[3]), "+v"(ps2[0]), "+v"(ps2[1]), "+v"(ps2[2]), "+v"(ps2[3]));
+#pragma unroll
+        for (int w = 0; w < W; ++w) asm volatile("" : "+v"(ps[w]), "+v"(ps2[w]));
         __builtin_amdgcn_sched_barrier(0);
       }
-      Prod py, p6, p7;
+      ProdW<W> py, p6, p7;
       selectors(x3v, sy);
       selectors(v, sv);
       lookups(q[8], t[8], sy, py);  // (g0^g1) x3
       lookups(q[6], t[6], sv, p6);  // g0 v
       lookups(q[7], t[7], sv, p7);  // g1 v
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {
+      for (int w = 0; w < W; ++w) {
         const uint32_t qy = x3(py.a[w], py.b[w], py.c[w]);
         c0[w] = x3(p6.a[w], p6.b[w], p6.c[w]) ^ qy;
         c1[w] = x3(p7.a[w], p7.b[w], p7.c[w]) ^ qy;
       }
     }
     if constexpr (PIN) {
-      asm volatile("" : "+v"(c0[0]), "+v"(c0[1]), "+v"(c0[2]), "+v"(c0[3]), "+v"(c1[0]), "+v"(c1[1]), "+v"(c1[2]), "+v"(c1[3]));
+#pragma unroll
+      for (int w = 0; w < W; ++w) asm volatile("" : "+v"(c0[w]), "+v"(c1[w]));
       __builtin_amdgcn_sched_barrier(0);
     }
     selectors(u, su);
     // one output at a time: out_j ^= h_j u ^ (shared s term) ^ (shared x3/v term)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      Prod p;
+      ProdW<W> p;
       const int qi = j < 2 ? j : j + 1;  // h0, h1, h2, h3 live at slots 0, 1, 3, 4
       lookups(q[qi], t[qi], su, p);
       const uint32_t* sh = j < 2 ? ps : ps2;
       const uint32_t* cc = (j & 1) ? c1 : c0;
 #pragma unroll
-      for (int w = 0; w < 4; ++w)
+      for (int w = 0; w < W; ++w)
         acc[4 * rb + j][w] = x3(x3(acc[4 * rb + j][w], p.a[w], p.b[w]), x3(p.c[w], sh[w], cc[w]), 0u);
       if constexpr (PIN) {
-        asm volatile("" : "+v"(acc[4 * rb + j][0]), "+v"(acc[4 * rb + j][1]), "+v"(acc[4 * rb + j][2]),
-                     "+v"(acc[4 * rb + j][3]));
+#pragma unroll
+        for (int w = 0; w < W; ++w) asm volatile("" : "+v"(acc[4 * rb + j][w]));
         __builtin_amdgcn_sched_barrier(0);
       }
     }

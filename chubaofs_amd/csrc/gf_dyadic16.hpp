@@ -51,32 +51,69 @@ __device__ __forceinline__ void build_dy16_tables(const uint8_t* coef, u32x4* ta
   }
 }
 
-using Vec = uint32_t[4];
-using Vec4 = uint32_t[4][4];
+// Lane chunks of W dwords (W = 4: 16 bytes per lane; W = 2: 8 bytes, half the registers)
+template <int W>
+using VecW4 = uint32_t[4][W];
 
-__device__ __forceinline__ Vec4& v4(uint32_t (&a)[4], int = 0) { return reinterpret_cast<Vec4&>(a); }
+template <int W>
+__device__ __forceinline__ VecW4<W>& v4(uint32_t (&a)[W]) { return reinterpret_cast<VecW4<W>&>(a); }
 
 // acc (4 rows) ^= leaf * [v[0..3]]
-template <bool PIN>
-__device__ __forceinline__ void leaf4(Vec4& acc, Vec4& v, const u32x4* tab01, const uint32_t* tab2, int leaf) {
+template <bool PIN, int W>
+__device__ __forceinline__ void leaf4(VecW4<W>& acc, VecW4<W>& v, const u32x4* tab01, const uint32_t* tab2, int leaf) {
   dy_col4<1, PIN>(acc, v[0], v[1], v[2], v[3], tab01 + leaf * 9, tab2 + leaf * 9, 0);
 }
 
-template <bool PIN>
-__device__ __forceinline__ void xor_into(Vec4& dst, const Vec4& src) {
+template <int W>
+__device__ __forceinline__ void xor_into(VecW4<W>& dst, const VecW4<W>& src) {
 #pragma unroll
   for (int r = 0; r < 4; ++r)
 #pragma unroll
-    for (int w = 0; w < 4; ++w) dst[r][w] ^= src[r][w];
+    for (int w = 0; w < W; ++w) dst[r][w] ^= src[r][w];
 }
 
-// Kernel body: 16 inputs, M = 16 + 4 R4 + E outputs; 256-thread workgroups, each lane one 16-byte
-// chunk of every row (tile 4 KiB), grid (tiles, stripes).  Output rows 16.. (the 4x4 row blocks,
-// then the E plain rows) are computed first, from the original inputs, and stored one group at a
-// time from acc[16..]; then the 16x16 block into acc[0..15].
-template <int M, int R4, int E, MatVecMode MODE, bool PIN = true>
+// W-dword lane chunk loads and stores (16 B: ld16 / st16_out; 8 B: the same on dwordx2)
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef u32x2 u32x2_ua __attribute__((aligned(1)));
+
+template <int W>
+__device__ __forceinline__ void ld_lane(const uint8_t* p, bool full, size_t rem, uint32_t (&x)[W]) {
+  if constexpr (W == 4) {
+    const u32x4 v = full ? ld16<true>(p) : ld_tail(p, rem);
+    x[0] = v.x, x[1] = v.y, x[2] = v.z, x[3] = v.w;
+  } else {
+    static_assert(W == 2, "lane chunk of 2 or 4 dwords");
+    if (full) {
+      const u32x2 v = __builtin_nontemporal_load(reinterpret_cast<const u32x2_ua*>(p));
+      x[0] = v.x, x[1] = v.y;
+    } else {
+      const u32x4 v = ld_tail(p, rem < 8 ? rem : 8);
+      x[0] = v.x, x[1] = v.y;
+    }
+  }
+}
+
+template <int W>
+__device__ __forceinline__ void st_lane(uint8_t* p, bool full, size_t rem, const uint32_t (&x)[W]) {
+  if constexpr (W == 4) {
+    const u32x4 v = u32x4{x[0], x[1], x[2], x[3]};
+    if (full) st16_out<true>(p, v);
+    else st_tail(p, v, rem);
+  } else if (full) {
+    asm volatile("global_store_dwordx2 %0, %1, off nt" ::"v"(p), "v"(u32x2{x[0], x[1]}) : "memory");
+  } else {
+    st_tail(p, u32x4{x[0], x[1], 0u, 0u}, rem < 8 ? rem : 8);
+  }
+}
+
+// Kernel body: 16 inputs, M = 16 + 4 R4 + E outputs; 256-thread workgroups, each lane one chunk of
+// W dwords of every row (tile 256 * 4W bytes), grid (tiles, stripes).  Output rows 16.. (the 4x4
+// row blocks, then the E plain rows) are computed first, from the original inputs, and stored one
+// group at a time from acc[16..]; then the 16x16 block into acc[0..15].
+template <int M, int R4, int E, MatVecMode MODE, bool PIN = true, int W = 4>
 __device__ __forceinline__ void matvec_dy16(const GfArgs& a) {
   constexpr int K = 16, N4 = R4 * 4 * 9;
+  constexpr uint32_t kLane = 4 * W;
   static_assert(M == 16 + 4 * R4 + E, "dyadic-16 shape");
   constexpr bool kVer = MODE == MatVecMode::kVerify;
   __shared__ u32x4 tab01[kDy16Leaves + N4 + K * E];
@@ -87,7 +124,7 @@ __device__ __forceinline__ void matvec_dy16(const GfArgs& a) {
   const uint32_t stripe = blockIdx.y, tile = blockIdx.x;
   const size_t ts = a.sstride ? 0 : (size_t)stripe;
   const int64_t sbase = (int64_t)stripe * a.sstride;
-  const uint32_t off = tile * (uint32_t)(256 * kLaneBytes) + (uint32_t)threadIdx.x * kLaneBytes;
+  const uint32_t off = tile * (256u * kLane) + (uint32_t)threadIdx.x * kLane;
   const uint8_t* row[K + M];
 #pragma unroll
   for (int c = 0; c < K; ++c) row[c] = a.ptr[ts * K + c] + sbase;
@@ -96,23 +133,20 @@ __device__ __forceinline__ void matvec_dy16(const GfArgs& a) {
   __builtin_amdgcn_sched_barrier(0);
 
   const uint64_t slen = stripe_len(a, stripe);
-  const bool full = (uint64_t)off + kLaneBytes <= slen;
+  const bool full = (uint64_t)off + kLane <= slen;
   const size_t rem = off < slen ? (size_t)(slen - off) : 0;
   uint32_t diff = 0;
   if (full || rem) {
     // rows 16.. share registers: the 4x4 row blocks, stored, then the plain rows in the same slots
     constexpr int NA = 16 + (4 * R4 > E ? 4 * R4 : E);
-    uint32_t acc[NA][4];
+    uint32_t acc[NA][W];
 #pragma unroll
     for (int r = 0; r < NA; ++r)
 #pragma unroll
-      for (int w = 0; w < 4; ++w) acc[r][w] = 0u;
-    uint32_t x[K][4];
+      for (int w = 0; w < W; ++w) acc[r][w] = 0u;
+    uint32_t x[K][W];
 #pragma unroll
-    for (int c = 0; c < K; ++c) {
-      const u32x4 v = full ? ld16<true>(row[c] + off) : ld_tail(row[c] + off, rem);
-      x[c][0] = v.x, x[c][1] = v.y, x[c][2] = v.z, x[c][3] = v.w;
-    }
+    for (int c = 0; c < K; ++c) ld_lane<W>(row[c] + off, full, rem, x[c]);
     const auto sb = [&]() {
       if constexpr (PIN) __builtin_amdgcn_sched_barrier(0);
     };
@@ -120,14 +154,13 @@ __device__ __forceinline__ void matvec_dy16(const GfArgs& a) {
     // 16x16 block's temporaries
     const auto put = [&](int r, int ai) {
       uint8_t* p = const_cast<uint8_t*>(row[K + r]) + off;
-      const u32x4 v = u32x4{acc[ai][0], acc[ai][1], acc[ai][2], acc[ai][3]};
       if constexpr (kVer) {
-        const u32x4 d = v ^ (full ? ld16<true>(p) : ld_tail(p, rem));
-        diff |= d.x | d.y | d.z | d.w;
-      } else if (full) {
-        st16_out<true>(p, v);
+        uint32_t y[W];
+        ld_lane<W>(p, full, rem, y);
+#pragma unroll
+        for (int w = 0; w < W; ++w) diff |= y[w] ^ acc[ai][w];
       } else {
-        st_tail(p, v, rem);
+        st_lane<W>(p, full, rem, acc[ai]);
       }
     };
     sb();
@@ -135,7 +168,7 @@ __device__ __forceinline__ void matvec_dy16(const GfArgs& a) {
     if constexpr (R4 > 0) {
       const u32x4* tq = tab01 + kDy16Leaves;
       const uint32_t* tt = tab2 + kDy16Leaves;
-      auto& racc = reinterpret_cast<uint32_t(&)[4 * R4][4]>(acc[16]);
+      auto& racc = reinterpret_cast<uint32_t(&)[4 * R4][W]>(acc[16]);
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb) {
         dy_col4<R4, PIN>(racc, x[4 * cb], x[4 * cb + 1], x[4 * cb + 2], x[4 * cb + 3], tq + cb * 9, tt + cb * 9, 4 * 9);
@@ -147,17 +180,19 @@ __device__ __forceinline__ void matvec_dy16(const GfArgs& a) {
 #pragma unroll
       for (int r = 16; r < NA; ++r)
 #pragma unroll
-        for (int w = 0; w < 4; ++w) acc[r][w] = 0u;
+        for (int w = 0; w < W; ++w) acc[r][w] = 0u;
     }
     if constexpr (E > 0) {
-      auto& eacc = reinterpret_cast<uint32_t(&)[E][4]>(acc[16]);
+      auto& eacc = reinterpret_cast<uint32_t(&)[E][W]>(acc[16]);
       constexpr int ND = kDy16Leaves + N4;
 #pragma unroll
       for (int c = 0; c < K; ++c) {
         mac_row_k<E>(eacc, x[c], tab01 + ND + c * E, tab2 + ND + c * E);
         if constexpr (PIN)
 #pragma unroll
-          for (int e = 0; e < E; ++e) asm volatile("" : "+v"(eacc[e][0]), "+v"(eacc[e][1]), "+v"(eacc[e][2]), "+v"(eacc[e][3]));
+          for (int e = 0; e < E; ++e)
+#pragma unroll
+            for (int w = 0; w < W; ++w) asm volatile("" : "+v"(eacc[e][w]));
         sb();
       }
 #pragma unroll
@@ -168,49 +203,49 @@ __device__ __forceinline__ void matvec_dy16(const GfArgs& a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j)
 #pragma unroll
-      for (int w = 0; w < 4; ++w) x[j][w] ^= x[j + 8][w];
+      for (int w = 0; w < W; ++w) x[j][w] ^= x[j + 8][w];
     // rows 8..15 = C Y, C = A + B (leaves 3..5): the 8x8 recursion on Y, rows 8..15 start at zero
-    leaf4<PIN>(v4(acc[12]), v4(x[12]), tab01, tab2, 4);  // C_c Y_hi
+    leaf4<PIN, W>(v4<W>(acc[12]), v4<W>(x[12]), tab01, tab2, 4);  // C_c Y_hi
 #pragma unroll
     for (int r = 8; r < 12; ++r)
 #pragma unroll
-      for (int w = 0; w < 4; ++w) acc[r][w] = acc[r + 4][w];
+      for (int w = 0; w < W; ++w) acc[r][w] = acc[r + 4][w];
 #pragma unroll
     for (int j = 8; j < 12; ++j)
 #pragma unroll
-      for (int w = 0; w < 4; ++w) x[j][w] ^= x[j + 4][w];  // Y_lo + Y_hi (Y is dead after this)
-    leaf4<PIN>(v4(acc[8]), v4(x[8]), tab01, tab2, 3);    // C_a
-    leaf4<PIN>(v4(acc[12]), v4(x[8]), tab01, tab2, 5);   // C_b
+      for (int w = 0; w < W; ++w) x[j][w] ^= x[j + 4][w];  // Y_lo + Y_hi (Y is dead after this)
+    leaf4<PIN, W>(v4<W>(acc[8]), v4<W>(x[8]), tab01, tab2, 3);    // C_a
+    leaf4<PIN, W>(v4<W>(acc[12]), v4<W>(x[8]), tab01, tab2, 5);   // C_b
     // rows 0..7 = C Y as well, then += A S; rows 8..15 += B S
 #pragma unroll
     for (int r = 0; r < 8; ++r)
 #pragma unroll
-      for (int w = 0; w < 4; ++w) acc[r][w] = acc[r + 8][w];
+      for (int w = 0; w < W; ++w) acc[r][w] = acc[r + 8][w];
     {
-      uint32_t tmp[4][4];
+      uint32_t tmp[4][W];
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int w = 0; w < 4; ++w) tmp[r][w] = 0u;
-      leaf4<PIN>(tmp, v4(x[4]), tab01, tab2, 1);  // A_c S_hi
-      xor_into<PIN>(v4(acc[0]), tmp);
-      xor_into<PIN>(v4(acc[4]), tmp);
+        for (int w = 0; w < W; ++w) tmp[r][w] = 0u;
+      leaf4<PIN, W>(tmp, v4<W>(x[4]), tab01, tab2, 1);  // A_c S_hi
+      xor_into<W>(v4<W>(acc[0]), tmp);
+      xor_into<W>(v4<W>(acc[4]), tmp);
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int w = 0; w < 4; ++w) tmp[r][w] = 0u;
-      leaf4<PIN>(tmp, v4(x[4]), tab01, tab2, 7);  // B_c S_hi
-      xor_into<PIN>(v4(acc[8]), tmp);
-      xor_into<PIN>(v4(acc[12]), tmp);
+        for (int w = 0; w < W; ++w) tmp[r][w] = 0u;
+      leaf4<PIN, W>(tmp, v4<W>(x[4]), tab01, tab2, 7);  // B_c S_hi
+      xor_into<W>(v4<W>(acc[8]), tmp);
+      xor_into<W>(v4<W>(acc[12]), tmp);
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int w = 0; w < 4; ++w) x[j][w] ^= x[j + 4][w];  // S_lo + S_hi, shared by A and B
-    leaf4<PIN>(v4(acc[0]), v4(x[0]), tab01, tab2, 0);   // A_a
-    leaf4<PIN>(v4(acc[4]), v4(x[0]), tab01, tab2, 2);   // A_b
-    leaf4<PIN>(v4(acc[8]), v4(x[0]), tab01, tab2, 6);   // B_a
-    leaf4<PIN>(v4(acc[12]), v4(x[0]), tab01, tab2, 8);  // B_b
+      for (int w = 0; w < W; ++w) x[j][w] ^= x[j + 4][w];  // S_lo + S_hi, shared by A and B
+    leaf4<PIN, W>(v4<W>(acc[0]), v4<W>(x[0]), tab01, tab2, 0);   // A_a
+    leaf4<PIN, W>(v4<W>(acc[4]), v4<W>(x[0]), tab01, tab2, 2);   // A_b
+    leaf4<PIN, W>(v4<W>(acc[8]), v4<W>(x[0]), tab01, tab2, 6);   // B_a
+    leaf4<PIN, W>(v4<W>(acc[12]), v4<W>(x[0]), tab01, tab2, 8);  // B_b
 #pragma unroll
     for (int r = 0; r < 16; ++r) put(r, r);
   }
