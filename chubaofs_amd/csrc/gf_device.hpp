@@ -138,6 +138,39 @@ __device__ __forceinline__ void st_tail(uint8_t* p, u32x4 v, size_t rem) {
     if ((size_t)i < rem) p[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
 }
 
+// Full lane chunks of LW dwords (16 or 8 bytes) for the fixed-K and 16x16-dyadic kernels.
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef u32x2 u32x2_ua __attribute__((aligned(1)));
+
+template <int LW, bool NT>
+__device__ __forceinline__ void ld_chunk(const uint8_t* p, uint32_t (&x)[LW]) {
+  static_assert(LW == 2 || LW == 4, "lane chunk of 2 or 4 dwords");
+  if constexpr (LW == 4) {
+    const u32x4 v = ld16<NT>(p);
+    x[0] = v.x, x[1] = v.y, x[2] = v.z, x[3] = v.w;
+  } else {
+    const u32x2 v = NT ? __builtin_nontemporal_load(reinterpret_cast<const u32x2_ua*>(p))
+                       : *reinterpret_cast<const u32x2_ua*>(p);
+    x[0] = v.x, x[1] = v.y;
+  }
+}
+
+template <int LW, bool NTS>
+__device__ __forceinline__ void st_chunk(uint8_t* p, const uint32_t (&x)[LW]) {
+  if constexpr (LW == 4) {
+    st16_out<NTS>(p, u32x4{x[0], x[1], x[2], x[3]});
+  } else if constexpr (NTS) {
+    asm volatile("global_store_dwordx2 %0, %1, off nt" ::"v"(p), "v"(u32x2{x[0], x[1]}) : "memory");
+  } else {
+    *reinterpret_cast<u32x2_ua*>(p) = u32x2{x[0], x[1]};
+  }
+}
+
+// Lane chunk of the fixed-K kernel for K inputs and M outputs per wave: 16 bytes, or 8 where the
+// wave holds many output rows -- K + M chunks of accumulators and inputs at 16 B per lane need
+// 130-210 VGPRs for M >= 10 (2-3 waves per SIMD), at 8 B half of that.
+constexpr int fixed_lane_dwords(int K, int M) { return M >= 10 ? 2 : 4; }
+
 // Product tables of one coefficient:
 //   t01 = {T0[0..3], T0[4..7], T1[0..3], T1[4..7]},  t2 = T2[0..3]
 // with T0[e] = coef*e, T1[e] = coef*(e<<3), T2[e] = coef*(e<<6).
@@ -308,14 +341,14 @@ __device__ __forceinline__ void mac_row_k(uint32_t (&acc)[M][W], const uint32_t 
 // Two input rows at once: acc ^= coef(a, r)*xa ^ coef(b, r)*xb.  The six table lookups per output
 // dword fold into acc with three 3-input XORs (v_bitop3_b32 0x96) instead of four XOR ops for
 // two single rows: 9 VALU ops per (output, dword, row pair) instead of 10.
-template <int M>
-__device__ __forceinline__ void mac_pair_k(uint32_t (&acc)[M][4], const uint32_t (&xa)[4],
-                                           const uint32_t (&xb)[4], const u32x4* __restrict__ tqa,
+template <int M, int W = 4>
+__device__ __forceinline__ void mac_pair_k(uint32_t (&acc)[M][W], const uint32_t (&xa)[W],
+                                           const uint32_t (&xb)[W], const u32x4* __restrict__ tqa,
                                            const uint32_t* __restrict__ t2a, const u32x4* __restrict__ tqb,
                                            const uint32_t* __restrict__ t2b) {
-  uint32_t a0[4], a1[4], a2[4], b0[4], b1[4], b2[4];
+  uint32_t a0[W], a1[W], a2[W], b0[W], b1[W], b2[W];
 #pragma unroll
-  for (int w = 0; w < 4; ++w) {
+  for (int w = 0; w < W; ++w) {
     a0[w] = xa[w] & 0x07070707u;
     a1[w] = (xa[w] >> 3) & 0x07070707u;
     a2[w] = (xa[w] >> 6) & 0x03030303u;
@@ -328,7 +361,7 @@ __device__ __forceinline__ void mac_pair_k(uint32_t (&acc)[M][4], const uint32_t
     const u32x4 qa = tqa[r], qb = tqb[r];
     const uint32_t ta = t2a[r], tb = t2b[r];
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
+    for (int w = 0; w < W; ++w) {
       const uint32_t u = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_perm(qa.y, qa.x, a0[w]),
                                                      __builtin_amdgcn_perm(qa.w, qa.z, a1[w]),
                                                      __builtin_amdgcn_perm(0u, ta, a2[w]), 0x96);
@@ -348,7 +381,7 @@ __device__ __forceinline__ void mac_pair_k(uint32_t (&acc)[M][4], const uint32_t
 // VGPRs for K=12, M=4: one or two waves per SIMD), so each row ends by pinning the accumulators
 // (empty asm) behind a sched_barrier, and the row pointers (uniform: SGPR bases, 32-bit lane
 // offsets) are loaded once up front.  tools/gf_pipe.hip measured the effect.
-template <int K, int M, int MT, MatVecMode MODE, int D, bool NTL, bool NTS, bool PAIR = true>
+template <int K, int M, int MT, MatVecMode MODE, int D, bool NTL, bool NTS, bool PAIR = true, int LW = 4>
 __device__ __forceinline__ void lane_tile_k(int m, int nstore, const u32x4* tab01, const uint32_t* tab2,
                                             const uint8_t* const* in, uint8_t* const* out, int og,
                                             int64_t sbase, uint32_t loff, uint32_t& diff) {
@@ -365,24 +398,21 @@ __device__ __forceinline__ void lane_tile_k(int m, int nstore, const u32x4* tab0
   for (int r = 0; r < R - K; ++r) row[K + r] = out[og + r < m ? og + r : og] + sbase;
   __builtin_amdgcn_sched_barrier(0);
 
-  uint32_t acc[M][4];
+  uint32_t acc[M][LW];
 #pragma unroll
   for (int r = 0; r < M; ++r)
 #pragma unroll
-    for (int w = 0; w < 4; ++w) acc[r][w] = 0u;
-  uint32_t x[R][4];
+    for (int w = 0; w < LW; ++w) acc[r][w] = 0u;
+  uint32_t x[R][LW];
   const auto load = [&](int c) {
     if (c >= K && (og + (c - K) >= m || og + (c - K) < nstore)) return;  // padding / stored row
-    const u32x4 v = ld16<NTL>(row[c] + loff);
-    x[c][0] = v.x;
-    x[c][1] = v.y;
-    x[c][2] = v.z;
-    x[c][3] = v.w;
+    ld_chunk<LW, NTL>(row[c] + loff, x[c]);
   };
   const auto pin = [&]() {
 #pragma unroll
     for (int r = 0; r < M; ++r)
-      asm volatile("" : "+v"(acc[r][0]), "+v"(acc[r][1]), "+v"(acc[r][2]), "+v"(acc[r][3]));
+#pragma unroll
+      for (int w = 0; w < LW; ++w) asm volatile("" : "+v"(acc[r][w]));
   };
 #pragma unroll
   for (int c = 0; c < D && c < R; ++c) load(c);
@@ -418,7 +448,8 @@ __device__ __forceinline__ void lane_tile_k(int m, int nstore, const u32x4* tab0
     __builtin_amdgcn_sched_barrier(0);
     if (og + (c - K) < m && og + (c - K) >= nstore) {
       const int r = c - K;
-      diff |= (acc[r][0] ^ x[c][0]) | (acc[r][1] ^ x[c][1]) | (acc[r][2] ^ x[c][2]) | (acc[r][3] ^ x[c][3]);
+#pragma unroll
+      for (int w = 0; w < LW; ++w) diff |= acc[r][w] ^ x[c][w];
     }
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -427,18 +458,23 @@ __device__ __forceinline__ void lane_tile_k(int m, int nstore, const u32x4* tab0
     for (int r = 0; r < M; ++r) {
       if (og + r < m && og + r < nstore) {
         uint8_t* p = out[og + r] + sbase + loff;
-        u32x4 v = u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
-        if constexpr (MODE == MatVecMode::kAccum) v ^= ld16<NTL>(p);
-        st16_out<NTS>(p, v);
+        if constexpr (MODE == MatVecMode::kAccum) {
+          uint32_t y[LW];
+          ld_chunk<LW, NTL>(p, y);
+#pragma unroll
+          for (int w = 0; w < LW; ++w) acc[r][w] ^= y[w];
+        }
+        st_chunk<LW, NTS>(p, acc[r]);
       }
     }
   }
 }
 
 // Kernel body for a compile-time input count (a.k == K, a.len < 4 GiB): 256-thread workgroups,
-// one 16-B chunk per lane, tile = (256/OS)*16 bytes of every row, grid (tiles, stripes);
-// otherwise as matvec below.
-template <int K, int M, MatVecMode MODE, int D, int OS, bool NTL = true, bool NTS = true, bool PAIR = true>
+// one chunk of LW dwords per lane, tile = (256/OS)*4*LW bytes of every row, grid (tiles,
+// stripes); otherwise as matvec below.
+template <int K, int M, MatVecMode MODE, int D, int OS, bool NTL = true, bool NTS = true, bool PAIR = true,
+          int LW = 4>
 __device__ __forceinline__ void matvec_k(const GfArgs& a) {
   constexpr int MT = M * OS;
   __shared__ u32x4 tab01[K * MT];
@@ -449,7 +485,8 @@ __device__ __forceinline__ void matvec_k(const GfArgs& a) {
   const int wave = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
   const int og = (wave % OS) * M;
   const int cw = wave / OS;
-  constexpr uint32_t kTile = uint32_t(kThreads / OS) * kLaneBytes;
+  constexpr uint32_t kLB = 4 * LW;  // bytes per lane chunk
+  constexpr uint32_t kTile = uint32_t(kThreads / OS) * kLB;
   // 2-D grid (x: tiles of a stripe, y: stripes): a division of blockIdx.x would expand to VALU
   // code and drag the row pointers into VGPRs
   const uint32_t stripe = blockIdx.y;
@@ -458,13 +495,13 @@ __device__ __forceinline__ void matvec_k(const GfArgs& a) {
   const int64_t sbase = (int64_t)stripe * a.sstride;
   const uint8_t* const* in = a.ptr + tstripe * K;
   uint8_t* const* out = const_cast<uint8_t* const*>(a.ptr + (size_t)a.tab * K + tstripe * a.m);
-  const uint32_t off = tile * kTile + (uint32_t)(cw * 64 + lane) * kLaneBytes;
+  const uint32_t off = tile * kTile + (uint32_t)(cw * 64 + lane) * kLB;
   const uint64_t len = stripe_len(a, stripe);
   uint32_t diff = 0;
   if (og < (int)a.m) {
-    if ((uint64_t)off + kLaneBytes <= len)
-      lane_tile_k<K, M, MT, MODE, D, NTL, NTS, PAIR>((int)a.m, (int)a.nstore, tab01, tab2, in, out, og, sbase, off,
-                                                     diff);
+    if ((uint64_t)off + kLB <= len)
+      lane_tile_k<K, M, MT, MODE, D, NTL, NTS, PAIR, LW>((int)a.m, (int)a.nstore, tab01, tab2, in, out, og, sbase,
+                                                         off, diff);
     else if (off < len)
       lane_tail<M, MT, MODE>(a, tab01, tab2, in, out, og, (size_t)sbase + off, len - off, diff);
   }

@@ -72,37 +72,27 @@ __device__ __forceinline__ void xor_into(VecW4<W>& dst, const VecW4<W>& src) {
     for (int w = 0; w < W; ++w) dst[r][w] ^= src[r][w];
 }
 
-// W-dword lane chunk loads and stores (16 B: ld16 / st16_out; 8 B: the same on dwordx2)
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-typedef u32x2 u32x2_ua __attribute__((aligned(1)));
-
+// W-dword lane chunk loads and stores, the shard tail byte-wise
 template <int W>
 __device__ __forceinline__ void ld_lane(const uint8_t* p, bool full, size_t rem, uint32_t (&x)[W]) {
-  if constexpr (W == 4) {
-    const u32x4 v = full ? ld16<true>(p) : ld_tail(p, rem);
-    x[0] = v.x, x[1] = v.y, x[2] = v.z, x[3] = v.w;
+  if (full) {
+    ld_chunk<W, true>(p, x);
   } else {
-    static_assert(W == 2, "lane chunk of 2 or 4 dwords");
-    if (full) {
-      const u32x2 v = __builtin_nontemporal_load(reinterpret_cast<const u32x2_ua*>(p));
-      x[0] = v.x, x[1] = v.y;
-    } else {
-      const u32x4 v = ld_tail(p, rem < 8 ? rem : 8);
-      x[0] = v.x, x[1] = v.y;
-    }
+    const u32x4 v = ld_tail(p, rem < 4 * W ? rem : 4 * W);
+#pragma unroll
+    for (int w = 0; w < W; ++w) x[w] = v[w];
   }
 }
 
 template <int W>
 __device__ __forceinline__ void st_lane(uint8_t* p, bool full, size_t rem, const uint32_t (&x)[W]) {
-  if constexpr (W == 4) {
-    const u32x4 v = u32x4{x[0], x[1], x[2], x[3]};
-    if (full) st16_out<true>(p, v);
-    else st_tail(p, v, rem);
-  } else if (full) {
-    asm volatile("global_store_dwordx2 %0, %1, off nt" ::"v"(p), "v"(u32x2{x[0], x[1]}) : "memory");
+  if (full) {
+    st_chunk<W, true>(p, x);
   } else {
-    st_tail(p, u32x4{x[0], x[1], 0u, 0u}, rem < 8 ? rem : 8);
+    u32x4 v{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int w = 0; w < W; ++w) v[w] = x[w];
+    st_tail(p, v, rem < 4 * W ? rem : 4 * W);
   }
 }
 

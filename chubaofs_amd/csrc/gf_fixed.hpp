@@ -14,7 +14,7 @@ constexpr int kFixedD = 2;
 
 template <int K, int M, MatVecMode MODE>
 __global__ __launch_bounds__(256) void gf_matvec_k_kernel(const dev::GfArgs a) {
-  dev::matvec_k<K, M, MODE, kFixedD, 1>(a);
+  dev::matvec_k<K, M, MODE, kFixedD, 1, true, true, true, dev::fixed_lane_dwords(K, M)>(a);
 }
 
 template <int K, MatVecMode MODE, int M>

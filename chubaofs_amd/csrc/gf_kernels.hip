@@ -167,7 +167,7 @@ hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
         dy16 = dyadic16_plan(sub.data(), mc, kc);
         if (!dy16) dy = dyadic_plan(sub.data(), mc, kc);
       }
-      const size_t tile = fixed ? size_t(256) * dev::kLaneBytes
+      const size_t tile = fixed ? size_t(256) * 4 * dev::fixed_lane_dwords(kc, mc)
                                 : size_t(threads / sh.OS) * dev::kLaneBytes * (verify ? kVerifyW : kStoreW);
       const int per_stripe = kc + mc;
       const int64_t sstride = affine_stride(job, c0, kc, r0, mc);
