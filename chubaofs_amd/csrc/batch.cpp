@@ -57,6 +57,7 @@ struct Group {
   std::vector<const uint8_t*> in;  // [tasks * k]
   std::vector<uint8_t*> out;       // [tasks * m]
   std::vector<uint64_t> lens;
+  std::vector<uint8_t*> hout;      // plan->dy16: [tasks * (nd + 20)] its output rows
   int flag0 = 0;                   // first flag word
 };
 
@@ -75,6 +76,11 @@ hipError_t launch_group(const Group& g, uint32_t* dflags, hipStream_t s) {
       if (addr(g.in[(t + 1) * k + c]) - addr(g.in[t * k + c]) != d) return false;
     for (size_t r = 0; r < m; ++r)
       if (addr(g.out[(t + 1) * m + r]) - addr(g.out[t * m + r]) != d) return false;
+    if (g.plan->dy16) {
+      const size_t mo = g.plan->dy16->rows.size();
+      for (size_t r = 0; r < mo; ++r)
+        if (addr(g.hout[(t + 1) * mo + r]) - addr(g.hout[t * mo + r]) != d) return false;
+    }
     return true;
   };
   size_t t0 = 0;
@@ -94,6 +100,23 @@ hipError_t launch_group(const Group& g, uint32_t* dflags, hipStream_t s) {
 // Stripes [t0, t1) of a group: the mixed store/compare product, split into a store and a compare
 // launch when the rows exceed one launch.
 hipError_t launch_group_run(const Group& g, size_t t0, size_t t1, uint32_t* dflags, hipStream_t s) {
+  if (const Dy16Plan* d = g.plan->dy16.get()) {
+    Dy16RepairJob job;
+    job.nd = d->nd;
+    job.coef = d->coef.v.data();
+    std::memcpy(job.src, d->src, 16);
+    job.pstore = d->pstore;
+    job.pcmp = d->pcmp;
+    job.nstripes = (int)(t1 - t0);
+    job.in = g.in.data() + t0 * 16;
+    job.out = g.hout.data() + t0 * (size_t)(d->nd + 20);
+    bool uniform = true;
+    for (size_t t = t0; t < t1; ++t) uniform = uniform && g.lens[t] == g.lens[t0];
+    job.lens = uniform ? nullptr : g.lens.data() + t0;
+    job.len = g.lens[t0];
+    job.flags = dflags + g.flag0 + t0;
+    return launch_dy16_repair(job, s);
+  }
   MatVecJob job;
   job.k = (int)g.plan->in.size();
   job.m = (int)g.plan->out.size();
@@ -147,11 +170,22 @@ std::vector<Group> make_groups(const std::vector<StripeTask*>& tasks, int* next_
   }
   for (Group& g : groups) {
     g.flag0 = *next_flag;
+    g.in.reserve(g.tasks.size() * g.plan->in.size());
+    g.out.reserve(g.tasks.size() * g.plan->out.size());
+    g.lens.reserve(g.tasks.size());
     for (size_t i = 0; i < g.tasks.size(); ++i) {
       StripeTask* t = g.tasks[i];
       for (int c : g.plan->in) g.in.push_back(ptr(t, c));
       for (int o : g.plan->out) g.out.push_back(const_cast<uint8_t*>(ptr(t, o)));
       g.lens.push_back(t->len);
+      if (g.plan->dy16)
+        for (int idx : g.plan->dy16->rows) {
+          // rows the kernel neither stores nor compares (inputs; parity not verified) get any
+          // pointer the task has
+          const bool known = std::find(g.plan->in.begin(), g.plan->in.end(), idx) != g.plan->in.end() ||
+                             std::find(g.plan->out.begin(), g.plan->out.end(), idx) != g.plan->out.end();
+          g.hout.push_back(const_cast<uint8_t*>(ptr(t, known ? idx : g.plan->in[0])));
+        }
     }
     *next_flag += (int)g.tasks.size();
   }
@@ -239,7 +273,48 @@ Status RSEngine::plan_stripe(const std::vector<bool>& present, bool verify, Stri
       }
     }
   }
+  plan_dy16(present, dec, plan);
   return CFSEC_OK;
+}
+
+namespace {
+// The parity rows of a 16 + 20 code in the form repair_dy16 takes: rows 0..15 one 16x16 dyadic
+// block, rows 16..19 4x4 dyadic blocks (KRS buildMatrix(16, 36): gf_dyadic16.hpp).
+bool parity_dy16(const Matrix& p) {
+  if (p.rows != 20 || p.cols != 16) return false;
+  for (int i = 0; i < 16; ++i)
+    for (int j = 0; j < 16; ++j)
+      if (p.at(i, j) != p.at(0, i ^ j)) return false;
+  for (int c0 = 0; c0 < 16; c0 += 4)
+    for (int i = 0; i < 4; ++i)
+      for (int j = 0; j < 4; ++j)
+        if (p.at(16 + i, c0 + j) != p.at(16, c0 + (i ^ j))) return false;
+  return true;
+}
+}  // namespace
+
+void RSEngine::plan_dy16(const std::vector<bool>& present, const Matrix& dec, StripePlan* plan) const {
+  plan->dy16.reset();
+  static const bool off = std::getenv("CFSEC_NO_DY16_REPAIR") != nullptr;  // A/B switch
+  if (off || k_ != 16 || m_ != 20 || !parity_dy16(parity_)) return;
+  auto d = std::make_shared<Dy16Plan>();
+  for (int i = 0; i < k_; ++i)
+    if (!present[i]) d->rows.push_back(i);
+  d->nd = (int)d->rows.size();
+  // products: 16 per decode row + 117 for the 20 parity rows, against 16 per output row
+  if (d->nd > 4 || 16 * d->nd + 117 >= 16 * (int)plan->out.size()) return;
+  for (int r = 0; r < m_; ++r) d->rows.push_back(k_ + r);
+  int slot = 0, j = 0;
+  for (int i = 0; i < k_; ++i) d->src[i] = present[i] ? (uint8_t)slot++ : (uint8_t)(16 + j++);
+  for (size_t o = 0; o < plan->out.size(); ++o) {
+    const int idx = plan->out[o];
+    if (idx < k_) continue;
+    (o < (size_t)plan->nstore ? d->pstore : d->pcmp) |= 1u << (idx - k_);
+  }
+  d->coef = Matrix(20 + d->nd, 16);
+  std::memcpy(d->coef.v.data(), parity_.v.data(), 20 * 16);
+  for (int q = 0; q < d->nd; ++q) std::memcpy(d->coef.row(20 + q), dec.row(d->rows[q]), 16);
+  plan->dy16 = std::move(d);
 }
 
 Status RSEngine::encode_stripes(cfsec_shard* const* stripes, int nst, int mem, int* status) {
@@ -300,6 +375,10 @@ void RSEngine::plan_reconstruct_tasks(cfsec_shard* const* stripes, int nst, bool
                                       int owner0, PlanStore* store, std::vector<StripeTask>* tasks) {
   StripePlan* vplan = nullptr;  // Verify as an encode-matrix pass (split_verify)
   std::map<const StripePlan*, StripePlan*> store_only;
+  tasks->reserve(tasks->size() + (size_t)nst);
+  // batches mostly repeat one erasure pattern: the previous stripe's plan is checked first
+  std::vector<bool> present(total()), last_present;
+  std::unique_ptr<StripePlan>* last_plan = nullptr;
   for (int s = 0; s < nst; ++s) {
     status[s] = CFSEC_OK;
     cfsec_shard* sh = stripes[s];
@@ -309,7 +388,6 @@ void RSEngine::plan_reconstruct_tasks(cfsec_shard* const* stripes, int nst, bool
       status[s] = st;
       continue;
     }
-    std::vector<bool> present(total());
     int np = 0;
     for (int i = 0; i < total(); ++i) {
       present[i] = sh[i].len != 0;
@@ -320,13 +398,17 @@ void RSEngine::plan_reconstruct_tasks(cfsec_shard* const* stripes, int nst, bool
       continue;
     }
     if (np == total() && (!verify || m_ == 0)) continue;  // Reconstruct of a full stripe is a no-op
-    auto& plan = store->by_pattern[present];
+    if (!last_plan || present != last_present) {
+      last_plan = &store->by_pattern[present];
+      last_present = present;
+    }
+    auto& plan = *last_plan;
     if (!plan) {
       plan.reset(new StripePlan());
       st = plan_stripe(present, verify, plan.get());
       if (st != CFSEC_OK) {
-        plan.reset();
         store->by_pattern.erase(present);
+        last_plan = nullptr;
         status[s] = st;
         continue;
       }
@@ -350,6 +432,7 @@ void RSEngine::plan_reconstruct_tasks(cfsec_shard* const* stripes, int nst, bool
       StripePlan*& so = store_only[plan.get()];
       if (!so) {
         StripePlan cut = *plan;
+        cut.dy16.reset();
         cut.out.resize(cut.nstore);
         cut.rows = Matrix(cut.nstore, k_);
         std::memcpy(cut.rows.v.data(), plan->rows.v.data(), (size_t)cut.nstore * k_);
@@ -692,39 +775,47 @@ Status LrcEncoder::reconstruct_batch(cfsec_shard* shards, int n, int nbids, cons
   // lrcencoder.go:161-171) (+ local Verify)
   // per AZ, in bid order: an AZ's views of bids carved from one pitched buffer sit at one stride
   // from each other, so each AZ runs as one affine launch
-  std::vector<std::vector<std::vector<cfsec_shard>>> views(AZ);
+  // views[a]: AZ a's local stripes of the bids, lsz headers each, back to back
+  std::vector<std::vector<cfsec_shard>> views(AZ);
   std::vector<std::vector<size_t>> vowner(AZ);
+  std::vector<std::vector<int>> idc(AZ), local_bad(AZ);
+  for (int a = 0; a < AZ; ++a) {
+    idc[a] = shards_in_idc(a);
+    views[a].reserve(stripes.size() * idc[a].size());
+    vowner[a].reserve(stripes.size());
+  }
   for (size_t i = 0; i < stripes.size(); ++i) {
     if (st1[i] != CFSEC_OK) continue;  // Reconstruct failed: no local pass
     cfsec_shard* sh = stripes[i];
     const int b = pos[i];
-    std::map<int, std::vector<int>> local_bad;
+    for (auto& v : local_bad) v.clear();
     for (int j = bad_off[b]; j < bad_off[b + 1]; ++j)
       if (bad[j] >= N + M) {
-        const int idc = (bad[j] - N - M) * AZ / L;
-        local_bad[idc].push_back(bad[j] - N - M - L / AZ * idc + (N + M) / AZ);
+        const int a = (bad[j] - N - M) * AZ / L;
+        local_bad[a].push_back(bad[j] - N - M - L / AZ * a + (N + M) / AZ);
       }
     for (int a = 0; a < AZ; ++a) {
-      const bool has_bad = local_bad.count(a) != 0;
+      const bool has_bad = !local_bad[a].empty();
       if (!has_bad && !verify) continue;
-      std::vector<cfsec_shard> ls;
-      for (int g : shards_in_idc(a)) ls.push_back(sh[g]);
+      const size_t at = views[a].size();
+      for (int g : idc[a]) views[a].push_back(sh[g]);
+      cfsec_shard* ls = views[a].data() + at;
       if (has_bad) {
-        const Status s = init_bad_shards(ls.data(), (int)ls.size(), local_bad[a]);
+        const Status s = init_bad_shards(ls, (int)idc[a].size(), local_bad[a]);
         if (s != CFSEC_OK) {
           st1[i] = s;
+          views[a].resize(at);
           break;
         }
       }
-      views[a].push_back(std::move(ls));
       vowner[a].push_back(i);
     }
   }
   std::vector<cfsec_shard*> lp;
   std::vector<size_t> owner;
   for (int a = 0; a < AZ; ++a)
-    for (size_t v = 0; v < views[a].size(); ++v) {
-      lp.push_back(views[a][v].data());
+    for (size_t v = 0; v < vowner[a].size(); ++v) {
+      lp.push_back(views[a].data() + v * idc[a].size());
       owner.push_back(vowner[a][v]);
     }
   std::vector<int> st2(lp.size());

@@ -119,6 +119,16 @@ struct ReconPlan {
   Matrix rows;               // outputs.size() x k, over the shards in `valid`
 };
 
+// The 16 + 20 code's reconstruct (+ verify) through its 16x16 dyadic parity block
+// (Dy16RepairJob): missing data rows from decode rows, then all 20 parity rows from the data.
+struct Dy16Plan {
+  int nd = 0;             // missing data rows
+  std::vector<int> rows;  // output shard indices: the nd missing data rows, parity rows k .. k+19
+  uint8_t src[16] = {};
+  uint32_t pstore = 0, pcmp = 0;
+  Matrix coef;  // (20 + nd) x 16: parity matrix, decode rows
+};
+
 // The product one stripe of a heterogeneous batch needs (batch.cpp): rows x shards[in]; rows
 // [0, nstore) are written to shards[out[0 .. nstore)), the rest compared with shards[out[nstore ..)]
 // (a mismatch raises the stripe's flag).  Shared by every stripe with the same erasure pattern.
@@ -127,6 +137,7 @@ struct StripePlan {
   std::vector<int> out;
   int nstore = 0;
   Matrix rows;  // out.size() x in.size()
+  std::shared_ptr<const Dy16Plan> dy16;  // set where that product is the cheaper one
 };
 
 // The device (0 .. ndev-1) each of n stripes of a host-memory batch runs on: contiguous runs
@@ -211,6 +222,8 @@ class RSEngine {
   Status run_stripes(std::vector<StripeTask>& tasks, int mem);
   // Plan of a Reconstruct (+ Verify) over the present shards.
   Status plan_stripe(const std::vector<bool>& present, bool verify, StripePlan* plan);
+  // plan->dy16 where the code and the erasure pattern make that product cheaper (batch.cpp).
+  void plan_dy16(const std::vector<bool>& present, const Matrix& dec, StripePlan* plan) const;
   // Run a plan's Verify as a separate encode-matrix pass instead of its compared rows.
   bool split_verify(const StripePlan& p) const;
 

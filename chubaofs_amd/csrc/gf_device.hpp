@@ -48,6 +48,8 @@ struct __attribute__((aligned(16))) GfArgs {
   uint32_t tab;                    // stripes held in ptr[]
   uint16_t nstore;                 // kStoreVerify: outputs [0, nstore) are stored, [nstore, m) compared
   uint16_t varlen;                 // nonzero: per-stripe lengths in slen[]
+  uint32_t pstore, pcmp;           // repair_dy16: parity rows stored / compared
+  uint8_t src[16];                 // repair_dy16: input slot of data row i (16 + j: missing row j)
   uint8_t coef[kMaxM * kMaxK];    // m x k, row stride k
   uint32_t slen[kLenSlots];
   const uint8_t* ptr[kPtrSlots];  // [tab*k inputs][tab*m outputs]

@@ -29,6 +29,25 @@ hipError_t launch_one(MatVecMode mode, const dev::GfArgs& a, unsigned ns, hipStr
 }
 }  // namespace
 
+template <int ND>
+__global__ __launch_bounds__(256) void gf_dy16_repair_kernel(const dev::GfArgs a) {
+  dev::repair_dy16<ND, true, CFSEC_DY16_W>(a);
+}
+
+hipError_t launch_dy16_repair_args(int nd, const dev::GfArgs& a, unsigned ns, hipStream_t st) {
+  constexpr uint64_t tile = 256 * 4 * CFSEC_DY16_W;
+  const dim3 grid((unsigned)((a.len + tile - 1) / tile), ns);
+  switch (nd) {
+    case 0: hipLaunchKernelGGL((gf_dy16_repair_kernel<0>), grid, dim3(256), 0, st, a); break;
+    case 1: hipLaunchKernelGGL((gf_dy16_repair_kernel<1>), grid, dim3(256), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((gf_dy16_repair_kernel<2>), grid, dim3(256), 0, st, a); break;
+    case 3: hipLaunchKernelGGL((gf_dy16_repair_kernel<3>), grid, dim3(256), 0, st, a); break;
+    case 4: hipLaunchKernelGGL((gf_dy16_repair_kernel<4>), grid, dim3(256), 0, st, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_dy16(int m, MatVecMode mode, const dev::GfArgs& a, unsigned ns, hipStream_t st) {
   switch (m) {
     case 20: return launch_one<20, 1, 0, CFSEC_DY16_W>(mode, a, ns, st);  // EC16P20 global parity

@@ -96,10 +96,110 @@ __device__ __forceinline__ void st_lane(uint8_t* p, bool full, size_t rem, const
   }
 }
 
+// The rows of a 16-input matrix opening with a 16x16 dyadic block: 16 + 4 R4 + E rows from the 16
+// input chunks x (clobbered), each handed to put(r, chunk) as soon as it is final.  Rows 16.. (the
+// 4x4 row blocks, then the E plain rows) come first, from the original inputs, one group at a time
+// in acc[16..]; then the 16x16 block into acc[0..15].
+template <int R4, int E, bool PIN, int W, class Put>
+__device__ __forceinline__ void dy16_rows(uint32_t (&x)[16][W], const u32x4* tab01, const uint32_t* tab2, Put&& put) {
+  constexpr int K = 16, N4 = R4 * 4 * 9;
+  constexpr int NA = 16 + (4 * R4 > E ? 4 * R4 : E);
+  uint32_t acc[NA][W];
+#pragma unroll
+  for (int r = 0; r < NA; ++r)
+#pragma unroll
+    for (int w = 0; w < W; ++w) acc[r][w] = 0u;
+  const auto sb = [&]() {
+    if constexpr (PIN) __builtin_amdgcn_sched_barrier(0);
+  };
+  sb();
+  if constexpr (R4 > 0) {
+    const u32x4* tq = tab01 + kDy16Leaves;
+    const uint32_t* tt = tab2 + kDy16Leaves;
+    auto& racc = reinterpret_cast<uint32_t(&)[4 * R4][W]>(acc[16]);
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      dy_col4<R4, PIN>(racc, x[4 * cb], x[4 * cb + 1], x[4 * cb + 2], x[4 * cb + 3], tq + cb * 9, tt + cb * 9, 4 * 9);
+      sb();
+    }
+#pragma unroll
+    for (int r = 16; r < 16 + 4 * R4; ++r) put(r, acc[r]);
+    sb();
+#pragma unroll
+    for (int r = 16; r < NA; ++r)
+#pragma unroll
+      for (int w = 0; w < W; ++w) acc[r][w] = 0u;
+  }
+  if constexpr (E > 0) {
+    auto& eacc = reinterpret_cast<uint32_t(&)[E][W]>(acc[16]);
+    constexpr int ND = kDy16Leaves + N4;
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+      mac_row_k<E>(eacc, x[c], tab01 + ND + c * E, tab2 + ND + c * E);
+      if constexpr (PIN)
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+#pragma unroll
+          for (int w = 0; w < W; ++w) asm volatile("" : "+v"(eacc[e][w]));
+      sb();
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) put(16 + 4 * R4 + e, acc[16 + e]);
+    sb();
+  }
+  // the 16x16 block: S = X + Y into x[0..7]
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int w = 0; w < W; ++w) x[j][w] ^= x[j + 8][w];
+  // rows 8..15 = C Y, C = A + B (leaves 3..5): the 8x8 recursion on Y, rows 8..15 start at zero
+  leaf4<PIN, W>(v4<W>(acc[12]), v4<W>(x[12]), tab01, tab2, 4);  // C_c Y_hi
+#pragma unroll
+  for (int r = 8; r < 12; ++r)
+#pragma unroll
+    for (int w = 0; w < W; ++w) acc[r][w] = acc[r + 4][w];
+#pragma unroll
+  for (int j = 8; j < 12; ++j)
+#pragma unroll
+    for (int w = 0; w < W; ++w) x[j][w] ^= x[j + 4][w];  // Y_lo + Y_hi (Y is dead after this)
+  leaf4<PIN, W>(v4<W>(acc[8]), v4<W>(x[8]), tab01, tab2, 3);    // C_a
+  leaf4<PIN, W>(v4<W>(acc[12]), v4<W>(x[8]), tab01, tab2, 5);   // C_b
+  // rows 0..7 = C Y as well, then += A S; rows 8..15 += B S
+#pragma unroll
+  for (int r = 0; r < 8; ++r)
+#pragma unroll
+    for (int w = 0; w < W; ++w) acc[r][w] = acc[r + 8][w];
+  {
+    uint32_t tmp[4][W];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int w = 0; w < W; ++w) tmp[r][w] = 0u;
+    leaf4<PIN, W>(tmp, v4<W>(x[4]), tab01, tab2, 1);  // A_c S_hi
+    xor_into<W>(v4<W>(acc[0]), tmp);
+    xor_into<W>(v4<W>(acc[4]), tmp);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int w = 0; w < W; ++w) tmp[r][w] = 0u;
+    leaf4<PIN, W>(tmp, v4<W>(x[4]), tab01, tab2, 7);  // B_c S_hi
+    xor_into<W>(v4<W>(acc[8]), tmp);
+    xor_into<W>(v4<W>(acc[12]), tmp);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int w = 0; w < W; ++w) x[j][w] ^= x[j + 4][w];  // S_lo + S_hi, shared by A and B
+  leaf4<PIN, W>(v4<W>(acc[0]), v4<W>(x[0]), tab01, tab2, 0);   // A_a
+  leaf4<PIN, W>(v4<W>(acc[4]), v4<W>(x[0]), tab01, tab2, 2);   // A_b
+  leaf4<PIN, W>(v4<W>(acc[8]), v4<W>(x[0]), tab01, tab2, 6);   // B_a
+  leaf4<PIN, W>(v4<W>(acc[12]), v4<W>(x[0]), tab01, tab2, 8);  // B_b
+#pragma unroll
+  for (int r = 0; r < 16; ++r) put(r, acc[r]);
+}
+
 // Kernel body: 16 inputs, M = 16 + 4 R4 + E outputs; 256-thread workgroups, each lane one chunk of
-// W dwords of every row (tile 256 * 4W bytes), grid (tiles, stripes).  Output rows 16.. (the 4x4
-// row blocks, then the E plain rows) are computed first, from the original inputs, and stored one
-// group at a time from acc[16..]; then the 16x16 block into acc[0..15].
+// W dwords of every row (tile 256 * 4W bytes), grid (tiles, stripes).
 template <int M, int R4, int E, MatVecMode MODE, bool PIN = true, int W = 4>
 __device__ __forceinline__ void matvec_dy16(const GfArgs& a) {
   constexpr int K = 16, N4 = R4 * 4 * 9;
@@ -127,121 +227,121 @@ __device__ __forceinline__ void matvec_dy16(const GfArgs& a) {
   const size_t rem = off < slen ? (size_t)(slen - off) : 0;
   uint32_t diff = 0;
   if (full || rem) {
-    // rows 16.. share registers: the 4x4 row blocks, stored, then the plain rows in the same slots
-    constexpr int NA = 16 + (4 * R4 > E ? 4 * R4 : E);
-    uint32_t acc[NA][W];
-#pragma unroll
-    for (int r = 0; r < NA; ++r)
-#pragma unroll
-      for (int w = 0; w < W; ++w) acc[r][w] = 0u;
     uint32_t x[K][W];
 #pragma unroll
     for (int c = 0; c < K; ++c) ld_lane<W>(row[c] + off, full, rem, x[c]);
-    const auto sb = [&]() {
-      if constexpr (PIN) __builtin_amdgcn_sched_barrier(0);
-    };
     // store (or compare) output row r as soon as it is final, so its registers are free for the
     // 16x16 block's temporaries
-    const auto put = [&](int r, int ai) {
+    dy16_rows<R4, E, PIN, W>(x, tab01, tab2, [&](int r, const uint32_t (&v)[W]) {
       uint8_t* p = const_cast<uint8_t*>(row[K + r]) + off;
       if constexpr (kVer) {
         uint32_t y[W];
         ld_lane<W>(p, full, rem, y);
 #pragma unroll
-        for (int w = 0; w < W; ++w) diff |= y[w] ^ acc[ai][w];
+        for (int w = 0; w < W; ++w) diff |= y[w] ^ v[w];
       } else {
-        st_lane<W>(p, full, rem, acc[ai]);
+        st_lane<W>(p, full, rem, v);
       }
-    };
-    sb();
-    // rows after the 16x16 block: 4x4 dyadic blocks and plain rows, on the original inputs
-    if constexpr (R4 > 0) {
-      const u32x4* tq = tab01 + kDy16Leaves;
-      const uint32_t* tt = tab2 + kDy16Leaves;
-      auto& racc = reinterpret_cast<uint32_t(&)[4 * R4][W]>(acc[16]);
-#pragma unroll
-      for (int cb = 0; cb < 4; ++cb) {
-        dy_col4<R4, PIN>(racc, x[4 * cb], x[4 * cb + 1], x[4 * cb + 2], x[4 * cb + 3], tq + cb * 9, tt + cb * 9, 4 * 9);
-        sb();
-      }
-#pragma unroll
-      for (int r = 16; r < 16 + 4 * R4; ++r) put(r, r);
-      sb();
-#pragma unroll
-      for (int r = 16; r < NA; ++r)
-#pragma unroll
-        for (int w = 0; w < W; ++w) acc[r][w] = 0u;
-    }
-    if constexpr (E > 0) {
-      auto& eacc = reinterpret_cast<uint32_t(&)[E][W]>(acc[16]);
-      constexpr int ND = kDy16Leaves + N4;
-#pragma unroll
-      for (int c = 0; c < K; ++c) {
-        mac_row_k<E>(eacc, x[c], tab01 + ND + c * E, tab2 + ND + c * E);
-        if constexpr (PIN)
-#pragma unroll
-          for (int e = 0; e < E; ++e)
-#pragma unroll
-            for (int w = 0; w < W; ++w) asm volatile("" : "+v"(eacc[e][w]));
-        sb();
-      }
-#pragma unroll
-      for (int e = 0; e < E; ++e) put(16 + 4 * R4 + e, 16 + e);
-      sb();
-    }
-    // the 16x16 block: S = X + Y into x[0..7]
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-#pragma unroll
-      for (int w = 0; w < W; ++w) x[j][w] ^= x[j + 8][w];
-    // rows 8..15 = C Y, C = A + B (leaves 3..5): the 8x8 recursion on Y, rows 8..15 start at zero
-    leaf4<PIN, W>(v4<W>(acc[12]), v4<W>(x[12]), tab01, tab2, 4);  // C_c Y_hi
-#pragma unroll
-    for (int r = 8; r < 12; ++r)
-#pragma unroll
-      for (int w = 0; w < W; ++w) acc[r][w] = acc[r + 4][w];
-#pragma unroll
-    for (int j = 8; j < 12; ++j)
-#pragma unroll
-      for (int w = 0; w < W; ++w) x[j][w] ^= x[j + 4][w];  // Y_lo + Y_hi (Y is dead after this)
-    leaf4<PIN, W>(v4<W>(acc[8]), v4<W>(x[8]), tab01, tab2, 3);    // C_a
-    leaf4<PIN, W>(v4<W>(acc[12]), v4<W>(x[8]), tab01, tab2, 5);   // C_b
-    // rows 0..7 = C Y as well, then += A S; rows 8..15 += B S
-#pragma unroll
-    for (int r = 0; r < 8; ++r)
-#pragma unroll
-      for (int w = 0; w < W; ++w) acc[r][w] = acc[r + 8][w];
-    {
-      uint32_t tmp[4][W];
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int w = 0; w < W; ++w) tmp[r][w] = 0u;
-      leaf4<PIN, W>(tmp, v4<W>(x[4]), tab01, tab2, 1);  // A_c S_hi
-      xor_into<W>(v4<W>(acc[0]), tmp);
-      xor_into<W>(v4<W>(acc[4]), tmp);
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int w = 0; w < W; ++w) tmp[r][w] = 0u;
-      leaf4<PIN, W>(tmp, v4<W>(x[4]), tab01, tab2, 7);  // B_c S_hi
-      xor_into<W>(v4<W>(acc[8]), tmp);
-      xor_into<W>(v4<W>(acc[12]), tmp);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int w = 0; w < W; ++w) x[j][w] ^= x[j + 4][w];  // S_lo + S_hi, shared by A and B
-    leaf4<PIN, W>(v4<W>(acc[0]), v4<W>(x[0]), tab01, tab2, 0);   // A_a
-    leaf4<PIN, W>(v4<W>(acc[4]), v4<W>(x[0]), tab01, tab2, 2);   // A_b
-    leaf4<PIN, W>(v4<W>(acc[8]), v4<W>(x[0]), tab01, tab2, 6);   // B_a
-    leaf4<PIN, W>(v4<W>(acc[12]), v4<W>(x[0]), tab01, tab2, 8);  // B_b
-#pragma unroll
-    for (int r = 0; r < 16; ++r) put(r, r);
+    });
   }
   if constexpr (kVer) {
     if (diff) atomicOr(a.flags + stripe, 1u);
   }
+}
+
+// Reconstruct (+ Verify) of a stripe of the 16 + 20 code (EC16P20 and EC16P20L2's global stripe)
+// whose first 16 present shards are ND < 5 parity rows and the 16 - ND surviving data rows: the
+// ND missing data rows from their decode rows (16 ND products), then all 20 parity rows from the
+// 16 data rows through the 16x16 dyadic block (117 products) -- every parity row the reference's
+// Reconstruct writes is stored, every one its Verify reads is compared, the rest dropped.  The plain
+// reconstruct-and-verify product over the first 16 present rows takes 16 per output row: 320 for
+// the 4-erasure repair of a tasklet bid (2 data + 2 parity missing, 16 compared).
+// Args: coef rows 0..19 the parity matrix, rows 20.. the decode rows; ptr per stripe: the 16
+// inputs, then ND + 20 outputs (the missing data rows, parity rows 0..19); src[i] = the input slot
+// of data row i, or 16 + j for missing data row j; pstore / pcmp: parity rows stored / compared.
+template <int ND, bool PIN = true, int W = 2>
+__device__ __forceinline__ void repair_dy16(const GfArgs& a) {
+  constexpr int K = 16, NDY = kDy16Leaves + 36, NT = NDY + K * (ND > 0 ? ND : 1), MO = ND + 20;
+  constexpr uint32_t kLane = 4 * W;
+  __shared__ u32x4 tab01[NT];
+  __shared__ uint32_t tab2[NT];
+  build_dy16_tables<1, 0>(a.coef, tab01, tab2);
+  for (int i = threadIdx.x; i < K * ND; i += (int)blockDim.x)  // slot NDY + c * ND + j: decode row j, column c
+    coef_tables(a.coef[(20 + i % ND) * K + i / ND], tab01[NDY + i], tab2[NDY + i]);
+  __syncthreads();
+
+  const uint32_t stripe = blockIdx.y, tile = blockIdx.x;
+  const size_t ts = a.sstride ? 0 : (size_t)stripe;
+  const int64_t sbase = (int64_t)stripe * a.sstride;
+  const uint32_t off = tile * (256u * kLane) + (uint32_t)threadIdx.x * kLane;
+  const uint64_t slen = stripe_len(a, stripe);
+  const bool full = (uint64_t)off + kLane <= slen;
+  const size_t rem = off < slen ? (size_t)(slen - off) : 0;
+  uint32_t diff = 0;
+  if (full || rem) {
+    const uint8_t* const* in = a.ptr + ts * K;
+    uint8_t* const* out = const_cast<uint8_t* const*>(a.ptr + (size_t)a.tab * K + ts * MO);
+    const auto sb = [&]() {
+      if constexpr (PIN) __builtin_amdgcn_sched_barrier(0);
+    };
+    uint32_t x[K][W];
+#pragma unroll
+    for (int c = 0; c < K; ++c) ld_lane<W>(in[c] + sbase + off, full, rem, x[c]);
+    sb();
+    if constexpr (ND > 0) {
+      // the missing data rows, stored
+      uint32_t rec[ND][W];
+#pragma unroll
+      for (int j = 0; j < ND; ++j)
+#pragma unroll
+        for (int w = 0; w < W; ++w) rec[j][w] = 0u;
+#pragma unroll
+      for (int c = 0; c < K; ++c) {
+        mac_row_k<ND>(rec, x[c], tab01 + NDY + c * ND, tab2 + NDY + c * ND);
+        if constexpr (PIN)
+#pragma unroll
+          for (int j = 0; j < ND; ++j)
+#pragma unroll
+            for (int w = 0; w < W; ++w) asm volatile("" : "+v"(rec[j][w]));
+        sb();
+      }
+#pragma unroll
+      for (int j = 0; j < ND; ++j) st_lane<W>(out[j] + sbase + off, full, rem, rec[j]);
+      // the data rows in order, in place: data row i is input slot i - (missing rows below i),
+      // so from the top down no slot is overwritten before it is read
+#pragma unroll
+      for (int i = K - 1; i >= 0; --i) {
+        const uint32_t s = a.src[i];
+#pragma unroll
+        for (int d = 0; d <= ND; ++d)
+          if (i - d >= 0 && s == (uint32_t)(i - d))
+#pragma unroll
+            for (int w = 0; w < W; ++w) x[i][w] = x[i - d][w];
+#pragma unroll
+        for (int j = 0; j < ND; ++j)
+          if (s == (uint32_t)(K + j))
+#pragma unroll
+            for (int w = 0; w < W; ++w) x[i][w] = rec[j][w];
+      }
+      sb();
+    }
+    const uint32_t pstore = a.pstore, pcmp = a.pcmp;
+    const uint8_t* spare = in[0] + sbase + off;  // just read: what rows not compared load instead
+    dy16_rows<1, 0, PIN, W>(x, tab01, tab2, [&](int r, const uint32_t (&v)[W]) {
+      // every row loads (its own chunk if compared, else the input chunk above, a cache hit) and
+      // the mask picks: no branch around the loads, so the compiler issues a group of them before
+      // the first wait (a branch per row exposed one load latency per compared row: +45 % time)
+      uint8_t* p = out[ND + r] + sbase + off;
+      const bool cmp = (pcmp >> r) & 1u;
+      uint32_t y[W];
+      ld_lane<W>(cmp ? p : spare, full, rem, y);
+      const uint32_t msk = cmp ? ~0u : 0u;
+#pragma unroll
+      for (int w = 0; w < W; ++w) diff |= (y[w] ^ v[w]) & msk;
+      if ((pstore >> r) & 1u) st_lane<W>(p, full, rem, v);
+    });
+  }
+  if (diff) atomicOr(a.flags + stripe, 1u);
 }
 
 }  // namespace dev

@@ -38,6 +38,7 @@
 //                tools/gf_variants.hip -- store/accum 256-thread, 1 chunk per lane, one row at a
 //                time; verify 128-thread, 2 chunks per lane, rows loaded in pairs
 #include <algorithm>
+#include <cstring>
 #include <vector>
 
 #include "gf_device.hpp"
@@ -243,6 +244,70 @@ hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
         if (e != hipSuccess) return e;
       }
     }
+  }
+  return hipSuccess;
+}
+
+hipError_t launch_dy16_repair(const Dy16RepairJob& job, hipStream_t stream) {
+  using dev::kPtrSlots;
+  const int nd = job.nd, mo = nd + 20;
+  if (nd < 0 || nd > 4 || job.nstripes < 0 || !job.coef || !job.in || !job.out || (job.pcmp && !job.flags) ||
+      (job.pstore | job.pcmp) >> 20)
+    return hipErrorInvalidValue;
+  if (job.nstripes == 0) return hipSuccess;
+  uint64_t maxlen = job.len;
+  if (job.lens) {
+    maxlen = 0;
+    for (int s = 0; s < job.nstripes; ++s) maxlen = std::max<uint64_t>(maxlen, job.lens[s]);
+  }
+  if (maxlen == 0) return hipSuccess;
+  if (maxlen > 0xFFFFFFFFull - 4096) return hipErrorInvalidValue;  // 32-bit lane offsets, slen[]
+  // one stride between stripes on every row: one affine launch
+  int64_t sstride = 0;
+  if (job.nstripes > 1 && !job.lens) {
+    const auto addr = [](const void* p) { return (int64_t)(uintptr_t)p; };
+    sstride = addr(job.in[16]) - addr(job.in[0]);
+    for (int s = 1; s < job.nstripes && sstride; ++s) {
+      for (int c = 0; c < 16 && sstride; ++c)
+        if (addr(job.in[(size_t)s * 16 + c]) != addr(job.in[c]) + s * sstride) sstride = 0;
+      for (int r = 0; r < mo && sstride; ++r)
+        if (addr(job.out[(size_t)s * mo + r]) != addr(job.out[r]) + s * sstride) sstride = 0;
+    }
+  }
+  int per = sstride ? std::min(job.nstripes, 65535) : kPtrSlots / (16 + mo);
+  if (job.lens) per = std::min(per, dev::kLenSlots);
+  dev::GfArgs a;
+  a.k = 16;
+  a.m = (uint32_t)mo;
+  a.sstride = sstride;
+  a.nstore = 0;
+  a.pstore = job.pstore;
+  a.pcmp = job.pcmp;
+  std::memcpy(a.src, job.src, 16);
+  std::memcpy(a.coef, job.coef, (size_t)(20 + nd) * 16);
+  for (int s0 = 0; s0 < job.nstripes; s0 += per) {
+    const int ns = std::min(per, job.nstripes - s0);
+    const int tab = sstride ? 1 : ns;
+    uint64_t llen = job.len;
+    a.varlen = job.lens ? 1 : 0;
+    if (job.lens) {
+      llen = 0;
+      for (int s = 0; s < ns; ++s) {
+        a.slen[s] = (uint32_t)job.lens[s0 + s];
+        llen = std::max<uint64_t>(llen, job.lens[s0 + s]);
+      }
+      if (llen == 0) continue;
+    }
+    a.len = llen;
+    a.nstripes = (uint32_t)ns;
+    a.tab = (uint32_t)tab;
+    a.flags = job.flags ? job.flags + s0 : nullptr;
+    for (int s = 0; s < tab; ++s) {
+      for (int c = 0; c < 16; ++c) a.ptr[s * 16 + c] = job.in[(size_t)(s0 + s) * 16 + c];
+      for (int r = 0; r < mo; ++r) a.ptr[tab * 16 + s * mo + r] = job.out[(size_t)(s0 + s) * mo + r];
+    }
+    const hipError_t e = launch_dy16_repair_args(nd, a, (unsigned)ns, stream);
+    if (e != hipSuccess) return e;
   }
   return hipSuccess;
 }

@@ -113,6 +113,44 @@ def test_reconstruct_stripes_mock_bids(k, m, memory):
 
 
 @pytest.mark.parametrize("memory", ["host", "device"])
+@pytest.mark.parametrize("verify", [True, False])
+def test_reconstruct_stripes_16_20_dyadic_repair(memory, verify):
+    """The 16 + 20 code (EC16P20, EC16P20L2's global stripe) with up to 4 data shards missing takes
+    repair_dy16 when it verifies (decode rows for the missing data, then all 20 parity rows through
+    the 16x16 dyadic block): every split of the erasures between data and parity, corrupted parity
+    outside and inside the first 16 present shards, odd sizes, against the oracle's two passes."""
+    from chubaofs_amd import reedsolomon
+    k, m = 16, 20
+    enc = reedsolomon.New(k, m, device=0)
+    r = random.Random(1620 + verify)
+    stripes, want, cases = [], [], []
+    b = 0
+    for nd in range(5):
+        for npar in (0, 1, 2, 4, 9):
+            for corrupt in ("none", "spare", "input"):
+                size = r.choice([1, 23, 4096, 4097, 65536 + 5, 262144])
+                good = codeword(k, m, size, b)
+                bad = sorted(r.sample(range(k), nd) + r.sample(range(k, k + m), npar))
+                src = [x.copy() for x in good]
+                present = [i for i in range(k + m) if i not in bad]
+                if corrupt == "spare" and len(present) > k:
+                    src[present[-1]][size // 2] ^= 0x5A  # verified, not an input
+                if corrupt == "input" and nd > 0:
+                    src[present[k - 1]][0] ^= 0x33  # a parity shard among the first 16 present
+                stripes.append(to_mem(src, memory))
+                mark_missing(stripes[-1], bad, memory)
+                want.append(reference_repair(k, m, src, bad, verify=verify))
+                cases.append((nd, npar, corrupt, size, bad))
+                b += 1
+    status = enc.ReconstructStripes(stripes, verify=verify)
+    for i, (st, shards) in enumerate(want):
+        assert status[i] == st, (cases[i], status[i], st)
+        got = [host(x) for x in stripes[i]]
+        for j in range(k + m):
+            assert np.array_equal(got[j], shards[j]), (cases[i], j)
+
+
+@pytest.mark.parametrize("memory", ["host", "device"])
 def test_reconstruct_stripes_many_patterns_and_launch_splits(memory):
     """70 stripes (more than one launch's 32 length slots), 9 erasure patterns, varied sizes."""
     from chubaofs_amd import reedsolomon
