@@ -436,6 +436,8 @@ def main():
         "cpu_baseline": cpu,
     }
     out.update(extra)
+    if "device_copy_GBps" in extra:
+        out["roofline"]["frac_of_measured_copy"] = round(achieved / extra["device_copy_GBps"], 4)
     print(json.dumps(out), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
@@ -513,6 +515,16 @@ def secondary(args, torch, enc, batch, ptrs, stream, S, nst, pitch, dev, launch_
                            "HIP events on the launch stream; roofline fractions use the same algorithmic bytes"),
     })
     del framed, unframed
+    # also against a measured device-copy peak -- torch's device-to-device copy of
+    # one batch (716 MB) into a scratch batch, rotated like the step, 2 x bytes moved per copy
+    scratch = torch.empty_like(batch[0])
+    with torch.cuda.stream(stream):
+        copy_ms = timed(lambda b: scratch.copy_(batch[b]))
+    copy_bytes = 2 * batch[0].numel()
+    out["device_copy_GBps"] = rate(copy_bytes, copy_ms)
+    out["device_copy_note"] = ("torch copy_ of one rotated batch into a scratch batch (the HIP runtime D2D copy, "
+                               "__amd_rocclr_copyBuffer), read + write bytes / time: a measured streaming peak")
+    del scratch
     return out
 
 

@@ -10,7 +10,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcfsec.so")
+# CFSEC_LIB_PATH: another build of the same library (A/B probes of kernel variants)
+LIB_PATH = os.environ.get("CFSEC_LIB_PATH") or os.path.join(_HERE, "libcfsec.so")
 
 MEM_HOST = 0
 MEM_DEVICE = 1

@@ -50,9 +50,9 @@ __device__ __forceinline__ void piece(const uint8_t* p, uint64_t len, uint32_t o
 }
 
 __global__ __launch_bounds__(256) void crc32_horner_kernel(const CrcArgs a) {
-  __shared__ uint32_t ct[crcdev::kNibTabWords];
+  __shared__ uint32_t ct[crcdev::kOnlyTabWords];
   __shared__ uint32_t red[4];
-  for (int i = threadIdx.x; i < crcdev::kNibTabWords; i += 256) ct[i] = a.tabs[crcdev::kByteTabWords + i];
+  for (int i = threadIdx.x; i < crcdev::kOnlyTabWords; i += 256) ct[i] = a.tabs[crcdev::kOnlyTabBase + i];
   __syncthreads();
   const uint32_t g = blockIdx.x, sh = blockIdx.y;
   const uint8_t* p = a.sstride ? a.ptr[0] + (int64_t)sh * a.sstride : a.ptr[sh];
@@ -62,7 +62,7 @@ __global__ __launch_bounds__(256) void crc32_horner_kernel(const CrcArgs a) {
   piece(p, a.len, t0 * kTile + lanepos, cur);
   for (uint32_t t = t0; t < t1; ++t) {
     if (t + 1 < t1) piece(p, a.len, (t + 1) * kTile + lanepos, nxt);
-    R = crcdev::crc_step_nib(ct, R, cur);
+    R = crcdev::only_step(ct, R, cur);
 #pragma unroll
     for (int w = 0; w < 4; ++w) cur[w] = nxt[w];
   }

@@ -91,9 +91,9 @@ __device__ __forceinline__ void load_piece(const uint8_t* src, uint32_t plen, ui
 // runs STORE, CRC and EPI on, pieces aligned to the destination).
 template <bool STORE = true, bool CRC = true, bool EPI = true, bool SRCALIGN = false, bool NTS = true>
 __global__ __launch_bounds__(256) void crc32block_kernel(const BlockArgs a) {
-  __shared__ uint32_t ct[crcdev::kNibTabWords];
+  __shared__ uint32_t ct[crcdev::kOnlyTabWords];
   __shared__ uint32_t red[4];
-  for (int i = threadIdx.x; i < crcdev::kNibTabWords; i += 256) ct[i] = a.tabs[crcdev::kByteTabWords + i];
+  for (int i = threadIdx.x; i < crcdev::kOnlyTabWords; i += 256) ct[i] = a.tabs[crcdev::kOnlyTabBase + i];
   // this thread's x^(8*16*(255 - j)): moves its Horner register from its piece to the tile end
   // (gf_crc.hip host_tables; one coalesced word per thread -- reading column x^0 of the
   // per-thread basis instead, 128 B apart, cost one L2 request per thread per block)
@@ -151,7 +151,7 @@ __global__ __launch_bounds__(256) void crc32block_kernel(const BlockArgs a) {
         if (t < tiles) {
           uint32_t (&cur)[4] = ring[k];
           const uint32_t p = t * 256 + threadIdx.x;
-          if constexpr (CRC) R = crcdev::crc_step_nib(ct, R, cur);
+          if constexpr (CRC) R = crcdev::only_step(ct, R, cur);
           else R ^= cur[0] ^ cur[1] ^ cur[2] ^ cur[3];
           const int64_t first = (int64_t)16 * p - h;
           if (STORE && first < (int64_t)plen) {
@@ -209,9 +209,9 @@ __global__ __launch_bounds__(256) void crc32block_kernel(const BlockArgs a) {
 // thread 0 only XORs four words and stores or compares the header.
 template <int RING, bool NTS = true, bool STRIDE = false>
 __global__ __launch_bounds__(256) void crc32block_block_kernel(const BlockArgs a) {
-  __shared__ uint32_t ct[crcdev::kNibTabWords];
+  __shared__ uint32_t ct[crcdev::kOnlyTabWords];
   __shared__ uint32_t redb[2][8];  // per wave: its share of the block's raw CRC, and of the object's
-  for (int i = threadIdx.x; i < crcdev::kNibTabWords; i += 256) ct[i] = a.tabs[crcdev::kByteTabWords + i];
+  for (int i = threadIdx.x; i < crcdev::kOnlyTabWords; i += 256) ct[i] = a.tabs[crcdev::kOnlyTabBase + i];
   const uint32_t tid = threadIdx.x;
   const uint32_t kj = a.tabs[kTabWords + crcdev::kBasisWords + tid];
   __syncthreads();
@@ -280,7 +280,7 @@ __global__ __launch_bounds__(256) void crc32block_block_kernel(const BlockArgs a
     // piece t*256 + tid: Horner step, then the copy to the destination
     const auto piece = [&](uint32_t t, uint32_t (&pc)[4]) {
       const uint32_t p = t * 256 + tid;
-      R = crcdev::crc_step_nib(ct, R, pc);
+      R = crcdev::only_step(ct, R, pc);
       const int64_t first = (int64_t)16 * p - cur.h;
       if (first + 16 > (int64_t)cur.sbeg && first < (int64_t)cur.lim) {  // sbeg > 0 is a piece boundary
         const int64_t q = (int64_t)cur.q0 + first;

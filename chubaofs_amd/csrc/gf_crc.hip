@@ -74,6 +74,22 @@ std::vector<uint32_t> host_tables() {
     }
   for (int q = 0; q < 8; ++q)  // Hq[n] = shift(n << 4q, 4096)
     for (uint32_t n = 0; n < 16; ++n) nt[(32 + q) * 16 + n] = mulmod(k4096, n << (4 * q));
+  uint32_t* ft = nt + crcdev::kNibTabWords;
+  for (int w = 0; w < 5; ++w)  // Q(w, f)[e]: word w of (d0..d3, R) = e << 5f, the rest 0
+    for (int f = 0; f < crcdev::kFiveFields; ++f)
+      for (uint32_t e = 0; e < (f < 6 ? 32u : 4u); ++e) {
+        const uint32_t v = e << (5 * f);
+        uint32_t c = 0;
+        if (w == 4) {
+          c = mulmod(k4096, v);
+        } else {
+          for (int i = 0; i < 16; ++i) {
+            c ^= i / 4 == w ? (v >> (8 * (i % 4))) & 0xFFu : 0u;
+            for (int q = 0; q < 8; ++q) c = (c & 1u) ? (c >> 1) ^ crcdev::kPoly : c >> 1;
+          }
+        }
+        ft[(w * crcdev::kFiveFields + f) * 32 + e] = c;
+      }
   for (int j = 0; j < 256; ++j) {  // basis of shift(., 16*(255-j)) for thread j
     const uint32_t kj = xpow(8LL * 16 * (255 - j));
     for (int i = 0; i < 32; ++i) t[crcdev::kTabWords + j * 32 + i] = mulmod(kj, 1u << i);
@@ -174,7 +190,10 @@ hipError_t launch_matvec_crc(const MatVecJob& job, uint32_t* crc, int crc_stride
   const int stripes_per_launch = std::min(per, 65535);
   // ~1024 workgroups per launch: each folds ~11 tiles per row before its per-thread basis
   // epilogue (16 rows x 32 columns); 512 / 2048 / 4096 were 3-7 % slower (profiles/r01/crc_wgs_sweep.txt)
-  const uint32_t want = std::max<uint32_t>(1, 1024u / (uint32_t)std::min(job.nstripes, stripes_per_launch));
+#ifndef CFSEC_CRC_GROUPS
+#define CFSEC_CRC_GROUPS 1024
+#endif
+  const uint32_t want = std::max<uint32_t>(1, CFSEC_CRC_GROUPS / (uint32_t)std::min(job.nstripes, stripes_per_launch));
   uint32_t groups = std::min<uint32_t>({tiles, want, (uint32_t)crcdev::kMaxGroups});
   const uint32_t tpw = (tiles + groups - 1) / groups;
   groups = (tiles + tpw - 1) / tpw;

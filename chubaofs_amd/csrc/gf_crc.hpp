@@ -38,7 +38,9 @@ constexpr int kTile = 4096;            // bytes per row per tile: 256 threads x 
 constexpr int kMaxK = 18, kMaxM = 6, kPtrSlots = 96, kMaxGroups = 384;
 constexpr int kByteTabWords = 20 * 256;  // F0..F15: bytes of a 16-B piece;  G0..G3: register bytes
 constexpr int kNibTabWords = 40 * 16;    // N0..N31: nibbles of a 16-B piece;  H0..H7: register nibbles
-constexpr int kTabWords = kByteTabWords + kNibTabWords;  // device table block, the basis follows
+constexpr int kFiveFields = 7;           // per 32-bit word: six 5-bit fields + one 2-bit field
+constexpr int kFiveTabWords = 5 * kFiveFields * 32;  // Q(w, f): 4 piece words + the register word
+constexpr int kTabWords = kByteTabWords + kNibTabWords + kFiveTabWords;  // device table block, the basis follows
 constexpr int kBasisWords = 256 * 32;  // thread j: the 32 columns of shift(., 16*(255-j))
 constexpr int kShiftWords = 256;  // after the basis: [j] = x^(8*16*(255-j)), its column x^0 (coalesced)
 
@@ -121,6 +123,81 @@ __device__ __forceinline__ uint32_t crc_step_nib(const uint32_t* nt, uint32_t r,
   return __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(a1, a2, a3, 0x96), a4, 0u, 0x96);
 }
 
+// 5-bit tables ft (kFiveTabWords, at kByteTabWords + kNibTabWords in the device block): the same
+// step as the XOR of 35 words.  Each 32-bit word v of (d0..d3, R) is cut into fields at bits 0, 5,
+// ..., 25 (5 bits) and 30 (2 bits); Q(w, f)[e] = the step's image of word w = e << 5f, all else 0.
+// A table of at most 32 words sits in 32 distinct banks, so ds_read_b32 (2 x 32-lane groups,
+// bank = word mod 32) never conflicts: 35 LDS cycles-per-group per piece against ~20 x 3.1 for the
+// byte step (SQ_LDS_BANK_CONFLICT, profiles/r01/pmc_lds_conflicts_crc.txt) and 40 for the nibble
+// step.  Addresses cost one VALU each: the odd fields (5, 15, 25) are extracted from v & mO and
+// the even ones (10, 20, 30) from v & mE, 7 bits starting 2 below the field, whose two low bits
+// belong to a field the mask cleared -- so the extract is already the byte offset 4 * field.
+// Field 0 takes a shift + mask.
+template <int W>
+__device__ __forceinline__ void five_word(const uint32_t* ft, uint32_t v, uint32_t* t) {
+  uint32_t e = v & 0xC1F07C00u, o = v & 0x3E0F83E0u;
+  asm volatile("" : "+v"(e), "+v"(o));  // keep the masked copies (no re-formed shift + mask per field)
+  const uint32_t off[kFiveFields] = {(v << 2) & 0x7Cu,       __builtin_amdgcn_ubfe(o, 3, 7),
+                                     __builtin_amdgcn_ubfe(e, 8, 7),  __builtin_amdgcn_ubfe(o, 13, 7),
+                                     __builtin_amdgcn_ubfe(e, 18, 7), __builtin_amdgcn_ubfe(o, 23, 7),
+                                     __builtin_amdgcn_ubfe(e, 28, 4)};
+#pragma unroll
+  for (int f = 0; f < kFiveFields; ++f) t[f] = nib_word(ft + (W * kFiveFields + f) * 32, off[f]);
+}
+
+__device__ __forceinline__ uint32_t crc_step5(const uint32_t* ft, uint32_t r, const uint32_t (&d)[4]) {
+  uint32_t t[5 * kFiveFields];
+  five_word<0>(ft, d[0], t);
+  five_word<1>(ft, d[1], t + kFiveFields);
+  five_word<2>(ft, d[2], t + 2 * kFiveFields);
+  five_word<3>(ft, d[3], t + 3 * kFiveFields);
+  five_word<4>(ft, r, t + 4 * kFiveFields);
+  // 35 -> 1 in 17 three-input XORs
+  uint32_t u[12];
+#pragma unroll
+  for (int i = 0; i < 11; ++i) u[i] = __builtin_amdgcn_bitop3_b32(t[3 * i], t[3 * i + 1], t[3 * i + 2], 0x96);
+  u[11] = t[33] ^ t[34];
+  const uint32_t a0 = __builtin_amdgcn_bitop3_b32(u[0], u[1], u[2], 0x96);
+  const uint32_t a1 = __builtin_amdgcn_bitop3_b32(u[3], u[4], u[5], 0x96);
+  const uint32_t a2 = __builtin_amdgcn_bitop3_b32(u[6], u[7], u[8], 0x96);
+  const uint32_t a3 = __builtin_amdgcn_bitop3_b32(u[9], u[10], u[11], 0x96);
+  return __builtin_amdgcn_bitop3_b32(a0, a1, a2 ^ a3, 0x96);
+}
+
+// The fused product+CRC kernel's step: 5-bit tables by default (CFSEC_FUSED_STEP=0: byte tables,
+// for A/B probes).
+#ifndef CFSEC_FUSED_STEP
+#define CFSEC_FUSED_STEP 1
+#endif
+#if CFSEC_FUSED_STEP
+constexpr int kFusedTabBase = kByteTabWords + kNibTabWords, kFusedTabWords = kFiveTabWords;
+__device__ __forceinline__ uint32_t fused_step(const uint32_t* ct, uint32_t r, const uint32_t (&d)[4]) {
+  return crc_step5(ct, r, d);
+}
+#else
+constexpr int kFusedTabBase = 0, kFusedTabWords = kByteTabWords;
+__device__ __forceinline__ uint32_t fused_step(const uint32_t* ct, uint32_t r, const uint32_t (&d)[4]) {
+  return crc_step(ct, r, d);
+}
+#endif
+
+// The CRC-only kernels' step (crc32.hip, crc32block.hip): 5-bit tables by default
+// (CFSEC_CRC_ONLY_STEP=0: nibble tables, for A/B probes).
+#ifndef CFSEC_CRC_ONLY_STEP
+#define CFSEC_CRC_ONLY_STEP 1
+#endif
+#if CFSEC_CRC_ONLY_STEP
+constexpr int kOnlyTabBase = kByteTabWords + kNibTabWords, kOnlyTabWords = kFiveTabWords;
+__device__ __forceinline__ uint32_t only_step(const uint32_t* ct, uint32_t r, const uint32_t (&d)[4]) {
+  return crc_step5(ct, r, d);
+}
+#else
+constexpr int kOnlyTabBase = kByteTabWords, kOnlyTabWords = kNibTabWords;
+__device__ __forceinline__ uint32_t only_step(const uint32_t* ct, uint32_t r, const uint32_t (&d)[4]) {
+  return crc_step_nib(ct, r, d);
+}
+#endif
+
 // a * b mod P (reflected: bit 31 = x^0)
 __device__ __forceinline__ uint32_t mulmod(uint32_t a, uint32_t b) {
   uint32_t p = 0;
@@ -132,14 +209,22 @@ __device__ __forceinline__ uint32_t mulmod(uint32_t a, uint32_t b) {
 }
 
 // One tile of the product for this thread (bytes [off, off+16) of every row) plus the Horner
-// step of every checksummed row.  Full pieces take the pipelined path of lane_tile_k; the
-// thread holding the shard end (or past it) reads/writes only bytes < len and checksums the
-// piece zero-padded, which is what the negative group shift undoes.
+// step of every checksummed row.  Full pieces take the pipelined path: input rows are loaded D
+// rows ahead of the product, and the last D loads of a tile fetch the first rows of the thread's
+// next tile when that one is full too (`next`; then `pre` says those rows are already in x).  The
+// thread holding the shard end (or past it) reads/writes only bytes < len and checksums the piece
+// zero-padded, which is what the negative group shift undoes.
+#ifndef CFSEC_CRC_LOOKAHEAD
+#define CFSEC_CRC_LOOKAHEAD 2
+#endif
 template <int K, int M, bool CIN>
 __device__ __forceinline__ void crc_tile(uint64_t len, const u32x4* tab01, const uint32_t* tab2,
                                          const uint32_t* ct, const uint8_t* const (&row)[K + M],
-                                         uint32_t off, uint32_t (&R)[(CIN ? K : 0) + M]) {
+                                         uint32_t off, bool pre, bool next, uint32_t (&x)[K][4],
+                                         uint32_t (&R)[(CIN ? K : 0) + M]) {
   constexpr int RO = CIN ? K : 0;  // register of output row 0
+  constexpr int D = CFSEC_CRC_LOOKAHEAD < K ? CFSEC_CRC_LOOKAHEAD : K;
+  static_assert(K % 2 == 0 && D % 2 == 0, "row pairs");
   uint32_t acc[M][4];
 #pragma unroll
   for (int r = 0; r < M; ++r)
@@ -151,27 +236,30 @@ __device__ __forceinline__ void crc_tile(uint64_t len, const u32x4* tab01, const
       asm volatile("" : "+v"(acc[r][0]), "+v"(acc[r][1]), "+v"(acc[r][2]), "+v"(acc[r][3]));
   };
   if ((uint64_t)off + dev::kLaneBytes <= len) {
-    uint32_t x[K][4];
-    const auto load = [&](int c) {
-      const u32x4 v = dev::ld16<true>(row[c] + off);
+    const auto load = [&](int c, uint32_t o) {
+      const u32x4 v = dev::ld16<true>(row[c] + o);
       x[c][0] = v.x;
       x[c][1] = v.y;
       x[c][2] = v.z;
       x[c][3] = v.w;
     };
-    load(0);
-    load(1);
+    if (!pre)
+#pragma unroll
+      for (int c = 0; c < D; ++c) load(c, off);
 #pragma unroll
     for (int c = 0; c < K; c += 2) {
-      if (c + 2 < K) load(c + 2);
-      if (c + 3 < K) load(c + 3);
+#pragma unroll
+      for (int j = c + D; j < c + D + 2; ++j) {
+        if (j < K) load(j, off);
+        else if (next) load(j - K, off + kTile);
+      }
       __builtin_amdgcn_sched_barrier(0);
       dev::mac_pair_k<M>(acc, x[c], x[c + 1], tab01 + c * M, tab2 + c * M, tab01 + (c + 1) * M,
                          tab2 + (c + 1) * M);
       pin();
       if constexpr (CIN) {
-        R[c] = crc_step(ct, R[c], x[c]);
-        R[c + 1] = crc_step(ct, R[c + 1], x[c + 1]);
+        R[c] = fused_step(ct, R[c], x[c]);
+        R[c + 1] = fused_step(ct, R[c + 1], x[c + 1]);
         asm volatile("" : "+v"(R[c]), "+v"(R[c + 1]));
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -191,7 +279,7 @@ __device__ __forceinline__ void crc_tile(uint64_t len, const u32x4* tab01, const
         xv[3] = v.w;
       }
       dev::mac_row_k<M>(acc, xv, tab01 + c * M, tab2 + c * M);
-      if constexpr (CIN) R[c] = crc_step(ct, R[c], xv);
+      if constexpr (CIN) R[c] = fused_step(ct, R[c], xv);
     }
     if (rem)
 #pragma unroll
@@ -200,19 +288,22 @@ __device__ __forceinline__ void crc_tile(uint64_t len, const u32x4* tab01, const
                      rem);
   }
 #pragma unroll
-  for (int r = 0; r < M; ++r) R[RO + r] = crc_step(ct, R[RO + r], acc[r]);
+  for (int r = 0; r < M; ++r) R[RO + r] = fused_step(ct, R[RO + r], acc[r]);
 }
 
 // grid (groups, stripes), 256 threads.  a.k == K, a.m == M.
+#ifndef CFSEC_CRC_WPE
+#define CFSEC_CRC_WPE 4  // minimum waves per SIMD the register allocation aims for
+#endif
 template <int K, int M, bool CIN>
-__global__ __launch_bounds__(256) void gf_crc_kernel(const GfCrcArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CFSEC_CRC_WPE, 8))) void gf_crc_kernel(const GfCrcArgs a) {
   constexpr int NR = (CIN ? K : 0) + M;  // checksummed rows
   __shared__ u32x4 tab01[K * M];
   __shared__ uint32_t tab2[K * M];
-  __shared__ uint32_t ct[kByteTabWords];
+  __shared__ uint32_t ct[kFusedTabWords];
   __shared__ uint32_t red[4][NR];
   dev::build_tables<M>(K, M, a.coef, tab01, tab2);
-  for (int i = threadIdx.x; i < kByteTabWords; i += 256) ct[i] = a.tabs[i];
+  for (int i = threadIdx.x; i < kFusedTabWords; i += 256) ct[i] = a.tabs[kFusedTabBase + i];
   __syncthreads();
 
   const uint32_t g = blockIdx.x, stripe = blockIdx.y;
@@ -229,7 +320,15 @@ __global__ __launch_bounds__(256) void gf_crc_kernel(const GfCrcArgs a) {
   const uint32_t t0 = g * a.tpw;
   const uint32_t t1 = min(t0 + a.tpw, a.tiles);
   const uint32_t lanepos = threadIdx.x * dev::kLaneBytes;
-  for (uint32_t t = t0; t < t1; ++t) crc_tile<K, M, CIN>(a.len, tab01, tab2, ct, row, t * kTile + lanepos, R);
+  uint32_t x[K][4];
+  bool pre = false;
+  for (uint32_t t = t0; t < t1; ++t) {
+    const uint32_t off = t * kTile + lanepos;
+    // the next tile is full for this thread: its first rows are fetched during this one
+    const bool next = t + 1 < t1 && (uint64_t)off + kTile + dev::kLaneBytes <= a.len;
+    crc_tile<K, M, CIN>(a.len, tab01, tab2, ct, row, off, pre, next, x, R);
+    pre = next && (uint64_t)off + dev::kLaneBytes <= a.len;
+  }
 
   // move every register from this thread's last piece end to the tile end t1*4096
   const u32x4* basis = reinterpret_cast<const u32x4*>(a.tabs + kTabWords + threadIdx.x * 32);
