@@ -709,10 +709,13 @@ def other_configs(args, torch, dev, stream, cpu):
 
     rate5 = api_rate(rep5, secs)
     assert list(st5) == [0] * nb5
-    # per bid: global pass reads 16 inputs + 16 checked parities, writes 4; local pass reads 2 x 19
-    alg5 = (16 + 16 + 4 + 2 * 19) * S5
+    # per bid, one pass: reads 16 inputs + the 16 other global parities and the 2 local parities
+    # it checks, writes 2 data + 2 parity rows (the local Verify rides in the global pass: the
+    # separate AZ-local pass would re-read 2 x 19 shards)
+    alg5 = (16 + 16 + 2 + 4) * S5
     c5 = {"workload": (f"EC16P20L2 repair tasklet on one GPU: {nb5} bids x S={S5}, erased {{0,1,16,17}}, "
-                       "Reconstruct + Verify per bid in one cfsec_ec_reconstruct_batch (global fused pass + AZ-local pass)"),
+                       "Reconstruct + Verify per bid in one cfsec_ec_reconstruct_batch: one fused pass per bid (16x16-dyadic "
+                       "repair kernel; global and local parities checked in it)"),
           "data_GBps": round(N5 * S5 * nb5 * rate5 / 1e9, 1),
           "roofline_frac": round(alg5 * nb5 * rate5 / 1e9 / HBM_PEAK_GBPS, 4),
           "algorithmic_bytes_per_bid": alg5,

@@ -109,7 +109,8 @@ hipError_t launch_group_run(const Group& g, size_t t0, size_t t1, uint32_t* dfla
     job.pcmp = d->pcmp;
     job.nstripes = (int)(t1 - t0);
     job.in = g.in.data() + t0 * 16;
-    job.out = g.hout.data() + t0 * (size_t)(d->nd + 20);
+    job.e = d->e;
+    job.out = g.hout.data() + t0 * d->rows.size();
     bool uniform = true;
     for (size_t t = t0; t < t1; ++t) uniform = uniform && g.lens[t] == g.lens[t0];
     job.lens = uniform ? nullptr : g.lens.data() + t0;
@@ -224,7 +225,8 @@ Status RSEngine::set_devices(const int* devices, int n) {
   return CFSEC_OK;
 }
 
-Status RSEngine::plan_stripe(const std::vector<bool>& present, bool verify, StripePlan* plan) {
+Status RSEngine::plan_stripe(const std::vector<bool>& present, bool verify, StripePlan* plan,
+                             const ExtraRows* extra) {
   // KRS/reedsolomon.go:1453-1501: the first k present rows in index order, decode matrix from the
   // inversion cache (key: the invalid rows met before the k-th valid one).
   std::vector<int> invalid;
@@ -257,6 +259,9 @@ Status RSEngine::plan_stripe(const std::vector<bool>& present, bool verify, Stri
   if (verify)
     for (int i = k_; i < total(); ++i)
       if (present[i] && std::find(plan->in.begin(), plan->in.end(), i) == plan->in.end()) plan->out.push_back(i);
+  // extra rows over the data (LRC local parities): compared like the parity rows above
+  plan->nextra = verify && extra ? (int)extra->idx.size() : 0;
+  for (int j = 0; j < plan->nextra; ++j) plan->out.push_back(extra->idx[j]);
   plan->rows = Matrix((int)plan->out.size(), k_);
   const GF& gf = GF::get();
   for (size_t o = 0; o < plan->out.size(); ++o) {
@@ -265,7 +270,8 @@ Status RSEngine::plan_stripe(const std::vector<bool>& present, bool verify, Stri
     if (idx < k_) {
       std::memcpy(dst, dec.row(idx), k_);
     } else {
-      const uint8_t* p = parity_.row(idx - k_);
+      const int xo = (int)o - ((int)plan->out.size() - plan->nextra);  // extra row, or < 0
+      const uint8_t* p = xo >= 0 ? extra->rows.row(xo) : parity_.row(idx - k_);
       for (int c = 0; c < k_; ++c) {
         uint8_t v = 0;
         for (int j = 0; j < k_; ++j) v ^= gf.mul(p[j], dec.at(j, c));
@@ -273,7 +279,7 @@ Status RSEngine::plan_stripe(const std::vector<bool>& present, bool verify, Stri
       }
     }
   }
-  plan_dy16(present, dec, plan);
+  plan_dy16(present, dec, plan, plan->nextra ? extra : nullptr);
   return CFSEC_OK;
 }
 
@@ -293,27 +299,36 @@ bool parity_dy16(const Matrix& p) {
 }
 }  // namespace
 
-void RSEngine::plan_dy16(const std::vector<bool>& present, const Matrix& dec, StripePlan* plan) const {
+void RSEngine::plan_dy16(const std::vector<bool>& present, const Matrix& dec, StripePlan* plan,
+                         const ExtraRows* extra) const {
   plan->dy16.reset();
   static const bool off = std::getenv("CFSEC_NO_DY16_REPAIR") != nullptr;  // A/B switch
   if (off || k_ != 16 || m_ != 20 || !parity_dy16(parity_)) return;
+  const int e = extra ? (int)extra->idx.size() : 0;
+  if (e != 0 && e != 2) return;  // kernels: 0 or 2 extra rows (EC16P20L2's two local parities)
   auto d = std::make_shared<Dy16Plan>();
   for (int i = 0; i < k_; ++i)
     if (!present[i]) d->rows.push_back(i);
   d->nd = (int)d->rows.size();
-  // products: 16 per decode row + 117 for the 20 parity rows, against 16 per output row
-  if (d->nd > 4 || 16 * d->nd + 117 >= 16 * (int)plan->out.size()) return;
+  d->e = e;
+  // products: 16 per decode row + 117 for the 20 parity rows + 16 per extra row, against 16 per
+  // output row
+  if (d->nd > 4 || 16 * d->nd + 117 + 16 * e >= 16 * (int)plan->out.size()) return;
   for (int r = 0; r < m_; ++r) d->rows.push_back(k_ + r);
+  for (int j = 0; j < e; ++j) d->rows.push_back(extra->idx[j]);
   int slot = 0, j = 0;
   for (int i = 0; i < k_; ++i) d->src[i] = present[i] ? (uint8_t)slot++ : (uint8_t)(16 + j++);
+  const int nx0 = (int)plan->out.size() - plan->nextra;
   for (size_t o = 0; o < plan->out.size(); ++o) {
     const int idx = plan->out[o];
     if (idx < k_) continue;
-    (o < (size_t)plan->nstore ? d->pstore : d->pcmp) |= 1u << (idx - k_);
+    const int bit = (int)o >= nx0 ? 20 + ((int)o - nx0) : idx - k_;
+    (o < (size_t)plan->nstore ? d->pstore : d->pcmp) |= 1u << bit;
   }
-  d->coef = Matrix(20 + d->nd, 16);
+  d->coef = Matrix(20 + e + d->nd, 16);
   std::memcpy(d->coef.v.data(), parity_.v.data(), 20 * 16);
-  for (int q = 0; q < d->nd; ++q) std::memcpy(d->coef.row(20 + q), dec.row(d->rows[q]), 16);
+  for (int q = 0; q < e; ++q) std::memcpy(d->coef.row(20 + q), extra->rows.row(q), 16);
+  for (int q = 0; q < d->nd; ++q) std::memcpy(d->coef.row(20 + e + q), dec.row(d->rows[q]), 16);
   plan->dy16 = std::move(d);
 }
 
@@ -372,7 +387,8 @@ Status RSEngine::reconstruct_stripes(cfsec_shard* const* stripes, int nst, int m
 }
 
 void RSEngine::plan_reconstruct_tasks(cfsec_shard* const* stripes, int nst, bool verify, int* status, int phase,
-                                      int owner0, PlanStore* store, std::vector<StripeTask>* tasks) {
+                                      int owner0, PlanStore* store, std::vector<StripeTask>* tasks,
+                                      const ExtraRows* extra, const std::vector<bool>* fuse) {
   StripePlan* vplan = nullptr;  // Verify as an encode-matrix pass (split_verify)
   std::map<const StripePlan*, StripePlan*> store_only;
   tasks->reserve(tasks->size() + (size_t)nst);
@@ -397,7 +413,10 @@ void RSEngine::plan_reconstruct_tasks(cfsec_shard* const* stripes, int nst, bool
       status[s] = CFSEC_ERR_TOO_FEW_SHARDS;
       continue;
     }
-    if (np == total() && (!verify || m_ == 0)) continue;  // Reconstruct of a full stripe is a no-op
+    const bool fx = verify && extra && fuse && (*fuse)[s];
+    if (np == total() && (!verify || (m_ == 0 && !fx))) continue;  // Reconstruct of a full stripe is a no-op
+    // plans are keyed by the present shards, plus whether the extra rows ride along
+    present.push_back(fx);
     if (!last_plan || present != last_present) {
       last_plan = &store->by_pattern[present];
       last_present = present;
@@ -405,14 +424,18 @@ void RSEngine::plan_reconstruct_tasks(cfsec_shard* const* stripes, int nst, bool
     auto& plan = *last_plan;
     if (!plan) {
       plan.reset(new StripePlan());
-      st = plan_stripe(present, verify, plan.get());
+      present.pop_back();
+      st = plan_stripe(present, verify, plan.get(), fx ? extra : nullptr);
+      present.push_back(fx);
       if (st != CFSEC_OK) {
         store->by_pattern.erase(present);
+        present.pop_back();
         last_plan = nullptr;
         status[s] = st;
         continue;
       }
     }
+    present.pop_back();
     for (int r = 0; r < plan->nstore && st == CFSEC_OK; ++r)
       if (!sh[plan->out[r]].data || sh[plan->out[r]].cap < S) st = CFSEC_ERR_INVALID_ARG;
     for (int c : plan->in)
@@ -456,7 +479,7 @@ void RSEngine::plan_reconstruct_tasks(cfsec_shard* const* stripes, int nst, bool
 
 bool RSEngine::split_verify(const StripePlan& p) const {
   const int checks = (int)p.out.size() - p.nstore;
-  if (checks <= 0) return false;
+  if (checks <= 0 || p.nextra > 0) return false;
   static const int mode = [] {
     const char* e = getenv("CFSEC_VERIFY_SPLIT");
     return e ? atoi(e) : -1;
@@ -766,7 +789,28 @@ Status LrcEncoder::reconstruct_batch(cfsec_shard* shards, int n, int nbids, cons
   PlanStore gstore, lstore;
   std::vector<StripeTask> tasks;
   std::vector<int> st1(stripes.size());
-  engine_->plan_reconstruct_tasks(stripes.data(), (int)stripes.size(), verify, st1.data(), 0, 0, &gstore, &tasks);
+  // A bid with no bad local shard has its local Verify done in the global pass: every local
+  // parity is a fixed row over the data (fused_, as in the fused LRC encode), compared there --
+  // the local pass would re-read the 2 x 19 shards of the AZs (C5: 74 -> 38 shard reads per bid).
+  ExtraRows extra;
+  std::vector<bool> fuse(stripes.size(), false);
+  if (verify && L > 0) {
+    extra.rows = Matrix(L, N);
+    std::memcpy(extra.rows.v.data(), fused_.row(M), (size_t)L * N);
+    for (int j = 0; j < L; ++j) extra.idx.push_back(N + M + j);
+    for (size_t i = 0; i < stripes.size(); ++i) {
+      const cfsec_shard* sh = stripes[i];
+      const int b = pos[i];
+      bool ok = true;
+      for (int j = bad_off[b]; j < bad_off[b + 1]; ++j) ok = ok && bad[j] < N + M;
+      size_t S = 0;
+      for (int g = 0; g < N + M && !S; ++g) S = sh[g].len;
+      for (int j = 0; j < L; ++j) ok = ok && sh[N + M + j].data && sh[N + M + j].len == S && S != 0;
+      fuse[i] = ok;
+    }
+  }
+  engine_->plan_reconstruct_tasks(stripes.data(), (int)stripes.size(), verify, st1.data(), 0, 0, &gstore, &tasks,
+                                  verify && L > 0 ? &extra : nullptr, &fuse);
   int lphase = 1;
   for (auto& t : tasks) lphase = std::max(lphase, t.phase + 1);
   ph.reset(new HostTimer("  local views + plan"));
@@ -796,7 +840,7 @@ Status LrcEncoder::reconstruct_batch(cfsec_shard* shards, int n, int nbids, cons
       }
     for (int a = 0; a < AZ; ++a) {
       const bool has_bad = !local_bad[a].empty();
-      if (!has_bad && !verify) continue;
+      if (!has_bad && (!verify || fuse[i])) continue;  // nothing to rebuild; Verify done (or not asked)
       const size_t at = views[a].size();
       for (int g : idc[a]) views[a].push_back(sh[g]);
       cfsec_shard* ls = views[a].data() + at;

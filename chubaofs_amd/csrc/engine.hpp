@@ -123,10 +123,19 @@ struct ReconPlan {
 // (Dy16RepairJob): missing data rows from decode rows, then all 20 parity rows from the data.
 struct Dy16Plan {
   int nd = 0;             // missing data rows
-  std::vector<int> rows;  // output shard indices: the nd missing data rows, parity rows k .. k+19
+  int e = 0;              // extra rows (ExtraRows) after the 20 parity rows
+  std::vector<int> rows;  // output shard indices: the nd missing data rows, parity rows k .. k+19, extras
   uint8_t src[16] = {};
   uint32_t pstore = 0, pcmp = 0;
-  Matrix coef;  // (20 + nd) x 16: parity matrix, decode rows
+  Matrix coef;  // (20 + e + nd) x 16: parity matrix, extra rows, decode rows
+};
+
+// Rows beyond a code's own that a Reconstruct + Verify pass can check on the way: row j over the
+// k data columns, compared with shard idx[j] of the stripe's shard array.  The LRC local parities
+// (LrcEncoder: the global pass also does the per-AZ local Verify, lrcencoder.go:89-131).
+struct ExtraRows {
+  Matrix rows;
+  std::vector<int> idx;
 };
 
 // The product one stripe of a heterogeneous batch needs (batch.cpp): rows x shards[in]; rows
@@ -136,6 +145,7 @@ struct StripePlan {
   std::vector<int> in;
   std::vector<int> out;
   int nstore = 0;
+  int nextra = 0;  // the last nextra rows of out are ExtraRows, compared
   Matrix rows;  // out.size() x in.size()
   std::shared_ptr<const Dy16Plan> dy16;  // set where that product is the cheaper one
 };
@@ -215,15 +225,19 @@ class RSEngine {
   // The planning half of reconstruct_stripes: checks every stripe (errors to status[s]), sets the
   // rebuilt shards' lengths and appends the tasks (phase `phase`, and phase + 1 for a split Verify)
   // that run_stripes executes; owner of stripe s = owner0 + s.
+  // extra / fuse (optional): stripe s also compares the ExtraRows when fuse[s] (and verify).
   void plan_reconstruct_tasks(cfsec_shard* const* stripes, int nst, bool verify, int* status, int phase,
-                              int owner0, PlanStore* store, std::vector<StripeTask>* tasks);
+                              int owner0, PlanStore* store, std::vector<StripeTask>* tasks,
+                              const ExtraRows* extra = nullptr, const std::vector<bool>* fuse = nullptr);
   // Run the tasks' products (device memory, pinned host memory in place, pageable host memory
   // through double-buffered staging), tasks partitioned over the devices.
   Status run_stripes(std::vector<StripeTask>& tasks, int mem);
   // Plan of a Reconstruct (+ Verify) over the present shards.
-  Status plan_stripe(const std::vector<bool>& present, bool verify, StripePlan* plan);
+  Status plan_stripe(const std::vector<bool>& present, bool verify, StripePlan* plan,
+                     const ExtraRows* extra = nullptr);
   // plan->dy16 where the code and the erasure pattern make that product cheaper (batch.cpp).
-  void plan_dy16(const std::vector<bool>& present, const Matrix& dec, StripePlan* plan) const;
+  void plan_dy16(const std::vector<bool>& present, const Matrix& dec, StripePlan* plan,
+                 const ExtraRows* extra = nullptr) const;
   // Run a plan's Verify as a separate encode-matrix pass instead of its compared rows.
   bool split_verify(const StripePlan& p) const;
 

@@ -29,23 +29,33 @@ hipError_t launch_one(MatVecMode mode, const dev::GfArgs& a, unsigned ns, hipStr
 }
 }  // namespace
 
-template <int ND>
+template <int ND, int E>
 __global__ __launch_bounds__(256) void gf_dy16_repair_kernel(const dev::GfArgs a) {
-  dev::repair_dy16<ND, true, CFSEC_DY16_W>(a);
+  dev::repair_dy16<ND, E, true, CFSEC_DY16_W>(a);
 }
 
-hipError_t launch_dy16_repair_args(int nd, const dev::GfArgs& a, unsigned ns, hipStream_t st) {
-  constexpr uint64_t tile = 256 * 4 * CFSEC_DY16_W;
-  const dim3 grid((unsigned)((a.len + tile - 1) / tile), ns);
+template <int E>
+hipError_t launch_repair_e(int nd, const dev::GfArgs& a, dim3 grid, hipStream_t st) {
   switch (nd) {
-    case 0: hipLaunchKernelGGL((gf_dy16_repair_kernel<0>), grid, dim3(256), 0, st, a); break;
-    case 1: hipLaunchKernelGGL((gf_dy16_repair_kernel<1>), grid, dim3(256), 0, st, a); break;
-    case 2: hipLaunchKernelGGL((gf_dy16_repair_kernel<2>), grid, dim3(256), 0, st, a); break;
-    case 3: hipLaunchKernelGGL((gf_dy16_repair_kernel<3>), grid, dim3(256), 0, st, a); break;
-    case 4: hipLaunchKernelGGL((gf_dy16_repair_kernel<4>), grid, dim3(256), 0, st, a); break;
+    case 0: hipLaunchKernelGGL((gf_dy16_repair_kernel<0, E>), grid, dim3(256), 0, st, a); break;
+    case 1: hipLaunchKernelGGL((gf_dy16_repair_kernel<1, E>), grid, dim3(256), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((gf_dy16_repair_kernel<2, E>), grid, dim3(256), 0, st, a); break;
+    case 3: hipLaunchKernelGGL((gf_dy16_repair_kernel<3, E>), grid, dim3(256), 0, st, a); break;
+    case 4: hipLaunchKernelGGL((gf_dy16_repair_kernel<4, E>), grid, dim3(256), 0, st, a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
+}
+
+// ne extra rows: 0, or 2 (EC16P20L2's local parities checked in the global pass)
+hipError_t launch_dy16_repair_args(int nd, int ne, const dev::GfArgs& a, unsigned ns, hipStream_t st) {
+  constexpr uint64_t tile = 256 * 4 * CFSEC_DY16_W;
+  const dim3 grid((unsigned)((a.len + tile - 1) / tile), ns);
+  switch (ne) {
+    case 0: return launch_repair_e<0>(nd, a, grid, st);
+    case 2: return launch_repair_e<2>(nd, a, grid, st);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 hipError_t launch_dy16(int m, MatVecMode mode, const dev::GfArgs& a, unsigned ns, hipStream_t st) {

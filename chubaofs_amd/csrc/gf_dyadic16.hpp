@@ -256,18 +256,22 @@ __device__ __forceinline__ void matvec_dy16(const GfArgs& a) {
 // Reconstruct writes is stored, every one its Verify reads is compared, the rest dropped.  The plain
 // reconstruct-and-verify product over the first 16 present rows takes 16 per output row: 320 for
 // the 4-erasure repair of a tasklet bid (2 data + 2 parity missing, 16 compared).
-// Args: coef rows 0..19 the parity matrix, rows 20.. the decode rows; ptr per stripe: the 16
-// inputs, then ND + 20 outputs (the missing data rows, parity rows 0..19); src[i] = the input slot
-// of data row i, or 16 + j for missing data row j; pstore / pcmp: parity rows stored / compared.
-template <int ND, bool PIN = true, int W = 2>
+// E extra rows over the data follow the parity rows (EC16P20L2: its 2 local parities, so the
+// global pass also does the local Verify, lrcencoder.go:89-131): E more plain rows of the 16 data
+// chunks, like the fused LRC encode (dy16_rows).
+// Args: coef rows 0..19 the parity matrix, rows 20..20+E-1 the extra rows, then the decode rows;
+// ptr per stripe: the 16 inputs, then ND + 20 + E outputs (the missing data rows, parity rows
+// 0..19, the extra rows); src[i] = the input slot of data row i, or 16 + j for missing data row j;
+// pstore / pcmp: parity (bits 0..19) and extra (20..) rows stored / compared.
+template <int ND, int E, bool PIN = true, int W = 2>
 __device__ __forceinline__ void repair_dy16(const GfArgs& a) {
-  constexpr int K = 16, NDY = kDy16Leaves + 36, NT = NDY + K * (ND > 0 ? ND : 1), MO = ND + 20;
+  constexpr int K = 16, NDY = kDy16Leaves + 36 + K * E, NT = NDY + K * (ND > 0 ? ND : 1), MO = ND + 20 + E;
   constexpr uint32_t kLane = 4 * W;
   __shared__ u32x4 tab01[NT];
   __shared__ uint32_t tab2[NT];
-  build_dy16_tables<1, 0>(a.coef, tab01, tab2);
+  build_dy16_tables<1, E>(a.coef, tab01, tab2);
   for (int i = threadIdx.x; i < K * ND; i += (int)blockDim.x)  // slot NDY + c * ND + j: decode row j, column c
-    coef_tables(a.coef[(20 + i % ND) * K + i / ND], tab01[NDY + i], tab2[NDY + i]);
+    coef_tables(a.coef[(20 + E + i % ND) * K + i / ND], tab01[NDY + i], tab2[NDY + i]);
   __syncthreads();
 
   const uint32_t stripe = blockIdx.y, tile = blockIdx.x;
@@ -327,7 +331,7 @@ __device__ __forceinline__ void repair_dy16(const GfArgs& a) {
     }
     const uint32_t pstore = a.pstore, pcmp = a.pcmp;
     const uint8_t* spare = in[0] + sbase + off;  // just read: what rows not compared load instead
-    dy16_rows<1, 0, PIN, W>(x, tab01, tab2, [&](int r, const uint32_t (&v)[W]) {
+    dy16_rows<1, E, PIN, W>(x, tab01, tab2, [&](int r, const uint32_t (&v)[W]) {
       // every row loads (its own chunk if compared, else the input chunk above, a cache hit) and
       // the mask picks: no branch around the loads, so the compiler issues a group of them before
       // the first wait (a branch per row exposed one load latency per compared row: +45 % time)

@@ -250,9 +250,9 @@ hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
 
 hipError_t launch_dy16_repair(const Dy16RepairJob& job, hipStream_t stream) {
   using dev::kPtrSlots;
-  const int nd = job.nd, mo = nd + 20;
-  if (nd < 0 || nd > 4 || job.nstripes < 0 || !job.coef || !job.in || !job.out || (job.pcmp && !job.flags) ||
-      (job.pstore | job.pcmp) >> 20)
+  const int nd = job.nd, ne = job.e, mo = nd + 20 + ne;
+  if (nd < 0 || nd > 4 || (ne != 0 && ne != 2) || job.nstripes < 0 || !job.coef || !job.in || !job.out ||
+      (job.pcmp && !job.flags) || (job.pstore | job.pcmp) >> (20 + ne))
     return hipErrorInvalidValue;
   if (job.nstripes == 0) return hipSuccess;
   uint64_t maxlen = job.len;
@@ -284,7 +284,7 @@ hipError_t launch_dy16_repair(const Dy16RepairJob& job, hipStream_t stream) {
   a.pstore = job.pstore;
   a.pcmp = job.pcmp;
   std::memcpy(a.src, job.src, 16);
-  std::memcpy(a.coef, job.coef, (size_t)(20 + nd) * 16);
+  std::memcpy(a.coef, job.coef, (size_t)(20 + ne + nd) * 16);
   for (int s0 = 0; s0 < job.nstripes; s0 += per) {
     const int ns = std::min(per, job.nstripes - s0);
     const int tab = sstride ? 1 : ns;
@@ -306,7 +306,7 @@ hipError_t launch_dy16_repair(const Dy16RepairJob& job, hipStream_t stream) {
       for (int c = 0; c < 16; ++c) a.ptr[s * 16 + c] = job.in[(size_t)(s0 + s) * 16 + c];
       for (int r = 0; r < mo; ++r) a.ptr[tab * 16 + s * mo + r] = job.out[(size_t)(s0 + s) * mo + r];
     }
-    const hipError_t e = launch_dy16_repair_args(nd, a, (unsigned)ns, stream);
+    const hipError_t e = launch_dy16_repair_args(nd, ne, a, (unsigned)ns, stream);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;

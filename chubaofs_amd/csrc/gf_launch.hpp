@@ -97,7 +97,7 @@ inline DyPlan dyadic_plan(const uint8_t* coef, int m, int k) {
 hipError_t launch_dy16(int m, MatVecMode mode, const dev::GfArgs& a, unsigned ns, hipStream_t st);
 
 // repair_dy16 on a GfArgs block (gf_dy16.hip); launch_dy16_repair (gf_kernels.hip) fills it.
-hipError_t launch_dy16_repair_args(int nd, const dev::GfArgs& a, unsigned ns, hipStream_t st);
+hipError_t launch_dy16_repair_args(int nd, int ne, const dev::GfArgs& a, unsigned ns, hipStream_t st);
 
 inline bool dyadic16_plan(const uint8_t* coef, int m, int k) {
   if (k != 16 || (m != 20 && m != 22)) return false;

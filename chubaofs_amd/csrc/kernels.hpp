@@ -41,14 +41,15 @@ struct MatVecJob {
 // row from the 16 data rows, stored (pstore bit r) or compared (pcmp bit r, mismatch -> flags).
 struct Dy16RepairJob {
   int nd = 0;                          // missing data rows
-  const uint8_t* coef = nullptr;       // host: parity matrix (20 x 16), then the nd decode rows (nd x 16)
+  int e = 0;                           // extra rows over the data after the parity rows (0 or 2)
+  const uint8_t* coef = nullptr;       // host: parity matrix (20 x 16), the e extra rows, the nd decode rows
   uint8_t src[16] = {};                // data row i: input slot, or 16 + j for missing data row j
-  uint32_t pstore = 0, pcmp = 0;       // parity rows stored / compared
+  uint32_t pstore = 0, pcmp = 0;       // parity (then extra) rows stored / compared
   size_t len = 0;
   const uint64_t* lens = nullptr;      // host [nstripes] per-stripe lengths, or NULL
   int nstripes = 0;
   const uint8_t* const* in = nullptr;  // host [nstripes * 16]: the first 16 present rows
-  uint8_t* const* out = nullptr;       // host [nstripes * (nd + 20)]: missing data rows, parity 0..19
+  uint8_t* const* out = nullptr;       // host [nstripes * (nd + 20 + e)]: missing data rows, parity 0..19, extras
   uint32_t* flags = nullptr;           // device [nstripes]
 };
 hipError_t launch_dy16_repair(const Dy16RepairJob& job, hipStream_t stream);

@@ -297,6 +297,52 @@ def test_ec_reconstruct_batch_matches_repair_loop(mode, memory):
                 assert np.array_equal(host(bids[b][i]), shards[i]), (b, bads[b], i)
 
 
+@pytest.mark.parametrize("memory", ["host", "device"])
+@pytest.mark.parametrize("mode", [cm.EC6P10L2, cm.EC16P20L2])
+def test_ec_reconstruct_batch_local_verify_in_global_pass(mode, memory):
+    """Bids with no bad local shard have their local Verify done in the global pass (the local
+    parities are compared there as rows over the data): every outcome equals the per-bid
+    Reconstruct + Verify calls -- a corrupted local parity of either AZ, a corrupted global parity,
+    a clean bid, and bids whose bad set holds a local parity (rebuilt by the local pass) mixed into
+    one tasklet; C5's pattern {0, 1, 16, 17} for EC16P20L2 runs the 16x16-dyadic repair kernel."""
+    t = cm.GetTactic(mode)
+    enc = ec_new(mode)
+    total = t.N + t.M + t.L
+    base = [0, 1, 16, 17] if mode == cm.EC16P20L2 else [0, 7]
+    cases = [("clean", base), ("local0", base), ("local1", base), ("global", base),
+             ("clean", base + [total - 1]), ("local0", base + [total - 1]), ("data", base)]
+    bids, bads, want = [], [], []
+    for b, (corrupt, bad) in enumerate(cases):
+        size = [262144, 4097, 65, 2048, 23, 1024, 777][b]
+        good = ec_full_codeword(enc, t, size, 40 + b)
+        src = [x.copy() for x in good]
+        at = (size * (b + 1)) // 8
+        if corrupt == "local0":
+            src[t.N + t.M][at] ^= 0x5A
+        elif corrupt == "local1":
+            src[t.N + t.M + t.L - 1][at] ^= 0x21
+        elif corrupt == "global":
+            src[t.N + t.M - 1][at] ^= 0x80
+        elif corrupt == "data":
+            src[t.N - 1][at] ^= 0x01  # an input: the rebuilt rows follow it, some check fails
+        want.append(sequential(enc, src, bad))
+        work = to_mem(src, memory)
+        for i in bad:
+            if memory == "device":
+                work[i].zero_()
+            else:
+                work[i][:] = 0
+        bids.append(work)
+        bads.append(bad)
+    status = enc.ReconstructBatch(bids, bads)
+    for b, (st, shards) in enumerate(want):
+        exp = 0 if cases[b][0] == "clean" else _lib.ErrVerify.status
+        assert st == exp, (b, cases[b], st)
+        assert status[b] == st, (b, cases[b], status[b], st)
+        for i in range(total):
+            assert np.array_equal(host(bids[b][i]), shards[i]), (b, cases[b], i)
+
+
 @pytest.mark.parametrize("mode", [cm.EC6P10L2, cm.EC16P20L2])
 def test_ec_reconstruct_batch_local_stripes(mode):
     """AZ-local repair (lrcencoder.go:147-152): a batch of local stripes (n = local stripe size)."""
