@@ -110,6 +110,8 @@ SIGNATURES = {
     "cfsec_ec_reconstruct_data": ([_V, P_SHARD, _I, _V, _I, _I, _V], _I),
     "cfsec_ec_verify": ([_V, P_SHARD, _I, _I, _V, _P(_I)], _I),
     "cfsec_ec_shards_in_idc": ([_V, _I, _V, _I, _P(_I)], _I),
+    "cfsec_ec_repair_rows": ([_V, _V, _I, _V, _I, _V, _V], _I),
+    "cfsec_ec_matvec_batch": ([_V, _V, _I, _V, _S, _I, _V], _I),
     "cfsec_ec_set_devices": ([_V, _V, _I], _I),
     "cfsec_ec_encode_batch": ([_V, P_SHARD, _I, _I, _I, _V], _I),
     "cfsec_ec_reconstruct_batch": ([_V, P_SHARD, _I, _I, _V, _V, _I, _I, _V], _I),

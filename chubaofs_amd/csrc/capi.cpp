@@ -432,6 +432,18 @@ int cfsec_ec_encode_batch(cfsec_ec* h, cfsec_shard* shards, int n, int nstripes,
   return guarded([&] { return h->e->encode_batch(shards, n, nstripes, mem, status); });
 }
 
+int cfsec_ec_repair_rows(cfsec_ec* h, const int* bad_idx, int nbad, const int* want, int nwant, int* in_idx,
+                         uint8_t* rows) {
+  if (!h) return CFSEC_ERR_INVALID_ARG;
+  return guarded([&] { return h->e->repair_rows(bad_idx, nbad, want, nwant, in_idx, rows); });
+}
+
+int cfsec_ec_matvec_batch(cfsec_ec* h, const uint8_t* coef, int rows, uint8_t* const* ptrs, size_t shard_size,
+                          int nstripes, void* stream) {
+  if (!h) return CFSEC_ERR_INVALID_ARG;
+  return guarded([&] { return h->e->matvec_batch(coef, rows, ptrs, shard_size, nstripes, as_stream(stream)); });
+}
+
 int cfsec_ec_shards_in_idc(const cfsec_ec* h, int idx, int* out, int out_cap, int* count) {
   if (!h || !count) return CFSEC_ERR_INVALID_ARG;
   const std::vector<int> v = h->e->shards_in_idc(idx);

@@ -724,6 +724,31 @@ Status RSEngine::encode_batch(uint8_t* const* ptrs, size_t S, int nstripes, hipS
   return hip_status(launch_matvec(job, stream), "launch_matvec(encode_batch)");
 }
 
+Status RSEngine::matvec_batch(const uint8_t* coef, int rows, uint8_t* const* ptrs, size_t S, int nstripes,
+                              hipStream_t stream) {
+  if (!ctx_) return CFSEC_ERR_DEVICE;
+  if (!coef || !ptrs || nstripes < 0 || rows < 0 || rows > 256) return CFSEC_ERR_INVALID_ARG;
+  if (rows == 0 || nstripes == 0 || S == 0) return CFSEC_OK;
+  const size_t w = (size_t)k_ + rows;
+  std::vector<const uint8_t*> in(size_t(nstripes) * k_);
+  std::vector<uint8_t*> out(size_t(nstripes) * rows);
+  for (int s = 0; s < nstripes; ++s) {
+    for (int c = 0; c < k_; ++c) in[size_t(s) * k_ + c] = ptrs[s * w + c];
+    for (int r = 0; r < rows; ++r) out[size_t(s) * rows + r] = ptrs[s * w + k_ + r];
+  }
+  DeviceGuard g(ctx_->device());
+  if (!g.ok()) return hip_status(hipErrorInvalidDevice, "hipSetDevice");
+  MatVecJob job;
+  job.k = k_;
+  job.m = rows;
+  job.coef = coef;
+  job.len = S;
+  job.nstripes = nstripes;
+  job.in = in.data();
+  job.out = out.data();
+  return hip_status(launch_matvec(job, stream), "launch_matvec(matvec_batch)");
+}
+
 Status RSEngine::verify_batch(uint8_t* const* ptrs, size_t S, int nstripes, uint32_t* flags,
                               hipStream_t stream) {
   if (!ctx_) return CFSEC_ERR_DEVICE;
@@ -976,6 +1001,56 @@ Status ECEncoder::reconstruct_data(cfsec_shard* shards, int n, const int* bad, i
   if (st != CFSEC_OK) return st;
   Slot slot(pool_.get());
   return engine_->reconstruct(shards, n, true, mem, s);
+}
+
+bool ECEncoder::row_over_data(int g, uint8_t* dst) const {
+  const int N = t_.n, M = t_.m;
+  if (g < 0 || g >= N + M) return false;
+  for (int c = 0; c < N; ++c) dst[c] = g < N ? uint8_t(g == c) : engine_->matrix().at(g, c);
+  return true;
+}
+
+bool LrcEncoder::row_over_data(int g, uint8_t* dst) const {
+  const int N = t_.n, M = t_.m, L = t_.l;
+  if (g < N + M) return ECEncoder::row_over_data(g, dst);
+  if (g >= N + M + L) return false;
+  std::memcpy(dst, fused_.row(M + g - N - M), N);  // lrcencoder.go: the local parity over the data
+  return true;
+}
+
+Status ECEncoder::repair_rows(const int* bad, int nbad, const int* want, int nwant, int* in, uint8_t* rows) {
+  const int N = t_.n, M = t_.m, L = t_.l;
+  if ((nbad && !bad) || nbad < 0 || nwant < 0 || (nwant && (!want || !rows)) || !in) return CFSEC_ERR_INVALID_ARG;
+  std::vector<bool> present(N + M, true);
+  for (int i = 0; i < nbad; ++i) {
+    if (bad[i] < 0 || bad[i] >= N + M + L) return CFSEC_ERR_INVALID_ARG;
+    if (bad[i] < N + M) present[bad[i]] = false;
+  }
+  ReconPlan rp;
+  Status st = engine_->plan_reconstruct(present, false, &rp);
+  if (st != CFSEC_OK) return st;
+  // D: the data over the N inputs (unit rows for surviving data, decode rows for the missing)
+  Matrix D(N, N);
+  for (int i = 0; i < N; ++i) {
+    const auto v = std::find(rp.valid.begin(), rp.valid.end(), i);
+    const auto o = std::find(rp.outputs.begin(), rp.outputs.end(), i);
+    if (v != rp.valid.end()) D.at(i, (int)(v - rp.valid.begin())) = 1;
+    else if (o != rp.outputs.end()) std::memcpy(D.row(i), rp.rows.row((int)(o - rp.outputs.begin())), N);
+    else return CFSEC_ERR_INVALID_ARG;
+  }
+  for (int c = 0; c < N; ++c) in[c] = rp.valid[c];
+  const GF& gf = GF::get();
+  std::vector<uint8_t> g(N);
+  for (int w = 0; w < nwant; ++w) {
+    if (!row_over_data(want[w], g.data())) return CFSEC_ERR_INVALID_ARG;
+    uint8_t* dst = rows + (size_t)w * N;
+    for (int c = 0; c < N; ++c) {
+      uint8_t v = 0;
+      for (int j = 0; j < N; ++j) v ^= gf.mul(g[j], D.at(j, c));
+      dst[c] = v;
+    }
+  }
+  return CFSEC_OK;
 }
 
 std::vector<int> ECEncoder::shards_in_idc(int idx) const {

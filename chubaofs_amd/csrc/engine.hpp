@@ -198,6 +198,10 @@ class RSEngine {
                       hipStream_t stream);
   Status reconstruct_batch(uint8_t* const* ptrs, size_t S, int nstripes, const int* erased,
                            int nerased, bool data_only, hipStream_t stream);
+  // outputs = coef (rows x k) x inputs for every stripe of a device batch: ptrs[s*(k+rows) ..] =
+  // the k inputs, then the rows outputs (any rows, e.g. ECEncoder::repair_rows).
+  Status matvec_batch(const uint8_t* coef, int rows, uint8_t* const* ptrs, size_t S, int nstripes,
+                      hipStream_t stream);
   // The same with crc32.ChecksumIEEE of the shards (fused into the kernel where supported):
   // crcs = device [nstripes * total()]; encode checksums every shard, reconstruct the rebuilt ones
   // (other words 0).
@@ -301,6 +305,14 @@ class ECEncoder {
   virtual Status verify(cfsec_shard* shards, int n, int mem, hipStream_t s, bool* ok);
   virtual std::vector<int> shards_in_idc(int idx) const;
   const cfsec_tactic& tactic() const { return t_; }
+  // Repair over survivors held elsewhere (chubaofs_amd/repair.py ships only the first N present
+  // global shards): in[0..N) = the first N global shards not in bad (KRS/reedsolomon.go:1453-1465),
+  // rows[w * N ..] = shard want[w] (data, global parity, or an LRC local parity) over them.
+  Status repair_rows(const int* bad, int nbad, const int* want, int nwant, int* in, uint8_t* rows);
+  Status matvec_batch(const uint8_t* coef, int rows, uint8_t* const* ptrs, size_t S, int nstripes,
+                      hipStream_t stream) {
+    return engine_->matvec_batch(coef, rows, ptrs, S, nstripes, stream);
+  }
   // Devices the batch entry points spread bids over (batch.cpp).
   virtual Status set_devices(const int* devices, int n);
   // blobnode's repair step over a batch of bids (work_shard_recover.go:708-771): for bid b, the
@@ -314,6 +326,8 @@ class ECEncoder {
   virtual Status encode_batch(cfsec_shard* shards, int n, int nstripes, int mem, int* status);
 
  protected:
+  // Shard index g (< N + M + L) as a row over the N data shards.
+  virtual bool row_over_data(int g, uint8_t* dst) const;
   struct Slot {
     explicit Slot(BlockingCount* p) : p_(p) { p_->acquire(); }
     ~Slot() { p_->release(); }
@@ -338,6 +352,9 @@ class LrcEncoder : public ECEncoder {
   Status reconstruct_batch(cfsec_shard* shards, int n, int nbids, const int* bad, const int* bad_off, int mem,
                            bool verify, int* status) override;
   Status encode_batch(cfsec_shard* shards, int n, int nstripes, int mem, int* status) override;
+
+ protected:
+  bool row_over_data(int g, uint8_t* dst) const override;
 
  private:
   friend class ECEncoder;

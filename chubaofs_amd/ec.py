@@ -165,6 +165,26 @@ class Encoder:
         shards[b:b + len(tail)] = tail
         return list(shards[idx * ln:b + len(tail)])
 
+    def repair_rows(self, bad, want):
+        """cfsec_ec_repair_rows: (the N input shard indices a Reconstruct decodes from with `bad`
+        lost, [rows over them, one bytes object of N per wanted shard index])."""
+        N = self.CodeMode.N
+        b = (ctypes.c_int * max(len(bad), 1))(*bad)
+        w = (ctypes.c_int * max(len(want), 1))(*want)
+        ins = (ctypes.c_int * N)()
+        rows = (ctypes.c_uint8 * max(N * len(want), 1))()
+        _lib.check(self._L.cfsec_ec_repair_rows(self._h, b, len(bad), w, len(want), ins, rows))
+        return [ins[i] for i in range(N)], [bytes(rows[r * N:(r + 1) * N]) for r in range(len(want))]
+
+    def matvec_batch(self, rows, ptrs, shard_size: int, nstripes: int, stream=None):
+        """cfsec_ec_matvec_batch: outputs = rows x inputs on device memory; ptrs (addresses) per
+        stripe: the N inputs, then one output per row."""
+        from ._shards import stream_ptr
+        coef = b"".join(rows)
+        arr = ptrs if isinstance(ptrs, ctypes.Array) else (ctypes.c_void_p * len(ptrs))(*ptrs)
+        _lib.check(self._L.cfsec_ec_matvec_batch(self._h, coef, len(rows), arr, int(shard_size), int(nstripes),
+                                                 stream_ptr(stream, device=self._engine.device)))
+
     def shards_in_idc(self, idx: int):
         out = (ctypes.c_int * 64)()
         cnt = ctypes.c_int(0)

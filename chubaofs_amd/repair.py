@@ -20,6 +20,14 @@ Two exchange strategies, both followed by one fused reconstruct launch per rank:
 
 Only the first k surviving shards in index order are needed: the reference decodes from exactly
 those (KRS/reedsolomon.go:1453-1465), so the exchange ships only them.
+
+LRC modes (an ec.Encoder, e.g. EC16P20L2): the erased set may hold local parities too; the
+survivors are the first N present *global* shards (lrcencoder.go:156-160 reconstructs the global
+stripe first) and every erased shard -- data, global or local parity -- is one row over them
+(cfsec_ec_repair_rows; a local parity through its AZ's local engine over the rebuilt AZ), so the
+decode stays one launch (cfsec_ec_matvec_batch) and the exchange is unchanged.  For a consistent
+stripe this equals the reference's global-then-local Reconstruct; the reference's local pass
+would read the AZ's stored shards, which this exchange does not ship.
 """
 from __future__ import annotations
 
@@ -58,9 +66,10 @@ class RepairPlan:
     survivors: List[int]  # first k present, index order
 
     @staticmethod
-    def make(k: int, total: int, erased) -> "RepairPlan":
+    def make(k: int, total: int, erased, nglobal: int = None) -> "RepairPlan":
+        """nglobal: the survivors come from shards [0, nglobal) (LRC: the global stripe)."""
         er = sorted(set(int(e) for e in erased))
-        surv = [i for i in range(total) if i not in er][:k]
+        surv = [i for i in range(total if nglobal is None else nglobal) if i not in er][:k]
         if len(surv) < k:
             from ._lib import ErrTooFewShards
             raise ErrTooFewShards("ErrTooFewShards")
@@ -147,9 +156,14 @@ def repair_batch(enc, local: torch.Tensor, erased, rank: int, world: int, strate
                  group=None, stream=None) -> torch.Tensor:
     """Rebuild `erased` shards of every bid of a batch whose shards are spread over `world` GPUs.
 
-    enc: reedsolomon.ReedSolomon for (k, total-k) on this rank's device.  Returns the rebuilt
-    rows this rank owns, [nbids, n_erased_owned(rank), S], erased shards in index order."""
-    plan = RepairPlan.make(enc.data_shards, enc.total_shards, erased)
+    enc: reedsolomon.ReedSolomon for (k, total-k), or an ec.Encoder (RS or LRC code mode), on this
+    rank's device.  Returns the rebuilt rows this rank owns, [nbids, n_erased_owned(rank), S],
+    erased shards in index order."""
+    if hasattr(enc, "repair_rows"):  # ec.Encoder
+        t = enc.CodeMode
+        plan = RepairPlan.make(t.N, t.N + t.M + t.L, erased, nglobal=t.N + t.M)
+    else:
+        plan = RepairPlan.make(enc.data_shards, enc.total_shards, erased)
     nb, S = local.shape[0], local.shape[2]
     er = plan.erased
     if strategy == "columns":
@@ -185,7 +199,17 @@ def repair_batch(enc, local: torch.Tensor, erased, rank: int, world: int, strate
 def _decode(enc, plan: RepairPlan, nb: int, L: int, src: Callable, dst: Callable, stream):
     """One fused reconstruct launch over all bids: a full shard-pointer table per bid with the
     survivors at their exchange addresses and the erased rows at their output slots.  Present
-    rows past the first k survivors are never read; they reuse a survivor's address."""
+    rows past the first k survivors are never read; they reuse a survivor's address.  With an
+    ec.Encoder: the erased shards' rows over the survivors, one product launch."""
+    if hasattr(enc, "repair_rows"):
+        ins, rows = enc.repair_rows(plan.erased, plan.erased)
+        assert ins == plan.survivors, (ins, plan.survivors)
+        ptrs = []
+        for b in range(nb):
+            ptrs += [src(i, b) for i in ins]
+            ptrs += [dst(e, b) for e in plan.erased]
+        enc.matvec_batch(rows, ptrs, L, nb, stream=stream)
+        return
     ptrs = []
     for b in range(nb):
         for i in range(plan.total):

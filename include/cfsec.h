@@ -214,6 +214,21 @@ int cfsec_ec_set_devices(cfsec_ec* h, const int* devices, int ndev);
  * modes as one fused (M+L) x N pass (lrcencoder.go:35-82).  status[s]: Encode's result (CFSEC_ERR_VERIFY
  * when the enabled Verify fails).  Memory and devices as for cfsec_rs_*_stripes. */
 int cfsec_ec_encode_batch(cfsec_ec* h, cfsec_shard* shards, int n, int nstripes, int mem, int* status);
+/* Repair over survivors held elsewhere (the multi-GPU repair of chubaofs_amd/repair.py ships only
+ * the shards a decode reads): with the shards in bad_idx[0..nbad) lost (global or LRC local
+ * indices), in_idx[0..N) = the first N present global shards in index order -- the ones
+ * Reconstruct decodes from (KRS/reedsolomon.go:1453-1465) -- and rows[w*N .. w*N+N) = shard
+ * want[w] (a data, global parity or local parity index) as a GF(2^8) row over them (the local
+ * parity through lrcencoder.go's local engine over the AZ's shards).  No reference counterpart:
+ * the reference repairs one bid at a time on one host. */
+int cfsec_ec_repair_rows(cfsec_ec* h, const int* bad_idx, int nbad, const int* want, int nwant,
+                         int* in_idx, uint8_t* rows);
+/* outputs = coef (rows x N) x inputs over device memory, asynchronously on `stream` (NULL: the
+ * legacy default stream): stripe s has N input pointers then `rows` output pointers at
+ * ptrs[s*(N+rows) ..], shard_size bytes each (the product kernel of cfsec_rs_encode_batch with
+ * caller rows, e.g. cfsec_ec_repair_rows'). */
+int cfsec_ec_matvec_batch(cfsec_ec* h, const uint8_t* coef, int rows, uint8_t* const* ptrs, size_t shard_size,
+                          int nstripes, void* stream);
 /* GetShardsInIdc index map (encoder.go:169-176 / lrcencoder.go:236-243): writes the global
  * shard indices of AZ idx into out (capacity out_cap) and their count into *count. */
 int cfsec_ec_shards_in_idc(const cfsec_ec* h, int idx, int* out, int out_cap, int* count);

@@ -149,3 +149,41 @@ def test_repair_gpu_tasklet_64_bids(nccl_world1):
     out = repair.repair_batch(enc, local, [0, 1, 16, 17], 0, 1, strategy="columns")
     torch.cuda.synchronize()
     assert torch.equal(out, want)
+
+
+def test_plan_lrc_survivors_are_global():
+    """LRC: the survivors are the first N present global shards, never a local parity."""
+    p = repair.RepairPlan.make(16, 38, [0, 36, 3], nglobal=36)
+    assert p.survivors == [i for i in range(36) if i not in (0, 3)][:16]
+    assert p.erased == [0, 3, 36]
+    with pytest.raises(Exception):
+        repair.RepairPlan.make(6, 18, list(range(11)), nglobal=16)  # 5 global shards left < 6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("strategy", ["columns", "allgather"])
+@pytest.mark.parametrize("mode,erased", [("EC16P20L2", [0, 1, 16, 36]), ("EC16P20L2", [5, 37]),
+                                         ("EC6P10L2", [0, 7, 17]), ("EC6P10L2", [16, 17])])
+def test_repair_gpu_lrc(mode, erased, strategy, nccl_world1):
+    """LRC repair over RCCL (world 1) with an ec.Encoder: erased data, global and local parities
+    rebuilt in one product launch from the first N global survivors; every rebuilt row equals the
+    shard ec.Encode produced (global + every AZ's local parity, pinned to the oracle elsewhere)."""
+    from chubaofs_amd import codemode as cm, ec
+    t = cm.GetTactic(getattr(cm, mode))
+    enc = ec.NewEncoder(ec.Config(CodeMode=t, EnableVerify=False), device=0)
+    total, S_, nb = t.N + t.M + t.L, 65536 + 13, 3
+    rng = np.random.default_rng(len(erased) + t.N)
+    full = []
+    for b in range(nb):
+        sh = [rng.integers(0, 256, S_, dtype=np.uint8) for _ in range(t.N)] + \
+             [np.zeros(S_, np.uint8) for _ in range(t.M + t.L)]
+        enc.Encode(sh)
+        full.append(sh)
+    local = torch.from_numpy(np.stack([np.stack(sh) for sh in full])).cuda()
+    local[:, erased] = 0
+    out = repair.repair_batch(enc, local, erased, 0, 1, strategy=strategy)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    for b in range(nb):
+        for q, e in enumerate(sorted(erased)):
+            assert np.array_equal(got[b, q], full[b][e]), (b, e)
