@@ -65,12 +65,12 @@ def parse():
     p.add_argument("--stripes", type=int, default=8, help="stripes per batch (per GPU per operation)")
     p.add_argument("--shard-size", type=int, default=S_DEFAULT)
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
-    p.add_argument("--op-seconds", type=float, default=0.6, help="device time per isolated-operation figure")
+    p.add_argument("--op-seconds", type=float, default=1.5, help="device time per isolated-operation figure")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-pmc", action="store_true")
     p.add_argument("--no-extra", action="store_true", help="skip the secondary per-operation figures")
     p.add_argument("--graph", action="store_true", help="replay each step as a captured HIP graph")
-    p.add_argument("--settle-ms", type=float, default=1000.0, help="untimed load before warmup (clock ramp)")
+    p.add_argument("--settle-ms", type=float, default=2000.0, help="untimed load before warmup (clock ramp)")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args()
 
@@ -385,6 +385,7 @@ def main():
         del batch, golden
         torch.cuda.empty_cache()
         extra["configs"] = other_configs(args, torch, dev, stream, cpu=(world == 1 and rank == 0 and not args.no_cpu))
+        extra["host_path"] = host_path(args, torch, dev, world)
 
     if rank != 0:
         if world > 1:
@@ -525,6 +526,46 @@ def secondary(args, torch, enc, batch, ptrs, stream, S, nst, pitch, dev, launch_
     out["device_copy_note"] = ("torch copy_ of one rotated batch into a scratch batch (the HIP runtime D2D copy, "
                                "__amd_rocclr_copyBuffer), read + write bytes / time: a measured streaming peak")
     del scratch
+    return out
+
+
+def host_path(args, torch, dev, world):
+    """PCIe-inclusive rate of the drop-in path itself -- shards in host memory, CFSEC_MEM_HOST, what
+    the cgo shim passes (go/cfsec) -- never `value`: EC12P4 Encode of 4 stripes of 64 MiB blobs per
+    cfsec_ec_encode_batch call, from page-locked (cfsec_host_alloc, the resourcepool hook) and from
+    pageable memory, on every rank at once.  Aggregate = all ranks' data / the slowest rank's time."""
+    import numpy as np
+
+    from chubaofs_amd import _lib, codemode as cm, ec
+    K, M, S, nst, reps = K_DATA, M_PARITY, args.shard_size, 4, 5
+    enc = ec.NewEncoder(ec.Config(CodeMode=cm.GetTactic(cm.EC12P4), EnableVerify=False), device=dev.index)
+    seed = np.random.default_rng(7).integers(0, 256, S, dtype=np.uint8)
+    out = {"workload": f"EC12P4 Encode, {nst} stripes of 64 MiB blobs (S={S}) per call, host memory, "
+                       f"{reps} calls per rank, all ranks concurrently",
+           "note": "PCIe-inclusive (H2D of 12 S + D2H of 4 S per stripe); the CPU baseline is the comparison"}
+    for kind in ("pinned", "pageable"):
+        buf = _lib.pinned_empty(nst * (K + M) * S) if kind == "pinned" else np.zeros(nst * (K + M) * S, np.uint8)
+        stripes = [[buf[(s * (K + M) + i) * S:(s * (K + M) + i + 1) * S] for i in range(K + M)] for s in range(nst)]
+        for s in range(nst):
+            for i in range(K):
+                stripes[s][i][:] = np.roll(seed, 977 * (s * K + i))
+        assert enc.EncodeBatch(stripes) == [0] * nst
+        assert enc.Verify(stripes[nst - 1])
+        if world > 1:
+            torch.distributed.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            st = enc.EncodeBatch(stripes)
+        dt = time.perf_counter() - t0
+        assert st == [0] * nst
+        if world > 1:
+            t = torch.tensor([dt], dtype=torch.float64, device=dev)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            dt = float(t.item())
+        out[kind] = {"data_GBps": round(world * nst * K * S * reps / dt / 1e9, 2),
+                     "pcie_GBps": round(world * nst * (K + M) * S * reps / dt / 1e9, 2),
+                     "per_gpu_data_GBps": round(nst * K * S * reps / dt / 1e9, 2), "n_gpus": world}
+        del stripes, buf
     return out
 
 
