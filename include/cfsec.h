@@ -204,8 +204,9 @@ int cfsec_ec_verify(cfsec_ec* h, cfsec_shard* shards, int n, int mem, void* stre
  * stripe indices, or local ones for a local stripe: n = its size); per bid exactly
  * encoder.Reconstruct(shards_b, bad_b) then, with verify != 0, encoder.Verify(shards_b).  status[b]:
  * the Reconstruct error, CFSEC_ERR_VERIFY when Verify returns false, or CFSEC_OK.  RS modes run one
- * fused Reconstruct+Verify pass; LRC modes the global pass then every AZ's local pass
- * (lrcencoder.go:133-186, 89-131).  Memory and devices as for cfsec_rs_*_stripes. */
+ * fused Reconstruct+Verify pass; LRC modes (lrcencoder.go:133-186, 89-131) one pass too for a bid
+ * with no bad local shard (its local parities compared in the global pass as rows over the data),
+ * else the global pass then every AZ's local pass.  Memory and devices as for cfsec_rs_*_stripes. */
 int cfsec_ec_reconstruct_batch(cfsec_ec* h, cfsec_shard* shards, int n, int nbids, const int* bad_idx,
                                const int* bad_off, int verify, int mem, int* status);
 int cfsec_ec_set_devices(cfsec_ec* h, const int* devices, int ndev);
