@@ -7,12 +7,12 @@ out=probes_bin/$name; mkdir -p $out/obj
 HIPCC=/opt/rocm/bin/hipcc
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result $*"
 objs=""
-for k in gf_crc_k6 gf_crc_k8 gf_crc_k12 gf_crc_k16 gf_crc_k18 crc32 crc32block; do
+for k in gf_crc gf_crc_k6 gf_crc_k8 gf_crc_k12 gf_crc_k16 gf_crc_k18 crc32 crc32block; do
   $HIPCC $F -c chubaofs_amd/csrc/$k.hip -o $out/obj/$k.o &
   objs="$objs $out/obj/$k.o"
 done
 wait
-for o in build/cfsec/*.o; do case $(basename $o) in gf_crc_k*|crc32.o|crc32block.o) ;; *) objs="$objs $o";; esac; done
+for o in build/cfsec/*.o; do case $(basename $o) in gf_crc*|crc32.o|crc32block.o) ;; *) objs="$objs $o";; esac; done
 $HIPCC --offload-arch=gfx950 -shared -fPIC -o $out/libcfsec.so $objs
 $HIPCC --offload-arch=gfx950 -O3 -std=c++17 -Ichubaofs_amd/csrc tools/gf_shapes.hip -L$out -lcfsec -Wl,-rpath,'$ORIGIN' -o $out/gf_shapes
 rm -rf $out/obj
