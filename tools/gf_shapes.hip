@@ -58,6 +58,12 @@ int main() {
       {"EC16P20L2 repair 4 erased", 16, 4, 262144, 64},
       {"EC15P12 encode", 15, 12, 349526, 32},
       {"EC16P4 encode", 16, 4, 262144, 64},
+      {"EC12P9 encode", 12, 9, 349526, 32},
+      {"EC10P4 encode", 10, 4, 419431, 32},
+      {"EC6P3 encode", 6, 3, 699051, 32},
+      {"EC6P8 encode", 6, 8, 699051, 32},
+      {"EC4P4 encode", 4, 4, 1048576, 16},
+      {"EC3P3 encode", 3, 3, 1398102, 16},
   };
   size_t maxbytes = 0;
   for (auto& s : shapes) maxbytes = std::max(maxbytes, ((s.S + 255) / 256 * 256) * (s.k + s.m) * s.stripes);
