@@ -171,7 +171,10 @@ __device__ __forceinline__ void st_chunk(uint8_t* p, const uint32_t (&x)[LW]) {
 // Lane chunk of the fixed-K kernel for K inputs and M outputs per wave: 16 bytes, or 8 where the
 // wave holds many output rows -- K + M chunks of accumulators and inputs at 16 B per lane need
 // 130-210 VGPRs for M >= 10 (2-3 waves per SIMD), at 8 B half of that.
-constexpr int fixed_lane_dwords(int K, int M) { return M >= 10 ? 2 : 4; }
+#ifndef CFSEC_LANE8_MIN_M
+#define CFSEC_LANE8_MIN_M 10
+#endif
+constexpr int fixed_lane_dwords(int K, int M) { return M >= CFSEC_LANE8_MIN_M ? 2 : 4; }
 
 // Product tables of one coefficient:
 //   t01 = {T0[0..3], T0[4..7], T1[0..3], T1[4..7]},  t2 = T2[0..3]
