@@ -174,19 +174,22 @@ std::vector<Group> make_groups(const std::vector<StripeTask*>& tasks, int* next_
     g.in.reserve(g.tasks.size() * g.plan->in.size());
     g.out.reserve(g.tasks.size() * g.plan->out.size());
     g.lens.reserve(g.tasks.size());
+    // dy16 output rows: rows the kernel neither stores nor compares (inputs; parity not verified)
+    // get any pointer the task has -- decided once per plan, not per task
+    std::vector<int> hrow;
+    if (g.plan->dy16)
+      for (int idx : g.plan->dy16->rows) {
+        const bool known = std::find(g.plan->in.begin(), g.plan->in.end(), idx) != g.plan->in.end() ||
+                           std::find(g.plan->out.begin(), g.plan->out.end(), idx) != g.plan->out.end();
+        hrow.push_back(known ? idx : g.plan->in[0]);
+      }
+    g.hout.reserve(g.tasks.size() * hrow.size());
     for (size_t i = 0; i < g.tasks.size(); ++i) {
       StripeTask* t = g.tasks[i];
       for (int c : g.plan->in) g.in.push_back(ptr(t, c));
       for (int o : g.plan->out) g.out.push_back(const_cast<uint8_t*>(ptr(t, o)));
       g.lens.push_back(t->len);
-      if (g.plan->dy16)
-        for (int idx : g.plan->dy16->rows) {
-          // rows the kernel neither stores nor compares (inputs; parity not verified) get any
-          // pointer the task has
-          const bool known = std::find(g.plan->in.begin(), g.plan->in.end(), idx) != g.plan->in.end() ||
-                             std::find(g.plan->out.begin(), g.plan->out.end(), idx) != g.plan->out.end();
-          g.hout.push_back(const_cast<uint8_t*>(ptr(t, known ? idx : g.plan->in[0])));
-        }
+      for (int idx : hrow) g.hout.push_back(const_cast<uint8_t*>(ptr(t, idx)));
     }
     *next_flag += (int)g.tasks.size();
   }
