@@ -249,11 +249,20 @@ def main():
 
     from chubaofs_amd import reedsolomon
 
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # CFSEC_BENCH_SHARE_DEVICE / CFSEC_BENCH_BACKEND: rehearsal of the N-rank flow on a box with
+    # fewer GPUs (ranks share devices round-robin, gloo instead of RCCL, which refuses two ranks on
+    # one GPU); the driver's multi-GPU runs use neither
+    ndev = torch.cuda.device_count()
+    gpu = local_rank % ndev if os.environ.get("CFSEC_BENCH_SHARE_DEVICE") else local_rank
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("CFSEC_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
         assert dist.get_world_size() == args.gpus
 
     total = K_DATA + M_PARITY
@@ -270,7 +279,7 @@ def main():
         base = batch[b].data_ptr()
         p = [base + (s * total + i) * pitch for s in range(nst) for i in range(total)]
         ptrs.append((ctypes.c_void_p * len(p))(*p))  # marshalled once, reused by every launch
-    enc = reedsolomon.New(K_DATA, M_PARITY, device=local_rank)
+    enc = reedsolomon.New(K_DATA, M_PARITY, device=dev.index)
     stream = torch.cuda.Stream(device=dev)
     launches = [0]  # launches of the step kernel so far (one per batch call: affine 8-stripe batch)
 
