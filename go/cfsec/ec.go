@@ -171,7 +171,8 @@ func (e *ECEncoder) Verify(shards [][]byte) (bool, error) {
 
 // ReconstructBatch runs blobnode's repair step (work_shard_recover.go:751-760) for a whole tasklet:
 // for every bid, Reconstruct(bids[b], badIdx[b]) then, with verify, Verify(bids[b]) -- one call,
-// one fused pass per bid (LRC: the global pass then the AZ-local pass).  errs[b] is what that bid's
+// one fused pass per bid (LRC: one pass too when no local shard is bad, else the global pass then
+// the AZ-local pass).  errs[b] is what that bid's
 // two calls would have reported (ErrVerify for a false Verify); err reports a failure of the call
 // itself.  Zero-size bids are skipped by the caller, as the reference loop does (:730-733).
 func (e *ECEncoder) ReconstructBatch(bids [][][]byte, badIdx [][]int, verify bool) (errs []error, err error) {
@@ -224,6 +225,35 @@ func (e *ECEncoder) ReconstructBatch(bids [][][]byte, badIdx [][]int, verify boo
 		errs[b] = ecError(status[b])
 	}
 	return errs, toError(st)
+}
+
+// RepairRows returns the first N present global shards a Reconstruct decodes from with badIdx lost
+// (KRS/reedsolomon.go:1453-1465) and, for every wanted shard index (data, global or LRC local
+// parity), its GF(2^8) row over them (cfsec_ec_repair_rows): the repair plan of survivors that
+// live elsewhere, e.g. on other GPUs.
+func (e *ECEncoder) RepairRows(badIdx, want []int) (in []int, rows [][]byte, err error) {
+	n := e.tactic.N
+	_, pbad := badVec(badIdx) // the pointer passed to C keeps the slice alive for the call
+	w := make([]C.int, len(want)+1)
+	for i, v := range want {
+		w[i] = C.int(v)
+	}
+	ci := make([]C.int, n)
+	flat := make([]byte, n*len(want)+1)
+	st := C.cfsec_ec_repair_rows(e.h, pbad, C.int(len(badIdx)), &w[0], C.int(len(want)), &ci[0],
+		(*C.uint8_t)(unsafe.Pointer(&flat[0])))
+	if st != C.CFSEC_OK {
+		return nil, nil, ecError(st)
+	}
+	in = make([]int, n)
+	for i := range in {
+		in[i] = int(ci[i])
+	}
+	rows = make([][]byte, len(want))
+	for r := range rows {
+		rows[r] = append([]byte(nil), flat[r*n:(r+1)*n]...)
+	}
+	return in, rows, nil
 }
 
 // ---- host bookkeeping, as encoder.go / lrcencoder.go ----

@@ -283,3 +283,32 @@ def test_segment_reconstruct_data(mode, memory):
         for i in range(t.N + t.M + t.L):  # nothing outside the range was touched
             assert np.array_equal(got[i][:off], origin[i][:off] if i not in bad else got[i][:off])
             assert np.array_equal(got[i][off + size:], origin[i][off + size:]), (off, size, i)
+
+
+@pytest.mark.gpu
+def test_repair_rows_match_reconstruct_and_errors():
+    """cfsec_ec_repair_rows: rows over the first N present global shards reproduce every erased
+    shard (data, global and local parity) through cfsec_ec_matvec_batch; out-of-range and
+    too-many-lost sets are refused with the reference's errors."""
+    import torch
+    from chubaofs_amd import _lib, codemode as cm, ec
+    t = cm.GetTactic(cm.EC6P10L2)
+    enc = ec.NewEncoder(ec.Config(CodeMode=t, EnableVerify=False), device=0)
+    total, S = t.N + t.M + t.L, 4096 + 5
+    rng = np.random.default_rng(9)
+    sh = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(t.N)] + [np.zeros(S, np.uint8) for _ in range(t.M + t.L)]
+    enc.Encode(sh)
+    bad = [0, 3, 7, 16]
+    ins, rows = enc.repair_rows(bad, bad)
+    assert ins == [i for i in range(t.N + t.M) if i not in bad][:t.N]
+    dev = torch.from_numpy(np.stack(sh)).cuda()
+    out = torch.zeros((len(bad), S), dtype=torch.uint8, device="cuda")
+    ptrs = [dev[i].data_ptr() for i in ins] + [out[q].data_ptr() for q in range(len(bad))]
+    enc.matvec_batch(rows, ptrs, S, 1)
+    torch.cuda.synchronize()
+    for q, e in enumerate(bad):
+        assert np.array_equal(out[q].cpu().numpy(), sh[e]), e
+    with pytest.raises(_lib.CfsecError):
+        enc.repair_rows([total], [0])
+    with pytest.raises(_lib.CfsecError):
+        enc.repair_rows(list(range(t.M + 1)), [0])  # 11 global shards lost, 5 left < N = 6
