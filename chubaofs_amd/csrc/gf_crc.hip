@@ -146,13 +146,13 @@ int64_t affine_stride(const MatVecJob& job) {
 }
 
 template <bool CIN>
-hipError_t launch_crc(int k, int m, const GfCrcArgs& a, dim3 grid, hipStream_t st) {
+hipError_t launch_crc(int k, int m, const GfCrcArgs& a, dim3 grid, hipStream_t st, bool dy) {
   switch (k) {
-    case 6: return crcdev::launch_crc_k<6, CIN>(m, a, grid, st);
-    case 8: return crcdev::launch_crc_k<8, CIN>(m, a, grid, st);
-    case 12: return crcdev::launch_crc_k<12, CIN>(m, a, grid, st);
-    case 16: return crcdev::launch_crc_k<16, CIN>(m, a, grid, st);
-    case 18: return crcdev::launch_crc_k<18, CIN>(m, a, grid, st);
+    case 6: return crcdev::launch_crc_k<6, CIN>(m, a, grid, st, dy);
+    case 8: return crcdev::launch_crc_k<8, CIN>(m, a, grid, st, dy);
+    case 12: return crcdev::launch_crc_k<12, CIN>(m, a, grid, st, dy);
+    case 16: return crcdev::launch_crc_k<16, CIN>(m, a, grid, st, dy);
+    case 18: return crcdev::launch_crc_k<18, CIN>(m, a, grid, st, dy);
     default: return hipErrorInvalidValue;
   }
 }
@@ -209,6 +209,10 @@ hipError_t launch_matvec_crc(const MatVecJob& job, uint32_t* crc, int crc_stride
   for (int i = 0; i < k + m; ++i) a.slot[i] = (uint8_t)std::max(slot[i], 0);
   for (int r = 0; r < m; ++r)
     for (int c = 0; c < k; ++c) a.coef[r * k + c] = job.coef[(size_t)r * k + c];
+  // 4 outputs made of 4x4 dyadic blocks (EC12P4 / EC16P4 encode, coset-aligned repairs): the
+  // reduced-product kernel
+  const DyPlan dp = m == 4 && k % 4 == 0 ? dyadic_plan(a.coef, m, k) : DyPlan{0, 0};
+  const bool dy = dp.B == 4 && dp.E == 0;
   for (uint32_t g = 0; g < groups; ++g) {
     const int64_t end = (int64_t)std::min<uint64_t>((uint64_t)(g + 1) * tpw, tiles) * crcdev::kTile;
     a.gconst[g] = xpow(8 * ((int64_t)job.len - end));
@@ -223,7 +227,7 @@ hipError_t launch_matvec_crc(const MatVecJob& job, uint32_t* crc, int crc_stride
       for (int r = 0; r < m; ++r) a.ptr[tab * k + s * m + r] = job.out[(size_t)(s0 + s) * m + r];
     }
     const dim3 grid(groups, (unsigned)ns);
-    e = cin ? launch_crc<true>(k, m, a, grid, stream) : launch_crc<false>(k, m, a, grid, stream);
+    e = cin ? launch_crc<true>(k, m, a, grid, stream, dy) : launch_crc<false>(k, m, a, grid, stream, dy);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;

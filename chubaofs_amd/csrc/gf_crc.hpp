@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 
 #include "gf_device.hpp"
+#include "gf_dyadic.hpp"
 #include "kernels.hpp"
 
 namespace cfsec {
@@ -291,18 +292,93 @@ __device__ __forceinline__ void crc_tile(uint64_t len, const u32x4* tab01, const
   for (int r = 0; r < M; ++r) R[RO + r] = fused_step(ct, R[RO + r], acc[r]);
 }
 
+// The product of a 4x4-dyadic matrix (EC12P4 / EC16P4 encode and their coset-aligned repairs,
+// gf_dyadic.hpp dy_col4: 9 products per 4x4 block instead of 16) in the fused kernel: rows loaded one
+// column block ahead, the CRC step of each block's 4 input rows after its product.  The kernel is
+// VALU-issue-bound (§4.1 of DESIGN.md), so fewer products pay even at 3 waves per SIMD (144 VGPRs):
+// EC12P4 8 x 64 MiB encode + CRC 242 -> 224 us (profiles/r02/fused_crc_ab.txt).
+template <int K, bool CIN>
+__device__ __forceinline__ void crc_tile_dy(uint64_t len, const u32x4* tab01, const uint32_t* tab2,
+                                            const uint32_t* ct, const uint8_t* const (&row)[K + 4],
+                                            uint32_t off, uint32_t (&R)[(CIN ? K : 0) + 4]) {
+  constexpr int RO = CIN ? K : 0, KB = K / 4;
+  uint32_t acc[4][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int w = 0; w < 4; ++w) acc[r][w] = 0u;
+  if ((uint64_t)off + dev::kLaneBytes <= len) {
+    uint32_t x[K][4];
+    const auto load = [&](int c) {
+      const u32x4 v = dev::ld16<true>(row[c] + off);
+      x[c][0] = v.x;
+      x[c][1] = v.y;
+      x[c][2] = v.z;
+      x[c][3] = v.w;
+    };
+#pragma unroll
+    for (int c = 0; c < 4; ++c) load(c);
+#pragma unroll
+    for (int cb = 0; cb < KB; ++cb) {
+      if (cb + 1 < KB)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) load(4 * cb + 4 + c);
+      __builtin_amdgcn_sched_barrier(0);
+      const int c0 = 4 * cb;
+      dev::dy_col4<1, true>(acc, x[c0], x[c0 + 1], x[c0 + 2], x[c0 + 3], tab01 + cb * 9, tab2 + cb * 9, KB * 9);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(acc[r][0]), "+v"(acc[r][1]), "+v"(acc[r][2]), "+v"(acc[r][3]));
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (CIN) {
+#pragma unroll
+        for (int c = c0; c < c0 + 4; ++c) {
+          R[c] = fused_step(ct, R[c], x[c]);
+          asm volatile("" : "+v"(R[c]));
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      dev::st16_out<true>(const_cast<uint8_t*>(row[K + r]) + off, u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]});
+  } else {
+    const size_t rem = off < len ? (size_t)(len - off) : 0;
+    for (int cb = 0; cb < KB; ++cb) {
+      uint32_t x[4][4];
+      for (int c = 0; c < 4; ++c) {
+        const u32x4 v = rem ? dev::ld_tail(row[4 * cb + c] + off, rem) : u32x4{0u, 0u, 0u, 0u};
+        x[c][0] = v.x;
+        x[c][1] = v.y;
+        x[c][2] = v.z;
+        x[c][3] = v.w;
+      }
+      dev::dy_col4<1, false>(acc, x[0], x[1], x[2], x[3], tab01 + cb * 9, tab2 + cb * 9, KB * 9);
+      if constexpr (CIN)
+        for (int c = 0; c < 4; ++c) R[4 * cb + c] = fused_step(ct, R[4 * cb + c], x[c]);
+    }
+    if (rem)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        dev::st_tail(const_cast<uint8_t*>(row[K + r]) + off, u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]}, rem);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) R[RO + r] = fused_step(ct, R[RO + r], acc[r]);
+}
+
 // grid (groups, stripes), 256 threads.  a.k == K, a.m == M.
-#ifndef CFSEC_CRC_WPE
-#define CFSEC_CRC_WPE 4  // minimum waves per SIMD the register allocation aims for
-#endif
-template <int K, int M, bool CIN>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CFSEC_CRC_WPE, 8))) void gf_crc_kernel(const GfCrcArgs a) {
+// DY: a.coef is 4 x K made of 4x4 dyadic blocks (checked by the launcher); the register allocation
+// aims at 4 waves per SIMD, 3 for the dyadic product
+template <int K, int M, bool CIN, bool DY>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DY ? 3 : 4, 8))) void gf_crc_kernel(const GfCrcArgs a) {
   constexpr int NR = (CIN ? K : 0) + M;  // checksummed rows
   __shared__ u32x4 tab01[K * M];
   __shared__ uint32_t tab2[K * M];
   __shared__ uint32_t ct[kFusedTabWords];
   __shared__ uint32_t red[4][NR];
-  dev::build_tables<M>(K, M, a.coef, tab01, tab2);
+  constexpr bool kDy = DY;
+  static_assert(!DY || (K % 4 == 0 && M == 4), "dyadic product: 4 outputs, column blocks of 4");
+  if constexpr (kDy) dev::build_dy_tables<K, 4, 4, 1, 0>(a.coef, tab01, tab2);
+  else dev::build_tables<M>(K, M, a.coef, tab01, tab2);
   for (int i = threadIdx.x; i < kFusedTabWords; i += 256) ct[i] = a.tabs[kFusedTabBase + i];
   __syncthreads();
 
@@ -326,7 +402,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CFSEC_CRC_W
     const uint32_t off = t * kTile + lanepos;
     // the next tile is full for this thread: its first rows are fetched during this one
     const bool next = t + 1 < t1 && (uint64_t)off + kTile + dev::kLaneBytes <= a.len;
-    crc_tile<K, M, CIN>(a.len, tab01, tab2, ct, row, off, pre, next, x, R);
+    if constexpr (kDy) crc_tile_dy<K, CIN>(a.len, tab01, tab2, ct, row, off, R);
+    else crc_tile<K, M, CIN>(a.len, tab01, tab2, ct, row, off, pre, next, x, R);
     pre = next && (uint64_t)off + dev::kLaneBytes <= a.len;
   }
 
@@ -361,13 +438,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CFSEC_CRC_W
   }
 }
 
-// Launch gf_crc_kernel<K, m, CIN> (instantiated for m = 1..6 in gf_crc_k<K>.hip).
+// Launch gf_crc_kernel<K, m, CIN> (instantiated for m = 1..6 in gf_crc_k<K>.hip); dy: the 4x4-dyadic
+// product (m = 4, K a multiple of 4).
 template <int K, bool CIN>
-hipError_t launch_crc_k(int m, const GfCrcArgs& a, dim3 grid, hipStream_t st) {
+hipError_t launch_crc_k(int m, const GfCrcArgs& a, dim3 grid, hipStream_t st, bool dy) {
+  if constexpr (K % 4 == 0) {
+    if (dy && m == 4) {
+      hipLaunchKernelGGL((gf_crc_kernel<K, 4, CIN, true>), grid, dim3(256), 0, st, a);
+      return hipGetLastError();
+    }
+  }
+  if (dy) return hipErrorInvalidValue;
   switch (m) {
 #define CFSEC_CRC_CASE(MV)                                                                       \
   case MV:                                                                                       \
-    hipLaunchKernelGGL((gf_crc_kernel<K, MV, CIN>), grid, dim3(256), 0, st, a);                  \
+    hipLaunchKernelGGL((gf_crc_kernel<K, MV, CIN, false>), grid, dim3(256), 0, st, a);           \
     break;
     CFSEC_CRC_CASE(1) CFSEC_CRC_CASE(2) CFSEC_CRC_CASE(3) CFSEC_CRC_CASE(4) CFSEC_CRC_CASE(5)
     CFSEC_CRC_CASE(6)
@@ -388,8 +473,8 @@ uint32_t crc_mulmod(uint32_t a, uint32_t b);  // a * b mod P
 namespace crcdev {
 
 #define CFSEC_CRC_EXTERN(K)                                                                         \
-  extern template hipError_t launch_crc_k<K, true>(int, const GfCrcArgs&, dim3, hipStream_t);       \
-  extern template hipError_t launch_crc_k<K, false>(int, const GfCrcArgs&, dim3, hipStream_t);
+  extern template hipError_t launch_crc_k<K, true>(int, const GfCrcArgs&, dim3, hipStream_t, bool);  \
+  extern template hipError_t launch_crc_k<K, false>(int, const GfCrcArgs&, dim3, hipStream_t, bool);
 
 }  // namespace crcdev
 }  // namespace cfsec
@@ -397,7 +482,7 @@ namespace crcdev {
 #define CFSEC_CRC_INSTANTIATE(K)                                                                     \
   namespace cfsec {                                                                                  \
   namespace crcdev {                                                                                 \
-  template hipError_t launch_crc_k<K, true>(int, const GfCrcArgs&, dim3, hipStream_t);              \
-  template hipError_t launch_crc_k<K, false>(int, const GfCrcArgs&, dim3, hipStream_t);             \
+  template hipError_t launch_crc_k<K, true>(int, const GfCrcArgs&, dim3, hipStream_t, bool);        \
+  template hipError_t launch_crc_k<K, false>(int, const GfCrcArgs&, dim3, hipStream_t, bool);       \
   }                                                                                                  \
   }
