@@ -146,7 +146,7 @@ int64_t affine_stride(const MatVecJob& job) {
 }
 
 template <bool CIN>
-hipError_t launch_crc(int k, int m, const GfCrcArgs& a, dim3 grid, hipStream_t st, bool dy) {
+hipError_t launch_crc(int k, int m, const GfCrcArgs& a, dim3 grid, hipStream_t st, int dy) {
   switch (k) {
     case 6: return crcdev::launch_crc_k<6, CIN>(m, a, grid, st, dy);
     case 8: return crcdev::launch_crc_k<8, CIN>(m, a, grid, st, dy);
@@ -209,10 +209,13 @@ hipError_t launch_matvec_crc(const MatVecJob& job, uint32_t* crc, int crc_stride
   for (int i = 0; i < k + m; ++i) a.slot[i] = (uint8_t)std::max(slot[i], 0);
   for (int r = 0; r < m; ++r)
     for (int c = 0; c < k; ++c) a.coef[r * k + c] = job.coef[(size_t)r * k + c];
-  // 4 outputs made of 4x4 dyadic blocks (EC12P4 / EC16P4 encode, coset-aligned repairs): the
-  // reduced-product kernel
-  const DyPlan dp = m == 4 && k % 4 == 0 ? dyadic_plan(a.coef, m, k) : DyPlan{0, 0};
-  const bool dy = dp.B == 4 && dp.E == 0;
+  // matrices of dyadic blocks the fused kernel has a reduced-product form for: 4 outputs of 4x4
+  // blocks (EC12P4 / EC16P4 encode, coset-aligned repairs), 6 x 6 of 2x2 blocks (EC6P6 encode)
+  const DyPlan dp = (m == 4 && k % 4 == 0) || (m == 6 && k == 6) ? dyadic_plan(a.coef, m, k) : DyPlan{0, 0};
+#ifndef CFSEC_CRC_DY2
+#define CFSEC_CRC_DY2 1  // A/B switch for the 2x2 form
+#endif
+  const int dy = dp.E == 0 && ((dp.B == 4 && m == 4) || (CFSEC_CRC_DY2 && dp.B == 2 && m == 6 && k == 6)) ? dp.B : 0;
   for (uint32_t g = 0; g < groups; ++g) {
     const int64_t end = (int64_t)std::min<uint64_t>((uint64_t)(g + 1) * tpw, tiles) * crcdev::kTile;
     a.gconst[g] = xpow(8 * ((int64_t)job.len - end));

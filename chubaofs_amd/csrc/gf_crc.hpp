@@ -292,21 +292,29 @@ __device__ __forceinline__ void crc_tile(uint64_t len, const u32x4* tab01, const
   for (int r = 0; r < M; ++r) R[RO + r] = fused_step(ct, R[RO + r], acc[r]);
 }
 
-// The product of a 4x4-dyadic matrix (EC12P4 / EC16P4 encode and their coset-aligned repairs,
-// gf_dyadic.hpp dy_col4: 9 products per 4x4 block instead of 16) in the fused kernel: rows loaded one
-// column block ahead, the CRC step of each block's 4 input rows after its product.  The kernel is
+// The product of a dyadic matrix in the fused kernel (gf_dyadic.hpp): 4x4 blocks for 4 outputs
+// (EC12P4 / EC16P4 encode and their coset-aligned repairs: dy_col4, 9 products per block instead of
+// 16), 2x2 blocks for 6 outputs of 6 inputs (EC6P6 encode: dy_col2, 3 instead of 4); rows loaded one
+// column block ahead, the CRC step of each block's input rows after its product.  The kernel is
 // VALU-issue-bound (§4.1 of DESIGN.md), so fewer products pay even at 3 waves per SIMD (144 VGPRs):
 // EC12P4 8 x 64 MiB encode + CRC 242 -> 224 us (profiles/r02/fused_crc_ab.txt).
-template <int K, bool CIN>
+template <int K, int M, int B, bool CIN>
 __device__ __forceinline__ void crc_tile_dy(uint64_t len, const u32x4* tab01, const uint32_t* tab2,
-                                            const uint32_t* ct, const uint8_t* const (&row)[K + 4],
-                                            uint32_t off, uint32_t (&R)[(CIN ? K : 0) + 4]) {
-  constexpr int RO = CIN ? K : 0, KB = K / 4;
-  uint32_t acc[4][4];
+                                            const uint32_t* ct, const uint8_t* const (&row)[K + M],
+                                            uint32_t off, uint32_t (&R)[(CIN ? K : 0) + M]) {
+  constexpr int RO = CIN ? K : 0, KB = K / B, MB = M / B, NC = dev::Dy<B>::NC;
+  static_assert(K % B == 0 && M % B == 0 && (B == 2 || (B == 4 && M == 4)), "dyadic shape");
+  uint32_t acc[M][4];
 #pragma unroll
-  for (int r = 0; r < 4; ++r)
+  for (int r = 0; r < M; ++r)
 #pragma unroll
     for (int w = 0; w < 4; ++w) acc[r][w] = 0u;
+  const auto product = [&](int cb, uint32_t (&xs)[B][4]) {
+    if constexpr (B == 4)
+      dev::dy_col4<1, true>(acc, xs[0], xs[1], xs[2], xs[3], tab01 + cb * NC, tab2 + cb * NC, KB * NC);
+    else
+      dev::dy_col2<MB, true>(acc, xs[0], xs[1], tab01 + cb * NC, tab2 + cb * NC, KB * NC);
+  };
   if ((uint64_t)off + dev::kLaneBytes <= len) {
     uint32_t x[K][4];
     const auto load = [&](int c) {
@@ -317,21 +325,20 @@ __device__ __forceinline__ void crc_tile_dy(uint64_t len, const u32x4* tab01, co
       x[c][3] = v.w;
     };
 #pragma unroll
-    for (int c = 0; c < 4; ++c) load(c);
+    for (int c = 0; c < B; ++c) load(c);
 #pragma unroll
     for (int cb = 0; cb < KB; ++cb) {
       if (cb + 1 < KB)
 #pragma unroll
-        for (int c = 0; c < 4; ++c) load(4 * cb + 4 + c);
+        for (int c = 0; c < B; ++c) load(B * cb + B + c);
       __builtin_amdgcn_sched_barrier(0);
-      const int c0 = 4 * cb;
-      dev::dy_col4<1, true>(acc, x[c0], x[c0 + 1], x[c0 + 2], x[c0 + 3], tab01 + cb * 9, tab2 + cb * 9, KB * 9);
+      product(cb, reinterpret_cast<uint32_t(&)[B][4]>(x[B * cb]));
 #pragma unroll
-      for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(acc[r][0]), "+v"(acc[r][1]), "+v"(acc[r][2]), "+v"(acc[r][3]));
+      for (int r = 0; r < M; ++r) asm volatile("" : "+v"(acc[r][0]), "+v"(acc[r][1]), "+v"(acc[r][2]), "+v"(acc[r][3]));
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (CIN) {
 #pragma unroll
-        for (int c = c0; c < c0 + 4; ++c) {
+        for (int c = B * cb; c < B * cb + B; ++c) {
           R[c] = fused_step(ct, R[c], x[c]);
           asm volatile("" : "+v"(R[c]));
         }
@@ -339,45 +346,43 @@ __device__ __forceinline__ void crc_tile_dy(uint64_t len, const u32x4* tab01, co
       __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+    for (int r = 0; r < M; ++r)
       dev::st16_out<true>(const_cast<uint8_t*>(row[K + r]) + off, u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]});
   } else {
     const size_t rem = off < len ? (size_t)(len - off) : 0;
     for (int cb = 0; cb < KB; ++cb) {
-      uint32_t x[4][4];
-      for (int c = 0; c < 4; ++c) {
-        const u32x4 v = rem ? dev::ld_tail(row[4 * cb + c] + off, rem) : u32x4{0u, 0u, 0u, 0u};
+      uint32_t x[B][4];
+      for (int c = 0; c < B; ++c) {
+        const u32x4 v = rem ? dev::ld_tail(row[B * cb + c] + off, rem) : u32x4{0u, 0u, 0u, 0u};
         x[c][0] = v.x;
         x[c][1] = v.y;
         x[c][2] = v.z;
         x[c][3] = v.w;
       }
-      dev::dy_col4<1, false>(acc, x[0], x[1], x[2], x[3], tab01 + cb * 9, tab2 + cb * 9, KB * 9);
+      product(cb, x);
       if constexpr (CIN)
-        for (int c = 0; c < 4; ++c) R[4 * cb + c] = fused_step(ct, R[4 * cb + c], x[c]);
+        for (int c = 0; c < B; ++c) R[B * cb + c] = fused_step(ct, R[B * cb + c], x[c]);
     }
     if (rem)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
+      for (int r = 0; r < M; ++r)
         dev::st_tail(const_cast<uint8_t*>(row[K + r]) + off, u32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]}, rem);
   }
 #pragma unroll
-  for (int r = 0; r < 4; ++r) R[RO + r] = fused_step(ct, R[RO + r], acc[r]);
+  for (int r = 0; r < M; ++r) R[RO + r] = fused_step(ct, R[RO + r], acc[r]);
 }
 
-// grid (groups, stripes), 256 threads.  a.k == K, a.m == M.
-// DY: a.coef is 4 x K made of 4x4 dyadic blocks (checked by the launcher); the register allocation
-// aims at 4 waves per SIMD, 3 for the dyadic product
-template <int K, int M, bool CIN, bool DY>
+// DY: a.coef is M x K made of DY x DY dyadic blocks (checked by the launcher; 0: plain product); the
+// register allocation aims at 4 waves per SIMD, 3 for the dyadic products
+template <int K, int M, bool CIN, int DY>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DY ? 3 : 4, 8))) void gf_crc_kernel(const GfCrcArgs a) {
   constexpr int NR = (CIN ? K : 0) + M;  // checksummed rows
   __shared__ u32x4 tab01[K * M];
   __shared__ uint32_t tab2[K * M];
   __shared__ uint32_t ct[kFusedTabWords];
   __shared__ uint32_t red[4][NR];
-  constexpr bool kDy = DY;
-  static_assert(!DY || (K % 4 == 0 && M == 4), "dyadic product: 4 outputs, column blocks of 4");
-  if constexpr (kDy) dev::build_dy_tables<K, 4, 4, 1, 0>(a.coef, tab01, tab2);
+  constexpr bool kDy = DY != 0;
+  if constexpr (kDy) dev::build_dy_tables<K, M, (DY ? DY : 1), M / (DY ? DY : 1), 0>(a.coef, tab01, tab2);
   else dev::build_tables<M>(K, M, a.coef, tab01, tab2);
   for (int i = threadIdx.x; i < kFusedTabWords; i += 256) ct[i] = a.tabs[kFusedTabBase + i];
   __syncthreads();
@@ -402,7 +407,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DY ? 3 : 4,
     const uint32_t off = t * kTile + lanepos;
     // the next tile is full for this thread: its first rows are fetched during this one
     const bool next = t + 1 < t1 && (uint64_t)off + kTile + dev::kLaneBytes <= a.len;
-    if constexpr (kDy) crc_tile_dy<K, CIN>(a.len, tab01, tab2, ct, row, off, R);
+    if constexpr (kDy) crc_tile_dy<K, M, DY, CIN>(a.len, tab01, tab2, ct, row, off, R);
     else crc_tile<K, M, CIN>(a.len, tab01, tab2, ct, row, off, pre, next, x, R);
     pre = next && (uint64_t)off + dev::kLaneBytes <= a.len;
   }
@@ -438,13 +443,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DY ? 3 : 4,
   }
 }
 
-// Launch gf_crc_kernel<K, m, CIN> (instantiated for m = 1..6 in gf_crc_k<K>.hip); dy: the 4x4-dyadic
-// product (m = 4, K a multiple of 4).
+// Launch gf_crc_kernel<K, m, CIN> (instantiated for m = 1..6 in gf_crc_k<K>.hip); dy: the dyadic
+// block size of the product (4: m = 4, K a multiple of 4; 2: K = m = 6; 0: plain).
 template <int K, bool CIN>
-hipError_t launch_crc_k(int m, const GfCrcArgs& a, dim3 grid, hipStream_t st, bool dy) {
+hipError_t launch_crc_k(int m, const GfCrcArgs& a, dim3 grid, hipStream_t st, int dy) {
   if constexpr (K % 4 == 0) {
-    if (dy && m == 4) {
-      hipLaunchKernelGGL((gf_crc_kernel<K, 4, CIN, true>), grid, dim3(256), 0, st, a);
+    if (dy == 4 && m == 4) {
+      hipLaunchKernelGGL((gf_crc_kernel<K, 4, CIN, 4>), grid, dim3(256), 0, st, a);
+      return hipGetLastError();
+    }
+  }
+  if constexpr (K == 6) {
+    if (dy == 2 && m == 6) {
+      hipLaunchKernelGGL((gf_crc_kernel<K, 6, CIN, 2>), grid, dim3(256), 0, st, a);
       return hipGetLastError();
     }
   }
@@ -452,7 +463,7 @@ hipError_t launch_crc_k(int m, const GfCrcArgs& a, dim3 grid, hipStream_t st, bo
   switch (m) {
 #define CFSEC_CRC_CASE(MV)                                                                       \
   case MV:                                                                                       \
-    hipLaunchKernelGGL((gf_crc_kernel<K, MV, CIN, false>), grid, dim3(256), 0, st, a);           \
+    hipLaunchKernelGGL((gf_crc_kernel<K, MV, CIN, 0>), grid, dim3(256), 0, st, a);           \
     break;
     CFSEC_CRC_CASE(1) CFSEC_CRC_CASE(2) CFSEC_CRC_CASE(3) CFSEC_CRC_CASE(4) CFSEC_CRC_CASE(5)
     CFSEC_CRC_CASE(6)
@@ -473,8 +484,8 @@ uint32_t crc_mulmod(uint32_t a, uint32_t b);  // a * b mod P
 namespace crcdev {
 
 #define CFSEC_CRC_EXTERN(K)                                                                         \
-  extern template hipError_t launch_crc_k<K, true>(int, const GfCrcArgs&, dim3, hipStream_t, bool);  \
-  extern template hipError_t launch_crc_k<K, false>(int, const GfCrcArgs&, dim3, hipStream_t, bool);
+  extern template hipError_t launch_crc_k<K, true>(int, const GfCrcArgs&, dim3, hipStream_t, int);  \
+  extern template hipError_t launch_crc_k<K, false>(int, const GfCrcArgs&, dim3, hipStream_t, int);
 
 }  // namespace crcdev
 }  // namespace cfsec
@@ -482,7 +493,7 @@ namespace crcdev {
 #define CFSEC_CRC_INSTANTIATE(K)                                                                     \
   namespace cfsec {                                                                                  \
   namespace crcdev {                                                                                 \
-  template hipError_t launch_crc_k<K, true>(int, const GfCrcArgs&, dim3, hipStream_t, bool);        \
-  template hipError_t launch_crc_k<K, false>(int, const GfCrcArgs&, dim3, hipStream_t, bool);       \
+  template hipError_t launch_crc_k<K, true>(int, const GfCrcArgs&, dim3, hipStream_t, int);        \
+  template hipError_t launch_crc_k<K, false>(int, const GfCrcArgs&, dim3, hipStream_t, int);       \
   }                                                                                                  \
   }
