@@ -358,8 +358,27 @@ Status RSEngine::encode_stripes(cfsec_shard* const* stripes, int nst, int mem, i
   return run_stripes(tasks, mem);
 }
 
+Status RSEngine::stripes_one_by_one(cfsec_shard* const* stripes, int nst, int mem, bool reconstruct, bool verify,
+                                   int* status) {
+  // More inputs than one compare launch carries (k > kLaunchMaxRows): the single-stripe calls,
+  // whose Verify stores into staging and compares there (run(): two_step_verify), stripe by stripe.
+  for (int s = 0; s < nst; ++s) {
+    Status st = stripes[s] ? CFSEC_OK : CFSEC_ERR_INVALID_ARG;
+    if (st == CFSEC_OK && reconstruct) st = this->reconstruct(stripes[s], total(), false, mem, nullptr);
+    if (st == CFSEC_OK && verify) {
+      bool ok = false;
+      st = this->verify(stripes[s], total(), mem, nullptr, &ok);
+      if (st == CFSEC_OK && !ok) st = CFSEC_ERR_VERIFY;
+    }
+    if (st == CFSEC_ERR_DEVICE) return st;
+    status[s] = st;
+  }
+  return CFSEC_OK;
+}
+
 Status RSEngine::verify_stripes(cfsec_shard* const* stripes, int nst, int mem, int* status) {
   if (!stripes || !status || nst < 0) return CFSEC_ERR_INVALID_ARG;
+  if (k_ > kLaunchMaxRows && m_ > 0) return stripes_one_by_one(stripes, nst, mem, false, true, status);
   StripePlan plan;
   for (int i = 0; i < k_; ++i) plan.in.push_back(i);
   for (int i = k_; i < total(); ++i) plan.out.push_back(i);
@@ -383,6 +402,7 @@ Status RSEngine::verify_stripes(cfsec_shard* const* stripes, int nst, int mem, i
 
 Status RSEngine::reconstruct_stripes(cfsec_shard* const* stripes, int nst, int mem, bool verify, int* status) {
   if (!stripes || !status || nst < 0) return CFSEC_ERR_INVALID_ARG;
+  if (verify && k_ > kLaunchMaxRows && m_ > 0) return stripes_one_by_one(stripes, nst, mem, true, true, status);
   PlanStore store;
   std::vector<StripeTask> tasks;
   plan_reconstruct_tasks(stripes, nst, verify, status, 0, 0, &store, &tasks);
@@ -758,6 +778,22 @@ Status LrcEncoder::reconstruct_batch(cfsec_shard* shards, int n, int nbids, cons
   HostTimer whole("lrc reconstruct_batch");
   const int N = t_.n, M = t_.m, L = t_.l, AZ = t_.az_count;
   const int lsz = (N + M + L) / AZ;
+  if (verify && std::max(N, local_->k()) > kLaunchMaxRows) {
+    // compared rows over more than one launch's inputs: the single calls, bid by bid (each takes
+    // its own concurrency slot)
+    for (int b = 0; b < nbids; ++b) {
+      cfsec_shard* sh = shards + (size_t)b * n;
+      Status st = reconstruct(sh, n, bad + bad_off[b], bad_off[b + 1] - bad_off[b], mem, nullptr);
+      if (st == CFSEC_OK) {
+        bool ok = false;
+        st = this->verify(sh, n, mem, nullptr, &ok);
+        if (st == CFSEC_OK && !ok) st = CFSEC_ERR_VERIFY;
+      }
+      if (st == CFSEC_ERR_DEVICE) return st;
+      status[b] = st;
+    }
+    return CFSEC_OK;
+  }
   Slot slot(pool_.get());
   std::unique_ptr<HostTimer> ph(new HostTimer("  init/fill"));
   std::vector<cfsec_shard*> stripes;
@@ -929,6 +965,13 @@ Status LrcEncoder::encode_batch(cfsec_shard* shards, int n, int nstripes, int me
   if (!shards || !status || nstripes < 0) return CFSEC_ERR_INVALID_ARG;
   const int N = t_.n, M = t_.m, L = t_.l;
   Slot slot(pool_.get());
+  if (enable_verify_ && N > kLaunchMaxRows) {  // the fused Verify's rows exceed one compare launch
+    for (int s = 0; s < nstripes; ++s) {
+      status[s] = n != N + M + L ? CFSEC_ERR_INVALID_SHARDS : encode_stripe(shards + (size_t)s * n, n, mem, nullptr);
+      if (status[s] == CFSEC_ERR_DEVICE) return status[s];
+    }
+    return CFSEC_OK;
+  }
   StripePlan plan;
   for (int i = 0; i < N; ++i) plan.in.push_back(i);
   for (int i = N; i < N + M + L; ++i) plan.out.push_back(i);
@@ -947,6 +990,12 @@ Status LrcEncoder::encode_batch(cfsec_shard* shards, int n, int nstripes, int me
     if (st == CFSEC_OK) st = stripe_size(sh, n, false, &S);
     for (int i = 0; i < n && st == CFSEC_OK; ++i)
       if (!sh[i].data) st = CFSEC_ERR_INVALID_ARG;
+    if (st == CFSEC_ERR_SHARD_SIZE && stripe_size(sh, N + M, false, &S) == CFSEC_OK) {
+      // only a local shard has another length: the reference still writes the global parity and
+      // the AZs that pass their check -- the single-stripe path restates that sequence
+      status[s] = encode_stripe(sh, n, mem, nullptr);
+      continue;
+    }
     if (st != CFSEC_OK) {
       status[s] = st;
       continue;

@@ -169,7 +169,7 @@ int crc32block_call(bool encode, const uint8_t* src, int64_t src_len, int64_t si
 
 extern "C" {
 
-const char* cfsec_version(void) { return "cfsec 0.1.0 (gfx950)"; }
+const char* cfsec_version(void) { return "cfsec 0.3.0 (gfx950)"; }
 
 const char* cfsec_last_error(void) { return cfsec::last_error_cstr(); }
 
@@ -422,6 +422,7 @@ int cfsec_ec_set_devices(cfsec_ec* h, const int* devices, int ndev) {
 int cfsec_ec_reconstruct_batch(cfsec_ec* h, cfsec_shard* shards, int n, int nbids, const int* bad_idx,
                                const int* bad_off, int verify, int mem, int* status) {
   if (!h || nbids < 0 || n <= 0 || (nbids > 0 && (!shards || !status || !bad_off))) return CFSEC_ERR_INVALID_ARG;
+  if (nbids > 0 && bad_off[0] != 0) return CFSEC_ERR_INVALID_ARG;  // offsets index bad_idx from 0
   for (int b = 0; b < nbids; ++b)
     if (bad_off[b + 1] < bad_off[b] || (bad_off[b + 1] > bad_off[b] && !bad_idx)) return CFSEC_ERR_INVALID_ARG;
   return guarded([&] { return h->e->reconstruct_batch(shards, n, nbids, bad_idx, bad_off, mem, verify != 0, status); });

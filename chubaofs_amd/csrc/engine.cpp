@@ -1075,6 +1075,11 @@ Status LrcEncoder::encode(cfsec_shard* shards, int n, int mem, hipStream_t s) {
   const int N = t_.n, M = t_.m, L = t_.l;
   if (!shards || n != N + M + L) return CFSEC_ERR_INVALID_SHARDS;
   Slot slot(pool_.get());
+  return encode_stripe(shards, n, mem, s);
+}
+
+Status LrcEncoder::encode_stripe(cfsec_shard* shards, int n, int mem, hipStream_t s) {
+  const int N = t_.n, M = t_.m, L = t_.l;
   Status st = fill_full_shards(shards, n);
   if (st != CFSEC_OK) return st;
   size_t S = 0;
@@ -1090,9 +1095,30 @@ Status LrcEncoder::encode(cfsec_shard* shards, int n, int mem, hipStream_t s) {
   std::vector<cfsec_shard*> ins, outs;
   for (int i = 0; i < N; ++i) ins.push_back(&shards[i]);
   if (local_err != CFSEC_OK) {
-    // global parity is written before the local engine reports its error
+    // The reference's sequence, step by step: global parity (+ Verify), then every AZ's local
+    // task -- task.Run lets each goroutine finish, so the AZs that pass checkShards are encoded
+    // -- and the first error in AZ order (oracle/ec_oracle.py: ECOracle.encode).
     st = engine_->encode(shards, N + M, mem, s);
-    return st != CFSEC_OK ? st : local_err;
+    if (st != CFSEC_OK) return st;
+    if (enable_verify_) {
+      bool ok = false;
+      st = engine_->verify(shards, N + M, mem, s, &ok);
+      if (st != CFSEC_OK) return st;
+      if (!ok) return CFSEC_ERR_VERIFY;
+    }
+    Status first = CFSEC_OK;
+    for (int a = 0; a < t_.az_count; ++a) {
+      std::vector<cfsec_shard> ls;
+      for (int g : shards_in_idc(a)) ls.push_back(shards[g]);
+      Status e = local_->encode(ls.data(), (int)ls.size(), mem, s);
+      if (e == CFSEC_OK && enable_verify_) {
+        bool ok = false;
+        e = local_->verify(ls.data(), (int)ls.size(), mem, s, &ok);
+        if (e == CFSEC_OK && !ok) e = CFSEC_ERR_VERIFY;
+      }
+      if (first == CFSEC_OK) first = e;
+    }
+    return first;
   }
   for (int i = N; i < N + M + L; ++i) outs.push_back(&shards[i]);
   st = engine_->run(fused_, ins, outs, S, mem, s, MatVecMode::kStore, nullptr);

@@ -242,6 +242,9 @@ class RSEngine {
   // plan->dy16 where the code and the erasure pattern make that product cheaper (batch.cpp).
   void plan_dy16(const std::vector<bool>& present, const Matrix& dec, StripePlan* plan,
                  const ExtraRows* extra = nullptr) const;
+  // The batch calls stripe by stripe through the single-stripe calls (k > kLaunchMaxRows Verify).
+  Status stripes_one_by_one(cfsec_shard* const* stripes, int nst, int mem, bool reconstruct, bool verify,
+                            int* status);
   // Run a plan's Verify as a separate encode-matrix pass instead of its compared rows.
   bool split_verify(const StripePlan& p) const;
 
@@ -357,6 +360,8 @@ class LrcEncoder : public ECEncoder {
   bool row_over_data(int g, uint8_t* dst) const override;
 
  private:
+  // Encode of one full stripe (n == N+M+L) without taking a concurrency slot (the caller holds one).
+  Status encode_stripe(cfsec_shard* shards, int n, int mem, hipStream_t s);
   friend class ECEncoder;
   std::unique_ptr<RSEngine> local_;
   Matrix fused_;  // (M+L) x N: global parity rows then local parity rows, over data

@@ -85,6 +85,9 @@ typedef struct cfsec_rs cfsec_rs;
 typedef struct cfsec_ec cfsec_ec;
 
 /* ---------------- library ---------------- */
+/* "cfsec MAJOR.MINOR.PATCH (gfx950)".  ABI history: 0.2.0 inserted src_len into
+ * cfsec_crc32block_decode / cfsec_crc32block_decode_batch (callers built against 0.1.0 must be
+ * rebuilt); 0.3.0 adds entry points only. */
 const char* cfsec_version(void);
 /* Message for the last CFSEC_ERR_DEVICE on this thread ("" if none). */
 const char* cfsec_last_error(void);
@@ -161,7 +164,9 @@ int cfsec_rs_reconstruct_crc_batch(cfsec_rs* h, uint8_t* const* ptrs, size_t sha
  * handle's devices (balanced by bytes), page-locked buffers (cfsec_host_alloc) are coded in place,
  * pageable ones through double-buffered staging, one host thread and stream pair per device.
  * mem = CFSEC_MEM_DEVICE: each stripe runs on the device its memory lives on (one of the handle's
- * devices), after the work queued on that device's legacy default stream.  Synchronous: returns
+ * devices), after the work queued on that device's legacy default stream; with a one-device handle
+ * every stripe must live on that device (only the first stripe's memory is queried -- one pointer
+ * query costs ~1 us -- so a stripe on another GPU is the caller's error, not detected).  Synchronous: returns
  * when every result is in place.  status[s] (nstripes words) receives stripe s's result as the
  * single-stripe call would return it; the return value reports failures of the call itself
  * (CFSEC_ERR_DEVICE, CFSEC_ERR_INVALID_ARG). */

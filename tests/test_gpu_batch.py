@@ -16,12 +16,13 @@ import pytest
 
 from chubaofs_amd import _lib, codemode as cm
 from oracle import oracle as O
+from oracle.ec_oracle import ECOracle, Slice
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 MOCK_SIZES = [1024, 2048, 0, 512, 23, 65, 12]  # worker_for_test.go:79-83
-RS_MODES = [(6, 6), (12, 4), (15, 12), (16, 20), (10, 4), (3, 3)]
+RS_MODES = [(6, 6), (12, 4), (15, 12), (16, 20), (10, 4), (3, 3), (40, 4)]  # k = 40: compared rows over > 32 inputs
 
 
 def gen_mock_bytes(letter, size):
@@ -248,25 +249,21 @@ def ec_full_codeword(enc, t, size, bid):
     return shards
 
 
-def sequential(enc, shards, bad):
-    """The reference loop body: Reconstruct then Verify, with the single-call engine."""
-    work = [s.copy() for s in shards]
-    try:
-        enc.Reconstruct(work, list(bad))
-    except _lib.CfsecError as e:
-        return e.status, work
-    try:
-        ok = enc.Verify(work)
-    except _lib.CfsecError as e:
-        return e.status, work
-    return (0 if ok else _lib.ErrVerify.status), work
+def sequential(enc, shards, bad, verify=True):
+    """The reference loop body (work_shard_recover.go:751-760): Reconstruct then Verify, restated on
+    the CPU by the ec oracle (oracle/ec_oracle.py: lrcencoder.go / encoder.go over the RS oracle) --
+    never by the GPU's own single-call path."""
+    orc = ECOracle.from_tactic(enc.CodeMode)
+    work = [Slice() if s.size == 0 else Slice.of(s) for s in shards]
+    st = orc.repair(work, list(bad), verify=verify)
+    return st, [w.view().copy() for w in work]
 
 
 @pytest.mark.parametrize("memory", ["host", "device"])
 @pytest.mark.parametrize("mode", [cm.EC6P6, cm.EC12P4, cm.EC15P12, cm.EC6P10L2, cm.EC16P20L2, cm.EC4P4L2, cm.EC6P3L3])
 def test_ec_reconstruct_batch_matches_repair_loop(mode, memory):
-    """cfsec_ec_reconstruct_batch over a tasklet == the per-bid Reconstruct + Verify calls (which the
-    single-call GPU tests pin to the oracle), global stripes, with corrupted bids."""
+    """cfsec_ec_reconstruct_batch over a tasklet == the per-bid Reconstruct + Verify of the ec oracle,
+    global stripes, with corrupted bids."""
     t = cm.GetTactic(mode)
     enc = ec_new(mode)
     total = t.N + t.M + t.L
@@ -371,22 +368,31 @@ def test_ec_reconstruct_batch_local_stripes(mode):
 @pytest.mark.parametrize("mode", [cm.EC6P6, cm.EC12P4, cm.EC6P10L2, cm.EC16P20L2, cm.EC6P3L3, cm.EC4P4L2])
 @pytest.mark.parametrize("verify", [False, True])
 def test_ec_encode_batch_matches_encode(mode, memory, verify):
-    """cfsec_ec_encode_batch (access puts batched, LRC fused) == per-stripe Encode, whose parity the
-    single-call tests pin to the oracle (global + every AZ's local parity)."""
+    """cfsec_ec_encode_batch (access puts batched, LRC fused) == per-stripe Encode of the ec oracle
+    (global + every AZ's local parity, lrcencoder.go:35-82), including stripes with missing parity
+    or local shards (fillFullShards), a missing data shard, and a local parity of another length
+    (global parity written, ErrShardSize)."""
     from chubaofs_amd import ec
     t = cm.GetTactic(mode)
     enc = ec.NewEncoder(ec.Config(CodeMode=t, EnableVerify=verify))
+    orc = ECOracle.from_tactic(t, enable_verify=verify)
     total = t.N + t.M + t.L
-    stripes, want = [], []
-    for b, size in enumerate([1, 23, 2048, 4097, 699051, 65536]):
+    stripes, want, exp = [], [], []
+    for b, size in enumerate([1, 23, 2048, 4097, 699051, 65536, 777, 1000]):
         data = [gen_mock_bytes(b * 7 + i, size) for i in range(t.N)]
-        ref = data + [np.zeros(size, np.uint8) for _ in range(total - t.N)]
-        ref = [x.copy() for x in ref]
-        enc.Encode(ref)
-        want.append(ref)
         src = data + [np.full(size, 0x5A, np.uint8) for _ in range(total - t.N)]
+        if b == 6:
+            src[total - 1] = src[total - 1][:0]  # a missing (local) parity: filled, then encoded
+            src[t.N] = src[t.N][:0]
+        if b == 7 and t.L:
+            src[total - 1] = np.zeros(size + 1, np.uint8)  # a local shard of another length
+        elif b == 7:
+            src[1] = src[1][:0]  # RS: a missing data shard is an error (checkShards)
+        ref = [Slice() if x.size == 0 else Slice.of(x) for x in src]
+        exp.append(orc.encode(ref))
+        want.append([r.view().copy() for r in ref])
         stripes.append(to_mem([x.copy() for x in src], memory))
-    assert enc.EncodeBatch(stripes) == [0] * len(stripes)
+    assert enc.EncodeBatch(stripes) == exp
     for b in range(len(stripes)):
         for i in range(total):
             assert np.array_equal(host(stripes[b][i]), want[b][i]), (b, i)
