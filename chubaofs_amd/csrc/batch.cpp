@@ -511,14 +511,14 @@ bool RSEngine::split_verify(const StripePlan& p) const {
   return false;
 }
 
-Status RSEngine::run_stripes(std::vector<StripeTask>& tasks, int mem) {
+Status RSEngine::run_stripes(std::vector<StripeTask>& tasks, int mem, const AsyncOut* async) {
   if (tasks.empty()) return CFSEC_OK;
   if (devs_.empty()) {
     set_last_error("no HIP device available to the cfsec engine");
     return CFSEC_ERR_DEVICE;
   }
   if (mem != CFSEC_MEM_HOST && mem != CFSEC_MEM_DEVICE) return CFSEC_ERR_INVALID_ARG;
-  const int nd = (int)devs_.size();
+  const int nd = async ? 1 : (int)devs_.size();
   if (mem == CFSEC_MEM_DEVICE && nd == 1) {
     // one device: the batch's memory must live on it (checked on the first stripe; per-stripe
     // pointer queries cost ~1 us each)
@@ -565,10 +565,10 @@ Status RSEngine::run_stripes(std::vector<StripeTask>& tasks, int mem) {
   for (int d = 1; d < nd; ++d)
     if (!per[d].empty())
       threads.emplace_back([&, d] {
-        st[d] = run_device(per[d], mem, devs_[d]);
+        st[d] = run_device(per[d], mem, devs_[d], nullptr);
         if (st[d] != CFSEC_OK) err[d] = last_error_cstr();
       });
-  if (!per[0].empty()) st[0] = run_device(per[0], mem, devs_[0]);
+  if (!per[0].empty()) st[0] = run_device(per[0], mem, devs_[0], async);
   for (auto& th : threads) th.join();
   for (int d = 1; d < nd; ++d)
     if (st[d] != CFSEC_OK && st[0] == CFSEC_OK) {
@@ -578,7 +578,7 @@ Status RSEngine::run_stripes(std::vector<StripeTask>& tasks, int mem) {
   return st[0];
 }
 
-Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceContext* ctx) {
+Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceContext* ctx, const AsyncOut* async) {
   HostTimer whole("  run_device");
   std::unique_ptr<HostTimer> tm(new HostTimer("    classify + acquire"));
   DeviceGuard g(ctx->device());
@@ -588,9 +588,12 @@ Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceCont
   // row the product touches) and which go through staging (pageable host memory)
   std::vector<StripeTask*> direct, staged;
   std::map<std::pair<const StripeTask*, int>, uint8_t*> alias;
-  int nphase = 1;
+  int nphase = 1, nitems = 0;
+  bool checks = false;  // some task compares rows (Verify)
   for (StripeTask* t : tasks) {
     nphase = std::max(nphase, t->phase + 1);
+    nitems = std::max(nitems, t->owner + 1);
+    checks = checks || t->plan->out.size() > (size_t)t->plan->nstore;
     bool in_place = true;
     if (mem == CFSEC_MEM_HOST) {
       for (int c : t->plan->in) {
@@ -606,6 +609,7 @@ Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceCont
     }
     (in_place ? direct : staged).push_back(t);
   }
+  if (async && (!staged.empty() || (checks && !async->flags))) return CFSEC_ERR_INVALID_ARG;
   // staging lanes: each holds whole stripes, at least the largest one
   size_t lane_bytes = 0, staged_total = 0;
   for (StripeTask* t : staged) {
@@ -614,23 +618,22 @@ Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceCont
     staged_total += b;
   }
   if (!staged.empty()) lane_bytes = std::max(lane_bytes, std::min(kLaneBudget, staged_total));
-  const int nlanes = staged_total > lane_bytes || nphase > 1 ? 2 : 1;
+  // two lanes only for staged chunks (a second phase of in-place stripes follows the first on one
+  // stream)
+  const int nlanes = !staged.empty() && (staged_total > lane_bytes || nphase > 1) ? 2 : 1;
   DeviceContext::Workspace* ws = nullptr;
-  Status st = ctx->acquire(lane_bytes * nlanes, (size_t)n, &ws);
+  Status st = ctx->acquire(lane_bytes * nlanes, (size_t)std::max(n, nitems), &ws, (size_t)n);
   if (st != CFSEC_OK) return st;
-  hipStream_t lane[2] = {ws->stream, ws->stream2};
+  // asynchronous calls run on the caller's stream (NULL: the legacy default stream); synchronous
+  // ones on the workspace's streams, ordered after the legacy default stream for device memory
+  hipStream_t lane[2] = {async ? async->stream : ws->stream, ws->stream2};
   // lane `to` waits for everything queued on lane `from` so far
   const auto join = [&](int from, int to) {
     Status e = hip_status(hipEventRecord(ws->ev, lane[from]), "hipEventRecord");
     if (e == CFSEC_OK) e = hip_status(hipStreamWaitEvent(lane[to], ws->ev, 0), "hipStreamWaitEvent");
     return e;
   };
-  // verify flags only where some task compares rows (a batch of pure stores skips the flag memset
-  // and read-back: ~10 us of a synchronous call)
-  bool checks = false;
-  for (StripeTask* t : tasks) checks = checks || t->plan->out.size() > (size_t)t->plan->nstore;
-  if (mem == CFSEC_MEM_DEVICE) st = ctx->order_after_default(ws);
-  if (st == CFSEC_OK && checks) st = hip_status(hipMemsetAsync(ws->dflags, 0, 4 * (size_t)n, lane[0]), "hipMemsetAsync");
+  if (mem == CFSEC_MEM_DEVICE && !async) st = ctx->order_after_default(ws);
   if (st == CFSEC_OK && nlanes > 1) st = join(0, 1);
   int next_flag = 0;
   std::vector<std::pair<StripeTask*, int>> flags;  // (task, flag word)
@@ -656,7 +659,7 @@ Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceCont
         return mem == CFSEC_MEM_DEVICE ? (const uint8_t*)t->shards[idx].data : (const uint8_t*)alias[{t, idx}];
       });
       for (const Group& gr : groups)
-        if (st == CFSEC_OK) st = hip_status(launch_group(gr, ws->dflags, lane[0]), "launch_matvec(batch)");
+        if (st == CFSEC_OK) st = hip_status(launch_group(gr, ws->bflags, lane[0]), "launch_matvec(batch)");
       record(groups);
     }
     // staged stripes: chunks of whole stripes alternating over the two lanes; each lane copies its
@@ -699,7 +702,7 @@ Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceCont
       std::vector<Group> groups =
           make_groups(part, &next_flag, [&](const StripeTask* t, int idx) { return (const uint8_t*)slot[{t, idx}]; });
       for (const Group& gr : groups)
-        if (st == CFSEC_OK) st = hip_status(launch_group(gr, ws->dflags, s), "launch_matvec(batch)");
+        if (st == CFSEC_OK) st = hip_status(launch_group(gr, ws->bflags, s), "launch_matvec(batch)");
       record(groups);
       for (StripeTask* t : part)
         for (int r = 0; r < t->plan->nstore && st == CFSEC_OK; ++r) {
@@ -710,11 +713,27 @@ Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceCont
       i0 = i1;
     }
   }
-  tm.reset(new HostTimer("    sync"));
   if (st == CFSEC_OK && nlanes > 1) st = join(1, 0);
-  if (st == CFSEC_OK && checks)
-    st = hip_status(hipMemcpyAsync(ws->hflags, ws->dflags, 4 * (size_t)n, hipMemcpyDeviceToHost, lane[0]),
-                    "hipMemcpyAsync D2H");
+  // Verify flags per batch item, gathered from the per-task words (which the gather resets): into
+  // the caller's device array (asynchronous), or straight into the pinned host words (no D2H copy)
+  if (st == CFSEC_OK && checks) {
+    std::vector<std::pair<int, int>> pairs;
+    for (auto& f : flags)
+      if (f.first->plan->out.size() > (size_t)f.first->plan->nstore) pairs.emplace_back(f.first->owner, f.second);
+    std::sort(pairs.begin(), pairs.end());
+    std::vector<int> item(pairs.size()), word(pairs.size());
+    for (size_t i = 0; i < pairs.size(); ++i) item[i] = pairs[i].first, word[i] = pairs[i].second;
+    st = hip_status(launch_flag_gather(ws->bflags, async ? async->flags : ws->hflags_dev, item.data(), word.data(),
+                                       (int)pairs.size(), async != nullptr, lane[0]),
+                    "launch_flag_gather");
+  }
+  if (st != CFSEC_OK) ws->bflags_clean = false;  // some task words may be left set: memset on reuse
+  if (async) {
+    tm.reset();
+    ctx->release_after(ws, lane[0]);
+    return st;
+  }
+  tm.reset(new HostTimer("    sync"));
   for (int l = 0; l < nlanes; ++l) {
     const Status sync = hip_status(hipStreamSynchronize(lane[l]), "hipStreamSynchronize");
     if (st == CFSEC_OK) st = sync;
@@ -722,7 +741,9 @@ Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceCont
   tm.reset();
   if (st == CFSEC_OK && checks)
     for (auto& f : flags)
-      if (ws->hflags[f.second] != 0 && *f.first->status == CFSEC_OK) *f.first->status = CFSEC_ERR_VERIFY;
+      if (f.first->plan->out.size() > (size_t)f.first->plan->nstore && ws->hflags[f.first->owner] != 0 &&
+          *f.first->status == CFSEC_OK)
+        *f.first->status = CFSEC_ERR_VERIFY;
   ctx->release(ws);
   return st;
 }
@@ -741,7 +762,7 @@ Status LrcEncoder::set_devices(const int* devices, int n) {
 }
 
 Status ECEncoder::reconstruct_batch(cfsec_shard* shards, int n, int nbids, const int* bad, const int* bad_off,
-                                    int mem, bool verify, int* status) {
+                                    int mem, bool verify, int* status, const AsyncOut* async) {
   // encoder.go:139-144 per bid (initBadShards, engine Reconstruct), then encoder.go:133-137 (Verify)
   if (!shards || !status || !bad_off || nbids < 0) return CFSEC_ERR_INVALID_ARG;
   Slot slot(pool_.get());
@@ -763,13 +784,22 @@ Status ECEncoder::reconstruct_batch(cfsec_shard* shards, int n, int nbids, const
     pos.push_back(b);
   }
   std::vector<int> st(stripes.size());
-  const Status rc = engine_->reconstruct_stripes(stripes.data(), (int)stripes.size(), mem, verify, st.data());
+  Status rc;
+  if (verify && engine_->k() > kLaunchMaxRows) {
+    rc = engine_->reconstruct_stripes(stripes.data(), (int)stripes.size(), mem, verify, st.data());
+  } else {
+    PlanStore store;
+    std::vector<StripeTask> tasks;
+    engine_->plan_reconstruct_tasks(stripes.data(), (int)stripes.size(), verify, st.data(), 0, 0, &store, &tasks);
+    for (auto& t : tasks) t.owner = pos[t.owner];  // the bid: its verify word
+    rc = engine_->run_stripes(tasks, mem, async);
+  }
   for (size_t i = 0; i < pos.size(); ++i) status[pos[i]] = st[i];
   return rc;
 }
 
 Status LrcEncoder::reconstruct_batch(cfsec_shard* shards, int n, int nbids, const int* bad, const int* bad_off,
-                                     int mem, bool verify, int* status) {
+                                     int mem, bool verify, int* status, const AsyncOut* async) {
   // lrcencoder.go:133-186 per bid, then lrcencoder.go:89-131 (Verify): a local stripe (n = its size)
   // is the local engine alone; a whole stripe is the global engine over its first N+M shards, then
   // each AZ's local engine over that AZ's local stripe -- planned together and run as two phases of
@@ -819,7 +849,11 @@ Status LrcEncoder::reconstruct_batch(cfsec_shard* shards, int n, int nbids, cons
   }
   if (n == lsz) {  // local stripes: local engine only (lrcencoder.go:93-99, 147-152)
     std::vector<int> st(stripes.size());
-    const Status rc = local_->reconstruct_stripes(stripes.data(), (int)stripes.size(), mem, verify, st.data());
+    PlanStore store;
+    std::vector<StripeTask> tasks;
+    local_->plan_reconstruct_tasks(stripes.data(), (int)stripes.size(), verify, st.data(), 0, 0, &store, &tasks);
+    for (auto& t : tasks) t.owner = pos[t.owner];
+    const Status rc = local_->run_stripes(tasks, mem, async);
     for (size_t i = 0; i < pos.size(); ++i) status[pos[i]] = st[i];
     return rc;
   }
@@ -910,7 +944,8 @@ Status LrcEncoder::reconstruct_batch(cfsec_shard* shards, int n, int nbids, cons
     tasks[t].owner = (int)owner[v];
   }
   ph.reset();
-  const Status rc = engine_->run_stripes(tasks, mem);
+  for (auto& t : tasks) t.owner = pos[t.owner];  // the bid: its device, its verify word
+  const Status rc = engine_->run_stripes(tasks, mem, async);
   // per bid: a Reconstruct error (global, then local) wins over a failed Verify
   std::vector<int> local_err(stripes.size(), CFSEC_OK);
   for (size_t v = 0; v < lp.size(); ++v) {
@@ -928,37 +963,64 @@ Status LrcEncoder::reconstruct_batch(cfsec_shard* shards, int n, int nbids, cons
   return rc;
 }
 
-Status ECEncoder::encode_batch(cfsec_shard* shards, int n, int nstripes, int mem, int* status) {
-  // encoder.go:114-131 per stripe: engine Encode, then Verify when EnableVerify
+Status ECEncoder::encode_batch(cfsec_shard* shards, int n, int nstripes, int mem, int* status,
+                               const AsyncOut* async) {
+  // encoder.go:114-131 per stripe: engine Encode, then Verify when EnableVerify -- the Verify pass in
+  // the same call (phase 1), after the encode
   if (!shards || !status || nstripes < 0) return CFSEC_ERR_INVALID_ARG;
   Slot slot(pool_.get());
-  std::vector<cfsec_shard*> stripes;
-  std::vector<int> pos;
-  for (int s = 0; s < nstripes; ++s) {
-    status[s] = CFSEC_OK;
-    if (n != engine_->total()) {
-      status[s] = CFSEC_ERR_TOO_FEW_SHARDS;  // reedsolomon.go:610-612
-      continue;
+  const int k = engine_->k(), m = engine_->m(), tot = k + m;
+  if (enable_verify_ && k > kLaunchMaxRows) {  // compared rows over more inputs than one launch carries
+    std::vector<cfsec_shard*> stripes;
+    std::vector<int> pos;
+    for (int s = 0; s < nstripes; ++s) {
+      status[s] = n != tot ? CFSEC_ERR_TOO_FEW_SHARDS : CFSEC_OK;
+      if (n == tot) stripes.push_back(shards + (size_t)s * n), pos.push_back(s);
     }
-    stripes.push_back(shards + (size_t)s * n);
-    pos.push_back(s);
-  }
-  std::vector<int> st(stripes.size());
-  Status rc = engine_->encode_stripes(stripes.data(), (int)stripes.size(), mem, st.data());
-  if (rc == CFSEC_OK && enable_verify_) {
+    std::vector<int> st(stripes.size());
+    Status rc = engine_->encode_stripes(stripes.data(), (int)stripes.size(), mem, st.data());
     std::vector<cfsec_shard*> ok;
     std::vector<size_t> okp;
     for (size_t i = 0; i < stripes.size(); ++i)
       if (st[i] == CFSEC_OK) ok.push_back(stripes[i]), okp.push_back(i);
     std::vector<int> vs(ok.size());
-    rc = engine_->verify_stripes(ok.data(), (int)ok.size(), mem, vs.data());
-    for (size_t i = 0; i < ok.size(); ++i) st[okp[i]] = vs[i];  // ErrVerify when Verify is false
+    if (rc == CFSEC_OK) rc = engine_->verify_stripes(ok.data(), (int)ok.size(), mem, vs.data());
+    for (size_t i = 0; i < ok.size(); ++i) st[okp[i]] = vs[i];
+    for (size_t i = 0; i < pos.size(); ++i) status[pos[i]] = st[i];
+    return rc;
   }
-  for (size_t i = 0; i < pos.size(); ++i) status[pos[i]] = st[i];
-  return rc;
+  StripePlan plan;
+  for (int i = 0; i < k; ++i) plan.in.push_back(i);
+  for (int i = k; i < tot; ++i) plan.out.push_back(i);
+  plan.nstore = m;
+  plan.rows = engine_->matrix_rows(k, m);
+  StripePlan vplan = plan;
+  vplan.nstore = 0;
+  std::vector<StripeTask> tasks;
+  for (int s = 0; s < nstripes; ++s) {
+    status[s] = CFSEC_OK;
+    cfsec_shard* sh = shards + (size_t)s * n;
+    if (n != tot) {
+      status[s] = CFSEC_ERR_TOO_FEW_SHARDS;  // reedsolomon.go:610-612
+      continue;
+    }
+    size_t S = 0;
+    Status st = stripe_size(sh, n, false, &S);
+    for (int i = 0; i < n && st == CFSEC_OK; ++i)
+      if (!sh[i].data) st = CFSEC_ERR_INVALID_ARG;
+    if (st != CFSEC_OK) {
+      status[s] = st;
+      continue;
+    }
+    if (m == 0) continue;
+    tasks.push_back(StripeTask{sh, &plan, S, &status[s], 0, 0, s});
+    if (enable_verify_) tasks.push_back(StripeTask{sh, &vplan, S, &status[s], 0, 1, s});
+  }
+  return engine_->run_stripes(tasks, mem, async);
 }
 
-Status LrcEncoder::encode_batch(cfsec_shard* shards, int n, int nstripes, int mem, int* status) {
+Status LrcEncoder::encode_batch(cfsec_shard* shards, int n, int nstripes, int mem, int* status,
+                                const AsyncOut* async) {
   // lrcencoder.go:35-82 per stripe, fused: global parity and every AZ's local parity as one
   // (M+L) x N product over the data (the same rows LrcEncoder::encode launches); EnableVerify
   // compares all M+L rows in a second pass (the reference verifies the global and the local stripes)
@@ -967,7 +1029,8 @@ Status LrcEncoder::encode_batch(cfsec_shard* shards, int n, int nstripes, int me
   Slot slot(pool_.get());
   if (enable_verify_ && N > kLaunchMaxRows) {  // the fused Verify's rows exceed one compare launch
     for (int s = 0; s < nstripes; ++s) {
-      status[s] = n != N + M + L ? CFSEC_ERR_INVALID_SHARDS : encode_stripe(shards + (size_t)s * n, n, mem, nullptr);
+      status[s] = n != N + M + L ? CFSEC_ERR_INVALID_SHARDS
+                                 : encode_stripe(shards + (size_t)s * n, n, mem, async ? async->stream : nullptr);
       if (status[s] == CFSEC_ERR_DEVICE) return status[s];
     }
     return CFSEC_OK;
@@ -993,7 +1056,7 @@ Status LrcEncoder::encode_batch(cfsec_shard* shards, int n, int nstripes, int me
     if (st == CFSEC_ERR_SHARD_SIZE && stripe_size(sh, N + M, false, &S) == CFSEC_OK) {
       // only a local shard has another length: the reference still writes the global parity and
       // the AZs that pass their check -- the single-stripe path restates that sequence
-      status[s] = encode_stripe(sh, n, mem, nullptr);
+      status[s] = encode_stripe(sh, n, mem, async ? async->stream : nullptr);
       continue;
     }
     if (st != CFSEC_OK) {
@@ -1013,7 +1076,7 @@ Status LrcEncoder::encode_batch(cfsec_shard* shards, int n, int nstripes, int me
       tasks.push_back(v);
     }
   }
-  return engine_->run_stripes(tasks, mem);
+  return engine_->run_stripes(tasks, mem, async);
 }
 
 }  // namespace cfsec

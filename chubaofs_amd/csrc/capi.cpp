@@ -433,6 +433,30 @@ int cfsec_ec_encode_batch(cfsec_ec* h, cfsec_shard* shards, int n, int nstripes,
   return guarded([&] { return h->e->encode_batch(shards, n, nstripes, mem, status); });
 }
 
+int cfsec_ec_reconstruct_batch_async(cfsec_ec* h, cfsec_shard* shards, int n, int nbids, const int* bad_idx,
+                                     const int* bad_off, int verify, int* status, uint32_t* flags, void* stream) {
+  if (!h || nbids < 0 || n <= 0 || (nbids > 0 && (!shards || !status || !bad_off))) return CFSEC_ERR_INVALID_ARG;
+  if (nbids > 0 && bad_off[0] != 0) return CFSEC_ERR_INVALID_ARG;
+  for (int b = 0; b < nbids; ++b)
+    if (bad_off[b + 1] < bad_off[b] || (bad_off[b + 1] > bad_off[b] && !bad_idx)) return CFSEC_ERR_INVALID_ARG;
+  if (verify && nbids > 0 && !flags) return CFSEC_ERR_INVALID_ARG;
+  cfsec::AsyncOut a;
+  a.stream = as_stream(stream);
+  a.flags = flags;
+  return guarded([&] {
+    return h->e->reconstruct_batch(shards, n, nbids, bad_idx, bad_off, CFSEC_MEM_DEVICE, verify != 0, status, &a);
+  });
+}
+
+int cfsec_ec_encode_batch_async(cfsec_ec* h, cfsec_shard* shards, int n, int nstripes, int* status, uint32_t* flags,
+                                void* stream) {
+  if (!h || nstripes < 0 || n <= 0 || (nstripes > 0 && (!shards || !status))) return CFSEC_ERR_INVALID_ARG;
+  cfsec::AsyncOut a;
+  a.stream = as_stream(stream);
+  a.flags = flags;
+  return guarded([&] { return h->e->encode_batch(shards, n, nstripes, CFSEC_MEM_DEVICE, status, &a); });
+}
+
 int cfsec_ec_repair_rows(cfsec_ec* h, const int* bad_idx, int nbad, const int* want, int nwant, int* in_idx,
                          uint8_t* rows) {
   if (!h) return CFSEC_ERR_INVALID_ARG;

@@ -119,17 +119,28 @@ DeviceContext* DeviceContext::get(int device) {
   return p.get();
 }
 
-Status DeviceContext::acquire(size_t bytes, size_t nflags, Workspace** out) {
+Status DeviceContext::acquire(size_t bytes, size_t nflags, Workspace** out, size_t nbflags) {
   Workspace* ws = nullptr;
   {
     std::lock_guard<std::mutex> l(mu_);
+    // a workspace an asynchronous call returned is free once its stream has passed the call
+    const auto ready = [](Workspace* w) {
+      if (!w->pending) return true;
+      const hipError_t q = hipEventQuery(w->done);
+      if (q == hipErrorNotReady) return false;
+      (void)hipGetLastError();
+      w->pending = false;
+      return true;
+    };
     // best fit among the free workspaces
     auto best = free_.end();
     for (auto it = free_.begin(); it != free_.end(); ++it)
-      if ((*it)->cap >= bytes && (*it)->nflags >= nflags &&
-          (best == free_.end() || (*it)->cap < (*best)->cap))
+      if ((*it)->cap >= bytes && (*it)->nflags >= nflags && (*it)->nbflags >= nbflags &&
+          (best == free_.end() || (*it)->cap < (*best)->cap) && ready(*it))
         best = it;
-    if (best == free_.end() && !free_.empty()) best = free_.begin();
+    if (best == free_.end())
+      for (auto it = free_.begin(); it != free_.end() && best == free_.end(); ++it)
+        if (ready(*it)) best = it;
     if (best != free_.end()) {
       ws = *best;
       free_.erase(best);
@@ -167,13 +178,33 @@ Status DeviceContext::acquire(size_t bytes, size_t nflags, Workspace** out) {
     if (ws->hflags) (void)hipHostFree(ws->hflags);
     ws->dflags = nullptr;
     ws->hflags = nullptr;
+    ws->hflags_dev = nullptr;
     ws->nflags = 0;
     st = hip_status(hipMalloc(reinterpret_cast<void**>(&ws->dflags), nf * 4), "hipMalloc(flags)");
     if (st == CFSEC_OK)
       st = hip_status(hipHostMalloc(reinterpret_cast<void**>(&ws->hflags), nf * 4, hipHostMallocDefault),
                       "hipHostMalloc(flags)");
+    if (st == CFSEC_OK)
+      st = hip_status(hipHostGetDevicePointer(reinterpret_cast<void**>(&ws->hflags_dev), ws->hflags, 0),
+                      "hipHostGetDevicePointer(flags)");
     if (st == CFSEC_OK) ws->nflags = nf;
   }
+  if (st == CFSEC_OK && ws->nbflags < nbflags) {
+    const size_t nf = std::max<size_t>(nbflags, 256);
+    if (ws->bflags) (void)hipFree(ws->bflags);
+    ws->bflags = nullptr;
+    ws->nbflags = 0;
+    ws->bflags_clean = false;
+    st = hip_status(hipMalloc(reinterpret_cast<void**>(&ws->bflags), nf * 4), "hipMalloc(batch flags)");
+    if (st == CFSEC_OK) ws->nbflags = nf;
+  }
+  if (st == CFSEC_OK && ws->bflags && !ws->bflags_clean) {
+    // once per allocation (or after a failed call): the gather kernel keeps them zero afterwards
+    st = hip_status(hipMemset(ws->bflags, 0, ws->nbflags * 4), "hipMemset(batch flags)");
+    if (st == CFSEC_OK) ws->bflags_clean = true;
+  }
+  if (st == CFSEC_OK && !ws->done)
+    st = hip_status(hipEventCreateWithFlags(&ws->done, hipEventDisableTiming), "hipEventCreate");
   if (st != CFSEC_OK) {
     release(ws);
     return st;
@@ -193,6 +224,18 @@ Status DeviceContext::order_after_default(Workspace* ws) {
 void DeviceContext::release(Workspace* ws) {
   std::lock_guard<std::mutex> l(mu_);
   free_.push_back(ws);
+}
+
+void DeviceContext::release_after(Workspace* ws, hipStream_t stream) {
+  // if the record fails the stream's work is unknown: wait for the device before reuse
+  if (hipEventRecord(ws->done, stream) != hipSuccess) {
+    (void)hipGetLastError();
+    (void)hipDeviceSynchronize();
+    ws->pending = false;
+  } else {
+    ws->pending = true;
+  }
+  release(ws);
 }
 
 // ---------------------------------------------------------------- inversion cache

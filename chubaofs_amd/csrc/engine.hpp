@@ -69,6 +69,16 @@ class DeviceContext {
     hipStream_t stream2 = nullptr;  // second lane of the chunked host pipeline
     hipEvent_t ev = nullptr;        // orders stream2 after work enqueued on stream
     hipEvent_t ev_in = nullptr;     // orders stream after the legacy default stream (no caller stream)
+    // batch calls (batch.cpp run_device): per-task verify words, kept zero between calls (the flag
+    // gather kernel resets the words it reads), and the device address of hflags
+    uint32_t* bflags = nullptr;
+    size_t nbflags = 0;
+    bool bflags_clean = false;
+    uint32_t* hflags_dev = nullptr;
+    // asynchronous calls: the workspace is reused only after `done` (recorded on the caller's
+    // stream after the call's last kernel) has completed
+    hipEvent_t done = nullptr;
+    bool pending = false;
   };
   // Order ws->stream after the work already queued on the legacy default stream (and, by that
   // stream's semantics, on every blocking stream of the device): a device-memory call made
@@ -76,9 +86,13 @@ class DeviceContext {
   // The workspace streams themselves are non-blocking, so concurrent callers do not serialise
   // on each other's null-stream work.
   Status order_after_default(Workspace* ws);
-  // Check out a workspace with at least `bytes` of staging and `nflags` flag words.
-  Status acquire(size_t bytes, size_t nflags, Workspace** out);
+  // Check out a workspace with at least `bytes` of staging, `nflags` flag words (device + pinned
+  // host) and `nbflags` batch flag words (zero on return).
+  Status acquire(size_t bytes, size_t nflags, Workspace** out, size_t nbflags = 0);
   void release(Workspace* ws);
+  // Return a workspace whose work is still queued on `stream`: it is handed out again only once
+  // the stream has passed this point.
+  void release_after(Workspace* ws, hipStream_t stream);
 
  private:
   explicit DeviceContext(int device) : device_(device) {}
@@ -154,6 +168,13 @@ struct StripePlan {
 // balanced by the bytes each stripe moves (cfsec_batch_partition).
 void partition_stripes(const uint64_t* bytes, int n, int ndev, int* dev);
 
+// An asynchronous batch call's destination: kernels on `stream`, per-item Verify mismatches OR-ed
+// into the device words flags[owner] (the caller zeroes them).
+struct AsyncOut {
+  hipStream_t stream = nullptr;
+  uint32_t* flags = nullptr;
+};
+
 // One stripe of a batch call: its shard vector, the plan, its length, its result.
 struct StripeTask {
   cfsec_shard* shards = nullptr;
@@ -162,7 +183,8 @@ struct StripeTask {
   int* status = nullptr;        // set to CFSEC_ERR_VERIFY when a compared row mismatches
   int dev = 0;                  // index into the engine's device list
   int phase = 0;                // tasks of phase p run after every task of phase p - 1 (same call)
-  int owner = 0;                // batch item: a host batch keeps an item's tasks on one device
+  int owner = 0;                // batch item: a host batch keeps an item's tasks on one device; the
+                                // item's Verify word (asynchronous calls: the caller's flags[owner])
 };
 
 // Plans built for one batch call (stable addresses for the tasks that point at them).
@@ -183,6 +205,13 @@ class RSEngine {
   int total() const { return k_ + m_; }
   int device() const { return ctx_ ? ctx_->device() : -1; }
   const Matrix& matrix() const { return mat_; }
+  // rows [r0, r0 + nr) of the encoding matrix (the parity rows: matrix_rows(k, m))
+  Matrix matrix_rows(int r0, int nr) const {
+    Matrix out(nr, k_);
+    for (int r = 0; r < nr; ++r)
+      for (int c = 0; c < k_; ++c) out.at(r, c) = mat_.at(r0 + r, c);
+    return out;
+  }
 
   Status encode(cfsec_shard* shards, int n, int mem, hipStream_t stream);
   // Encode + crc32.ChecksumIEEE of every shard into host crcs[n], one fused pass.
@@ -235,7 +264,9 @@ class RSEngine {
                               const ExtraRows* extra = nullptr, const std::vector<bool>* fuse = nullptr);
   // Run the tasks' products (device memory, pinned host memory in place, pageable host memory
   // through double-buffered staging), tasks partitioned over the devices.
-  Status run_stripes(std::vector<StripeTask>& tasks, int mem);
+  // async (device memory, the handle's first device): enqueue on async->stream and return; verify
+  // mismatches OR 1 into async->flags[owner] instead of setting the tasks' status.
+  Status run_stripes(std::vector<StripeTask>& tasks, int mem, const AsyncOut* async = nullptr);
   // Plan of a Reconstruct (+ Verify) over the present shards.
   Status plan_stripe(const std::vector<bool>& present, bool verify, StripePlan* plan,
                      const ExtraRows* extra = nullptr);
@@ -271,7 +302,7 @@ class RSEngine {
   InversionCache tree_;
   DeviceContext* ctx_ = nullptr;
   std::vector<DeviceContext*> devs_;  // batch devices, ctx_ first
-  Status run_device(std::vector<StripeTask*>& tasks, int mem, DeviceContext* ctx);
+  Status run_device(std::vector<StripeTask*>& tasks, int mem, DeviceContext* ctx, const AsyncOut* async);
 };
 
 // Counting semaphore (util/limit/count.NewBlockingCount, encoder.go:90).
@@ -322,11 +353,14 @@ class ECEncoder {
   // n shards at shards[b*n ..], Reconstruct(shards_b, bad_b) then Verify(shards_b), where bad_b =
   // bad[bad_off[b] .. bad_off[b+1]); status[b] = the Reconstruct error, CFSEC_ERR_VERIFY when Verify
   // returns false, or CFSEC_OK.  verify = false: Reconstruct only.
+  // async (device memory, asynchronous on async->stream): status[b] gets the planning result at
+  // return; a Verify mismatch ORs 1 into async->flags[b] when the stream gets there.
   virtual Status reconstruct_batch(cfsec_shard* shards, int n, int nbids, const int* bad, const int* bad_off,
-                                   int mem, bool verify, int* status);
+                                   int mem, bool verify, int* status, const AsyncOut* async = nullptr);
   // Encode over a batch of stripes of n shards each (access puts, stream_put.go:104-143), with
   // the Config's EnableVerify; status[s] as Encode would return it.
-  virtual Status encode_batch(cfsec_shard* shards, int n, int nstripes, int mem, int* status);
+  virtual Status encode_batch(cfsec_shard* shards, int n, int nstripes, int mem, int* status,
+                              const AsyncOut* async = nullptr);
 
  protected:
   // Shard index g (< N + M + L) as a row over the N data shards.
@@ -353,8 +387,9 @@ class LrcEncoder : public ECEncoder {
   std::vector<int> shards_in_idc(int idx) const override;
   Status set_devices(const int* devices, int n) override;
   Status reconstruct_batch(cfsec_shard* shards, int n, int nbids, const int* bad, const int* bad_off, int mem,
-                           bool verify, int* status) override;
-  Status encode_batch(cfsec_shard* shards, int n, int nstripes, int mem, int* status) override;
+                           bool verify, int* status, const AsyncOut* async = nullptr) override;
+  Status encode_batch(cfsec_shard* shards, int n, int nstripes, int mem, int* status,
+                      const AsyncOut* async = nullptr) override;
 
  protected:
   bool row_over_data(int g, uint8_t* dst) const override;

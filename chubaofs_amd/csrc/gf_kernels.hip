@@ -248,6 +248,63 @@ hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
   return hipSuccess;
 }
 
+namespace {
+constexpr int kGatherSlots = 256;  // items and words per gather launch (argument block < 3 KiB)
+struct GatherArgs {
+  uint32_t* tmp;
+  uint32_t* out;
+  uint32_t nitems;
+  uint32_t acc;
+  uint32_t item[kGatherSlots];
+  uint32_t word[kGatherSlots];
+  uint16_t first[kGatherSlots + 1];
+};
+
+// One thread per item: OR of its tasks' words, which are reset to 0.
+__global__ __launch_bounds__(kGatherSlots) void flag_gather_kernel(const GatherArgs a) {
+  const uint32_t o = threadIdx.x;
+  if (o >= a.nitems) return;
+  uint32_t v = 0;
+  for (int j = a.first[o]; j < a.first[o + 1]; ++j) {
+    v |= a.tmp[a.word[j]];
+    a.tmp[a.word[j]] = 0;
+  }
+  uint32_t* p = a.out + a.item[o];
+  *p = a.acc ? (*p | (v != 0 ? 1u : 0u)) : (v != 0 ? 1u : 0u);
+}
+}  // namespace
+
+hipError_t launch_flag_gather(uint32_t* tmp, uint32_t* out, const int* item, const int* word, int n,
+                              bool accumulate, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  if (!tmp || !out || !item || !word) return hipErrorInvalidValue;
+  GatherArgs a;
+  a.tmp = tmp;
+  a.out = out;
+  a.acc = accumulate ? 1u : 0u;
+  int j = 0;
+  while (j < n) {
+    // one launch: whole items only, up to kGatherSlots items and kGatherSlots words
+    int ni = 0, nw = 0;
+    a.first[0] = 0;
+    while (j < n && ni < kGatherSlots) {
+      int e = j;
+      while (e < n && item[e] == item[j]) ++e;
+      if (e - j > kGatherSlots) return hipErrorInvalidValue;
+      if (nw + (e - j) > kGatherSlots) break;
+      a.item[ni] = (uint32_t)item[j];
+      for (int q = j; q < e; ++q) a.word[nw++] = (uint32_t)word[q];
+      a.first[++ni] = (uint16_t)nw;
+      j = e;
+    }
+    a.nitems = (uint32_t)ni;
+    hipLaunchKernelGGL(flag_gather_kernel, dim3(1), dim3(kGatherSlots), 0, stream, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
 hipError_t launch_dy16_repair(const Dy16RepairJob& job, hipStream_t stream) {
   using dev::kPtrSlots;
   const int nd = job.nd, ne = job.e, mo = nd + 20 + ne;

@@ -54,6 +54,14 @@ struct Dy16RepairJob {
 };
 hipError_t launch_dy16_repair(const Dy16RepairJob& job, hipStream_t stream);
 
+// Verify flags of a batch call gathered per batch item (batch.cpp run_device): for every item o,
+// out[o] = OR of the per-task words tmp[word[j]] of the pairs (o, word[j]) -- `accumulate`: out[o] |=
+// (v != 0), else out[o] = (v != 0) -- and those tmp words are reset to 0, so a workspace's flag words
+// stay zero between calls (no memset per call).  pairs: n (item, word) entries sorted by item; out
+// may be host-mapped pinned memory (the synchronous calls read it after the sync, no D2H copy).
+hipError_t launch_flag_gather(uint32_t* tmp, uint32_t* out, const int* item, const int* word, int n,
+                              bool accumulate, hipStream_t stream);
+
 // Rows one launch carries (dev::kMaxK / dev::kMaxM); kStoreVerify needs m <= kLaunchMaxRows.
 constexpr int kLaunchMaxRows = 32;
 

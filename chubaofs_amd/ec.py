@@ -122,6 +122,47 @@ class Encoder:
         _lib.check(st)
         return [int(status[i]) for i in range(len(bids))]
 
+    def ReconstructBatchAsync(self, bids, badIdx, flags=None, verify: bool = True, stream=None):
+        """cfsec_ec_reconstruct_batch_async: bids of device tensors; enqueues on `stream` (default:
+        torch's current stream) and returns the per-bid planning status right away.  flags: a zeroed
+        device int32 tensor of len(bids) words; flags[b] != 0 once the stream has passed the call
+        where Verify is false."""
+        if len(bids) != len(badIdx):
+            raise ValueError("one bad-index list per bid")
+        n = len(bids[0]) if bids else 0
+        bm = BatchMarshal(bids, n, fill=True)
+        if bids and bm.mem != _lib.MEM_DEVICE:
+            raise TypeError("the asynchronous batch takes device tensors")
+        flat = [i for b in badIdx for i in b]
+        off = [0]
+        for b in badIdx:
+            off.append(off[-1] + len(b))
+        bad = (ctypes.c_int * max(len(flat), 1))(*flat)
+        offs = (ctypes.c_int * len(off))(*off)
+        status = (ctypes.c_int * max(len(bids), 1))()
+        like = next((x for st in bids for x in st if x is not None and x.numel()), None)
+        st = self._L.cfsec_ec_reconstruct_batch_async(self._h, bm.arr, n, len(bids), bad, offs, int(verify), status,
+                                                      None if flags is None else flags.data_ptr(),
+                                                      stream_ptr(stream, like))
+        bm.writeback()
+        _lib.check(st)
+        return [int(status[i]) for i in range(len(bids))]
+
+    def EncodeBatchAsync(self, stripes, flags=None, stream=None):
+        """cfsec_ec_encode_batch_async: as EncodeBatch on device tensors, enqueued on `stream`; with
+        EnableVerify a false Verify sets flags[s] (zeroed device int32 tensor) on the stream."""
+        n = len(stripes[0]) if stripes else 0
+        bm = BatchMarshal(stripes, n, fill=True)
+        if stripes and bm.mem != _lib.MEM_DEVICE:
+            raise TypeError("the asynchronous batch takes device tensors")
+        status = (ctypes.c_int * max(len(stripes), 1))()
+        like = next((x for st in stripes for x in st if x is not None and x.numel()), None)
+        st = self._L.cfsec_ec_encode_batch_async(self._h, bm.arr, n, len(stripes), status,
+                                                 None if flags is None else flags.data_ptr(), stream_ptr(stream, like))
+        bm.writeback()
+        _lib.check(st)
+        return [int(status[i]) for i in range(len(stripes))]
+
     # -- slice bookkeeping (host) --
     def Split(self, data, length: int | None = None):
         """encoder.go:153-155 / lrcencoder.go:203-222.  data: uint8 array; data[:length] is the

@@ -220,6 +220,22 @@ int cfsec_ec_set_devices(cfsec_ec* h, const int* devices, int ndev);
  * modes as one fused (M+L) x N pass (lrcencoder.go:35-82).  status[s]: Encode's result (CFSEC_ERR_VERIFY
  * when the enabled Verify fails).  Memory and devices as for cfsec_rs_*_stripes. */
 int cfsec_ec_encode_batch(cfsec_ec* h, cfsec_shard* shards, int n, int nstripes, int mem, int* status);
+/* Asynchronous forms of the two batch calls above, for device memory on the handle's (first) device:
+ * the call plans the batch, enqueues its kernels on `stream` (hipStream_t; NULL = the legacy default
+ * stream) and returns without waiting, so a caller overlaps the next tasklet's planning with this
+ * one's kernels.  status[b] (host) receives at return what the synchronous call would report
+ * except a false Verify: the shard checks and planning errors (the buffers of a failed bid are not
+ * touched).  flags (device, one uint32 per bid, zeroed by the caller; may be NULL when no Verify is
+ * asked for): once the stream has passed the call, flags[b] != 0 where Verify is false
+ * (CFSEC_ERR_VERIFY of the synchronous call).  Missing shards' lengths are set at return, as in the
+ * synchronous call; the bytes are there when the stream gets there.  The library keeps no caller
+ * pointer after the call returns (the shard pointers are copied into the kernel arguments).  Shapes
+ * the kernels cannot compare in one pass (more than 32 inputs with Verify, an LRC stripe whose
+ * local shard has another length) run synchronously on `stream` and report ErrVerify in status[b]. */
+int cfsec_ec_reconstruct_batch_async(cfsec_ec* h, cfsec_shard* shards, int n, int nbids, const int* bad_idx,
+                                     const int* bad_off, int verify, int* status, uint32_t* flags, void* stream);
+int cfsec_ec_encode_batch_async(cfsec_ec* h, cfsec_shard* shards, int n, int nstripes, int* status, uint32_t* flags,
+                                void* stream);
 /* Repair over survivors held elsewhere (the multi-GPU repair of chubaofs_amd/repair.py ships only
  * the shards a decode reads): with the shards in bad_idx[0..nbad) lost (global or LRC local
  * indices), in_idx[0..N) = the first N present global shards in index order -- the ones
