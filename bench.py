@@ -591,26 +591,85 @@ def cpu_rate(fn, seconds):
             return n / dt
 
 
-def api_rate(fn, seconds):
-    """Synchronous calls of fn per second over ~seconds (after two warm calls)."""
-    fn()
-    fn()
-    n, t0 = 0, time.perf_counter()
-    while True:
-        fn()
-        n += 1
-        dt = time.perf_counter() - t0
-        if dt >= seconds:
-            return n / dt
+def cpu_saturated_rate(make_worker, seconds, callers):
+    """BASELINE.md's saturated CPU mode for a config: `callers` concurrent single-threaded callers
+    (one per usable host CPU), each with its own buffers (make_worker(w) returns its call); total
+    calls per second."""
+    import threading
+    callers = max(1, int(callers))
+    fns = [make_worker(w) for w in range(callers)]
+    for f in fns:
+        f()
+    done = [0] * callers
+    stop = time.perf_counter() + seconds
+
+    def loop(w):
+        while time.perf_counter() < stop:
+            fns[w]()
+            done[w] += 1
+
+    t0 = time.perf_counter()
+    th = [threading.Thread(target=loop, args=(w,)) for w in range(callers)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    return sum(done) / (time.perf_counter() - t0)
+
+
+def gated_calls(torch, stream, call, nbatch, seconds, zero, check, sync_call):
+    """Time a config's GPU calls with the headline's gate: after two warm calls per batch the rows
+    the calls write are zeroed (`zero`), the timed calls run over the rotated batches (at least one
+    per batch), and afterwards every written row must equal the golden bytes again (`check`).
+
+    sync_call: the calls are synchronous library calls -> calls per second of wall time.  Else they
+    are enqueued on `stream`: each call is bracketed by its own HIP event pair on that stream, so the
+    sum of the pairs is the device time of the calls' kernels alone ("kernel-only"), and the first
+    to last event the pipelined rate (host planning of call i+1 overlapping the kernels of call i).
+    Returns dict(calls_per_s=..., kernel_ms_per_call=..., n=...)."""
+    for i in range(2 * nbatch):
+        call(i)
+    torch.cuda.synchronize()
+    zero()
+    torch.cuda.synchronize()
+    if sync_call:
+        n, t0 = 0, time.perf_counter()
+        while True:
+            call(n)
+            n += 1
+            dt = time.perf_counter() - t0
+            if dt >= seconds and n >= nbatch:
+                break
+        torch.cuda.synchronize()
+        check()
+        return {"calls_per_s": n / dt, "n": n}
+    # estimate the count from a short untimed run, then the timed run with per-call events
+    t0 = time.perf_counter()
+    for i in range(nbatch):
+        call(i)
+    torch.cuda.synchronize()
+    est = max((time.perf_counter() - t0) / nbatch, 1e-5)
+    n = max(3 * nbatch, int(seconds / est) // nbatch * nbatch)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+    for i in range(n):
+        evs[i][0].record(stream)
+        call(i)
+        evs[i][1].record(stream)
+    torch.cuda.synchronize()
+    check()
+    kern = sum(a.elapsed_time(b) for a, b in evs) / n
+    wall = evs[0][0].elapsed_time(evs[-1][1]) / n
+    return {"calls_per_s": 1e3 / wall, "kernel_ms_per_call": kern, "n": n}
 
 
 def other_configs(args, torch, dev, stream, cpu):
     """BASELINE.json configs[0], [3] and [4] on this GPU, each with the klauspost-strategy CPU port
-    (oracle/cpu_simd.c, 4 threads per call as the reference with GFNI) timed beside it on the same
-    shapes.  GPU rates: C1 from HIP events around back-to-back launches (device-resident batch);
-    C4 / C5 from the synchronous batch calls a caller makes (cfsec_ec_encode_batch,
-    cfsec_ec_reconstruct_batch on device memory: planning, launches and the final sync included,
-    so their roofline fraction is a lower bound for the kernels)."""
+    (oracle/cpu_simd.c) timed beside it on the same shapes: 4 threads per call as the reference with
+    GFNI, and saturated (one single-threaded caller per usable host CPU).  Every GPU rate is gated
+    like the headline (gated_calls: the rows the timed calls write are zeroed first and must equal the
+    golden bytes afterwards, so a kernel that writes nothing fails).  C4 / C5 report both the
+    synchronous batch calls a caller makes (planning, launches, sync) and the asynchronous calls
+    (cfsec_ec_*_batch_async) on one stream, with their kernel-only time from per-call HIP events."""
     import numpy as np
 
     from chubaofs_amd import _lib, codemode as cm, ec, reedsolomon
@@ -623,6 +682,8 @@ def other_configs(args, torch, dev, stream, cpu):
         from oracle import oracle as O
     gfni = cpu and O.simd_features()["gfni"]
     thr = 4 if gfni else 8
+    callers = host_cpu_share()["usable"]
+    frac = lambda nbytes, ms: round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
 
     # ---- C1: EC6P6 encode of 1 MiB blobs, 256 blobs per batch (configs[0])
     k, m, nb = 6, 6, 256
@@ -636,30 +697,40 @@ def other_configs(args, torch, dev, stream, cpu):
     for b in range(NBATCH):
         r6.encode_batch(pt[b], S1, nb, stream=stream)
     torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    n = 30
-    e0.record(stream)
-    for i in range(n):
-        r6.encode_batch(pt[i % NBATCH], S1, nb, stream=stream)
-    e1.record(stream)
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / n
+    gold1 = b1[:, :, k:, :S1].clone()
+
+    def check1():
+        assert torch.equal(b1[:, :, k:, :S1], gold1), "C1: parity after the timed encodes differs from the golden"
+
+    r = gated_calls(torch, stream, lambda i: r6.encode_batch(pt[i % NBATCH], S1, nb, stream=stream), NBATCH, secs,
+                    lambda: b1[:, :, k:, :].zero_(), check1, sync_call=False)
+    ms = r["kernel_ms_per_call"]
     c1 = {"workload": f"EC6P6 encode, {nb} blobs of 1 MiB (S={S1}), device-resident, one launch",
           "data_GBps": round(k * S1 * nb / (ms * 1e-3) / 1e9, 1),
-          "roofline_frac": round((k + m) * S1 * nb / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
-          "avg_launch_ms": round(ms, 4), "algorithmic_bytes_per_launch": (k + m) * S1 * nb}
+          "roofline_frac": frac((k + m) * S1 * nb, ms),
+          "avg_launch_ms": round(ms, 4), "algorithmic_bytes_per_launch": (k + m) * S1 * nb,
+          "gate": "parity rows zeroed before the timed launches, equal to the golden parity after"}
     if cpu:
         full = O.build_matrix(k, k + m)
         h = b1[0, 0, :k, :S1].cpu().numpy()
         data = [np.ascontiguousarray(h[i]) for i in range(k)]
         par = [np.zeros(S1, np.uint8) for _ in range(m)]
         rate = cpu_rate(lambda: O.simd_code(full[k:], data, par, thr), cpu_secs)
-        ok = all(np.array_equal(par[r], b1[0, 0, k + r, :S1].cpu().numpy()) for r in range(m))
+        ok = all(np.array_equal(par[r_], b1[0, 0, k + r_, :S1].cpu().numpy()) for r_ in range(m))
+
+        def w1(w):
+            d = [np.roll(x, w) for x in data]
+            p = [np.zeros(S1, np.uint8) for _ in range(m)]
+            return lambda: O.simd_code(full[k:], d, p, 1)
+
+        sat = cpu_saturated_rate(w1, cpu_secs, callers)
         c1["cpu_baseline"] = {"value": round(k * S1 * rate / 1e9, 3), "unit": "GB/s", "cores": thr, "kind": "port",
                               "sample": f"one 1 MiB blob encoded repeatedly for ~{cpu_secs:.0f}s",
-                              "parity_equals_gpu": bool(ok)}
+                              "parity_equals_gpu": bool(ok),
+                              "saturated": {"value": round(k * S1 * sat / 1e9, 3), "unit": "GB/s", "cores": callers,
+                                            "sample": f"{callers} single-threaded callers, one blob each"}}
     out["C1_EC6P6_1MiB_encode"] = c1
-    del b1, pt
+    del b1, pt, gold1
 
     # ---- C4: EC6P10L2 fused LRC encode + AZ-local repair, 4 MiB blobs (configs[3])
     t4 = cm.GetTactic(cm.EC6P10L2)
@@ -672,35 +743,72 @@ def other_configs(args, torch, dev, stream, cpu):
     b4 = torch.randint(0, 256, (NBATCH, nb4, tot4, p4), dtype=torch.uint8, device=dev)
     bms = [BatchMarshal([[b4[b, s, i, :S4] for i in range(tot4)] for s in range(nb4)], tot4) for b in range(NBATCH)]
     st4 = (ctypes.c_int * nb4)()
-    rot = [0]
+    for b in range(NBATCH):
+        _lib.check(e4._L.cfsec_ec_encode_batch(e4._h, bms[b].arr, tot4, nb4, bms[b].mem, st4))
+    torch.cuda.synchronize()
+    gold4 = b4[:, :, :, :S4].clone()
 
-    def enc4():
-        bm = bms[rot[0] % NBATCH]
-        rot[0] += 1
+    def check4(rows):
+        def f():
+            assert torch.equal(b4[:, :, rows, :S4], gold4[:, :, rows]), f"C4: rows {rows} differ from the golden"
+        return f
+
+    def zero4(rows):
+        return lambda: b4[:, :, rows, :].zero_()
+
+    par4 = list(range(N, tot4))
+
+    def enc4(i):
+        bm = bms[i % NBATCH]
         _lib.check(e4._L.cfsec_ec_encode_batch(e4._h, bm.arr, tot4, nb4, bm.mem, st4))
 
-    rate = api_rate(enc4, secs)
+    def enc4a(i):
+        bm = bms[i % NBATCH]
+        _lib.check(e4._L.cfsec_ec_encode_batch_async(e4._h, bm.arr, tot4, nb4, st4, None, None, stream.cuda_stream))
+
+    rs = gated_calls(torch, stream, enc4, NBATCH, secs, zero4(par4), check4(par4), sync_call=True)
     assert list(st4) == [0] * nb4
+    ra = gated_calls(torch, stream, enc4a, NBATCH, secs, zero4(par4), check4(par4), sync_call=False)
+    assert list(st4) == [0] * nb4
+    enc_bytes = tot4 * S4 * nb4
     c4 = {"workload": f"EC6P10L2 fused LRC encode (global + 2 local parities in one pass), {nb4} blobs of 4 MiB (S={S4})",
-          "encode_data_GBps": round(N * S4 * nb4 * rate / 1e9, 1),
-          "encode_roofline_frac": round((N + M + L) * S4 * nb4 * rate / 1e9 / HBM_PEAK_GBPS, 4)}
+          "encode_data_GBps": round(N * S4 * nb4 * rs["calls_per_s"] / 1e9, 1),
+          "encode_roofline_frac": round(enc_bytes * rs["calls_per_s"] / 1e9 / HBM_PEAK_GBPS, 4),
+          "encode_async_data_GBps": round(N * S4 * nb4 * ra["calls_per_s"] / 1e9, 1),
+          "encode_kernel_ms": round(ra["kernel_ms_per_call"], 4),
+          "encode_kernel_roofline_frac": frac(enc_bytes, ra["kernel_ms_per_call"])}
     # AZ-local repair: AZ0's local stripe (8 + 1 shards) per blob, local index 0 lost
     idx0, _, _ = t4.LocalStripeInAZ(0)
     lsz = len(idx0)
     lbm = [BatchMarshal([[b4[b, s, i, :S4] for i in idx0] for s in range(nb4)], lsz) for b in range(NBATCH)]
     bad = (ctypes.c_int * nb4)(*([0] * nb4))
     off = (ctypes.c_int * (nb4 + 1))(*range(nb4 + 1))
+    fl4 = torch.zeros(nb4, dtype=torch.int32, device=dev)
 
-    def rep4():
-        bm = lbm[rot[0] % NBATCH]
-        rot[0] += 1
+    def rep4(i):
+        bm = lbm[i % NBATCH]
         _lib.check(e4._L.cfsec_ec_reconstruct_batch(e4._h, bm.arr, lsz, nb4, bad, off, 1, bm.mem, st4))
 
-    rate_r = api_rate(rep4, secs)
+    def rep4a(i):
+        bm = lbm[i % NBATCH]
+        _lib.check(e4._L.cfsec_ec_reconstruct_batch_async(e4._h, bm.arr, lsz, nb4, bad, off, 1, st4,
+                                                          fl4.data_ptr(), None, stream.cuda_stream))
+
+    lost = [idx0[0]]
+    rs = gated_calls(torch, stream, rep4, NBATCH, secs, zero4(lost), check4(lost), sync_call=True)
     assert list(st4) == [0] * nb4
-    c4.update({"local_repair_data_GBps": round((lsz - 1) * S4 * nb4 * rate_r / 1e9, 1),
-               "local_repair_roofline_frac": round(lsz * S4 * nb4 * rate_r / 1e9 / HBM_PEAK_GBPS, 4),
-               "timing": "synchronous batch calls on device memory (planning + launch + sync)"})
+    ra = gated_calls(torch, stream, rep4a, NBATCH, secs, zero4(lost), check4(lost), sync_call=False)
+    assert list(st4) == [0] * nb4 and not bool(fl4.any().item()), "C4: local Verify failed"
+    rep_bytes = lsz * S4 * nb4
+    c4.update({"local_repair_data_GBps": round((lsz - 1) * S4 * nb4 * rs["calls_per_s"] / 1e9, 1),
+               "local_repair_roofline_frac": round(rep_bytes * rs["calls_per_s"] / 1e9 / HBM_PEAK_GBPS, 4),
+               "local_repair_async_data_GBps": round((lsz - 1) * S4 * nb4 * ra["calls_per_s"] / 1e9, 1),
+               "local_repair_kernel_ms": round(ra["kernel_ms_per_call"], 4),
+               "local_repair_kernel_roofline_frac": frac(rep_bytes, ra["kernel_ms_per_call"]),
+               "timing": ("*_data_GBps / *_roofline_frac: synchronous batch calls on device memory (planning + "
+                          "launch + sync); *_async_*: cfsec_ec_*_batch_async back to back on one stream; "
+                          "*_kernel_*: per-call HIP event pairs around the async calls (device time only)"),
+               "gate": "rows each timed call writes zeroed before, equal to the golden after (sync and async runs)"})
     if cpu:
         G = O.build_matrix(N, N + M)
         Lm = O.build_matrix(lsz - 1, lsz)
@@ -709,30 +817,45 @@ def other_configs(args, torch, dev, stream, cpu):
         gpar = [np.zeros(S4, np.uint8) for _ in range(M)]
         lpar = [np.zeros(S4, np.uint8) for _ in range(L)]
 
-        def cpu_enc4():  # lrcencoder.go:35-82: global Encode, then each AZ's local Encode
-            O.simd_code(G[N:], data, gpar, thr)
-            full = data + gpar
-            for a in range(t4.AZCount):
-                ia, _, _ = t4.LocalStripeInAZ(a)
-                O.simd_code(Lm[lsz - 1:], [full[i] for i in ia[:lsz - 1]], [lpar[a]], thr)
+        def cpu_enc4(data, gpar, lpar, thr):  # lrcencoder.go:35-82: global Encode, then each AZ's local Encode
+            def f():
+                O.simd_code(G[N:], data, gpar, thr)
+                full = data + gpar
+                for a in range(t4.AZCount):
+                    ia, _, _ = t4.LocalStripeInAZ(a)
+                    O.simd_code(Lm[lsz - 1:], [full[i] for i in ia[:lsz - 1]], [lpar[a]], thr)
+            return f
 
-        rate_c = cpu_rate(cpu_enc4, cpu_secs)
-        ok = all(np.array_equal(gpar[r], h[N + r]) for r in range(M)) and \
+        rate_c = cpu_rate(cpu_enc4(data, gpar, lpar, thr), cpu_secs)
+        ok = all(np.array_equal(gpar[r_], h[N + r_]) for r_ in range(M)) and \
             all(np.array_equal(lpar[a], h[N + M + a]) for a in range(L))
+        sat_e = cpu_saturated_rate(lambda w: cpu_enc4([x.copy() for x in data], [np.zeros(S4, np.uint8) for _ in range(M)],
+                                                      [np.zeros(S4, np.uint8) for _ in range(L)], 1),
+                                   cpu_secs, callers)
         err, dec = O.invert(Lm[1:lsz])  # local stripe with index 0 lost: survivors 1..8
         assert err == 0
         surv = [np.ascontiguousarray(h[i]) for i in idx0[1:]]
         rebuilt = [np.zeros(S4, np.uint8)]
         rate_cr = cpu_rate(lambda: O.simd_code(dec[:1], surv, rebuilt, thr), cpu_secs)
+
+        def w4r(w):
+            sv = [x.copy() for x in surv]
+            rb = [np.zeros(S4, np.uint8)]
+            return lambda: O.simd_code(dec[:1], sv, rb, 1)
+
+        sat_r = cpu_saturated_rate(w4r, cpu_secs, callers)
         c4["cpu_baseline"] = {
             "encode": {"value": round(N * S4 * rate_c / 1e9, 3), "unit": "GB/s", "cores": thr, "kind": "port",
                        "sample": "one blob: global (6,10) encode + two local (8,1) encodes, repeated",
-                       "parity_equals_gpu": bool(ok)},
+                       "parity_equals_gpu": bool(ok),
+                       "saturated": {"value": round(N * S4 * sat_e / 1e9, 3), "unit": "GB/s", "cores": callers}},
             "local_repair": {"value": round((lsz - 1) * S4 * rate_cr / 1e9, 3), "unit": "GB/s", "cores": thr,
                              "kind": "port", "sample": "one local stripe: the lost shard rebuilt from 8, repeated",
-                             "equals_original": bool(np.array_equal(rebuilt[0], h[idx0[0]]))}}
+                             "equals_original": bool(np.array_equal(rebuilt[0], h[idx0[0]])),
+                             "saturated": {"value": round((lsz - 1) * S4 * sat_r / 1e9, 3), "unit": "GB/s",
+                                           "cores": callers}}}
     out["C4_EC6P10L2_lrc_encode_local_repair"] = c4
-    del bms, lbm, b4
+    del bms, lbm, b4, gold4
 
     # ---- C5: EC16P20L2 repair tasklet, 64 bids of 4 MiB blobs, erased {0, 1, 16, 17} (configs[4]),
     # on one GPU: Reconstruct + Verify per bid (blobnode/work_shard_recover.go:751-757)
@@ -748,17 +871,29 @@ def other_configs(args, torch, dev, stream, cpu):
     for b in range(NBATCH):
         _lib.check(e5._L.cfsec_ec_encode_batch(e5._h, bm5[b].arr, tot5, nb5, bm5[b].mem, st5))
     torch.cuda.synchronize()
+    gold5 = b5[:, :, :, :S5].clone()
     er5 = [0, 1, 16, 17]
     bad5 = (ctypes.c_int * (4 * nb5))(*(er5 * nb5))
     off5 = (ctypes.c_int * (nb5 + 1))(*range(0, 4 * nb5 + 1, 4))
+    fl5 = torch.zeros(nb5, dtype=torch.int32, device=dev)
 
-    def rep5():
-        bm = bm5[rot[0] % NBATCH]
-        rot[0] += 1
+    def check5():
+        assert torch.equal(b5[:, :, er5, :S5], gold5[:, :, er5]), "C5: rebuilt rows differ from the golden"
+
+    def rep5(i):
+        bm = bm5[i % NBATCH]
         _lib.check(e5._L.cfsec_ec_reconstruct_batch(e5._h, bm.arr, tot5, nb5, bad5, off5, 1, bm.mem, st5))
 
-    rate5 = api_rate(rep5, secs)
+    def rep5a(i):
+        bm = bm5[i % NBATCH]
+        _lib.check(e5._L.cfsec_ec_reconstruct_batch_async(e5._h, bm.arr, tot5, nb5, bad5, off5, 1, st5,
+                                                          fl5.data_ptr(), None, stream.cuda_stream))
+
+    zero5 = lambda: b5[:, :, er5, :].zero_()
+    rs = gated_calls(torch, stream, rep5, NBATCH, secs, zero5, check5, sync_call=True)
     assert list(st5) == [0] * nb5
+    ra = gated_calls(torch, stream, rep5a, NBATCH, secs, zero5, check5, sync_call=False)
+    assert list(st5) == [0] * nb5 and not bool(fl5.any().item()), "C5: Verify failed"
     # per bid, one pass: reads 16 inputs + the 16 other global parities and the 2 local parities
     # it checks, writes 2 data + 2 parity rows (the local Verify rides in the global pass: the
     # separate AZ-local pass would re-read 2 x 19 shards)
@@ -766,10 +901,16 @@ def other_configs(args, torch, dev, stream, cpu):
     c5 = {"workload": (f"EC16P20L2 repair tasklet on one GPU: {nb5} bids x S={S5}, erased {{0,1,16,17}}, "
                        "Reconstruct + Verify per bid in one cfsec_ec_reconstruct_batch: one fused pass per bid (16x16-dyadic "
                        "repair kernel; global and local parities checked in it)"),
-          "data_GBps": round(N5 * S5 * nb5 * rate5 / 1e9, 1),
-          "roofline_frac": round(alg5 * nb5 * rate5 / 1e9 / HBM_PEAK_GBPS, 4),
+          "data_GBps": round(N5 * S5 * nb5 * rs["calls_per_s"] / 1e9, 1),
+          "roofline_frac": round(alg5 * nb5 * rs["calls_per_s"] / 1e9 / HBM_PEAK_GBPS, 4),
+          "async_data_GBps": round(N5 * S5 * nb5 * ra["calls_per_s"] / 1e9, 1),
+          "kernel_ms": round(ra["kernel_ms_per_call"], 4),
+          "kernel_roofline_frac": frac(alg5 * nb5, ra["kernel_ms_per_call"]),
           "algorithmic_bytes_per_bid": alg5,
-          "timing": "synchronous batch calls on device memory (planning + launches + sync)",
+          "timing": ("data_GBps / roofline_frac: synchronous cfsec_ec_reconstruct_batch calls (planning + launches + "
+                     "sync); async_*: cfsec_ec_reconstruct_batch_async back to back on one stream; kernel_*: per-call "
+                     "HIP event pairs around the async calls"),
+          "gate": "rows {0,1,16,17} zeroed before the timed calls, equal to the golden after (sync and async runs)",
           "multi_gpu_note": "the RCCL exchange of survivors spread over 8 GPUs is chubaofs_amd/repair.py (gloo-tested; "
                             "not run by this 1-GPU bench)"}
     if cpu:
@@ -777,34 +918,40 @@ def other_configs(args, torch, dev, stream, cpu):
         l5 = (N5 + t5.M) // t5.AZCount
         Lm5 = O.build_matrix(l5, l5 + 1)
         h = b5[0, 0, :, :S5].cpu().numpy()
-        sh = [np.ascontiguousarray(h[i]) for i in range(tot5)]
         valid = [i for i in range(N5 + t5.M) if i not in er5][:N5]
         err, dec = O.invert(G5[valid])
         assert err == 0
-        outs = [np.zeros(S5, np.uint8) for _ in range(4)]
-        tmp = [np.zeros(S5, np.uint8) for _ in range(t5.M)]
-        ltmp = [np.zeros(S5, np.uint8)]
         rows_data = dec[[0, 1]]
         prow = G5[[16, 17]]
 
-        def cpu_rep5():  # Reconstruct (data rows, then parity rows) + Verify (global, then local)
-            ins = [sh[i] for i in valid]
-            O.simd_code(rows_data, ins, outs[:2], thr)
-            O.simd_code(prow, [sh[i] for i in range(N5)], outs[2:], thr)
-            O.simd_code(G5[N5:], [sh[i] for i in range(N5)], tmp, thr)
-            ok = all(np.array_equal(tmp[r], sh[N5 + r]) for r in range(t5.M))
-            for a in range(t5.AZCount):
-                ia, _, _ = t5.LocalStripeInAZ(a)
-                O.simd_code(Lm5[l5:], [sh[i] for i in ia[:l5]], ltmp, thr)
-                ok = ok and np.array_equal(ltmp[0], sh[ia[l5]])
-            return ok
+        def cpu_rep5(sh, thr):  # Reconstruct (data rows, then parity rows) + Verify (global, then local)
+            outs = [np.zeros(S5, np.uint8) for _ in range(4)]
+            tmp = [np.zeros(S5, np.uint8) for _ in range(t5.M)]
+            ltmp = [np.zeros(S5, np.uint8)]
 
-        assert cpu_rep5()
-        rate_c5 = cpu_rate(cpu_rep5, cpu_secs)
+            def f():
+                ins = [sh[i] for i in valid]
+                O.simd_code(rows_data, ins, outs[:2], thr)
+                O.simd_code(prow, [sh[i] for i in range(N5)], outs[2:], thr)
+                O.simd_code(G5[N5:], [sh[i] for i in range(N5)], tmp, thr)
+                ok = all(np.array_equal(tmp[r_], sh[N5 + r_]) for r_ in range(t5.M))
+                for a in range(t5.AZCount):
+                    ia, _, _ = t5.LocalStripeInAZ(a)
+                    O.simd_code(Lm5[l5:], [sh[i] for i in ia[:l5]], ltmp, thr)
+                    ok = ok and np.array_equal(ltmp[0], sh[ia[l5]])
+                return ok
+            return f
+
+        sh = [np.ascontiguousarray(h[i]) for i in range(tot5)]
+        assert cpu_rep5(sh, thr)()
+        rate_c5 = cpu_rate(cpu_rep5(sh, thr), cpu_secs)
+        sat5 = cpu_saturated_rate(lambda w: cpu_rep5([x.copy() for x in sh], 1), cpu_secs, callers)
         c5["cpu_baseline"] = {"value": round(N5 * S5 * rate_c5 / 1e9, 3), "unit": "GB/s", "cores": thr, "kind": "port",
-                              "sample": "one bid: reconstruct 2 data + 2 parity rows, global and 2 local verifies, repeated"}
+                              "sample": "one bid: reconstruct 2 data + 2 parity rows, global and 2 local verifies, repeated",
+                              "saturated": {"value": round(N5 * S5 * sat5 / 1e9, 3), "unit": "GB/s", "cores": callers,
+                                            "sample": f"{callers} single-threaded callers, one bid each"}}
     out["C5_EC16P20L2_repair_tasklet"] = c5
-    del bm5, b5
+    del bm5, b5, gold5
     return out
 
 

@@ -115,8 +115,10 @@ SIGNATURES = {
     "cfsec_ec_set_devices": ([_V, _V, _I], _I),
     "cfsec_ec_encode_batch": ([_V, P_SHARD, _I, _I, _I, _V], _I),
     "cfsec_ec_reconstruct_batch": ([_V, P_SHARD, _I, _I, _V, _V, _I, _I, _V], _I),
-    "cfsec_ec_reconstruct_batch_async": ([_V, P_SHARD, _I, _I, _V, _V, _I, _V, _V, _V], _I),
-    "cfsec_ec_encode_batch_async": ([_V, P_SHARD, _I, _I, _V, _V, _V], _I),
+    "cfsec_ec_reconstruct_batch_async": ([_V, P_SHARD, _I, _I, _V, _V, _I, _V, _V, _V, _V], _I),
+    "cfsec_ec_encode_batch_async": ([_V, P_SHARD, _I, _I, _V, _V, _V, _V], _I),
+    "cfsec_ec_encode_batch_crc": ([_V, P_SHARD, _I, _I, _I, _V, _V], _I),
+    "cfsec_ec_reconstruct_batch_crc": ([_V, P_SHARD, _I, _I, _V, _V, _I, _I, _V, _V], _I),
     "cfsec_crc32_ieee_batch": ([_V, _S, _I, _V, _I, _V], _I),
     "cfsec_host_alloc": ([_S, _P(_V)], _I),
     "cfsec_host_free": ([_V], _I),

@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <set>
 #include <thread>
 
 #include "engine.hpp"
@@ -214,9 +215,14 @@ void partition_stripes(const uint64_t* bytes, int n, int ndev, int* dev) {
 
 Status RSEngine::set_devices(const int* devices, int n) {
   if (!devices || n <= 0) return CFSEC_ERR_INVALID_ARG;
+  // CFSEC_DEVICE_REHEARSAL=1: a repeated ordinal is another context on that device (own thread,
+  // streams and staging), so the multi-device split runs on a one-GPU machine
+  const char* reh = std::getenv("CFSEC_DEVICE_REHEARSAL");
+  const bool rehearsal = reh && *reh && *reh != '0';
   std::vector<DeviceContext*> v;
   for (int i = 0; i < n; ++i) {
-    DeviceContext* c = DeviceContext::get(devices[i]);
+    const int slot = rehearsal ? (int)std::count(devices, devices + i, devices[i]) : 0;
+    DeviceContext* c = DeviceContext::get(devices[i], slot);
     if (!c) {
       set_last_error("set_devices: device " + std::to_string(devices[i]) + " does not exist");
       return CFSEC_ERR_DEVICE;
@@ -511,7 +517,7 @@ bool RSEngine::split_verify(const StripePlan& p) const {
   return false;
 }
 
-Status RSEngine::run_stripes(std::vector<StripeTask>& tasks, int mem, const AsyncOut* async) {
+Status RSEngine::run_stripes(std::vector<StripeTask>& tasks, int mem, const AsyncOut* async, const CrcOut* crc) {
   if (tasks.empty()) return CFSEC_OK;
   if (devs_.empty()) {
     set_last_error("no HIP device available to the cfsec engine");
@@ -559,16 +565,26 @@ Status RSEngine::run_stripes(std::vector<StripeTask>& tasks, int mem, const Asyn
   }
   std::vector<std::vector<StripeTask*>> per(nd);
   for (auto& t : tasks) per[t.dev].push_back(&t);
+  const bool trace = std::getenv("CFSEC_TRACE_BATCH") != nullptr;  // the split, for tests
+  if (trace)
+    for (int d = 0; d < nd; ++d) {
+      std::set<int> items;
+      for (StripeTask* t : per[d]) items.insert(t->owner);
+      std::fprintf(stderr, "cfsec batch: device index %d (ordinal %d): %zu tasks, items", d, devs_[d]->device(),
+                   per[d].size());
+      for (int it : items) std::fprintf(stderr, " %d", it);
+      std::fprintf(stderr, "\n");
+    }
   std::vector<Status> st(nd, CFSEC_OK);
   std::vector<std::string> err(nd);
   std::vector<std::thread> threads;
   for (int d = 1; d < nd; ++d)
     if (!per[d].empty())
       threads.emplace_back([&, d] {
-        st[d] = run_device(per[d], mem, devs_[d], nullptr);
+        st[d] = run_device(per[d], mem, devs_[d], nullptr, crc);
         if (st[d] != CFSEC_OK) err[d] = last_error_cstr();
       });
-  if (!per[0].empty()) st[0] = run_device(per[0], mem, devs_[0], async);
+  if (!per[0].empty()) st[0] = run_device(per[0], mem, devs_[0], async, crc);
   for (auto& th : threads) th.join();
   for (int d = 1; d < nd; ++d)
     if (st[d] != CFSEC_OK && st[0] == CFSEC_OK) {
@@ -578,7 +594,8 @@ Status RSEngine::run_stripes(std::vector<StripeTask>& tasks, int mem, const Asyn
   return st[0];
 }
 
-Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceContext* ctx, const AsyncOut* async) {
+Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceContext* ctx, const AsyncOut* async,
+                            const CrcOut* crc) {
   HostTimer whole("  run_device");
   std::unique_ptr<HostTimer> tm(new HostTimer("    classify + acquire"));
   DeviceGuard g(ctx->device());
@@ -590,7 +607,9 @@ Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceCont
   std::map<std::pair<const StripeTask*, int>, uint8_t*> alias;
   int nphase = 1, nitems = 0;
   bool checks = false;  // some task compares rows (Verify)
+  bool sums = false;    // some task checksums rows
   for (StripeTask* t : tasks) {
+    sums = sums || (t->crc && crc && crc->words && crc->n);
     nphase = std::max(nphase, t->phase + 1);
     nitems = std::max(nitems, t->owner + 1);
     checks = checks || t->plan->out.size() > (size_t)t->plan->nstore;
@@ -622,8 +641,12 @@ Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceCont
   // stream)
   const int nlanes = !staged.empty() && (staged_total > lane_bytes || nphase > 1) ? 2 : 1;
   DeviceContext::Workspace* ws = nullptr;
-  Status st = ctx->acquire(lane_bytes * nlanes, (size_t)std::max(n, nitems), &ws, (size_t)n);
+  Status st = ctx->acquire(lane_bytes * nlanes, (size_t)std::max(n, nitems), &ws, (size_t)n,
+                           sums && !async ? crc->n : 0);
   if (st != CFSEC_OK) return st;
+  // checksum words: the caller's device array (asynchronous) or the workspace's, zeroed first (the
+  // CRC kernel XOR-accumulates)
+  uint32_t* dcrc = !sums ? nullptr : async ? crc->words : ws->dcrc;
   // asynchronous calls run on the caller's stream (NULL: the legacy default stream); synchronous
   // ones on the workspace's streams, ordered after the legacy default stream for device memory
   hipStream_t lane[2] = {async ? async->stream : ws->stream, ws->stream2};
@@ -634,7 +657,34 @@ Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceCont
     return e;
   };
   if (mem == CFSEC_MEM_DEVICE && !async) st = ctx->order_after_default(ws);
+  if (st == CFSEC_OK && sums) st = hip_status(hipMemsetAsync(dcrc, 0, crc->n * 4, lane[0]), "hipMemsetAsync(crc)");
   if (st == CFSEC_OK && nlanes > 1) st = join(0, 1);
+  // crc32.ChecksumIEEE of the rows the tasks of a launched part name, on the part's stream, from the
+  // same device addresses the product used (staged rows before their lane is reused)
+  const auto checksum = [&](const std::vector<StripeTask*>& part, auto ptr, hipStream_t s) -> Status {
+    if (!sums) return CFSEC_OK;
+    std::map<size_t, std::pair<std::vector<const uint8_t*>, std::vector<uint32_t>>> by_len;
+    for (StripeTask* t : part) {
+      if (!t->crc || t->len == 0) continue;
+      auto& v = by_len[t->len];
+      const auto add = [&](int row) {
+        const int64_t w = t->crc_word + (t->crc_map ? t->crc_map[row] : row);
+        if (w < 0 || (size_t)w >= crc->n) return;
+        v.first.push_back(ptr(t, row));
+        v.second.push_back((uint32_t)w);
+      };
+      if (t->crc == 2)
+        for (int c : t->plan->in) add(c);
+      for (int r = 0; r < t->plan->nstore; ++r) add(t->plan->out[r]);
+    }
+    for (auto& kv : by_len) {
+      const Status e = hip_status(launch_crc32_to(kv.second.first.data(), kv.first, (int)kv.second.first.size(), dcrc,
+                                                  kv.second.second.data(), crc32_shift_ones(kv.first), s),
+                                  "launch_crc32_to(batch)");
+      if (e != CFSEC_OK) return e;
+    }
+    return CFSEC_OK;
+  };
   int next_flag = 0;
   std::vector<std::pair<StripeTask*, int>> flags;  // (task, flag word)
   const auto record = [&](const std::vector<Group>& groups) {
@@ -655,12 +705,14 @@ Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceCont
     for (StripeTask* t : staged)
       if (t->phase == ph) sph.push_back(t);
     if (st == CFSEC_OK && !dph.empty()) {
-      std::vector<Group> groups = make_groups(dph, &next_flag, [&](const StripeTask* t, int idx) {
+      const auto dptr = [&](const StripeTask* t, int idx) {
         return mem == CFSEC_MEM_DEVICE ? (const uint8_t*)t->shards[idx].data : (const uint8_t*)alias[{t, idx}];
-      });
+      };
+      std::vector<Group> groups = make_groups(dph, &next_flag, dptr);
       for (const Group& gr : groups)
         if (st == CFSEC_OK) st = hip_status(launch_group(gr, ws->bflags, lane[0]), "launch_matvec(batch)");
       record(groups);
+      if (st == CFSEC_OK) st = checksum(dph, dptr, lane[0]);
     }
     // staged stripes: chunks of whole stripes alternating over the two lanes; each lane copies its
     // chunk in, runs it and copies the stored rows back while the other lane's chunk moves
@@ -699,11 +751,12 @@ Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceCont
                             "hipMemcpyAsync H2D");
           }
       }
-      std::vector<Group> groups =
-          make_groups(part, &next_flag, [&](const StripeTask* t, int idx) { return (const uint8_t*)slot[{t, idx}]; });
+      const auto sptr = [&](const StripeTask* t, int idx) { return (const uint8_t*)slot[{t, idx}]; };
+      std::vector<Group> groups = make_groups(part, &next_flag, sptr);
       for (const Group& gr : groups)
         if (st == CFSEC_OK) st = hip_status(launch_group(gr, ws->bflags, s), "launch_matvec(batch)");
       record(groups);
+      if (st == CFSEC_OK) st = checksum(part, sptr, s);
       for (StripeTask* t : part)
         for (int r = 0; r < t->plan->nstore && st == CFSEC_OK; ++r) {
           const int o = t->plan->out[r];
@@ -714,6 +767,9 @@ Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceCont
     }
   }
   if (st == CFSEC_OK && nlanes > 1) st = join(1, 0);
+  if (st == CFSEC_OK && sums && !async)
+    st = hip_status(hipMemcpyAsync(ws->hcrc, ws->dcrc, crc->n * 4, hipMemcpyDeviceToHost, lane[0]),
+                    "hipMemcpyAsync D2H(crc)");
   // Verify flags per batch item, gathered from the per-task words (which the gather resets): into
   // the caller's device array (asynchronous), or straight into the pinned host words (no D2H copy)
   if (st == CFSEC_OK && checks) {
@@ -744,6 +800,17 @@ Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceCont
       if (f.first->plan->out.size() > (size_t)f.first->plan->nstore && ws->hflags[f.first->owner] != 0 &&
           *f.first->status == CFSEC_OK)
         *f.first->status = CFSEC_ERR_VERIFY;
+  if (st == CFSEC_OK && sums)  // this device's words only (another device of the call fills the rest)
+    for (StripeTask* t : tasks) {
+      if (!t->crc) continue;
+      const auto put = [&](int row) {
+        const int64_t w = t->crc_word + (t->crc_map ? t->crc_map[row] : row);
+        if (w >= 0 && (size_t)w < crc->n) crc->words[w] = ws->hcrc[w];
+      };
+      if (t->crc == 2)
+        for (int c : t->plan->in) put(c);
+      for (int r = 0; r < t->plan->nstore; ++r) put(t->plan->out[r]);
+    }
   ctx->release(ws);
   return st;
 }
@@ -754,6 +821,18 @@ Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceCont
 
 namespace cfsec {
 
+namespace {
+// Synchronous calls return checksums only for the items that succeeded (the reference checksums
+// after a successful Encode / repair): the words of a failed item are zeroed.  (Asynchronous calls
+// learn a false Verify on the stream; their caller skips the words of flagged items.)
+void clear_failed_crcs(const CrcOut* crc, const AsyncOut* async, const int* status, int nitems, int n) {
+  if (!crc || async) return;
+  for (int b = 0; b < nitems; ++b)
+    if (status[b] != CFSEC_OK)
+      for (int i = 0; i < n && (size_t)b * n + i < crc->n; ++i) crc->words[(size_t)b * n + i] = 0;
+}
+}  // namespace
+
 Status ECEncoder::set_devices(const int* devices, int n) { return engine_->set_devices(devices, n); }
 
 Status LrcEncoder::set_devices(const int* devices, int n) {
@@ -762,7 +841,7 @@ Status LrcEncoder::set_devices(const int* devices, int n) {
 }
 
 Status ECEncoder::reconstruct_batch(cfsec_shard* shards, int n, int nbids, const int* bad, const int* bad_off,
-                                    int mem, bool verify, int* status, const AsyncOut* async) {
+                                    int mem, bool verify, int* status, const AsyncOut* async, const CrcOut* crc) {
   // encoder.go:139-144 per bid (initBadShards, engine Reconstruct), then encoder.go:133-137 (Verify)
   if (!shards || !status || !bad_off || nbids < 0) return CFSEC_ERR_INVALID_ARG;
   Slot slot(pool_.get());
@@ -786,20 +865,26 @@ Status ECEncoder::reconstruct_batch(cfsec_shard* shards, int n, int nbids, const
   std::vector<int> st(stripes.size());
   Status rc;
   if (verify && engine_->k() > kLaunchMaxRows) {
+    if (crc) return CFSEC_ERR_NOT_SUPPORTED;
     rc = engine_->reconstruct_stripes(stripes.data(), (int)stripes.size(), mem, verify, st.data());
   } else {
     PlanStore store;
     std::vector<StripeTask> tasks;
     engine_->plan_reconstruct_tasks(stripes.data(), (int)stripes.size(), verify, st.data(), 0, 0, &store, &tasks);
-    for (auto& t : tasks) t.owner = pos[t.owner];  // the bid: its verify word
-    rc = engine_->run_stripes(tasks, mem, async);
+    for (auto& t : tasks) {
+      t.owner = pos[t.owner];  // the bid: its verify word
+      t.crc = crc ? 1 : 0;     // the rebuilt shards' checksums (blobnode ShardCrc32)
+      t.crc_word = (int64_t)t.owner * n;
+    }
+    rc = engine_->run_stripes(tasks, mem, async, crc);
   }
   for (size_t i = 0; i < pos.size(); ++i) status[pos[i]] = st[i];
+  clear_failed_crcs(crc, async, status, nbids, n);
   return rc;
 }
 
 Status LrcEncoder::reconstruct_batch(cfsec_shard* shards, int n, int nbids, const int* bad, const int* bad_off,
-                                     int mem, bool verify, int* status, const AsyncOut* async) {
+                                     int mem, bool verify, int* status, const AsyncOut* async, const CrcOut* crc) {
   // lrcencoder.go:133-186 per bid, then lrcencoder.go:89-131 (Verify): a local stripe (n = its size)
   // is the local engine alone; a whole stripe is the global engine over its first N+M shards, then
   // each AZ's local engine over that AZ's local stripe -- planned together and run as two phases of
@@ -809,6 +894,7 @@ Status LrcEncoder::reconstruct_batch(cfsec_shard* shards, int n, int nbids, cons
   const int N = t_.n, M = t_.m, L = t_.l, AZ = t_.az_count;
   const int lsz = (N + M + L) / AZ;
   if (verify && std::max(N, local_->k()) > kLaunchMaxRows) {
+    if (crc) return CFSEC_ERR_NOT_SUPPORTED;
     // compared rows over more than one launch's inputs: the single calls, bid by bid (each takes
     // its own concurrency slot)
     for (int b = 0; b < nbids; ++b) {
@@ -852,9 +938,14 @@ Status LrcEncoder::reconstruct_batch(cfsec_shard* shards, int n, int nbids, cons
     PlanStore store;
     std::vector<StripeTask> tasks;
     local_->plan_reconstruct_tasks(stripes.data(), (int)stripes.size(), verify, st.data(), 0, 0, &store, &tasks);
-    for (auto& t : tasks) t.owner = pos[t.owner];
-    const Status rc = local_->run_stripes(tasks, mem, async);
+    for (auto& t : tasks) {
+      t.owner = pos[t.owner];
+      t.crc = crc ? 1 : 0;
+      t.crc_word = (int64_t)t.owner * n;
+    }
+    const Status rc = local_->run_stripes(tasks, mem, async, crc);
     for (size_t i = 0; i < pos.size(); ++i) status[pos[i]] = st[i];
+    clear_failed_crcs(crc, async, status, nbids, n);
     return rc;
   }
   // phase 0 (1): global Reconstruct (+ global Verify) over shards [0, N+M)
@@ -930,10 +1021,12 @@ Status LrcEncoder::reconstruct_batch(cfsec_shard* shards, int n, int nbids, cons
   }
   std::vector<cfsec_shard*> lp;
   std::vector<size_t> owner;
+  std::vector<int> vaz;  // the AZ of each local view
   for (int a = 0; a < AZ; ++a)
     for (size_t v = 0; v < vowner[a].size(); ++v) {
       lp.push_back(views[a].data() + v * idc[a].size());
       owner.push_back(vowner[a][v]);
+      vaz.push_back(a);
     }
   std::vector<int> st2(lp.size());
   const size_t first_local = tasks.size();
@@ -942,10 +1035,15 @@ Status LrcEncoder::reconstruct_batch(cfsec_shard* shards, int n, int nbids, cons
     // owner: the bid (a host batch keeps a bid's passes on one device)
     const size_t v = (size_t)(tasks[t].status - st2.data());
     tasks[t].owner = (int)owner[v];
+    tasks[t].crc_map = idc[vaz[v]].data();  // local index -> global shard index
   }
   ph.reset();
-  for (auto& t : tasks) t.owner = pos[t.owner];  // the bid: its device, its verify word
-  const Status rc = engine_->run_stripes(tasks, mem, async);
+  for (auto& t : tasks) {
+    t.owner = pos[t.owner];  // the bid: its device, its verify word
+    t.crc = crc ? 1 : 0;     // rebuilt shards, global or local (blobnode ShardCrc32)
+    t.crc_word = (int64_t)t.owner * n;
+  }
+  const Status rc = engine_->run_stripes(tasks, mem, async, crc);
   // per bid: a Reconstruct error (global, then local) wins over a failed Verify
   std::vector<int> local_err(stripes.size(), CFSEC_OK);
   for (size_t v = 0; v < lp.size(); ++v) {
@@ -960,17 +1058,19 @@ Status LrcEncoder::reconstruct_batch(cfsec_shard* shards, int n, int nbids, cons
     }
     status[pos[i]] = s;
   }
+  clear_failed_crcs(crc, async, status, nbids, n);
   return rc;
 }
 
 Status ECEncoder::encode_batch(cfsec_shard* shards, int n, int nstripes, int mem, int* status,
-                               const AsyncOut* async) {
+                               const AsyncOut* async, const CrcOut* crc) {
   // encoder.go:114-131 per stripe: engine Encode, then Verify when EnableVerify -- the Verify pass in
   // the same call (phase 1), after the encode
   if (!shards || !status || nstripes < 0) return CFSEC_ERR_INVALID_ARG;
   Slot slot(pool_.get());
   const int k = engine_->k(), m = engine_->m(), tot = k + m;
   if (enable_verify_ && k > kLaunchMaxRows) {  // compared rows over more inputs than one launch carries
+    if (crc) return CFSEC_ERR_NOT_SUPPORTED;
     std::vector<cfsec_shard*> stripes;
     std::vector<int> pos;
     for (int s = 0; s < nstripes; ++s) {
@@ -1012,15 +1112,19 @@ Status ECEncoder::encode_batch(cfsec_shard* shards, int n, int nstripes, int mem
       status[s] = st;
       continue;
     }
-    if (m == 0) continue;
+    if (m == 0 && !crc) continue;
     tasks.push_back(StripeTask{sh, &plan, S, &status[s], 0, 0, s});
-    if (enable_verify_) tasks.push_back(StripeTask{sh, &vplan, S, &status[s], 0, 1, s});
+    tasks.back().crc = crc ? 2 : 0;  // every shard (access/stream_put.go:249-253)
+    tasks.back().crc_word = (int64_t)s * n;
+    if (enable_verify_ && m > 0) tasks.push_back(StripeTask{sh, &vplan, S, &status[s], 0, 1, s});
   }
-  return engine_->run_stripes(tasks, mem, async);
+  const Status rc = engine_->run_stripes(tasks, mem, async, crc);
+  clear_failed_crcs(crc, async, status, nstripes, n);
+  return rc;
 }
 
 Status LrcEncoder::encode_batch(cfsec_shard* shards, int n, int nstripes, int mem, int* status,
-                                const AsyncOut* async) {
+                                const AsyncOut* async, const CrcOut* crc) {
   // lrcencoder.go:35-82 per stripe, fused: global parity and every AZ's local parity as one
   // (M+L) x N product over the data (the same rows LrcEncoder::encode launches); EnableVerify
   // compares all M+L rows in a second pass (the reference verifies the global and the local stripes)
@@ -1028,6 +1132,7 @@ Status LrcEncoder::encode_batch(cfsec_shard* shards, int n, int nstripes, int me
   const int N = t_.n, M = t_.m, L = t_.l;
   Slot slot(pool_.get());
   if (enable_verify_ && N > kLaunchMaxRows) {  // the fused Verify's rows exceed one compare launch
+    if (crc) return CFSEC_ERR_NOT_SUPPORTED;
     for (int s = 0; s < nstripes; ++s) {
       status[s] = n != N + M + L ? CFSEC_ERR_INVALID_SHARDS
                                  : encode_stripe(shards + (size_t)s * n, n, mem, async ? async->stream : nullptr);
@@ -1064,6 +1169,8 @@ Status LrcEncoder::encode_batch(cfsec_shard* shards, int n, int nstripes, int me
       continue;
     }
     tasks.push_back(StripeTask{sh, &plan, S, &status[s], 0, 0, s});
+    tasks.back().crc = crc ? 2 : 0;  // every shard, global and local (access/stream_put.go:249-253)
+    tasks.back().crc_word = (int64_t)s * n;
   }
   StripePlan vplan = plan;
   vplan.nstore = 0;
@@ -1073,10 +1180,13 @@ Status LrcEncoder::encode_batch(cfsec_shard* shards, int n, int nstripes, int me
       StripeTask v = tasks[i];
       v.plan = &vplan;
       v.phase = 1;
+      v.crc = 0;
       tasks.push_back(v);
     }
   }
-  return engine_->run_stripes(tasks, mem, async);
+  const Status rc = engine_->run_stripes(tasks, mem, async, crc);
+  clear_failed_crcs(crc, async, status, nstripes, n);
+  return rc;
 }
 
 }  // namespace cfsec

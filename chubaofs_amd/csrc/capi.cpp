@@ -4,6 +4,8 @@
 #include <new>
 #include <vector>
 
+#include <cstring>
+
 #include "engine.hpp"
 
 namespace cfsec {
@@ -433,8 +435,35 @@ int cfsec_ec_encode_batch(cfsec_ec* h, cfsec_shard* shards, int n, int nstripes,
   return guarded([&] { return h->e->encode_batch(shards, n, nstripes, mem, status); });
 }
 
+int cfsec_ec_reconstruct_batch_crc(cfsec_ec* h, cfsec_shard* shards, int n, int nbids, const int* bad_idx,
+                                   const int* bad_off, int verify, int mem, int* status, uint32_t* crcs) {
+  if (!h || nbids < 0 || n <= 0 || (nbids > 0 && (!shards || !status || !bad_off || !crcs)))
+    return CFSEC_ERR_INVALID_ARG;
+  if (nbids > 0 && bad_off[0] != 0) return CFSEC_ERR_INVALID_ARG;
+  for (int b = 0; b < nbids; ++b)
+    if (bad_off[b + 1] < bad_off[b] || (bad_off[b + 1] > bad_off[b] && !bad_idx)) return CFSEC_ERR_INVALID_ARG;
+  std::memset(crcs, 0, sizeof(uint32_t) * (size_t)nbids * n);
+  cfsec::CrcOut c;
+  c.words = crcs;
+  c.n = (size_t)nbids * n;
+  return guarded([&] {
+    return h->e->reconstruct_batch(shards, n, nbids, bad_idx, bad_off, mem, verify != 0, status, nullptr, &c);
+  });
+}
+
+int cfsec_ec_encode_batch_crc(cfsec_ec* h, cfsec_shard* shards, int n, int nstripes, int mem, int* status,
+                              uint32_t* crcs) {
+  if (!h || nstripes < 0 || n <= 0 || (nstripes > 0 && (!shards || !status || !crcs))) return CFSEC_ERR_INVALID_ARG;
+  std::memset(crcs, 0, sizeof(uint32_t) * (size_t)nstripes * n);
+  cfsec::CrcOut c;
+  c.words = crcs;
+  c.n = (size_t)nstripes * n;
+  return guarded([&] { return h->e->encode_batch(shards, n, nstripes, mem, status, nullptr, &c); });
+}
+
 int cfsec_ec_reconstruct_batch_async(cfsec_ec* h, cfsec_shard* shards, int n, int nbids, const int* bad_idx,
-                                     const int* bad_off, int verify, int* status, uint32_t* flags, void* stream) {
+                                     const int* bad_off, int verify, int* status, uint32_t* flags, uint32_t* crcs,
+                                     void* stream) {
   if (!h || nbids < 0 || n <= 0 || (nbids > 0 && (!shards || !status || !bad_off))) return CFSEC_ERR_INVALID_ARG;
   if (nbids > 0 && bad_off[0] != 0) return CFSEC_ERR_INVALID_ARG;
   for (int b = 0; b < nbids; ++b)
@@ -443,18 +472,27 @@ int cfsec_ec_reconstruct_batch_async(cfsec_ec* h, cfsec_shard* shards, int n, in
   cfsec::AsyncOut a;
   a.stream = as_stream(stream);
   a.flags = flags;
+  cfsec::CrcOut c;
+  c.words = crcs;
+  c.n = (size_t)nbids * n;
   return guarded([&] {
-    return h->e->reconstruct_batch(shards, n, nbids, bad_idx, bad_off, CFSEC_MEM_DEVICE, verify != 0, status, &a);
+    return h->e->reconstruct_batch(shards, n, nbids, bad_idx, bad_off, CFSEC_MEM_DEVICE, verify != 0, status, &a,
+                                   crcs ? &c : nullptr);
   });
 }
 
 int cfsec_ec_encode_batch_async(cfsec_ec* h, cfsec_shard* shards, int n, int nstripes, int* status, uint32_t* flags,
-                                void* stream) {
+                                uint32_t* crcs, void* stream) {
   if (!h || nstripes < 0 || n <= 0 || (nstripes > 0 && (!shards || !status))) return CFSEC_ERR_INVALID_ARG;
   cfsec::AsyncOut a;
   a.stream = as_stream(stream);
   a.flags = flags;
-  return guarded([&] { return h->e->encode_batch(shards, n, nstripes, CFSEC_MEM_DEVICE, status, &a); });
+  cfsec::CrcOut c;
+  c.words = crcs;
+  c.n = (size_t)nstripes * n;
+  return guarded([&] {
+    return h->e->encode_batch(shards, n, nstripes, CFSEC_MEM_DEVICE, status, &a, crcs ? &c : nullptr);
+  });
 }
 
 int cfsec_ec_repair_rows(cfsec_ec* h, const int* bad_idx, int nbad, const int* want, int nwant, int* in_idx,

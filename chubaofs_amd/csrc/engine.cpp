@@ -108,18 +108,18 @@ DeviceGuard::~DeviceGuard() {
   }
 }
 
-DeviceContext* DeviceContext::get(int device) {
+DeviceContext* DeviceContext::get(int device, int slot) {
   static std::mutex mu;
-  static std::unordered_map<int, std::unique_ptr<DeviceContext>> ctxs;
+  static std::map<std::pair<int, int>, std::unique_ptr<DeviceContext>> ctxs;
   int count = 0;
-  if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count) return nullptr;
+  if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count || slot < 0) return nullptr;
   std::lock_guard<std::mutex> l(mu);
-  auto& p = ctxs[device];
+  auto& p = ctxs[{device, slot}];
   if (!p) p.reset(new DeviceContext(device));
   return p.get();
 }
 
-Status DeviceContext::acquire(size_t bytes, size_t nflags, Workspace** out, size_t nbflags) {
+Status DeviceContext::acquire(size_t bytes, size_t nflags, Workspace** out, size_t nbflags, size_t ncrc) {
   Workspace* ws = nullptr;
   {
     std::lock_guard<std::mutex> l(mu_);
@@ -135,7 +135,7 @@ Status DeviceContext::acquire(size_t bytes, size_t nflags, Workspace** out, size
     // best fit among the free workspaces
     auto best = free_.end();
     for (auto it = free_.begin(); it != free_.end(); ++it)
-      if ((*it)->cap >= bytes && (*it)->nflags >= nflags && (*it)->nbflags >= nbflags &&
+      if ((*it)->cap >= bytes && (*it)->nflags >= nflags && (*it)->nbflags >= nbflags && (*it)->ncrc >= ncrc &&
           (best == free_.end() || (*it)->cap < (*best)->cap) && ready(*it))
         best = it;
     if (best == free_.end())
@@ -202,6 +202,19 @@ Status DeviceContext::acquire(size_t bytes, size_t nflags, Workspace** out, size
     // once per allocation (or after a failed call): the gather kernel keeps them zero afterwards
     st = hip_status(hipMemset(ws->bflags, 0, ws->nbflags * 4), "hipMemset(batch flags)");
     if (st == CFSEC_OK) ws->bflags_clean = true;
+  }
+  if (st == CFSEC_OK && ws->ncrc < ncrc) {
+    const size_t nc = std::max<size_t>(ncrc, 256);
+    if (ws->dcrc) (void)hipFree(ws->dcrc);
+    if (ws->hcrc) (void)hipHostFree(ws->hcrc);
+    ws->dcrc = nullptr;
+    ws->hcrc = nullptr;
+    ws->ncrc = 0;
+    st = hip_status(hipMalloc(reinterpret_cast<void**>(&ws->dcrc), nc * 4), "hipMalloc(crc words)");
+    if (st == CFSEC_OK)
+      st = hip_status(hipHostMalloc(reinterpret_cast<void**>(&ws->hcrc), nc * 4, hipHostMallocDefault),
+                      "hipHostMalloc(crc words)");
+    if (st == CFSEC_OK) ws->ncrc = nc;
   }
   if (st == CFSEC_OK && !ws->done)
     st = hip_status(hipEventCreateWithFlags(&ws->done, hipEventDisableTiming), "hipEventCreate");

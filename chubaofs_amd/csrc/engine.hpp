@@ -56,7 +56,9 @@ bool device_alias(uint8_t* p, uint8_t** dptr);
 // Per-device streams and staging workspaces, shared by every engine on the device.
 class DeviceContext {
  public:
-  static DeviceContext* get(int device);  // nullptr if the device does not exist
+  // nullptr if the device does not exist.  slot > 0: another context on the same device (its own
+  // streams and workspaces) -- the multi-device rehearsal of set_devices on a one-GPU machine.
+  static DeviceContext* get(int device, int slot = 0);
   int device() const { return device_; }
 
   struct Workspace {
@@ -79,6 +81,10 @@ class DeviceContext {
     // stream after the call's last kernel) has completed
     hipEvent_t done = nullptr;
     bool pending = false;
+    // batch calls with shard checksums: device words (accumulated by the CRC kernel) + pinned mirror
+    uint32_t* dcrc = nullptr;
+    uint32_t* hcrc = nullptr;
+    size_t ncrc = 0;
   };
   // Order ws->stream after the work already queued on the legacy default stream (and, by that
   // stream's semantics, on every blocking stream of the device): a device-memory call made
@@ -88,7 +94,7 @@ class DeviceContext {
   Status order_after_default(Workspace* ws);
   // Check out a workspace with at least `bytes` of staging, `nflags` flag words (device + pinned
   // host) and `nbflags` batch flag words (zero on return).
-  Status acquire(size_t bytes, size_t nflags, Workspace** out, size_t nbflags = 0);
+  Status acquire(size_t bytes, size_t nflags, Workspace** out, size_t nbflags = 0, size_t ncrc = 0);
   void release(Workspace* ws);
   // Return a workspace whose work is still queued on `stream`: it is handed out again only once
   // the stream has passed this point.
@@ -175,6 +181,15 @@ struct AsyncOut {
   uint32_t* flags = nullptr;
 };
 
+// Shard checksums a batch call returns (crc32.ChecksumIEEE, access/stream_put.go:249-253,
+// blobnode/work_shard_recover.go:335-342): words[w] for the rows the tasks name (StripeTask::crc);
+// host memory for the synchronous calls (words the call does not compute are left alone), device
+// memory on the call's stream for the asynchronous ones (zeroed by the call first).
+struct CrcOut {
+  uint32_t* words = nullptr;
+  size_t n = 0;
+};
+
 // One stripe of a batch call: its shard vector, the plan, its length, its result.
 struct StripeTask {
   cfsec_shard* shards = nullptr;
@@ -185,6 +200,9 @@ struct StripeTask {
   int phase = 0;                // tasks of phase p run after every task of phase p - 1 (same call)
   int owner = 0;                // batch item: a host batch keeps an item's tasks on one device; the
                                 // item's Verify word (asynchronous calls: the caller's flags[owner])
+  int crc = 0;                  // checksums: 0 none, 1 the stored rows, 2 every row (inputs + stored)
+  int64_t crc_word = 0;         // CrcOut word of shard index 0 of this task's item
+  const int* crc_map = nullptr; // shard index -> index in the item (local views), or identity
 };
 
 // Plans built for one batch call (stable addresses for the tasks that point at them).
@@ -266,7 +284,8 @@ class RSEngine {
   // through double-buffered staging), tasks partitioned over the devices.
   // async (device memory, the handle's first device): enqueue on async->stream and return; verify
   // mismatches OR 1 into async->flags[owner] instead of setting the tasks' status.
-  Status run_stripes(std::vector<StripeTask>& tasks, int mem, const AsyncOut* async = nullptr);
+  Status run_stripes(std::vector<StripeTask>& tasks, int mem, const AsyncOut* async = nullptr,
+                     const CrcOut* crc = nullptr);
   // Plan of a Reconstruct (+ Verify) over the present shards.
   Status plan_stripe(const std::vector<bool>& present, bool verify, StripePlan* plan,
                      const ExtraRows* extra = nullptr);
@@ -302,7 +321,8 @@ class RSEngine {
   InversionCache tree_;
   DeviceContext* ctx_ = nullptr;
   std::vector<DeviceContext*> devs_;  // batch devices, ctx_ first
-  Status run_device(std::vector<StripeTask*>& tasks, int mem, DeviceContext* ctx, const AsyncOut* async);
+  Status run_device(std::vector<StripeTask*>& tasks, int mem, DeviceContext* ctx, const AsyncOut* async,
+                    const CrcOut* crc);
 };
 
 // Counting semaphore (util/limit/count.NewBlockingCount, encoder.go:90).
@@ -355,12 +375,15 @@ class ECEncoder {
   // returns false, or CFSEC_OK.  verify = false: Reconstruct only.
   // async (device memory, asynchronous on async->stream): status[b] gets the planning result at
   // return; a Verify mismatch ORs 1 into async->flags[b] when the stream gets there.
+  // crc: the rebuilt shards' checksums into crc->words[b * n + shard] (other words untouched).
   virtual Status reconstruct_batch(cfsec_shard* shards, int n, int nbids, const int* bad, const int* bad_off,
-                                   int mem, bool verify, int* status, const AsyncOut* async = nullptr);
+                                   int mem, bool verify, int* status, const AsyncOut* async = nullptr,
+                                   const CrcOut* crc = nullptr);
   // Encode over a batch of stripes of n shards each (access puts, stream_put.go:104-143), with
   // the Config's EnableVerify; status[s] as Encode would return it.
+  // crc: every shard's checksum after the Encode into crc->words[s * n + shard].
   virtual Status encode_batch(cfsec_shard* shards, int n, int nstripes, int mem, int* status,
-                              const AsyncOut* async = nullptr);
+                              const AsyncOut* async = nullptr, const CrcOut* crc = nullptr);
 
  protected:
   // Shard index g (< N + M + L) as a row over the N data shards.
@@ -387,9 +410,10 @@ class LrcEncoder : public ECEncoder {
   std::vector<int> shards_in_idc(int idx) const override;
   Status set_devices(const int* devices, int n) override;
   Status reconstruct_batch(cfsec_shard* shards, int n, int nbids, const int* bad, const int* bad_off, int mem,
-                           bool verify, int* status, const AsyncOut* async = nullptr) override;
+                           bool verify, int* status, const AsyncOut* async = nullptr,
+                           const CrcOut* crc = nullptr) override;
   Status encode_batch(cfsec_shard* shards, int n, int nstripes, int mem, int* status,
-                      const AsyncOut* async = nullptr) override;
+                      const AsyncOut* async = nullptr, const CrcOut* crc = nullptr) override;
 
  protected:
   bool row_over_data(int g, uint8_t* dst) const override;

@@ -90,21 +90,30 @@ class Encoder:
         arr = (ctypes.c_int * len(devices))(*devices)
         _lib.check(self._L.cfsec_ec_set_devices(self._h, arr, len(devices)))
 
-    def EncodeBatch(self, stripes):
+    def EncodeBatch(self, stripes, crcs: bool = False):
         """Encode every stripe (each a list of N+M+L shards; sizes may differ per stripe) in one
-        call, EnableVerify included; returns per-stripe status codes."""
+        call, EnableVerify included; returns per-stripe status codes, and with crcs=True also
+        crc32.ChecksumIEEE of every shard per stripe (cfsec_ec_encode_batch_crc)."""
         n = len(stripes[0]) if stripes else 0
         bm = BatchMarshal(stripes, n, fill=True)
         status = (ctypes.c_int * max(len(stripes), 1))()
-        st = self._L.cfsec_ec_encode_batch(self._h, bm.arr, n, len(stripes), bm.mem, status)
+        if crcs:
+            words = (ctypes.c_uint32 * max(len(stripes) * n, 1))()
+            st = self._L.cfsec_ec_encode_batch_crc(self._h, bm.arr, n, len(stripes), bm.mem, status, words)
+        else:
+            st = self._L.cfsec_ec_encode_batch(self._h, bm.arr, n, len(stripes), bm.mem, status)
         bm.writeback()
         _lib.check(st)
-        return [int(status[i]) for i in range(len(stripes))]
+        out = [int(status[i]) for i in range(len(stripes))]
+        if crcs:
+            return out, [[int(words[s * n + i]) for i in range(n)] for s in range(len(stripes))]
+        return out
 
-    def ReconstructBatch(self, bids, badIdx, verify: bool = True):
+    def ReconstructBatch(self, bids, badIdx, verify: bool = True, crcs: bool = False):
         """bids: list of shard lists (one per bid, all of one length n); badIdx: one index list per
         bid.  Per bid Reconstruct(shards, bad) then Verify(shards), one batched call; returns the
-        per-bid status codes (0 ok, ErrVerify.status when Verify is false, else the error)."""
+        per-bid status codes (0 ok, ErrVerify.status when Verify is false, else the error), and with
+        crcs=True also per bid the checksums of the shards it rebuilt (0 elsewhere)."""
         if len(bids) != len(badIdx):
             raise ValueError("one bad-index list per bid")
         n = len(bids[0]) if bids else 0
@@ -116,17 +125,26 @@ class Encoder:
         bad = (ctypes.c_int * max(len(flat), 1))(*flat)
         offs = (ctypes.c_int * len(off))(*off)
         status = (ctypes.c_int * max(len(bids), 1))()
-        st = self._L.cfsec_ec_reconstruct_batch(self._h, bm.arr, n, len(bids), bad, offs, int(verify), bm.mem,
-                                                status)
+        if crcs:
+            words = (ctypes.c_uint32 * max(len(bids) * n, 1))()
+            st = self._L.cfsec_ec_reconstruct_batch_crc(self._h, bm.arr, n, len(bids), bad, offs, int(verify),
+                                                        bm.mem, status, words)
+        else:
+            st = self._L.cfsec_ec_reconstruct_batch(self._h, bm.arr, n, len(bids), bad, offs, int(verify), bm.mem,
+                                                    status)
         bm.writeback()
         _lib.check(st)
-        return [int(status[i]) for i in range(len(bids))]
+        out = [int(status[i]) for i in range(len(bids))]
+        if crcs:
+            return out, [[int(words[b * n + i]) for i in range(n)] for b in range(len(bids))]
+        return out
 
-    def ReconstructBatchAsync(self, bids, badIdx, flags=None, verify: bool = True, stream=None):
+    def ReconstructBatchAsync(self, bids, badIdx, flags=None, verify: bool = True, stream=None, crcs=None):
         """cfsec_ec_reconstruct_batch_async: bids of device tensors; enqueues on `stream` (default:
         torch's current stream) and returns the per-bid planning status right away.  flags: a zeroed
         device int32 tensor of len(bids) words; flags[b] != 0 once the stream has passed the call
-        where Verify is false."""
+        where Verify is false.  crcs: optional device int32 tensor of len(bids) * n words for the
+        rebuilt shards' checksums."""
         if len(bids) != len(badIdx):
             raise ValueError("one bad-index list per bid")
         n = len(bids[0]) if bids else 0
@@ -143,14 +161,16 @@ class Encoder:
         like = next((x for st in bids for x in st if x is not None and x.numel()), None)
         st = self._L.cfsec_ec_reconstruct_batch_async(self._h, bm.arr, n, len(bids), bad, offs, int(verify), status,
                                                       None if flags is None else flags.data_ptr(),
+                                                      None if crcs is None else crcs.data_ptr(),
                                                       stream_ptr(stream, like))
         bm.writeback()
         _lib.check(st)
         return [int(status[i]) for i in range(len(bids))]
 
-    def EncodeBatchAsync(self, stripes, flags=None, stream=None):
+    def EncodeBatchAsync(self, stripes, flags=None, stream=None, crcs=None):
         """cfsec_ec_encode_batch_async: as EncodeBatch on device tensors, enqueued on `stream`; with
-        EnableVerify a false Verify sets flags[s] (zeroed device int32 tensor) on the stream."""
+        EnableVerify a false Verify sets flags[s] (zeroed device int32 tensor) on the stream; crcs:
+        optional device int32 tensor of len(stripes) * n words for every shard's checksum."""
         n = len(stripes[0]) if stripes else 0
         bm = BatchMarshal(stripes, n, fill=True)
         if stripes and bm.mem != _lib.MEM_DEVICE:
@@ -158,7 +178,8 @@ class Encoder:
         status = (ctypes.c_int * max(len(stripes), 1))()
         like = next((x for st in stripes for x in st if x is not None and x.numel()), None)
         st = self._L.cfsec_ec_encode_batch_async(self._h, bm.arr, n, len(stripes), status,
-                                                 None if flags is None else flags.data_ptr(), stream_ptr(stream, like))
+                                                 None if flags is None else flags.data_ptr(),
+                                                 None if crcs is None else crcs.data_ptr(), stream_ptr(stream, like))
         bm.writeback()
         _lib.check(st)
         return [int(status[i]) for i in range(len(stripes))]

@@ -220,6 +220,18 @@ int cfsec_ec_set_devices(cfsec_ec* h, const int* devices, int ndev);
  * modes as one fused (M+L) x N pass (lrcencoder.go:35-82).  status[s]: Encode's result (CFSEC_ERR_VERIFY
  * when the enabled Verify fails).  Memory and devices as for cfsec_rs_*_stripes. */
 int cfsec_ec_encode_batch(cfsec_ec* h, cfsec_shard* shards, int n, int nstripes, int mem, int* status);
+/* The two batch calls above returning the shard checksums CubeFS takes right after coding
+ * (crc32.ChecksumIEEE): crcs is a host array of nstripes * n (nbids * n) words, indexed
+ * [item][shard].  Encode: every shard of the stripe after the Encode (access/stream_put.go:249-253).
+ * Reconstruct: the shards the call rebuilt -- global or local, data or parity -- (blobnode's
+ * ShardCrc32 of each repaired shard, blobnode/work_shard_recover.go:335-342), 0 for the others.
+ * Items whose status is not CFSEC_OK get all-zero words.  Computed on the GPU from the rows the
+ * product wrote (device or staged copies), before they leave HBM.  CFSEC_ERR_NOT_SUPPORTED for
+ * shapes with more than 32 inputs and Verify. */
+int cfsec_ec_encode_batch_crc(cfsec_ec* h, cfsec_shard* shards, int n, int nstripes, int mem, int* status,
+                              uint32_t* crcs);
+int cfsec_ec_reconstruct_batch_crc(cfsec_ec* h, cfsec_shard* shards, int n, int nbids, const int* bad_idx,
+                                   const int* bad_off, int verify, int mem, int* status, uint32_t* crcs);
 /* Asynchronous forms of the two batch calls above, for device memory on the handle's (first) device:
  * the call plans the batch, enqueues its kernels on `stream` (hipStream_t; NULL = the legacy default
  * stream) and returns without waiting, so a caller overlaps the next tasklet's planning with this
@@ -231,11 +243,15 @@ int cfsec_ec_encode_batch(cfsec_ec* h, cfsec_shard* shards, int n, int nstripes,
  * synchronous call; the bytes are there when the stream gets there.  The library keeps no caller
  * pointer after the call returns (the shard pointers are copied into the kernel arguments).  Shapes
  * the kernels cannot compare in one pass (more than 32 inputs with Verify, an LRC stripe whose
- * local shard has another length) run synchronously on `stream` and report ErrVerify in status[b]. */
+ * local shard has another length) run synchronously on `stream` and report ErrVerify in status[b].
+ * crcs (device, nbids * n / nstripes * n words, may be NULL): the checksums of the _crc forms,
+ * written on the stream (zeroed by the call first); a flagged or failed item's words are
+ * meaningless. */
 int cfsec_ec_reconstruct_batch_async(cfsec_ec* h, cfsec_shard* shards, int n, int nbids, const int* bad_idx,
-                                     const int* bad_off, int verify, int* status, uint32_t* flags, void* stream);
+                                     const int* bad_off, int verify, int* status, uint32_t* flags, uint32_t* crcs,
+                                     void* stream);
 int cfsec_ec_encode_batch_async(cfsec_ec* h, cfsec_shard* shards, int n, int nstripes, int* status, uint32_t* flags,
-                                void* stream);
+                                uint32_t* crcs, void* stream);
 /* Repair over survivors held elsewhere (the multi-GPU repair of chubaofs_amd/repair.py ships only
  * the shards a decode reads): with the shards in bad_idx[0..nbad) lost (global or LRC local
  * indices), in_idx[0..N) = the first N present global shards in index order -- the ones

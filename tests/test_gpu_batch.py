@@ -480,3 +480,192 @@ def test_async_rejects_host_memory_and_missing_flags():
     dev = [to_mem(good, "device")]
     with pytest.raises(_lib.ErrInvalidArg):
         enc.ReconstructBatchAsync(dev, [[0]], flags=None, verify=True)
+
+
+# ------------------------------------------------------------------ multi-device split, rehearsed
+
+def _trace_split(err):
+    """{device index: [items]} from the library's CFSEC_TRACE_BATCH lines."""
+    out = {}
+    for line in err.splitlines():
+        if line.startswith("cfsec batch: device index"):
+            head, items = line.split(", items")
+            d = int(head.split("device index")[1].split()[0])
+            out.setdefault(d, []).append([int(x) for x in items.split()])
+    return out
+
+
+@pytest.mark.parametrize("memory", ["host", "pinned"])
+def test_two_device_split_rehearsed(memory, monkeypatch, capfd):
+    """The device-set path (run_stripes: one host thread, stream pair and staging per device, stripes
+    split by cfsec_batch_partition) with two contexts on device 0 (CFSEC_DEVICE_REHEARSAL): bytes
+    equal the oracle's two-pass reconstruct + Verify, and the split is the partition's."""
+    from chubaofs_amd import reedsolomon
+    monkeypatch.setenv("CFSEC_DEVICE_REHEARSAL", "1")
+    monkeypatch.setenv("CFSEC_TRACE_BATCH", "1")
+    k, m = 12, 4
+    enc = reedsolomon.New(k, m, device=0)
+    enc.SetDevices([0, 0])
+    sizes = [4096, 300001, 23, 1 << 20, 65537, 777, 200000, 5]
+    bad = [0, 5, 13]
+    stripes, want = [], []
+    for b, size in enumerate(sizes):
+        good = codeword(k, m, size, b + 3)
+        src = [x.copy() for x in good]
+        if b == 2:
+            src[15][size // 2] ^= 0x40  # a compared parity: Verify false
+        want.append(reference_repair(k, m, src, bad))
+        stripes.append(to_mem(src, memory))
+        mark_missing(stripes[-1], bad, memory)
+    capfd.readouterr()
+    status = enc.ReconstructStripes(stripes, verify=True)
+    err = capfd.readouterr().err
+    for b, (st, shards) in enumerate(want):
+        assert status[b] == st, (b, status[b], st)
+        for i in range(k + m):
+            assert np.array_equal(host(stripes[b][i]), shards[i]), (b, i)
+    # every stripe moves (k inputs + 3 rebuilt + 1 compared parity) rows of its size
+    expect = _lib.batch_partition([s * (k + 4) for s in sizes], 2)
+    split = _trace_split(err)
+    assert set(split) == {0, 1}, err
+    got = {d: sorted(i for call in v for i in call) for d, v in split.items()}
+    assert got == {d: [i for i, x in enumerate(expect) if x == d] for d in (0, 1)}, (got, expect)
+
+
+def test_two_device_lrc_tasklet_rehearsed(monkeypatch, capfd):
+    """An LRC tasklet (global pass, then AZ-local passes of the bids with a bad local shard) over two
+    rehearsed device contexts: every pass of a bid stays on one device, results equal the ec oracle."""
+    monkeypatch.setenv("CFSEC_DEVICE_REHEARSAL", "1")
+    monkeypatch.setenv("CFSEC_TRACE_BATCH", "1")
+    t = cm.GetTactic(cm.EC6P10L2)
+    enc = ec_new(cm.EC6P10L2)
+    enc.SetDevices([0, 0])
+    total = t.N + t.M + t.L
+    bids, bads, want = [], [], []
+    for b, size in enumerate([4097, 65536, 23, 262144, 1000, 12]):
+        good = ec_full_codeword(enc, t, size, 70 + b)
+        bad = [0, total - 1] if b % 2 else [2, 9]
+        src = [x.copy() for x in good]
+        if b == 3:
+            src[t.N + t.M][7] ^= 1
+        want.append(sequential(enc, src, bad))
+        work = to_mem(src, "pinned" if b % 3 == 0 else "host")
+        for i in bad:
+            work[i][:] = 0
+        bids.append(work)
+        bads.append(bad)
+    capfd.readouterr()
+    status = enc.ReconstructBatch(bids, bads)
+    err = capfd.readouterr().err
+    for b, (st, shards) in enumerate(want):
+        assert status[b] == st, (b, status[b], st)
+        for i in range(total):
+            assert np.array_equal(host(bids[b][i]), shards[i]), (b, i)
+    split = _trace_split(err)
+    assert set(split) == {0, 1}, err
+    seen = {}
+    for d, calls in split.items():
+        for call in calls:
+            for it in call:
+                assert seen.setdefault(it, d) == d, ("a bid's passes split over devices", it)
+
+
+# ------------------------------------------------------------------ checksums from the batch calls
+
+def crc_of(a):
+    return O.crc32_ieee(np.ascontiguousarray(a)) if a.size else 0
+
+
+@pytest.mark.parametrize("memory", ["host", "pinned", "device"])
+@pytest.mark.parametrize("mode", [cm.EC6P6, cm.EC12P4, cm.EC6P10L2, cm.EC16P20L2])
+def test_ec_encode_batch_crc(mode, memory):
+    """cfsec_ec_encode_batch_crc: the ec oracle's Encode, then crc32.ChecksumIEEE of every shard
+    (access/stream_put.go:249-253) -- zlib-equal words from the GPU; a failed stripe's words are 0."""
+    from chubaofs_amd import ec
+    t = cm.GetTactic(mode)
+    enc = ec.NewEncoder(ec.Config(CodeMode=t, EnableVerify=True), device=0)
+    orc = ECOracle.from_tactic(t, enable_verify=True)
+    total = t.N + t.M + t.L
+    stripes, want, exp = [], [], []
+    for b, size in enumerate([1, 23, 4096, 4097, 262144, 0, 65537]):
+        src = [gen_mock_bytes(b * 11 + i, size) for i in range(t.N)] + \
+              [np.full(size, 0x42, np.uint8) for _ in range(total - t.N)]
+        ref = [Slice() if x.size == 0 else Slice.of(x) for x in src]
+        exp.append(orc.encode(ref))
+        want.append([x.view().copy() for x in ref])
+        stripes.append(to_mem(src, memory))
+    st, crcs = enc.EncodeBatch(stripes, crcs=True)
+    assert st == exp
+    for b in range(len(stripes)):
+        for i in range(total):
+            assert np.array_equal(host(stripes[b][i]), want[b][i]), (b, i)
+            w = crc_of(want[b][i]) if exp[b] == 0 else 0
+            assert crcs[b][i] == w, (b, i, hex(crcs[b][i]), hex(w))
+    import zlib
+    assert crcs[3][0] == zlib.crc32(want[3][0].tobytes())
+
+
+@pytest.mark.parametrize("memory", ["host", "pinned", "device"])
+@pytest.mark.parametrize("mode", [cm.EC12P4, cm.EC16P20L2, cm.EC6P10L2, cm.EC6P6])
+def test_ec_reconstruct_batch_crc(mode, memory):
+    """cfsec_ec_reconstruct_batch_crc: the rebuilt shards' checksums (blobnode's ShardCrc32 of each
+    repaired shard, work_shard_recover.go:335-342) -- global, data and local parity alike -- 0 for
+    the shards not rebuilt and for bids whose status is not OK; C5's pattern at S = 262,144."""
+    t = cm.GetTactic(mode)
+    enc = ec_new(mode)
+    total = t.N + t.M + t.L
+    r = random.Random(mode + 17)
+    bids, bads, want = [], [], []
+    for b, size in enumerate([262144, 4097, 23, 65536, 1, 2048, 777]):
+        good = ec_full_codeword(enc, t, size, 30 + b)
+        if mode == cm.EC16P20L2 and b == 0:
+            bad = [0, 1, 16, 17]
+        elif t.L and b == 1:
+            bad = [2, total - 1]
+        else:
+            bad = sorted(r.sample(range(total), r.randint(1, t.M)))
+        src = [x.copy() for x in good]
+        if b == 5:
+            cand = [i for i in range(t.N, total) if i not in bad]
+            src[cand[0]][size // 2] ^= 0x18
+        want.append(sequential(enc, src, bad))
+        work = to_mem(src, memory)
+        for i in bad:
+            if memory == "device":
+                work[i].zero_()
+            else:
+                work[i][:] = 0
+        bids.append(work)
+        bads.append(bad)
+    st, crcs = enc.ReconstructBatch(bids, bads, crcs=True)
+    for b, (exp, shards) in enumerate(want):
+        assert st[b] == exp, (b, st[b], exp)
+        for i in range(total):
+            assert np.array_equal(host(bids[b][i]), shards[i]), (b, i)
+            w = crc_of(shards[i]) if exp == 0 and i in bads[b] else 0
+            assert crcs[b][i] == w, (cm.Name(mode), b, bads[b], i, hex(crcs[b][i]), hex(w))
+
+
+def test_ec_reconstruct_batch_async_crc():
+    t = cm.GetTactic(cm.EC16P20L2)
+    enc = ec_new(cm.EC16P20L2)
+    total = t.N + t.M + t.L
+    bids, bads, want = [], [], []
+    for b, size in enumerate([262144, 4096, 5]):
+        good = ec_full_codeword(enc, t, size, 90 + b)
+        bad = [0, 1, 16, 17] if b != 1 else [3, total - 2]
+        want.append(sequential(enc, good, bad))
+        work = to_mem(good, "device")
+        for i in bad:
+            work[i].zero_()
+        bids.append(work)
+        bads.append(bad)
+    flags = torch.zeros(len(bids), dtype=torch.int32, device="cuda")
+    crcs = torch.full((len(bids) * total,), -1, dtype=torch.int32, device="cuda")
+    st = enc.ReconstructBatchAsync(bids, bads, flags=flags, crcs=crcs)
+    torch.cuda.synchronize()
+    assert st == [0] * len(bids) and not flags.any().item()
+    got = crcs.cpu().numpy().astype(np.uint32).reshape(len(bids), total)
+    for b, (_, shards) in enumerate(want):
+        for i in range(total):
+            assert got[b][i] == (crc_of(shards[i]) if i in bads[b] else 0), (b, i)

@@ -55,3 +55,29 @@ bad = (ctypes.c_int * nb4)(*([0] * nb4))
 off = (ctypes.c_int * (nb4 + 1))(*range(nb4 + 1))
 run("C4 local reconstruct_batch", lambda: _lib.check(e4._L.cfsec_ec_reconstruct_batch(e4._h, lbm.arr, len(idx0), nb4, bad,
                                                                                         off, 1, lbm.mem, st4)))
+
+# asynchronous forms: wall time of the enqueue alone (a sync after each call, outside the timing)
+stream = torch.cuda.Stream()
+fl = torch.zeros(64, dtype=torch.int32, device=dev)
+
+
+def timed_async(name, fn, n=20):
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(n):
+        sys.stderr.write(f"--- {name}\n")
+        t0 = time.perf_counter()
+        fn()
+        ts.append((time.perf_counter() - t0) * 1e6)
+        torch.cuda.synchronize()
+    ts.sort()
+    print(f"{name:28s} enqueue median {ts[n // 2]:8.1f} us  min {ts[0]:8.1f} us", flush=True)
+
+
+timed_async("C5 reconstruct_batch_async", lambda: _lib.check(e5._L.cfsec_ec_reconstruct_batch_async(
+    e5._h, bm5.arr, tot5, nb5, bad5, off5, 1, st5, fl.data_ptr(), None, stream.cuda_stream)))
+timed_async("C4 local reconstruct_async", lambda: _lib.check(e4._L.cfsec_ec_reconstruct_batch_async(
+    e4._h, lbm.arr, len(idx0), nb4, bad, off, 1, st4, fl.data_ptr(), None, stream.cuda_stream)))
+timed_async("C4 encode_batch_async", lambda: _lib.check(e4._L.cfsec_ec_encode_batch_async(
+    e4._h, bm4.arr, tot4, nb4, st4, None, None, stream.cuda_stream)))
