@@ -119,6 +119,14 @@ SIGNATURES = {
     "cfsec_ec_encode_batch_async": ([_V, P_SHARD, _I, _I, _V, _V, _V, _V], _I),
     "cfsec_ec_encode_batch_crc": ([_V, P_SHARD, _I, _I, _I, _V, _V], _I),
     "cfsec_ec_reconstruct_batch_crc": ([_V, P_SHARD, _I, _I, _V, _V, _I, _I, _V, _V], _I),
+    "cfsec_rs_encode_contig": ([_V, _V, _S, _S, _I, _I, _V], _I),
+    "cfsec_rs_verify_contig": ([_V, _V, _S, _S, _I, _I, _V, _P(_I)], _I),
+    "cfsec_rs_reconstruct_contig": ([_V, _V, _S, _S, _I, _V, _I, _I, _I, _V], _I),
+    "cfsec_ec_encode_contig": ([_V, _V, _S, _S, _I, _I, _V], _I),
+    "cfsec_ec_verify_contig": ([_V, _V, _S, _S, _I, _I, _V, _P(_I)], _I),
+    "cfsec_ec_reconstruct_contig": ([_V, _V, _S, _S, _I, _V, _I, _I, _I, _V], _I),
+    "cfsec_ec_encode_batch_contig": ([_V, _V, _S, _S, _S, _I, _I, _I, _V, _V], _I),
+    "cfsec_ec_reconstruct_batch_contig": ([_V, _V, _V, _V, _I, _I, _V, _V, _I, _I, _V, _V], _I),
     "cfsec_crc32_ieee_batch": ([_V, _S, _I, _V, _I, _V], _I),
     "cfsec_host_alloc": ([_S, _P(_V)], _I),
     "cfsec_host_free": ([_V], _I),

@@ -646,3 +646,105 @@ int cfsec_crc32block_decode_batch(const uint8_t* const* srcs, int64_t src_len, u
 }
 
 }  // extern "C"
+
+// ---------------- contiguous stripes (ec.Buffer layout) ----------------
+
+namespace {
+// Shard headers of a contiguous stripe: shard i at base + i * stride, `size` bytes, missing[] (when
+// given) marked len 0 with their buffer kept as capacity.
+int contig_shards(uint8_t* base, size_t size, size_t stride, int n, const int* missing, int nmissing,
+                  std::vector<cfsec_shard>* out) {
+  if (!base || n <= 0 || size == 0 || stride < size || nmissing < 0 || (nmissing > 0 && !missing))
+    return CFSEC_ERR_INVALID_ARG;
+  out->assign((size_t)n, cfsec_shard{nullptr, 0, 0});
+  for (int i = 0; i < n; ++i) (*out)[i] = cfsec_shard{base + (size_t)i * stride, size, size};
+  for (int j = 0; j < nmissing; ++j) {
+    if (missing[j] < 0 || missing[j] >= n) return CFSEC_ERR_INVALID_ARG;
+    (*out)[missing[j]].len = 0;
+  }
+  return CFSEC_OK;
+}
+}  // namespace
+
+int cfsec_rs_encode_contig(cfsec_rs* h, uint8_t* base, size_t shard_size, size_t stride, int n, int mem,
+                           void* stream) {
+  std::vector<cfsec_shard> v;
+  const int st = contig_shards(base, shard_size, stride, n, nullptr, 0, &v);
+  if (!h || st != CFSEC_OK) return CFSEC_ERR_INVALID_ARG;
+  return cfsec_rs_encode(h, v.data(), n, mem, stream);
+}
+
+int cfsec_rs_verify_contig(cfsec_rs* h, uint8_t* base, size_t shard_size, size_t stride, int n, int mem,
+                           void* stream, int* ok) {
+  std::vector<cfsec_shard> v;
+  const int st = contig_shards(base, shard_size, stride, n, nullptr, 0, &v);
+  if (!h || st != CFSEC_OK) return CFSEC_ERR_INVALID_ARG;
+  return cfsec_rs_verify(h, v.data(), n, mem, stream, ok);
+}
+
+int cfsec_rs_reconstruct_contig(cfsec_rs* h, uint8_t* base, size_t shard_size, size_t stride, int n,
+                                const int* missing, int nmissing, int data_only, int mem, void* stream) {
+  std::vector<cfsec_shard> v;
+  const int st = contig_shards(base, shard_size, stride, n, missing, nmissing, &v);
+  if (!h || st != CFSEC_OK) return CFSEC_ERR_INVALID_ARG;
+  return data_only ? cfsec_rs_reconstruct_data(h, v.data(), n, mem, stream)
+                   : cfsec_rs_reconstruct(h, v.data(), n, mem, stream);
+}
+
+int cfsec_ec_encode_contig(cfsec_ec* h, uint8_t* base, size_t shard_size, size_t stride, int n, int mem,
+                           void* stream) {
+  std::vector<cfsec_shard> v;
+  const int st = contig_shards(base, shard_size, stride, n, nullptr, 0, &v);
+  if (!h || st != CFSEC_OK) return CFSEC_ERR_INVALID_ARG;
+  return cfsec_ec_encode(h, v.data(), n, mem, stream);
+}
+
+int cfsec_ec_verify_contig(cfsec_ec* h, uint8_t* base, size_t shard_size, size_t stride, int n, int mem,
+                           void* stream, int* ok) {
+  std::vector<cfsec_shard> v;
+  const int st = contig_shards(base, shard_size, stride, n, nullptr, 0, &v);
+  if (!h || st != CFSEC_OK) return CFSEC_ERR_INVALID_ARG;
+  return cfsec_ec_verify(h, v.data(), n, mem, stream, ok);
+}
+
+int cfsec_ec_reconstruct_contig(cfsec_ec* h, uint8_t* base, size_t shard_size, size_t stride, int n,
+                                const int* bad_idx, int nbad, int data_only, int mem, void* stream) {
+  std::vector<cfsec_shard> v;
+  const int st = contig_shards(base, shard_size, stride, n, nullptr, 0, &v);
+  if (!h || st != CFSEC_OK) return CFSEC_ERR_INVALID_ARG;
+  return data_only ? cfsec_ec_reconstruct_data(h, v.data(), n, bad_idx, nbad, mem, stream)
+                   : cfsec_ec_reconstruct(h, v.data(), n, bad_idx, nbad, mem, stream);
+}
+
+int cfsec_ec_encode_batch_contig(cfsec_ec* h, uint8_t* base, size_t shard_size, size_t stride, size_t stripe_stride,
+                                 int n, int nstripes, int mem, int* status, uint32_t* crcs) {
+  if (!h || nstripes < 0 || n <= 0 || (nstripes > 0 && (!base || !status))) return CFSEC_ERR_INVALID_ARG;
+  if (nstripes > 1 && stripe_stride < stride * (size_t)n) return CFSEC_ERR_INVALID_ARG;  // stripes overlap
+  std::vector<cfsec_shard> all((size_t)nstripes * n), one;
+  for (int s = 0; s < nstripes; ++s) {
+    if (contig_shards(base + (size_t)s * stripe_stride, shard_size, stride, n, nullptr, 0, &one) != CFSEC_OK)
+      return CFSEC_ERR_INVALID_ARG;
+    std::copy(one.begin(), one.end(), all.begin() + (size_t)s * n);
+  }
+  return crcs ? cfsec_ec_encode_batch_crc(h, all.data(), n, nstripes, mem, status, crcs)
+              : cfsec_ec_encode_batch(h, all.data(), n, nstripes, mem, status);
+}
+
+int cfsec_ec_reconstruct_batch_contig(cfsec_ec* h, uint8_t* base, const uint64_t* bid_off,
+                                      const uint64_t* bid_shard_size, int n, int nbids, const int* bad_idx,
+                                      const int* bad_off, int verify, int mem, int* status, uint32_t* crcs) {
+  if (!h || nbids < 0 || n <= 0 || (nbids > 0 && (!base || !bid_off || !bid_shard_size || !status)))
+    return CFSEC_ERR_INVALID_ARG;
+  std::vector<cfsec_shard> all((size_t)nbids * n), one;
+  for (int b = 0; b < nbids; ++b) {
+    const size_t S = (size_t)bid_shard_size[b];
+    if (S == 0) {  // a zero-size bid: every shard empty (the reference loop skips those, :730-733)
+      for (int i = 0; i < n; ++i) all[(size_t)b * n + i] = cfsec_shard{base + bid_off[b], 0, 0};
+      continue;
+    }
+    if (contig_shards(base + bid_off[b], S, S, n, nullptr, 0, &one) != CFSEC_OK) return CFSEC_ERR_INVALID_ARG;
+    std::copy(one.begin(), one.end(), all.begin() + (size_t)b * n);
+  }
+  return crcs ? cfsec_ec_reconstruct_batch_crc(h, all.data(), n, nbids, bad_idx, bad_off, verify, mem, status, crcs)
+              : cfsec_ec_reconstruct_batch(h, all.data(), n, nbids, bad_idx, bad_off, verify, mem, status);
+}

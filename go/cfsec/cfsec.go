@@ -7,6 +7,13 @@
 // ReconstructData, Split, Join -- go to libcfsec.so; EncodeIdx, ReconstructSome
 // and Update, which CubeFS never calls, return reedsolomon.ErrNotSupported.
 //
+// Go releases.  CubeFS builds with Go 1.17 (go.mod:3, docker/Dockerfile:1), whose cgo rules forbid a
+// C array holding Go pointers.  So every call first looks for the one-allocation layout that
+// ec.Buffer and Split produce (stripeOf: shard i at base + i*stride) and passes that stripe as a
+// single pointer to the cfsec_*_contig entry points -- legal on every Go release.  Any other shard
+// vector goes through callVec: with Go >= 1.21 the buffers are pinned (runtime.Pinner, vec_pin.go),
+// before that they are staged through C memory (vec_copy.go).
+//
 // Source only: this container has no Go toolchain, so the package is not built or
 // tested here (see INTEGRATION.md for the build line and the test plan).
 package cfsec
@@ -28,6 +35,81 @@ import (
 
 	"github.com/klauspost/reedsolomon"
 )
+
+// stripeOf reports whether every shard is size bytes at one stride from the first (ec.Buffer's
+// layout, common/ec/buf.go:83-84, which encoder.Split carves): then the stripe crosses the C ABI as
+// its base pointer alone (cfsec_*_contig).
+func stripeOf(shards [][]byte) (base *C.uint8_t, size, stride int, ok bool) {
+	if len(shards) == 0 || len(shards[0]) == 0 {
+		return nil, 0, 0, false
+	}
+	size = len(shards[0])
+	p0 := uintptr(unsafe.Pointer(&shards[0][0]))
+	stride = size
+	if len(shards) > 1 && len(shards[1]) == size {
+		stride = int(uintptr(unsafe.Pointer(&shards[1][0])) - p0)
+	}
+	if stride < size {
+		return nil, 0, 0, false
+	}
+	for i, s := range shards {
+		if len(s) != size || uintptr(unsafe.Pointer(&s[0])) != p0+uintptr(i*stride) {
+			return nil, 0, 0, false
+		}
+	}
+	return (*C.uint8_t)(unsafe.Pointer(&shards[0][0])), size, stride, true
+}
+
+// stripeOfMissing is stripeOf for a Reconstruct input: a missing shard (len 0) counts when its
+// capacity holds the shard at its place in the stripe; missing lists those indices.
+func stripeOfMissing(shards [][]byte) (base *C.uint8_t, size, stride int, missing []C.int, ok bool) {
+	first := -1
+	for i, s := range shards {
+		if len(s) != 0 {
+			first, size = i, len(s)
+			break
+		}
+	}
+	if first < 0 {
+		return nil, 0, 0, nil, false
+	}
+	addr := make([]uintptr, len(shards))
+	for i, s := range shards {
+		switch {
+		case len(s) == size:
+			addr[i] = uintptr(unsafe.Pointer(&s[0]))
+		case len(s) == 0 && cap(s) >= size:
+			addr[i] = uintptr(unsafe.Pointer(&s[:1][0]))
+			missing = append(missing, C.int(i))
+		default:
+			return nil, 0, 0, nil, false
+		}
+	}
+	stride = size
+	if len(shards) > 1 {
+		stride = int(addr[1] - addr[0])
+	}
+	if stride < size {
+		return nil, 0, 0, nil, false
+	}
+	for i := range shards {
+		if addr[i] != addr[0]+uintptr(i*stride) {
+			return nil, 0, 0, nil, false
+		}
+	}
+	return (*C.uint8_t)(unsafe.Pointer(addr[0])), size, stride, missing, true
+}
+
+func cints(v []int) ([]C.int, *C.int) {
+	if len(v) == 0 {
+		return nil, nil
+	}
+	c := make([]C.int, len(v))
+	for i, x := range v {
+		c[i] = C.int(x)
+	}
+	return c, &c[0]
+}
 
 // Engine is a reedsolomon.Encoder whose arithmetic runs on a GPU.
 type Engine struct {
@@ -84,74 +166,24 @@ func New(dataShards, parityShards int) (*Engine, error) {
 	return e, nil
 }
 
-// shardVec pins the caller's byte slices and lays them out as a C cfsec_shard array.
-// The C side never keeps a pointer after the call returns.
-type shardVec struct {
-	pin runtime.Pinner
-	arr *C.cfsec_shard
-	n   int
-}
-
-func newShardVec(shards [][]byte) *shardVec {
-	v := &shardVec{n: len(shards)}
-	if v.n == 0 {
-		return v
-	}
-	v.arr = (*C.cfsec_shard)(C.malloc(C.size_t(v.n) * C.size_t(unsafe.Sizeof(C.cfsec_shard{}))))
-	elems := unsafe.Slice(v.arr, v.n)
-	for i, s := range shards {
-		elems[i] = C.cfsec_shard{data: nil, len: C.size_t(len(s)), cap: C.size_t(cap(s))}
-		if cap(s) > 0 {
-			p := &s[:cap(s)][0]
-			v.pin.Pin(p)
-			elems[i].data = (*C.uint8_t)(unsafe.Pointer(p))
-		}
-	}
-	return v
-}
-
-func (v *shardVec) ptr() *C.cfsec_shard { return v.arr }
-
-// lens copies the lengths the engine left in the headers back into the Go slices.
-func (v *shardVec) lens(shards [][]byte) {
-	if v.n == 0 {
-		return
-	}
-	for i, e := range unsafe.Slice(v.arr, v.n) {
-		if int(e.len) != len(shards[i]) {
-			shards[i] = shards[i][:int(e.len)]
-		}
-	}
-}
-
-func (v *shardVec) free() {
-	if v.arr != nil {
-		C.free(unsafe.Pointer(v.arr))
-	}
-	v.pin.Unpin()
-}
-
 func (e *Engine) Encode(shards [][]byte) error {
-	v := newShardVec(shards)
-	defer v.free()
-	return toError(C.cfsec_rs_encode(e.h, v.ptr(), C.int(v.n), C.CFSEC_MEM_HOST, nil))
+	if base, size, stride, ok := stripeOf(shards); ok {
+		return toError(C.cfsec_rs_encode_contig(e.h, base, C.size_t(size), C.size_t(stride), C.int(len(shards)),
+			C.CFSEC_MEM_HOST, nil))
+	}
+	return toError(callVec(shards, func(v *C.cfsec_shard, n C.int) C.int {
+		return C.cfsec_rs_encode(e.h, v, n, C.CFSEC_MEM_HOST, nil)
+	}))
 }
 
 // EncodeCRC is Encode followed by crc32.ChecksumIEEE of every shard -- what access computes
 // right after encoding (blobstore/access/stream_put.go:249-253) -- in one fused GPU pass.
 func (e *Engine) EncodeCRC(shards [][]byte) ([]uint32, error) {
-	v := newShardVec(shards)
-	defer v.free()
-	crcs := make([]uint32, v.n)
-	if v.n == 0 {
-		return crcs, toError(C.cfsec_rs_encode(e.h, v.ptr(), 0, C.CFSEC_MEM_HOST, nil))
-	}
-	var pin runtime.Pinner
-	pin.Pin(&crcs[0])
-	defer pin.Unpin()
-	err := toError(C.cfsec_rs_encode_crc(e.h, v.ptr(), C.int(v.n), C.CFSEC_MEM_HOST, nil,
-		(*C.uint32_t)(unsafe.Pointer(&crcs[0]))))
-	return crcs, err
+	crcs := make([]uint32, len(shards)+1) // +1: a valid address even for an empty vector
+	st := callVec(shards, func(v *C.cfsec_shard, n C.int) C.int {
+		return C.cfsec_rs_encode_crc(e.h, v, n, C.CFSEC_MEM_HOST, nil, (*C.uint32_t)(unsafe.Pointer(&crcs[0])))
+	})
+	return crcs[:len(shards)], toError(st)
 }
 
 // HostAlloc returns size bytes of page-locked C memory (cfsec_host_alloc) as a byte slice: the
@@ -173,15 +205,20 @@ func HostFree(b []byte) error {
 	if cap(b) == 0 {
 		return nil
 	}
-	return toError(C.cfsec_host_free(unsafe.Pointer(unsafe.SliceData(b[:1]))))
+	return toError(C.cfsec_host_free(unsafe.Pointer(&b[:1][0])))
 }
 
 func (e *Engine) Verify(shards [][]byte) (bool, error) {
-	v := newShardVec(shards)
-	defer v.free()
-	var ok C.int
-	err := toError(C.cfsec_rs_verify(e.h, v.ptr(), C.int(v.n), C.CFSEC_MEM_HOST, nil, &ok))
-	return ok != 0, err
+	ok := make([]C.int, 1)
+	if base, size, stride, contig := stripeOf(shards); contig {
+		err := toError(C.cfsec_rs_verify_contig(e.h, base, C.size_t(size), C.size_t(stride), C.int(len(shards)),
+			C.CFSEC_MEM_HOST, nil, &ok[0]))
+		return ok[0] != 0, err
+	}
+	err := toError(callVec(shards, func(v *C.cfsec_shard, n C.int) C.int {
+		return C.cfsec_rs_verify(e.h, v, n, C.CFSEC_MEM_HOST, nil, &ok[0])
+	}))
+	return ok[0] != 0, err
 }
 
 // prepareMissing gives every zero-length shard a buffer of the shard size, as
@@ -204,59 +241,100 @@ func prepareMissing(shards [][]byte) {
 	}
 }
 
-func (e *Engine) Reconstruct(shards [][]byte) error {
+func (e *Engine) reconstruct(shards [][]byte, dataOnly bool) error {
+	donly := C.int(0)
+	if dataOnly {
+		donly = 1
+	}
+	// ec.Buffer's stripe with some shards marked missing: one pointer, rebuilt in place
+	if base, size, stride, missing, ok := stripeOfMissing(shards); ok && len(shards) == e.dataShards+e.parityShards {
+		var mp *C.int
+		if len(missing) > 0 {
+			mp = &missing[0]
+		}
+		err := toError(C.cfsec_rs_reconstruct_contig(e.h, base, C.size_t(size), C.size_t(stride), C.int(len(shards)),
+			mp, C.int(len(missing)), donly, C.CFSEC_MEM_HOST, nil))
+		if err == nil {
+			// the rebuilt shards get their length, as KRS/reedsolomon.go:1514-1518 and :1539-1543 do
+			present := len(shards) - len(missing)
+			dataPresent := 0
+			for i := 0; i < e.dataShards; i++ {
+				if len(shards[i]) != 0 {
+					dataPresent++
+				}
+			}
+			if present < len(shards) && !(dataOnly && dataPresent == e.dataShards) {
+				for _, i := range missing {
+					if !dataOnly || int(i) < e.dataShards {
+						shards[i] = shards[i][:size]
+					}
+				}
+			}
+		}
+		return err
+	}
 	prepareMissing(shards)
-	v := newShardVec(shards)
-	defer v.free()
-	st := C.cfsec_rs_reconstruct(e.h, v.ptr(), C.int(v.n), C.CFSEC_MEM_HOST, nil)
-	v.lens(shards)
-	return toError(st)
+	return toError(callVec(shards, func(v *C.cfsec_shard, n C.int) C.int {
+		if dataOnly {
+			return C.cfsec_rs_reconstruct_data(e.h, v, n, C.CFSEC_MEM_HOST, nil)
+		}
+		return C.cfsec_rs_reconstruct(e.h, v, n, C.CFSEC_MEM_HOST, nil)
+	}))
 }
 
-func (e *Engine) ReconstructData(shards [][]byte) error {
-	prepareMissing(shards)
-	v := newShardVec(shards)
-	defer v.free()
-	st := C.cfsec_rs_reconstruct_data(e.h, v.ptr(), C.int(v.n), C.CFSEC_MEM_HOST, nil)
-	v.lens(shards)
-	return toError(st)
-}
+func (e *Engine) Reconstruct(shards [][]byte) error { return e.reconstruct(shards, false) }
 
+func (e *Engine) ReconstructData(shards [][]byte) error { return e.reconstruct(shards, true) }
+
+// Split is host bookkeeping (KRS/reedsolomon.go:1574-1632) and stays in Go: the shards are views
+// into data (its spare capacity zeroed and used), the tail in AllocAligned padding, each capped at
+// the shard size as the reference's three-index slices are.
 func (e *Engine) Split(data []byte) ([][]byte, error) {
 	total := e.dataShards + e.parityShards
 	if len(data) == 0 {
 		return nil, reedsolomon.ErrShortData
 	}
-	out := make([]C.cfsec_shard, total)
-	var pin runtime.Pinner
-	defer pin.Unpin()
-	base := &data[:cap(data)][0]
-	pin.Pin(base)
-	var need C.size_t
-	st := C.cfsec_rs_split(e.h, (*C.uint8_t)(unsafe.Pointer(base)), C.size_t(len(data)), C.size_t(cap(data)),
-		&out[0], nil, 0, &need)
-	var pad []byte
-	if st == C.CFSEC_ERR_INVALID_ARG && need > 0 {
-		pad = reedsolomon.AllocAligned(1, int(need))[0]
-		pin.Pin(&pad[0])
-		st = C.cfsec_rs_split(e.h, (*C.uint8_t)(unsafe.Pointer(base)), C.size_t(len(data)), C.size_t(cap(data)),
-			&out[0], (*C.uint8_t)(unsafe.Pointer(&pad[0])), need, &need)
+	if total == 1 {
+		return [][]byte{data}, nil
 	}
-	if err := toError(st); err != nil {
-		return nil, err
-	}
-	full := data[:cap(data)]
-	res := make([][]byte, total)
-	for i, s := range out {
-		off := uintptr(unsafe.Pointer(s.data)) - uintptr(unsafe.Pointer(base))
-		if off < uintptr(len(full)) {
-			res[i] = full[off : off+uintptr(s.len) : off+uintptr(s.len)]
+	dataLen := len(data)
+	per := (dataLen + e.dataShards - 1) / e.dataShards
+	need := total * per
+	if cap(data) > len(data) {
+		if cap(data) > need {
+			data = data[:need]
 		} else {
-			off = uintptr(unsafe.Pointer(s.data)) - uintptr(unsafe.Pointer(&pad[0]))
-			res[i] = pad[off : off+uintptr(s.len) : off+uintptr(s.len)]
+			data = data[:cap(data)]
+		}
+		for i := dataLen; i < len(data); i++ {
+			data[i] = 0
 		}
 	}
-	return res, nil
+	var padding [][]byte
+	if len(data) < need {
+		full := len(data) / per
+		padding = reedsolomon.AllocAligned(total-full, per)
+		if dataLen > per*full {
+			rest := data[per*full : dataLen]
+			for i := range padding {
+				if len(rest) == 0 {
+					break
+				}
+				rest = rest[copy(padding[i], rest):]
+			}
+		}
+	}
+	out := make([][]byte, total)
+	i := 0
+	for ; i < total && len(data) >= per; i++ {
+		out[i] = data[:per:per]
+		data = data[per:]
+	}
+	for j := 0; i+j < total; j++ {
+		out[i+j] = padding[0]
+		padding = padding[1:]
+	}
+	return out, nil
 }
 
 // Join is pure host bookkeeping (KRS/reedsolomon.go:1646-1684); it stays in Go so the
@@ -328,17 +406,14 @@ func BlockEncode(payload []byte, blockLen int64) ([]byte, uint32, error) {
 	if len(payload) == 0 {
 		return out, 0, nil
 	}
-	var pin runtime.Pinner
-	pin.Pin(&payload[0])
-	pin.Pin(&out[0])
-	defer pin.Unpin()
-	var crc C.uint32_t
+	crc := make([]C.uint32_t, 1)
+	// Go pointers passed as arguments to memory holding no Go pointers: legal without pinning
 	st := C.cfsec_crc32block_encode((*C.uint8_t)(unsafe.Pointer(&payload[0])), C.int64_t(len(payload)),
-		C.int64_t(blockLen), (*C.uint8_t)(unsafe.Pointer(&out[0])), &crc, C.CFSEC_MEM_HOST, -1, nil)
+		C.int64_t(blockLen), (*C.uint8_t)(unsafe.Pointer(&out[0])), &crc[0], C.CFSEC_MEM_HOST, -1, nil)
 	if st == C.CFSEC_ERR_INVALID_BLOCK {
 		return nil, 0, ErrInvalidBlock
 	}
-	return out, uint32(crc), toError(st)
+	return out, uint32(crc[0]), toError(st)
 }
 
 // BlockDecode returns payload bytes [from, to) of a framed object whose payload is size bytes,
@@ -348,20 +423,16 @@ func BlockDecode(framed []byte, size, from, to, blockLen int64) ([]byte, error) 
 		return nil, errInvalidArg
 	}
 	out := make([]byte, to-from)
-	var pin runtime.Pinner
-	defer pin.Unpin()
 	var src, dst *C.uint8_t
 	if len(framed) > 0 {
-		pin.Pin(&framed[0])
 		src = (*C.uint8_t)(unsafe.Pointer(&framed[0]))
 	}
 	if len(out) > 0 {
-		pin.Pin(&out[0])
 		dst = (*C.uint8_t)(unsafe.Pointer(&out[0]))
 	}
-	var bad C.int64_t
+	bad := make([]C.int64_t, 1)
 	switch st := C.cfsec_crc32block_decode(src, C.int64_t(len(framed)), C.int64_t(size), C.int64_t(blockLen),
-		C.int64_t(from), C.int64_t(to), dst, &bad, C.CFSEC_MEM_HOST, -1, nil); st {
+		C.int64_t(from), C.int64_t(to), dst, &bad[0], C.CFSEC_MEM_HOST, -1, nil); st {
 	case C.CFSEC_ERR_MISMATCHED_CRC:
 		return nil, ErrMismatchedCrc
 	case C.CFSEC_ERR_INVALID_BLOCK:

@@ -87,6 +87,13 @@ func (e *ECEncoder) SetDevices(devices []int) error {
 	return toError(C.cfsec_ec_set_devices(e.h, &d[0], C.int(len(d))))
 }
 
+func intPtr(v []C.int) *C.int {
+	if len(v) == 0 {
+		return nil
+	}
+	return &v[0]
+}
+
 // reserve gives every zero-length shard capacity for the shard size, as ec.fillFullShards and
 // KRS/reedsolomon.go:1514-1518 allocate when cap is short (the C side writes into cap only).
 func reserve(shards [][]byte) {
@@ -108,26 +115,28 @@ func reserve(shards [][]byte) {
 }
 
 func (e *ECEncoder) Encode(shards [][]byte) error {
+	if base, size, stride, ok := stripeOf(shards); ok {
+		return ecError(C.cfsec_ec_encode_contig(e.h, base, C.size_t(size), C.size_t(stride), C.int(len(shards)),
+			C.CFSEC_MEM_HOST, nil))
+	}
 	reserve(shards)
-	v := newShardVec(shards)
-	defer v.free()
-	st := C.cfsec_ec_encode(e.h, v.ptr(), C.int(v.n), C.CFSEC_MEM_HOST, nil)
-	v.lens(shards)
-	return ecError(st)
-}
-
-func badVec(badIdx []int) ([]C.int, *C.int) {
-	if len(badIdx) == 0 {
-		return nil, nil
-	}
-	b := make([]C.int, len(badIdx))
-	for i, v := range badIdx {
-		b[i] = C.int(v)
-	}
-	return b, &b[0]
+	return ecError(callVec(shards, func(v *C.cfsec_shard, n C.int) C.int {
+		return C.cfsec_ec_encode(e.h, v, n, C.CFSEC_MEM_HOST, nil)
+	}))
 }
 
 func (e *ECEncoder) reconstruct(shards [][]byte, badIdx []int, dataOnly bool) error {
+	donly := C.int(0)
+	if dataOnly {
+		donly = 1
+	}
+	b, bp := cints(badIdx)
+	// blobnode and access hand over full-length shards of one ec.Buffer with the broken ones named
+	// in badIdx: one pointer, rebuilt in place
+	if base, size, stride, ok := stripeOf(shards); ok {
+		return ecError(C.cfsec_ec_reconstruct_contig(e.h, base, C.size_t(size), C.size_t(stride), C.int(len(shards)),
+			bp, C.int(len(b)), donly, C.CFSEC_MEM_HOST, nil))
+	}
 	// initBadShards (encoder.go:182-188) happens in C; a bad shard keeps its buffer as capacity
 	for _, i := range badIdx {
 		if i >= 0 && i < len(shards) && len(shards[i]) != 0 {
@@ -135,22 +144,12 @@ func (e *ECEncoder) reconstruct(shards [][]byte, badIdx []int, dataOnly bool) er
 		}
 	}
 	reserve(shards)
-	v := newShardVec(shards)
-	defer v.free()
-	b, bp := badVec(badIdx)
-	var pin runtime.Pinner
-	if bp != nil {
-		pin.Pin(bp)
-	}
-	defer pin.Unpin()
-	var st C.int
-	if dataOnly {
-		st = C.cfsec_ec_reconstruct_data(e.h, v.ptr(), C.int(v.n), bp, C.int(len(b)), C.CFSEC_MEM_HOST, nil)
-	} else {
-		st = C.cfsec_ec_reconstruct(e.h, v.ptr(), C.int(v.n), bp, C.int(len(b)), C.CFSEC_MEM_HOST, nil)
-	}
-	v.lens(shards)
-	return ecError(st)
+	return ecError(callVec(shards, func(v *C.cfsec_shard, n C.int) C.int {
+		if dataOnly {
+			return C.cfsec_ec_reconstruct_data(e.h, v, n, bp, C.int(len(b)), C.CFSEC_MEM_HOST, nil)
+		}
+		return C.cfsec_ec_reconstruct(e.h, v, n, bp, C.int(len(b)), C.CFSEC_MEM_HOST, nil)
+	}))
 }
 
 func (e *ECEncoder) Reconstruct(shards [][]byte, badIdx []int) error {
@@ -162,26 +161,43 @@ func (e *ECEncoder) ReconstructData(shards [][]byte, badIdx []int) error {
 }
 
 func (e *ECEncoder) Verify(shards [][]byte) (bool, error) {
-	v := newShardVec(shards)
-	defer v.free()
-	var ok C.int
-	err := ecError(C.cfsec_ec_verify(e.h, v.ptr(), C.int(v.n), C.CFSEC_MEM_HOST, nil, &ok))
-	return ok != 0, err
+	ok := make([]C.int, 1)
+	if base, size, stride, contig := stripeOf(shards); contig {
+		err := ecError(C.cfsec_ec_verify_contig(e.h, base, C.size_t(size), C.size_t(stride), C.int(len(shards)),
+			C.CFSEC_MEM_HOST, nil, &ok[0]))
+		return ok[0] != 0, err
+	}
+	err := ecError(callVec(shards, func(v *C.cfsec_shard, n C.int) C.int {
+		return C.cfsec_ec_verify(e.h, v, n, C.CFSEC_MEM_HOST, nil, &ok[0])
+	}))
+	return ok[0] != 0, err
 }
 
 // ReconstructBatch runs blobnode's repair step (work_shard_recover.go:751-760) for a whole tasklet:
 // for every bid, Reconstruct(bids[b], badIdx[b]) then, with verify, Verify(bids[b]) -- one call,
 // one fused pass per bid (LRC: one pass too when no local shard is bad, else the global pass then
-// the AZ-local pass).  errs[b] is what that bid's
-// two calls would have reported (ErrVerify for a false Verify); err reports a failure of the call
-// itself.  Zero-size bids are skipped by the caller, as the reference loop does (:730-733).
+// the AZ-local pass).  errs[b] is what that bid's two calls would have reported (ErrVerify for a
+// false Verify); err reports a failure of the call itself.  Zero-size bids are skipped by the
+// caller, as the reference loop does (:730-733).
 func (e *ECEncoder) ReconstructBatch(bids [][][]byte, badIdx [][]int, verify bool) (errs []error, err error) {
+	errs, _, err = e.reconstructBatch(bids, badIdx, verify, false)
+	return errs, err
+}
+
+// ReconstructBatchCRC is ReconstructBatch returning, per bid, crc32.ChecksumIEEE of every shard it
+// rebuilt (0 for the others and for failed bids): the ShardCrc32 blobnode stores with each repaired
+// shard (work_shard_recover.go:335-342), computed on the GPU before the shard leaves HBM.
+func (e *ECEncoder) ReconstructBatchCRC(bids [][][]byte, badIdx [][]int, verify bool) ([]error, [][]uint32, error) {
+	return e.reconstructBatch(bids, badIdx, verify, true)
+}
+
+func (e *ECEncoder) reconstructBatch(bids [][][]byte, badIdx [][]int, verify, wantCRC bool) ([]error, [][]uint32, error) {
 	if len(bids) != len(badIdx) {
-		return nil, errInvalidArg
+		return nil, nil, errInvalidArg
 	}
-	errs = make([]error, len(bids))
+	errs := make([]error, len(bids))
 	if len(bids) == 0 {
-		return errs, nil
+		return errs, nil, nil
 	}
 	n := len(bids[0])
 	flat := make([][]byte, 0, n*len(bids))
@@ -189,7 +205,7 @@ func (e *ECEncoder) ReconstructBatch(bids [][][]byte, badIdx [][]int, verify boo
 	off := make([]C.int, 1, len(bids)+1)
 	for b, shards := range bids {
 		if len(shards) != n {
-			return nil, errInvalidArg
+			return nil, nil, errInvalidArg
 		}
 		for _, i := range badIdx[b] {
 			if i >= 0 && i < n && len(shards[i]) != 0 {
@@ -201,30 +217,171 @@ func (e *ECEncoder) ReconstructBatch(bids [][][]byte, badIdx [][]int, verify boo
 		flat = append(flat, shards...)
 		off = append(off, C.int(len(bad)))
 	}
-	v := newShardVec(flat)
-	defer v.free()
+	bp := intPtr(bad)
 	status := make([]C.int, len(bids))
-	var pin runtime.Pinner
-	defer pin.Unpin()
-	pin.Pin(&status[0])
-	pin.Pin(&off[0])
-	var bp *C.int
-	if len(bad) > 0 {
-		pin.Pin(&bad[0])
-		bp = &bad[0]
+	words := make([]C.uint32_t, len(bids)*n+1)
+	vf := C.int(0)
+	if verify {
+		vf = 1
+	}
+	st := callVec(flat, func(v *C.cfsec_shard, _ C.int) C.int {
+		if wantCRC {
+			return C.cfsec_ec_reconstruct_batch_crc(e.h, v, C.int(n), C.int(len(bids)), bp, &off[0], vf,
+				C.CFSEC_MEM_HOST, &status[0], &words[0])
+		}
+		return C.cfsec_ec_reconstruct_batch(e.h, v, C.int(n), C.int(len(bids)), bp, &off[0], vf,
+			C.CFSEC_MEM_HOST, &status[0])
+	})
+	var crcs [][]uint32
+	if wantCRC {
+		crcs = make([][]uint32, len(bids))
+	}
+	for b := range bids {
+		copy(bids[b], flat[b*n:(b+1)*n])
+		errs[b] = ecError(status[b])
+		if wantCRC {
+			crcs[b] = make([]uint32, n)
+			for i := range crcs[b] {
+				crcs[b][i] = uint32(words[b*n+i])
+			}
+		}
+	}
+	return errs, crcs, toError(st)
+}
+
+// EncodeBatch is access's Put over a batch of blobs (stream_put.go:104-143 encodes them one by one):
+// every stripe Encoded as Encode would (EnableVerify included; the LRC modes as one fused pass) in
+// one call; errs[s] is what Encode(stripes[s]) would have returned.
+func (e *ECEncoder) EncodeBatch(stripes [][][]byte) (errs []error, err error) {
+	errs, _, err = e.encodeBatch(stripes, false)
+	return errs, err
+}
+
+// EncodeBatchCRC is EncodeBatch returning crc32.ChecksumIEEE of every shard of every stripe -- the
+// checksums access takes right after encoding (stream_put.go:249-253) -- from the GPU.
+func (e *ECEncoder) EncodeBatchCRC(stripes [][][]byte) ([]error, [][]uint32, error) {
+	return e.encodeBatch(stripes, true)
+}
+
+func (e *ECEncoder) encodeBatch(stripes [][][]byte, wantCRC bool) ([]error, [][]uint32, error) {
+	errs := make([]error, len(stripes))
+	if len(stripes) == 0 {
+		return errs, nil, nil
+	}
+	n := len(stripes[0])
+	flat := make([][]byte, 0, n*len(stripes))
+	for _, shards := range stripes {
+		if len(shards) != n {
+			return nil, nil, errInvalidArg
+		}
+		reserve(shards)
+		flat = append(flat, shards...)
+	}
+	status := make([]C.int, len(stripes))
+	words := make([]C.uint32_t, len(stripes)*n+1)
+	st := callVec(flat, func(v *C.cfsec_shard, _ C.int) C.int {
+		if wantCRC {
+			return C.cfsec_ec_encode_batch_crc(e.h, v, C.int(n), C.int(len(stripes)), C.CFSEC_MEM_HOST, &status[0],
+				&words[0])
+		}
+		return C.cfsec_ec_encode_batch(e.h, v, C.int(n), C.int(len(stripes)), C.CFSEC_MEM_HOST, &status[0])
+	})
+	var crcs [][]uint32
+	if wantCRC {
+		crcs = make([][]uint32, len(stripes))
+	}
+	for s := range stripes {
+		copy(stripes[s], flat[s*n:(s+1)*n])
+		errs[s] = ecError(status[s])
+		if wantCRC {
+			crcs[s] = make([]uint32, n)
+			for i := range crcs[s] {
+				crcs[s][i] = uint32(words[s*n+i])
+			}
+		}
+	}
+	return errs, crcs, toError(st)
+}
+
+// EncodeBuffer encodes nstripes stripes that live in one allocation (stripe s at s*stripeStride,
+// its shards at s*stripeStride + i*stride, shardSize bytes each): one Go pointer for the whole batch
+// (cfsec_ec_encode_batch_contig), so it is legal on every Go release with no staging copy.  With
+// wantCRC it also returns every shard's checksum.
+func (e *ECEncoder) EncodeBuffer(buf []byte, shardSize, stride, stripeStride, nstripes int, wantCRC bool) ([]error, [][]uint32, error) {
+	n := e.tactic.N + e.tactic.M + e.tactic.L
+	if nstripes <= 0 || shardSize <= 0 || stride < shardSize || len(buf) < (nstripes-1)*stripeStride+(n-1)*stride+shardSize {
+		return nil, nil, errInvalidArg
+	}
+	status := make([]C.int, nstripes)
+	words := make([]C.uint32_t, nstripes*n)
+	var wp *C.uint32_t
+	if wantCRC {
+		wp = &words[0]
+	}
+	st := C.cfsec_ec_encode_batch_contig(e.h, (*C.uint8_t)(unsafe.Pointer(&buf[0])), C.size_t(shardSize), C.size_t(stride),
+		C.size_t(stripeStride), C.int(n), C.int(nstripes), C.CFSEC_MEM_HOST, &status[0], wp)
+	errs := make([]error, nstripes)
+	var crcs [][]uint32
+	for s := range errs {
+		errs[s] = ecError(status[s])
+		if wantCRC {
+			c := make([]uint32, n)
+			for i := range c {
+				c[i] = uint32(words[s*n+i])
+			}
+			crcs = append(crcs, c)
+		}
+	}
+	return errs, crcs, toError(st)
+}
+
+// RepairBuffer is ReconstructBatch[CRC] for a tasklet whose bids live in one allocation: bid b at
+// bidOff[b], its n shards packed at its own shard size bidSize[b] (cfsec_ec_reconstruct_batch_contig).
+func (e *ECEncoder) RepairBuffer(buf []byte, bidOff, bidSize []uint64, badIdx [][]int, verify, wantCRC bool) ([]error, [][]uint32, error) {
+	n := e.tactic.N + e.tactic.M + e.tactic.L
+	nb := len(bidOff)
+	if nb == 0 || len(bidSize) != nb || len(badIdx) != nb || len(buf) == 0 {
+		return nil, nil, errInvalidArg
+	}
+	for b := range bidOff {
+		if bidOff[b]+uint64(n)*bidSize[b] > uint64(len(buf)) {
+			return nil, nil, errInvalidArg
+		}
+	}
+	var bad []C.int
+	off := []C.int{0}
+	for _, bb := range badIdx {
+		for _, i := range bb {
+			bad = append(bad, C.int(i))
+		}
+		off = append(off, C.int(len(bad)))
+	}
+	status := make([]C.int, nb)
+	words := make([]C.uint32_t, nb*n)
+	var wp *C.uint32_t
+	if wantCRC {
+		wp = &words[0]
 	}
 	vf := C.int(0)
 	if verify {
 		vf = 1
 	}
-	st := C.cfsec_ec_reconstruct_batch(e.h, v.ptr(), C.int(n), C.int(len(bids)), bp, &off[0], vf,
-		C.CFSEC_MEM_HOST, &status[0])
-	v.lens(flat)
-	for b := range bids {
-		copy(bids[b], flat[b*n:(b+1)*n])
+	st := C.cfsec_ec_reconstruct_batch_contig(e.h, (*C.uint8_t)(unsafe.Pointer(&buf[0])),
+		(*C.uint64_t)(unsafe.Pointer(&bidOff[0])), (*C.uint64_t)(unsafe.Pointer(&bidSize[0])), C.int(n), C.int(nb),
+		intPtr(bad), &off[0], vf, C.CFSEC_MEM_HOST, &status[0], wp)
+	errs := make([]error, nb)
+	var crcs [][]uint32
+	for b := range errs {
 		errs[b] = ecError(status[b])
+		if wantCRC {
+			c := make([]uint32, n)
+			for i := range c {
+				c[i] = uint32(words[b*n+i])
+			}
+			crcs = append(crcs, c)
+		}
 	}
-	return errs, toError(st)
+	return errs, crcs, toError(st)
 }
 
 // RepairRows returns the first N present global shards a Reconstruct decodes from with badIdx lost
@@ -233,7 +390,7 @@ func (e *ECEncoder) ReconstructBatch(bids [][][]byte, badIdx [][]int, verify boo
 // live elsewhere, e.g. on other GPUs.
 func (e *ECEncoder) RepairRows(badIdx, want []int) (in []int, rows [][]byte, err error) {
 	n := e.tactic.N
-	_, pbad := badVec(badIdx) // the pointer passed to C keeps the slice alive for the call
+	_, pbad := cints(badIdx) // the pointer passed to C keeps the slice alive for the call
 	w := make([]C.int, len(want)+1)
 	for i, v := range want {
 		w[i] = C.int(v)

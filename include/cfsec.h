@@ -271,6 +271,37 @@ int cfsec_ec_matvec_batch(cfsec_ec* h, const uint8_t* coef, int rows, uint8_t* c
  * shard indices of AZ idx into out (capacity out_cap) and their count into *count. */
 int cfsec_ec_shards_in_idc(const cfsec_ec* h, int idx, int* out, int out_cap, int* count);
 
+/* ---------------- contiguous stripes (ec.Buffer's layout) ----------------
+ * ec.Buffer carves a stripe's N+M+L shards at one stride from one allocation (common/ec/buf.go:
+ * 83-84) and encoder.Split hands out exactly those slices (KRS/reedsolomon.go:1574-1632).  These
+ * entry points take such a stripe as (base, shard_size, stride): shard i is shard_size bytes at
+ * base + i * stride (stride >= shard_size), every shard present -- the broken ones are named by
+ * bad_idx (ec) or missing (reedsolomon: what a len-0 shard marks in the vector forms) and rebuilt in
+ * place.  One pointer per call: a Go caller passes Go memory under cgo's pointer rules as they stand
+ * since Go 1.6 (no runtime.Pinner, no C array holding Go pointers), which is what CubeFS's Go 1.17
+ * toolchain (go.mod:3, docker/Dockerfile:1) can build.  Semantics otherwise those of the vector
+ * calls. */
+int cfsec_rs_encode_contig(cfsec_rs* h, uint8_t* base, size_t shard_size, size_t stride, int n, int mem,
+                           void* stream);
+int cfsec_rs_verify_contig(cfsec_rs* h, uint8_t* base, size_t shard_size, size_t stride, int n, int mem,
+                           void* stream, int* ok);
+int cfsec_rs_reconstruct_contig(cfsec_rs* h, uint8_t* base, size_t shard_size, size_t stride, int n,
+                                const int* missing, int nmissing, int data_only, int mem, void* stream);
+int cfsec_ec_encode_contig(cfsec_ec* h, uint8_t* base, size_t shard_size, size_t stride, int n, int mem,
+                           void* stream);
+int cfsec_ec_verify_contig(cfsec_ec* h, uint8_t* base, size_t shard_size, size_t stride, int n, int mem,
+                           void* stream, int* ok);
+int cfsec_ec_reconstruct_contig(cfsec_ec* h, uint8_t* base, size_t shard_size, size_t stride, int n,
+                                const int* bad_idx, int nbad, int data_only, int mem, void* stream);
+/* Batches in one allocation: stripe s at base + s * stripe_stride (encode); bid b at
+ * base + bid_off[b] with its shards packed at its own shard size bid_shard_size[b] (repair tasklet;
+ * a zero-size bid is all empty shards).  crcs (host, may be NULL): the _crc forms' checksums. */
+int cfsec_ec_encode_batch_contig(cfsec_ec* h, uint8_t* base, size_t shard_size, size_t stride, size_t stripe_stride,
+                                 int n, int nstripes, int mem, int* status, uint32_t* crcs);
+int cfsec_ec_reconstruct_batch_contig(cfsec_ec* h, uint8_t* base, const uint64_t* bid_off,
+                                      const uint64_t* bid_shard_size, int n, int nbids, const int* bad_idx,
+                                      const int* bad_off, int verify, int mem, int* status, uint32_t* crcs);
+
 /* ---------------- pinned host memory ---------------- */
 /* Page-locked host memory for shard buffers (the hook is resourcepool.NewMemPoolWith,
  * common/resourcepool/mempool.go:60, which ec.Buffer draws from, common/ec/buf.go:93-117).

@@ -171,6 +171,74 @@ int main(int argc, char** argv) {
   for (int b = 0; b < 3; ++b) rec("batch_after", bb[b], T * bs[b]);
   rec("batch_status", bst, sizeof bst);
 
+  /* ---- contiguous stripes (ec.Buffer layout): the Go 1.17 cgo path, one pointer per call ---- */
+  {
+    /* EC6P10L2 stripe of 4097-byte shards at stride 4100 inside one pageable allocation */
+    const size_t CS = 4097, CST = 4100;
+    uint8_t* cb = calloc((size_t)LT, CST);
+    for (int i = 0; i < t.n; ++i)
+      for (size_t j = 0; j < CS; ++j) cb[i * CST + j] = sm_byte();
+    CHECK(cfsec_ec_encode_contig(lrc, cb, CS, CST, LT, CFSEC_MEM_HOST, NULL));
+    rec("ct_enc", cb, (size_t)LT * CST);
+    CHECK(cfsec_ec_verify_contig(lrc, cb, CS, CST, LT, CFSEC_MEM_HOST, NULL, &ok));
+    rec_int("ct_ok", ok);
+    const int cbad[3] = {1, 7, LT - 1}; /* a data, a global and a local parity shard */
+    for (int e = 0; e < 3; ++e) memset(cb + cbad[e] * CST, 0xA5, CS);
+    CHECK(cfsec_ec_reconstruct_contig(lrc, cb, CS, CST, LT, cbad, 3, 0, CFSEC_MEM_HOST, NULL));
+    rec("ct_rec", cb, (size_t)LT * CST);
+    /* reedsolomon seam: EC12P4 on pinned memory, shards packed, {2, 14} missing */
+    uint8_t* rp = NULL;
+    CHECK(cfsec_host_alloc(T * 5000, (void**)&rp));
+    for (size_t i = 0; i < K * 5000; ++i) rp[i] = sm_byte();
+    CHECK(cfsec_rs_encode_contig(rs, rp, 5000, 5000, T, CFSEC_MEM_HOST, NULL));
+    rec("ct_rs_enc", rp, T * 5000);
+    const int miss[2] = {2, 14};
+    memset(rp + 2 * 5000, 0, 5000);
+    memset(rp + 14 * 5000, 0, 5000);
+    CHECK(cfsec_rs_reconstruct_contig(rs, rp, 5000, 5000, T, miss, 2, 0, CFSEC_MEM_HOST, NULL));
+    rec("ct_rs_rec", rp, T * 5000);
+    CHECK(cfsec_host_free(rp));
+    /* encode batch of 3 stripes in one allocation, with checksums */
+    const size_t BS = 3000, BST = 3 * (size_t)LT * BS;
+    uint8_t* eb = calloc(3, (size_t)LT * BS);
+    (void)BST;
+    for (int s = 0; s < 3; ++s)
+      for (size_t j = 0; j < (size_t)t.n * BS; ++j) eb[(size_t)s * LT * BS + j] = sm_byte();
+    int est[3] = {-1, -1, -1};
+    uint32_t ecrc[3 * 64];
+    CHECK(cfsec_ec_encode_batch_contig(lrc, eb, BS, BS, (size_t)LT * BS, LT, 3, CFSEC_MEM_HOST, est, ecrc));
+    rec("ct_batch", eb, 3 * (size_t)LT * BS);
+    rec("ct_batch_st", est, sizeof est);
+    rec("ct_batch_crc", ecrc, sizeof(uint32_t) * 3 * LT);
+    /* repair tasklet of 2 bids at offsets in one allocation, sizes 3000 and 1500 */
+    const uint64_t boff[2] = {0, (uint64_t)LT * 3000 + 64};
+    const uint64_t bsz[2] = {3000, 1500};
+    uint8_t* rb = calloc(1, boff[1] + (size_t)LT * 1500);
+    memcpy(rb, eb, (size_t)LT * 3000);
+    int one = 0;
+    uint8_t* s1 = rb + boff[1];
+    for (size_t j = 0; j < (size_t)t.n * 1500; ++j) s1[j] = sm_byte();
+    CHECK(cfsec_ec_encode_contig(lrc, s1, 1500, 1500, LT, CFSEC_MEM_HOST, NULL));
+    (void)one;
+    rec("ct_tasklet_good", rb, boff[1] + (size_t)LT * 1500);
+    const int tb[] = {0, 16, 5, 17};
+    const int to[] = {0, 2, 4};
+    memset(rb + 0 * 3000, 0, 3000);
+    memset(rb + 16 * 3000, 0, 3000);
+    memset(s1 + 5 * 1500, 0, 1500);
+    memset(s1 + 17 * 1500, 0, 1500);
+    int tst[2] = {-1, -1};
+    uint32_t tcrc[2 * 64];
+    CHECK(cfsec_ec_reconstruct_batch_contig(lrc, rb, boff, bsz, LT, 2, tb, to, 1, CFSEC_MEM_HOST, tst, tcrc));
+    rec("ct_tasklet", rb, boff[1] + (size_t)LT * 1500);
+    rec("ct_tasklet_st", tst, sizeof tst);
+    rec("ct_tasklet_crc", tcrc, sizeof(uint32_t) * 2 * LT);
+    rec_int("ct_err_overlap", cfsec_ec_encode_contig(lrc, cb, CS, CS - 1, LT, CFSEC_MEM_HOST, NULL));
+    free(cb);
+    free(eb);
+    free(rb);
+  }
+
   /* ---- crc32block framing (blobnode datafile) ---- */
   const int64_t PL = 200000;
   const int64_t FL = cfsec_crc32block_encode_size(PL, 65536);

@@ -129,3 +129,52 @@ def test_crc32block(run):
     assert as_int(run["blk_mismatch"][0]) == _lib.ErrMismatchedCrc.status
     assert as_int(run["blk_badblock"][0]) == 1
     assert as_int(run["blk_short"][0]) == _lib.ErrShortData.status
+
+
+def test_contiguous_stripes(run):
+    """cfsec_*_contig (ec.Buffer's one-allocation layout, the Go 1.17 cgo path): encode, verify,
+    reconstruct of data/global/local shards, the reedsolomon seam with missing shards, the encode
+    batch and the repair tasklet with checksums -- against the ec oracle and zlib."""
+    from chubaofs_amd import codemode as cm
+    from oracle.ec_oracle import ECOracle, Slice
+    t = cm.GetTactic(cm.EC6P10L2)
+    LT = t.N + t.M + t.L
+    CS, CST = 4097, 4100
+    enc = run["ct_enc"][0].reshape(LT, CST)
+    want = [Slice.of(enc[i, :CS]) for i in range(t.N)] + [Slice(np.zeros(CS, np.uint8)) for _ in range(t.M + t.L)]
+    orc = ECOracle.from_tactic(t, enable_verify=True)
+    assert orc.encode(want) == 0
+    for i in range(LT):
+        assert np.array_equal(enc[i, :CS], want[i].view()), i
+        assert not enc[i, CS:].any(), i  # the gaps between shards are not touched
+    assert as_int(run["ct_ok"][0]) == 1
+    rec = run["ct_rec"][0].reshape(LT, CST)
+    for i in range(LT):
+        assert np.array_equal(rec[i, :CS], want[i].view()), i
+    rs_enc = split(run["ct_rs_enc"][0], 16)
+    ref = [x.copy() for x in rs_enc[:12]] + [np.zeros(5000, np.uint8) for _ in range(4)]
+    assert O.encode(12, 4, ref) == 0
+    assert all(np.array_equal(a, b) for a, b in zip(rs_enc, ref))
+    assert all(np.array_equal(a, b) for a, b in zip(split(run["ct_rs_rec"][0], 16), ref))
+    # encode batch with checksums
+    batch = run["ct_batch"][0].reshape(3, LT, 3000)
+    crc = np.frombuffer(run["ct_batch_crc"][0].tobytes(), np.uint32).reshape(3, LT)
+    assert list(np.frombuffer(run["ct_batch_st"][0].tobytes(), np.int32)) == [0, 0, 0]
+    for s in range(3):
+        w = [Slice.of(batch[s, i]) for i in range(t.N)] + [Slice(np.zeros(3000, np.uint8)) for _ in range(t.M + t.L)]
+        assert orc.encode(w) == 0
+        for i in range(LT):
+            assert np.array_equal(batch[s, i], w[i].view()), (s, i)
+            assert int(crc[s, i]) == zlib.crc32(w[i].view().tobytes()) & 0xFFFFFFFF, (s, i)
+    # repair tasklet: bid 0 (3000 B, bad {0, 16}) and bid 1 (1500 B, bad {5, 17})
+    good = run["ct_tasklet_good"][0]
+    after = run["ct_tasklet"][0]
+    assert np.array_equal(after, good)
+    off1 = LT * 3000 + 64
+    crc = np.frombuffer(run["ct_tasklet_crc"][0].tobytes(), np.uint32).reshape(2, LT)
+    assert list(np.frombuffer(run["ct_tasklet_st"][0].tobytes(), np.int32)) == [0, 0]
+    for b, (o, S, bad) in enumerate([(0, 3000, [0, 16]), (off1, 1500, [5, 17])]):
+        for i in range(LT):
+            shard = good[o + i * S:o + (i + 1) * S]
+            assert int(crc[b, i]) == ((zlib.crc32(shard.tobytes()) & 0xFFFFFFFF) if i in bad else 0), (b, i)
+    assert as_int(run["ct_err_overlap"][0]) == _lib.ErrInvalidArg.status
