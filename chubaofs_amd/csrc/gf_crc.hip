@@ -130,6 +130,11 @@ uint32_t crc_mulmod(uint32_t a, uint32_t b) { return mulmod(a, b); }
 
 namespace {
 
+uint32_t env_u32(const char* name, uint32_t dflt) {
+  const char* v = std::getenv(name);
+  return v && *v ? (uint32_t)std::strtoul(v, nullptr, 10) : dflt;
+}
+
 // As gf_kernels.hip's affine_stride, for the whole job.
 int64_t affine_stride(const MatVecJob& job) {
   if (job.nstripes < 2) return 0;
@@ -143,6 +148,28 @@ int64_t affine_stride(const MatVecJob& job) {
       if (addr(job.out[(size_t)s * job.m + r]) != addr(job.out[r]) + s * ss) return 0;
   }
   return ss;
+}
+
+template <bool CIN>
+int lds_per_cu(int k, int m) {
+  static std::mutex mu;
+  static std::map<std::pair<int, int>, int> cache;  // (device, k * 8 + m)
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  std::lock_guard<std::mutex> l(mu);
+  const auto key = std::make_pair(dev, k * 8 + m);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  int n = 0;
+  switch (k) {
+    case 6: n = crcdev::lds_blocks_per_cu<6, CIN>(m); break;
+    case 8: n = crcdev::lds_blocks_per_cu<8, CIN>(m); break;
+    case 12: n = crcdev::lds_blocks_per_cu<12, CIN>(m); break;
+    case 16: n = crcdev::lds_blocks_per_cu<16, CIN>(m); break;
+    default: n = 0;
+  }
+  cache.emplace(key, n);
+  return n;
 }
 
 template <bool CIN>
@@ -188,12 +215,39 @@ hipError_t launch_matvec_crc(const MatVecJob& job, uint32_t* crc, int crc_stride
   const int64_t sstride = affine_stride(job);
   const int per = sstride ? job.nstripes : crcdev::kPtrSlots / (k + m);
   const int stripes_per_launch = std::min(per, 65535);
-  // ~1024 workgroups per launch: each folds ~11 tiles per row before its per-thread basis
-  // epilogue (16 rows x 32 columns); 512 / 2048 / 4096 were 3-7 % slower (profiles/r01/crc_wgs_sweep.txt)
+  for (int r = 0; r < m; ++r)
+    for (int c = 0; c < k; ++c) a.coef[r * k + c] = job.coef[(size_t)r * k + c];
+  // matrices of dyadic blocks the v_perm kernel has a reduced-product form for: 4 outputs of 4x4
+  // blocks (EC12P4 / EC16P4 encode, coset-aligned repairs), 6 x 6 of 2x2 blocks (EC6P6 encode)
+  const DyPlan dp = (m == 4 && k % 4 == 0) || (m == 6 && k == 6) ? dyadic_plan(a.coef, m, k) : DyPlan{0, 0};
+#ifndef CFSEC_CRC_DY2
+#define CFSEC_CRC_DY2 1  // A/B switch for the 2x2 form
+#endif
+  int dy = dp.E == 0 && ((dp.B == 4 && m == 4) || (CFSEC_CRC_DY2 && dp.B == 2 && m == 6 && k == 6)) ? dp.B : 0;
+  // m <= 4, k <= 16: the lookup-product kernel (gf_crc_lds_kernel; CFSEC_CRC_LDS=0 keeps the v_perm
+  // kernels for A/B): EC12P4 8 x 64 MiB encode + 16 checksums 225-230 -> 200 us
+  // (profiles/r03/crc_lds_ab*.txt)
+  static const uint32_t kLds = env_u32("CFSEC_CRC_LDS", 1);
+  if (kLds && m <= 4 && k <= 16) dy = -1;
+  // Workgroups per launch.  The v_perm kernels: ~1024, each folding ~11 tiles per row before its
+  // per-thread basis epilogue (16 rows x 32 columns); 512 / 2048 / 4096 were 3-7 % slower
+  // (profiles/r01/crc_wgs_sweep.txt).  The lookup kernel: exactly the resident count (its 48-64 KiB
+  // LDS table allows 2-3 per CU), so no second partial wave of workgroups: 768 vs 1024 for k = 12
+  // is 200 vs 220 us.  CFSEC_CRC_GROUPS overrides (probes).
 #ifndef CFSEC_CRC_GROUPS
 #define CFSEC_CRC_GROUPS 1024
 #endif
-  const uint32_t want = std::max<uint32_t>(1, CFSEC_CRC_GROUPS / (uint32_t)std::min(job.nstripes, stripes_per_launch));
+  static const uint32_t kGroupsEnv = env_u32("CFSEC_CRC_GROUPS", 0);
+  uint32_t total = CFSEC_CRC_GROUPS;
+  if (dy == -1) {
+    const int per_cu = cin ? lds_per_cu<true>(k, m) : lds_per_cu<false>(k, m);
+    int dev = 0, cus = 0;
+    if (per_cu > 0 && hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
+      total = (uint32_t)(per_cu * cus * crcdev::kLdsV);
+  }
+  if (kGroupsEnv) total = kGroupsEnv;
+  const uint32_t want = std::max<uint32_t>(1, total / (uint32_t)std::min(job.nstripes, stripes_per_launch));
   uint32_t groups = std::min<uint32_t>({tiles, want, (uint32_t)crcdev::kMaxGroups});
   const uint32_t tpw = (tiles + groups - 1) / groups;
   groups = (tiles + tpw - 1) / tpw;
@@ -207,15 +261,6 @@ hipError_t launch_matvec_crc(const MatVecJob& job, uint32_t* crc, int crc_stride
   a.fin = crc32_shift_ones(job.len);
   a.crc_stride = (uint32_t)crc_stride;
   for (int i = 0; i < k + m; ++i) a.slot[i] = (uint8_t)std::max(slot[i], 0);
-  for (int r = 0; r < m; ++r)
-    for (int c = 0; c < k; ++c) a.coef[r * k + c] = job.coef[(size_t)r * k + c];
-  // matrices of dyadic blocks the fused kernel has a reduced-product form for: 4 outputs of 4x4
-  // blocks (EC12P4 / EC16P4 encode, coset-aligned repairs), 6 x 6 of 2x2 blocks (EC6P6 encode)
-  const DyPlan dp = (m == 4 && k % 4 == 0) || (m == 6 && k == 6) ? dyadic_plan(a.coef, m, k) : DyPlan{0, 0};
-#ifndef CFSEC_CRC_DY2
-#define CFSEC_CRC_DY2 1  // A/B switch for the 2x2 form
-#endif
-  const int dy = dp.E == 0 && ((dp.B == 4 && m == 4) || (CFSEC_CRC_DY2 && dp.B == 2 && m == 6 && k == 6)) ? dp.B : 0;
   for (uint32_t g = 0; g < groups; ++g) {
     const int64_t end = (int64_t)std::min<uint64_t>((uint64_t)(g + 1) * tpw, tiles) * crcdev::kTile;
     a.gconst[g] = xpow(8 * ((int64_t)job.len - end));
@@ -229,7 +274,8 @@ hipError_t launch_matvec_crc(const MatVecJob& job, uint32_t* crc, int crc_stride
       for (int c = 0; c < k; ++c) a.ptr[s * k + c] = job.in[(size_t)(s0 + s) * k + c];
       for (int r = 0; r < m; ++r) a.ptr[tab * k + s * m + r] = job.out[(size_t)(s0 + s) * m + r];
     }
-    const dim3 grid(groups, (unsigned)ns);
+    // the lookup kernel runs kLdsV virtual groups per workgroup (a trailing one past the tiles idles)
+    const dim3 grid(dy == -1 ? (groups + crcdev::kLdsV - 1) / crcdev::kLdsV : groups, (unsigned)ns);
     e = cin ? launch_crc<true>(k, m, a, grid, stream, dy) : launch_crc<false>(k, m, a, grid, stream, dy);
     if (e != hipSuccess) return e;
   }

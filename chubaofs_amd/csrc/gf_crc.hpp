@@ -372,6 +372,43 @@ __device__ __forceinline__ void crc_tile_dy(uint64_t len, const u32x4* tab01, co
   for (int r = 0; r < M; ++r) R[RO + r] = fused_step(ct, R[RO + r], acc[r]);
 }
 
+// The end of a fused kernel: every Horner register R[i] (row i of the checksummed rows, inputs first
+// when CIN) moves from this thread's last piece end to its workgroup's tile end, the workgroup
+// XOR-reduces, one multiply by the host constant moves the sum to the shard end, and the word is
+// XOR-ed into the row's checksum.
+template <int K, int NR, bool CIN>
+__device__ __forceinline__ void crc_epilogue(const GfCrcArgs& a, const uint32_t (&R)[NR], uint32_t (&red)[4][NR],
+                                             uint32_t g, uint32_t stripe, uint32_t tid, bool live = true) {
+  const u32x4* basis = reinterpret_cast<const u32x4*>(a.tabs + kTabWords + tid * 32);
+  uint32_t col[32];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const u32x4 v = basis[q];
+    col[4 * q] = v.x;
+    col[4 * q + 1] = v.y;
+    col[4 * q + 2] = v.z;
+    col[4 * q + 3] = v.w;
+  }
+  const int wave = (int)(tid >> 6), lane = (int)(tid & 63);
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int b = 0; b < 32; ++b) o ^= (0u - ((R[i] >> b) & 1u)) & col[b];
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) o ^= (uint32_t)__shfl_xor((int)o, d);
+    if (lane == 0) red[wave][i] = o;
+  }
+  __syncthreads();
+  if (live && (int)tid < NR) {
+    const int i = (int)tid;
+    uint32_t v = red[0][i] ^ red[1][i] ^ red[2][i] ^ red[3][i];
+    v = mulmod(a.gconst[g], v);
+    if (g == 0) v ^= a.fin;
+    atomicXor(a.crc + (size_t)stripe * a.crc_stride + a.slot[CIN ? i : K + i], v);
+  }
+}
+
 // DY: a.coef is M x K made of DY x DY dyadic blocks (checked by the launcher; 0: plain product); the
 // register allocation aims at 4 waves per SIMD, 3 for the dyadic products
 template <int K, int M, bool CIN, int DY>
@@ -411,42 +448,348 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DY ? 3 : 4,
     else crc_tile<K, M, CIN>(a.len, tab01, tab2, ct, row, off, pre, next, x, R);
     pre = next && (uint64_t)off + dev::kLaneBytes <= a.len;
   }
+  crc_epilogue<K, NR, CIN>(a, R, red, g, stripe, threadIdx.x);
+}
 
-  // move every register from this thread's last piece end to the tile end t1*4096
-  const u32x4* basis = reinterpret_cast<const u32x4*>(a.tabs + kTabWords + threadIdx.x * 32);
-  uint32_t col[32];
+// ---------------------------------------------------------------------------------------------
+// Product and checksum from one set of lookups (m <= 4 outputs).
+//
+// The CRC step needs a table lookup per field of every piece anyway; a ds_read_b64 costs the LDS
+// the same 2 cycles as a ds_read_b32 (bank = dword mod 64 per 32-lane group, MI355X_MICROARCH.md
+// §LDS) and a 16-entry table of 8-byte entries spans the 64 banks once, so nibble lookups are
+// conflict-free and can return two words: E_c[p][h][n] = (f(0, the piece whose byte p is n << 4h),
+// the m products coef[r][c] * (n << 4h) as bytes r of the second word).  Per 16-byte piece of input
+// row c: 32 lookups give the row's CRC step (XOR of the first words) and the 16 bytes' products for
+// every output (XOR-accumulated byte-transposed: g[p] byte r = output r's byte p), so the GF product
+// costs no v_perm_b32 at all -- the fused kernel was VALU-issue-bound on half-rate v_perm /
+// v_bitop3.  Output rows are transposed once per tile (8 v_perm per dword) and
+// checksummed through the first words of E_0 (ds_read_b32 at stride 8 B: 16 even banks, no
+// conflicts).  The Horner jump shift(R, 4096) takes the 5-bit tables of the register word (7 reads).
+// E is 4 KiB per input row (K = 12: 48 KiB; 3 workgroups per CU).
+__device__ __forceinline__ uint32_t gf_mul_dev(uint32_t c, uint32_t v) {
+  uint32_t p = 0;
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const u32x4 v = basis[q];
-    col[4 * q] = v.x;
-    col[4 * q + 1] = v.y;
-    col[4 * q + 2] = v.z;
-    col[4 * q + 3] = v.w;
+  for (int b = 0; b < 8; ++b) {
+    if ((v >> b) & 1u) p ^= c;
+    c = dev::gf_xtime(c);
   }
-  const int wave = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+  return p;
+}
+
+constexpr int kLdsRowBytes = 16 * 2 * 16 * 8;  // E_c: 16 positions x 2 nibbles x 16 values x 8 B
+
+// Lookups of one 16-byte piece d in E (bytes; E_c for an input row, E_0 for an output row).  GF:
+// accumulate the second words into g as well (input rows).
+template <bool GF>
+__device__ __forceinline__ uint32_t piece_lookup(const char* E, const uint32_t (&d)[4], uint32_t (&g)[16]) {
+  uint32_t cr0 = 0u, cr1 = 0u;
 #pragma unroll
-  for (int i = 0; i < NR; ++i) {
-    uint32_t o = 0;
+  for (int w = 0; w < 4; ++w) {
+    // byte j of lo / hi = 8 x (low / high nibble of byte j): the byte offset of the entry
+    uint32_t lo = (d[w] << 3) & 0x78787878u, hi = (d[w] >> 1) & 0x78787878u;
+    asm volatile("" : "+v"(lo), "+v"(hi));
 #pragma unroll
-    for (int b = 0; b < 32; ++b) o ^= (0u - ((R[i] >> b) & 1u)) & col[b];
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) o ^= (uint32_t)__shfl_xor((int)o, d);
-    if (lane == 0) red[wave][i] = o;
+    for (int j = 0; j < 4; ++j) {
+      const int p = 4 * w + j;
+      const uint32_t al = (lo >> (8 * j)) & 0xFFu, ah = (hi >> (8 * j)) & 0xFFu;
+      uint32_t& cr = (w & 1) ? cr1 : cr0;
+      if constexpr (GF) {
+        const dev::u32x2 el = *reinterpret_cast<const dev::u32x2*>(E + p * 256 + al);
+        const dev::u32x2 eh = *reinterpret_cast<const dev::u32x2*>(E + p * 256 + 128 + ah);
+        cr = __builtin_amdgcn_bitop3_b32(cr, el.x, eh.x, 0x96);
+        g[p] = __builtin_amdgcn_bitop3_b32(g[p], el.y, eh.y, 0x96);
+      } else {
+        const uint32_t el = *reinterpret_cast<const uint32_t*>(E + p * 256 + al);
+        const uint32_t eh = *reinterpret_cast<const uint32_t*>(E + p * 256 + 128 + ah);
+        cr = __builtin_amdgcn_bitop3_b32(cr, el, eh, 0x96);
+      }
+    }
   }
-  __syncthreads();
-  if ((int)threadIdx.x < NR) {
-    const int i = (int)threadIdx.x;
-    uint32_t v = red[0][i] ^ red[1][i] ^ red[2][i] ^ red[3][i];
-    v = mulmod(a.gconst[g], v);
-    if (g == 0) v ^= a.fin;
-    atomicXor(a.crc + (size_t)stripe * a.crc_stride + a.slot[CIN ? i : K + i], v);
+  return cr0 ^ cr1;
+}
+
+// shift(r, 4096) from the 5-bit tables of the register word (rt = Q(4, .), 7 x 32 words)
+__device__ __forceinline__ uint32_t rshift4096(const uint32_t* rt, uint32_t r) {
+  uint32_t t[kFiveFields];
+  five_word<0>(rt, r, t);
+  return __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(t[0], t[1], t[2], 0x96),
+                                     __builtin_amdgcn_bitop3_b32(t[3], t[4], t[5], 0x96), t[6], 0x96);
+}
+
+// Output dwords from the byte-transposed accumulators: o[r][w] byte i = byte r of g[4w + i].
+template <int M>
+__device__ __forceinline__ void untranspose(const uint32_t (&g)[16], uint32_t (&o)[M][4]) {
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const uint32_t a = g[4 * w], b = g[4 * w + 1], c = g[4 * w + 2], d = g[4 * w + 3];
+    const uint32_t ab_lo = __builtin_amdgcn_perm(b, a, 0x05010400u);  // a0 b0 a1 b1
+    const uint32_t cd_lo = __builtin_amdgcn_perm(d, c, 0x05010400u);  // c0 d0 c1 d1
+    o[0][w] = __builtin_amdgcn_perm(cd_lo, ab_lo, 0x05040100u);       // a0 b0 c0 d0
+    if constexpr (M > 1) o[1][w] = __builtin_amdgcn_perm(cd_lo, ab_lo, 0x07060302u);
+    if constexpr (M > 2) {
+      const uint32_t ab_hi = __builtin_amdgcn_perm(b, a, 0x07030602u);  // a2 b2 a3 b3
+      const uint32_t cd_hi = __builtin_amdgcn_perm(d, c, 0x07030602u);
+      o[2][w] = __builtin_amdgcn_perm(cd_hi, ab_hi, 0x05040100u);
+      if constexpr (M > 3) o[3][w] = __builtin_amdgcn_perm(cd_hi, ab_hi, 0x07060302u);
+    }
   }
 }
 
+#ifndef CFSEC_LDS_LOOKAHEAD
+#define CFSEC_LDS_LOOKAHEAD 4
+#endif
+// Lookups in flight: the 8 reads of word step s + P are issued before word step s is consumed
+// (a step = one dword of one row's piece), so a wave keeps ~8P reads outstanding instead of
+// draining its LDS queue after every few (lgkmcnt counts to 15).  P = 0: one row at a time.
+#ifndef CFSEC_LDS_PIPE
+#define CFSEC_LDS_PIPE 1
+#endif
+template <int K, int M, bool CIN>
+__device__ __forceinline__ void crc_tile_lds(uint64_t len, const char* E, const uint32_t* rt,
+                                             const uint8_t* const (&row)[K + M], uint32_t off, bool pre, bool next,
+                                             uint32_t (&x)[K][4], uint32_t (&R)[(CIN ? K : 0) + M]) {
+  constexpr int RO = CIN ? K : 0;
+  constexpr int D = CFSEC_LDS_LOOKAHEAD < K ? CFSEC_LDS_LOOKAHEAD : K;
+  constexpr int P = CFSEC_LDS_PIPE;
+  uint32_t g[16];
+#pragma unroll
+  for (int p = 0; p < 16; ++p) g[p] = 0u;
+  // one pipelined pass; the thread holding the shard end (or past it) loads its piece
+  // byte-granular, zero-padded
+  const bool full = (uint64_t)off + dev::kLaneBytes <= len;
+  const uint32_t rem = full ? 16u : (off < len ? (uint32_t)(len - off) : 0u);
+  const auto load = [&](int c, uint32_t o, bool f) {
+    u32x4 v;
+    if (f) v = dev::ld16<true>(row[c] + o);
+    else v = rem ? dev::ld_tail(row[c] + o, rem) : u32x4{0u, 0u, 0u, 0u};
+    x[c][0] = v.x;
+    x[c][1] = v.y;
+    x[c][2] = v.z;
+    x[c][3] = v.w;
+  };
+  const auto load_ahead = [&](int c) {  // the row D after input row c
+    const int j = c + D;
+    if (j < K) load(j, off, full);
+    else if (next) load(j - K, off + kTile, true);
+  };
+  if (!pre)
+#pragma unroll
+    for (int c = 0; c < D; ++c) load(c, off, full);
+  if constexpr (P == 0) {
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+      load_ahead(c);
+      __builtin_amdgcn_sched_barrier(0);
+      const uint32_t cr = piece_lookup<true>(E + c * kLdsRowBytes, x[c], g);
+      if constexpr (CIN) {
+        R[c] = cr ^ rshift4096(rt, R[c]);
+        asm volatile("" : "+v"(R[c]));  // computed here, not sunk to its next use (all the reads would stay live)
+      }
+#pragma unroll
+      for (int p = 0; p < 16; ++p) asm volatile("" : "+v"(g[p]));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
+    // input steps s = 4c + w: 8 ds_read_b64 each (+ the 7 register-shift reads of row c at w = 0)
+    dev::u32x2 L[P + 1][8];
+    uint32_t rs[2][kFiveFields];
+    uint32_t cr0 = 0u, cr1 = 0u;
+    const auto issue = [&](int s) {
+      const int c = s >> 2, w = s & 3;
+      if (w == 0) {
+        load_ahead(c);
+        if constexpr (CIN) five_word<0>(rt, R[c], rs[c & 1]);
+      }
+      uint32_t lo = (x[c][w] << 3) & 0x78787878u, hi = (x[c][w] >> 1) & 0x78787878u;
+      asm volatile("" : "+v"(lo), "+v"(hi));
+      const char* t = E + c * kLdsRowBytes + 4 * w * 256;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        L[s % (P + 1)][2 * j] = *reinterpret_cast<const dev::u32x2*>(t + j * 256 + ((lo >> (8 * j)) & 0xFFu));
+        L[s % (P + 1)][2 * j + 1] = *reinterpret_cast<const dev::u32x2*>(t + j * 256 + 128 + ((hi >> (8 * j)) & 0xFFu));
+      }
+    };
+    const auto consume = [&](int s) {
+      const int c = s >> 2, w = s & 3;
+      const dev::u32x2(&l)[8] = L[s % (P + 1)];
+      uint32_t& cr = (w & 1) ? cr1 : cr0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        cr = __builtin_amdgcn_bitop3_b32(cr, l[2 * j].x, l[2 * j + 1].x, 0x96);
+        g[4 * w + j] = __builtin_amdgcn_bitop3_b32(g[4 * w + j], l[2 * j].y, l[2 * j + 1].y, 0x96);
+      }
+      if (w == 3) {
+        if constexpr (CIN) {
+          const uint32_t(&t)[kFiveFields] = rs[c & 1];
+          R[c] = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(cr0, cr1, t[0], 0x96),
+                                             __builtin_amdgcn_bitop3_b32(t[1], t[2], t[3], 0x96),
+                                             __builtin_amdgcn_bitop3_b32(t[4], t[5], t[6], 0x96), 0x96);
+          asm volatile("" : "+v"(R[c]));
+        }
+        cr0 = cr1 = 0u;
+      }
+#pragma unroll
+      for (int p = 0; p < 4; ++p) asm volatile("" : "+v"(g[4 * w + p]));
+    };
+#pragma unroll
+    for (int s = 0; s < P && s < 4 * K; ++s) issue(s);
+#pragma clang loop unroll(full)
+    for (int s = 0; s < 4 * K; ++s) {
+      if (s + P < 4 * K) issue(s + P);
+      __builtin_amdgcn_sched_barrier(0);
+      consume(s);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  uint32_t o[M][4];
+  untranspose<M>(g, o);
+  if (full) {
+#pragma unroll
+    for (int r = 0; r < M; ++r)
+      dev::st16_out<true>(const_cast<uint8_t*>(row[K + r]) + off, u32x4{o[r][0], o[r][1], o[r][2], o[r][3]});
+  } else if (rem) {
+#pragma unroll
+    for (int r = 0; r < M; ++r)
+      dev::st_tail(const_cast<uint8_t*>(row[K + r]) + off, u32x4{o[r][0], o[r][1], o[r][2], o[r][3]}, rem);
+  }
+  if constexpr (P == 0) {
+#pragma unroll
+    for (int r = 0; r < M; ++r) {
+      R[RO + r] = piece_lookup<false>(E, o[r], g) ^ rshift4096(rt, R[RO + r]);
+      asm volatile("" : "+v"(R[RO + r]));
+    }
+  } else {
+    // output steps s = 4r + w: 8 ds_read_b32 of the first words of E_0
+    uint32_t L[P + 1][8];
+    uint32_t rs[M][kFiveFields];
+#pragma unroll
+    for (int r = 0; r < M; ++r) five_word<0>(rt, R[RO + r], rs[r]);
+    uint32_t cr0 = 0u, cr1 = 0u;
+    const auto issue = [&](int s) {
+      const int r = s >> 2, w = s & 3;
+      uint32_t lo = (o[r][w] << 3) & 0x78787878u, hi = (o[r][w] >> 1) & 0x78787878u;
+      asm volatile("" : "+v"(lo), "+v"(hi));
+      const char* t = E + 4 * w * 256;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        L[s % (P + 1)][2 * j] = *reinterpret_cast<const uint32_t*>(t + j * 256 + ((lo >> (8 * j)) & 0xFFu));
+        L[s % (P + 1)][2 * j + 1] = *reinterpret_cast<const uint32_t*>(t + j * 256 + 128 + ((hi >> (8 * j)) & 0xFFu));
+      }
+    };
+    const auto consume = [&](int s) {
+      const int r = s >> 2, w = s & 3;
+      const uint32_t(&l)[8] = L[s % (P + 1)];
+      uint32_t& cr = (w & 1) ? cr1 : cr0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) cr = __builtin_amdgcn_bitop3_b32(cr, l[2 * j], l[2 * j + 1], 0x96);
+      if (w == 3) {
+        const uint32_t(&t)[kFiveFields] = rs[r];
+        R[RO + r] = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(cr0, cr1, t[0], 0x96),
+                                                __builtin_amdgcn_bitop3_b32(t[1], t[2], t[3], 0x96),
+                                                __builtin_amdgcn_bitop3_b32(t[4], t[5], t[6], 0x96), 0x96);
+        asm volatile("" : "+v"(R[RO + r]));
+        cr0 = cr1 = 0u;
+      }
+    };
+#pragma unroll
+    for (int s = 0; s < P && s < 4 * M; ++s) issue(s);
+#pragma clang loop unroll(full)
+    for (int s = 0; s < 4 * M; ++s) {
+      if (s + P < 4 * M) issue(s + P);
+      __builtin_amdgcn_sched_barrier(0);
+      consume(s);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
+// V: 256-thread virtual groups per workgroup, each an independent run of tiles with its own
+// epilogue; they share one copy of E (the LDS, not the registers, bounds the waves per CU).
+#ifndef CFSEC_LDS_V
+#define CFSEC_LDS_V 1
+#endif
+#ifndef CFSEC_LDS_WPE
+#define CFSEC_LDS_WPE 3
+#endif
+constexpr int kLdsV = CFSEC_LDS_V;
+template <int K, int M, bool CIN>
+__global__ __launch_bounds__(256 * kLdsV) __attribute__((amdgpu_waves_per_eu(CFSEC_LDS_WPE, 8))) void gf_crc_lds_kernel(
+    const GfCrcArgs a) {
+  static_assert(M >= 1 && M <= 4, "the second word of an entry holds at most 4 products");
+  constexpr int NR = (CIN ? K : 0) + M;
+  constexpr int NT = 256 * kLdsV;
+  __shared__ dev::u32x2 E[K * kLdsRowBytes / 8];
+  __shared__ uint32_t rt[kFiveFields * 32];
+  __shared__ uint32_t gfw[K * 32];
+  __shared__ uint32_t red[kLdsV][4][NR];
+  // gfw[c][h][n]: the M products of input row c's coefficients with n << 4h
+  for (int i = threadIdx.x; i < K * 32; i += NT) {
+    const int c = i >> 5;
+    const uint32_t v = (uint32_t)(i & 15) << (4 * ((i >> 4) & 1));
+    uint32_t w = 0;
+#pragma unroll
+    for (int r = 0; r < M; ++r) w |= gf_mul_dev(a.coef[r * K + c], v) << (8 * r);
+    gfw[i] = w;
+  }
+  // Q(4, f): the register word's 5-bit tables
+  for (int i = threadIdx.x; i < kFiveFields * 32; i += NT)
+    rt[i] = a.tabs[kByteTabWords + kNibTabWords + 4 * kFiveFields * 32 + i];
+  __syncthreads();
+  // E_c[q][n] (q = 2p + h) = (N_q[n], gfw[c][h][n]); N_q are the device block's nibble tables
+  // (entry i & 511 of E_c takes N word i & 511: a thread meets at most two of them)
+  const uint32_t* nt = a.tabs + kByteTabWords;
+  const uint32_t nA = nt[threadIdx.x & 511], nB = nt[(threadIdx.x + 256) & 511];
+  for (int i = threadIdx.x; i < K * 512; i += NT) {
+    const int c = i >> 9, q = (i >> 4) & 31, n = i & 15;
+    E[i] = dev::u32x2{(i & 511) == (int)(threadIdx.x & 511) ? nA : nB, gfw[c * 32 + (q & 1) * 16 + n]};
+  }
+  __syncthreads();
+
+  const uint32_t vg = threadIdx.x >> 8, tid = threadIdx.x & 255;
+  const uint32_t g = blockIdx.x * kLdsV + vg, stripe = blockIdx.y;
+  const size_t ts = a.sstride ? 0 : (size_t)stripe;
+  const int64_t sbase = (int64_t)stripe * a.sstride;
+  const uint8_t* row[K + M];
+#pragma unroll
+  for (int c = 0; c < K; ++c) row[c] = a.ptr[ts * K + c] + sbase;
+#pragma unroll
+  for (int r = 0; r < M; ++r) row[K + r] = a.ptr[(size_t)a.tab * K + ts * M + r] + sbase;
+  uint32_t R[NR];
+#pragma unroll
+  for (int i = 0; i < NR; ++i) R[i] = 0u;
+  const uint32_t t0 = g * a.tpw;
+  const uint32_t t1 = min(t0 + a.tpw, a.tiles);
+  const uint32_t lanepos = tid * dev::kLaneBytes;
+  uint32_t x[K][4];
+  bool pre = false;
+  for (uint32_t t = t0; t < t1; ++t) {
+    const uint32_t off = t * kTile + lanepos;
+    const bool next = t + 1 < t1 && (uint64_t)off + kTile + dev::kLaneBytes <= a.len;
+    crc_tile_lds<K, M, CIN>(a.len, reinterpret_cast<const char*>(E), rt, row, off, pre, next, x, R);
+    pre = next && (uint64_t)off + dev::kLaneBytes <= a.len;
+  }
+  crc_epilogue<K, NR, CIN>(a, R, red[vg], g, stripe, tid, t0 < a.tiles);
+}
+
 // Launch gf_crc_kernel<K, m, CIN> (instantiated for m = 1..6 in gf_crc_k<K>.hip); dy: the dyadic
-// block size of the product (4: m = 4, K a multiple of 4; 2: K = m = 6; 0: plain).
+// block size of the product (4: m = 4, K a multiple of 4; 2: K = m = 6; 0: plain); dy = -1: the
+// lookup-product kernel gf_crc_lds_kernel (m <= 4).
 template <int K, bool CIN>
 hipError_t launch_crc_k(int m, const GfCrcArgs& a, dim3 grid, hipStream_t st, int dy) {
+  if (dy == -1) {
+    if constexpr (K > 16) {
+      return hipErrorInvalidValue;  // E would pass 64 KiB
+    } else {
+      switch (m) {
+        case 1: hipLaunchKernelGGL((gf_crc_lds_kernel<K, 1, CIN>), grid, dim3(256 * kLdsV), 0, st, a); break;
+        case 2: hipLaunchKernelGGL((gf_crc_lds_kernel<K, 2, CIN>), grid, dim3(256 * kLdsV), 0, st, a); break;
+        case 3: hipLaunchKernelGGL((gf_crc_lds_kernel<K, 3, CIN>), grid, dim3(256 * kLdsV), 0, st, a); break;
+        case 4: hipLaunchKernelGGL((gf_crc_lds_kernel<K, 4, CIN>), grid, dim3(256 * kLdsV), 0, st, a); break;
+        default: return hipErrorInvalidValue;
+      }
+      return hipGetLastError();
+    }
+  }
   if constexpr (K % 4 == 0) {
     if (dy == 4 && m == 4) {
       hipLaunchKernelGGL((gf_crc_kernel<K, 4, CIN, 4>), grid, dim3(256), 0, st, a);
@@ -483,9 +826,30 @@ uint32_t crc_mulmod(uint32_t a, uint32_t b);  // a * b mod P
 
 namespace crcdev {
 
+// Workgroups of gf_crc_lds_kernel<K, m, CIN> resident per CU (its LDS table bounds them), 0 if none.
+template <int K, bool CIN>
+int lds_blocks_per_cu(int m) {
+  if constexpr (K > 16) {
+    return 0;
+  } else {
+    const void* f = nullptr;
+    switch (m) {
+      case 1: f = reinterpret_cast<const void*>(&gf_crc_lds_kernel<K, 1, CIN>); break;
+      case 2: f = reinterpret_cast<const void*>(&gf_crc_lds_kernel<K, 2, CIN>); break;
+      case 3: f = reinterpret_cast<const void*>(&gf_crc_lds_kernel<K, 3, CIN>); break;
+      case 4: f = reinterpret_cast<const void*>(&gf_crc_lds_kernel<K, 4, CIN>); break;
+      default: return 0;
+    }
+    int n = 0;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, 256 * kLdsV, 0) == hipSuccess ? n : 0;
+  }
+}
+
 #define CFSEC_CRC_EXTERN(K)                                                                         \
   extern template hipError_t launch_crc_k<K, true>(int, const GfCrcArgs&, dim3, hipStream_t, int);  \
-  extern template hipError_t launch_crc_k<K, false>(int, const GfCrcArgs&, dim3, hipStream_t, int);
+  extern template hipError_t launch_crc_k<K, false>(int, const GfCrcArgs&, dim3, hipStream_t, int); \
+  extern template int lds_blocks_per_cu<K, true>(int);                                              \
+  extern template int lds_blocks_per_cu<K, false>(int);
 
 }  // namespace crcdev
 }  // namespace cfsec
@@ -495,5 +859,7 @@ namespace crcdev {
   namespace crcdev {                                                                                 \
   template hipError_t launch_crc_k<K, true>(int, const GfCrcArgs&, dim3, hipStream_t, int);        \
   template hipError_t launch_crc_k<K, false>(int, const GfCrcArgs&, dim3, hipStream_t, int);       \
+  template int lds_blocks_per_cu<K, true>(int);                                                      \
+  template int lds_blocks_per_cu<K, false>(int);                                                     \
   }                                                                                                  \
   }
