@@ -54,7 +54,10 @@ ERASED = [0, 1, 2, 3]
 NBATCH = 3  # batches rotated through the step (no Infinity-Cache reuse between launches)
 HBM_PEAK_GBPS = 8000.0  # MI355X spec (MI355X_MICROARCH.md)
 CPU_SHARE = 16  # host CPUs leased with one GPU on the bench pool
-KERNEL = "gf_dy_kernel<12, 4, 4, (cfsec::MatVecMode)0, 0>"  # both step kernels: 12 -> 4 rows, 4x4-dyadic matrices
+# Both step launches (encode, reconstruct of {0,1,2,3}) are 12 -> 4 row products: the lookup-product
+# kernel (csrc/gf_lut.hpp), or with CFSEC_LUT=0 the 4x4-dyadic v_perm kernel (A/B)
+LUT = os.environ.get("CFSEC_LUT", "1") != "0"
+KERNEL = "gf_lut_kernel<12, 4, 4, (cfsec::MatVecMode)0" if LUT else "gf_dy_kernel<12, 4, 4, (cfsec::MatVecMode)0, 0>"
 
 
 def parse():
@@ -375,7 +378,7 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
-    # both step kernels are gf_dy_kernel<12, 4, 4, kStore> moving the same algorithmic bytes
+    # both step launches are the same 12 -> 4 kernel moving the same algorithmic bytes
     avg_ms = ev0.elapsed_time(ev1) / (2 * args.steps)
 
     # correctness gate: every row the timed launches wrote is the golden codeword again
@@ -430,7 +433,9 @@ def main():
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
             "traffic": None if traffic is None else int(traffic),
-            "kernel": "gf_dy_kernel<12, 4, 4, kStore, 0> (encode and reconstruct launches: both matrices are 4x4-dyadic)",
+            "kernel": ("gf_lut_kernel<12, 4, 4, kStore> (encode and reconstruct launches: lookup-product kernel)" if LUT
+                       else "gf_dy_kernel<12, 4, 4, kStore, 0> (encode and reconstruct launches: both matrices are 4x4-dyadic)"),
+            "kernel_match": KERNEL,
             "algorithmic_bytes_per_launch": launch_bytes,
             "avg_launch_ms": round(avg_ms, 4),
             "launch_timing": ("HIP event pair on the launch stream around the timed region / launches"

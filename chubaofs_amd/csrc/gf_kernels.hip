@@ -27,6 +27,9 @@
 // concurrent callers and hipGraph capture).
 //
 // Kernel families, first match wins:
+//   lookup-product (gf_lut.hpp): the products of each input byte with a whole column from two LDS
+//                table reads, for the shapes lut_outputs() names (EC12P4 / EC12P9 / EC15P12 and
+//                their repairs); CFSEC_LUT=0 disables (A/B)
 //   16x16-dyadic (gf_dyadic16.hpp): EC16P20's 20 parity rows
 //   dyadic-block (gf_dyadic.hpp): 4x4 / 2x2 dyadic matrices (code-mode encodes, coset-aligned
 //                repairs, fused LRC encodes with 2 plain rows)
@@ -38,11 +41,13 @@
 //                tools/gf_variants.hip -- store/accum 256-thread, 1 chunk per lane, one row at a
 //                time; verify 128-thread, 2 chunks per lane, rows loaded in pairs
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
 #include "gf_device.hpp"
 #include "gf_launch.hpp"
+#include "gf_lut_launch.hpp"
 #include "kernels.hpp"
 
 namespace cfsec {
@@ -159,9 +164,14 @@ hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
       const int threads = (!fixed && verify && sh.OS == 1) ? 128 : 256;
       // matrices of 4x4 / 2x2 dyadic blocks (encode of every code mode but the LRC local stripes,
       // coset-aligned reconstructs such as EC12P4's worst case) take the reduced-product kernel
+      static const bool kLut = [] {
+        const char* v = std::getenv("CFSEC_LUT");
+        return !(v && v[0] == '0');
+      }();
+      const bool lut = kLut && fixed && lut_outputs(kc, mc) > 0;
       DyPlan dy{0, 0};
       bool dy16 = false;
-      if (fixed && r0 == 0 && mc == job.m && mode != MatVecMode::kStoreVerify) {
+      if (fixed && !lut && r0 == 0 && mc == job.m && mode != MatVecMode::kStoreVerify) {
         std::vector<uint8_t> sub((size_t)mc * kc);
         for (int r = 0; r < mc; ++r)
           for (int c = 0; c < kc; ++c) sub[(size_t)r * kc + c] = job.coef[(size_t)r * job.k + c];
@@ -213,6 +223,12 @@ hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
         }
         const dim3 grid((unsigned)(ltiles * ns));
         hipError_t e;
+        if (lut) {
+          const dim3 lgrid((unsigned)((llen + 4095) / 4096), (unsigned)ns);  // 4 KiB tiles
+          e = launch_lut(kc, mc, mode, a, lgrid, stream);
+          if (e != hipSuccess) return e;
+          continue;
+        }
         if (fixed && dy16) {
           e = launch_dy16(mc, mode, a, (unsigned)ns, stream);
           if (e != hipSuccess) return e;

@@ -37,7 +37,8 @@ __device__ __forceinline__ uint32_t xtime4(uint32_t v) {
 }
 
 // T_c[h][n] word q (c < K, h < 2, n < 16, q < EW) at word index ((c*2 + h)*16 + n)*EW + q.
-template <int K, int M>
+// (the first M rows of a coefficient matrix with row stride KS)
+template <int K, int M, int KS>
 __device__ __forceinline__ void build_lut(const uint8_t* coef, uint32_t* T, uint32_t* pw) {
   constexpr int EW = entry_words(M), NQ = (M + 3) / 4;
   // pw[(c*NQ + q)*8 + i] = bytes b of coef[4q+b][c] * 2^i (rows past M: 0)
@@ -46,7 +47,7 @@ __device__ __forceinline__ void build_lut(const uint8_t* coef, uint32_t* T, uint
     uint32_t v = 0;
 #pragma unroll
     for (int b = 0; b < 4; ++b)
-      if (4 * q + b < M) v |= (uint32_t)coef[(4 * q + b) * K + c] << (8 * b);
+      if (4 * q + b < M) v |= (uint32_t)coef[(4 * q + b) * KS + c] << (8 * b);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       pw[t * 8 + i] = v;
@@ -111,20 +112,30 @@ __device__ __forceinline__ void untranspose4(const uint32_t (&g)[16], uint32_t (
 #endif
 
 // One 16-byte chunk of every row at byte `off` of the stripe (all in bounds, or the tail chunk with
-// rem < 16 valid bytes).  MODE: kStore (outputs written), kVerify (compared: diff), kStoreVerify
-// (rows < nstore written, the rest compared).
-template <int K, int M, MatVecMode MODE>
-__device__ __forceinline__ void lut_chunk(const char* T, const uint8_t* const* in, uint8_t* const* out, int nstore,
-                                          int64_t sbase, uint32_t off, uint32_t rem, uint32_t& diff) {
-  constexpr int EW = entry_words(M), NQ = (M + 3) / 4, EB = 4 * EW;
-  constexpr int D = CFSEC_LUT_LOOKAHEAD < K ? CFSEC_LUT_LOOKAHEAD : K;
+// rem < 16 valid bytes).  Outputs [0, ML) come from the lookups, [ML, M) from the v_perm product
+// (tab01 / tab2 of gf_device.hpp, slot c * MP + r), which keeps both the LDS pipe and the VALU busy:
+// per input byte the lookups cost the LDS 2 reads of ~3.2 effective cycles (b64, measured:
+// tools/lds_rate.hip) and the VALU ~13 cycles for 8 outputs, the v_perm product ~4.7 VALU cycles
+// per output.  MODE: kStore (outputs written), kVerify (compared: diff), kStoreVerify (rows < nstore
+// written, the rest compared).
+template <int K, int M, int ML, MatVecMode MODE, int LA = CFSEC_LUT_LOOKAHEAD>
+__device__ __forceinline__ void lut_chunk(const char* T, const u32x4* tab01, const uint32_t* tab2,
+                                          const uint8_t* const* in, uint8_t* const* out, int nstore, int64_t sbase,
+                                          uint32_t off, uint32_t rem, uint32_t& diff) {
+  constexpr int EW = entry_words(ML), NQ = (ML + 3) / 4, EB = 4 * EW, MP = M - ML;
+  constexpr int D = LA < K ? LA : K;
   constexpr int SHIFT = EW == 1 ? 2 : (EW == 2 ? 3 : 4);  // log2 of the entry bytes
   const bool full = rem >= 16;
-  uint32_t acc[16][NQ];
+  uint32_t acc[16][NQ > 0 ? NQ : 1];
+  uint32_t accp[MP > 0 ? MP : 1][4];
 #pragma unroll
   for (int p = 0; p < 16; ++p)
 #pragma unroll
     for (int q = 0; q < NQ; ++q) acc[p][q] = 0u;
+#pragma unroll
+  for (int r = 0; r < MP; ++r)
+#pragma unroll
+    for (int w = 0; w < 4; ++w) accp[r][w] = 0u;
   uint32_t x[K][4];
   const auto load = [&](int c) {
     u32x4 v;
@@ -141,35 +152,57 @@ __device__ __forceinline__ void lut_chunk(const char* T, const uint8_t* const* i
   for (int c = 0; c < K; ++c) {
     if (c + D < K) load(c + D);
     __builtin_amdgcn_sched_barrier(0);
-    const char* tc = T + c * 2 * 16 * EB;
+    if constexpr (NQ > 0) {
+      const char* tc = T + c * 2 * 16 * EB;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      // byte j of lo / hi = EB x (low / high nibble of byte j): the entry's byte offset
-      uint32_t lo, hi;
-      if constexpr (SHIFT == 4) {
-        lo = (x[c][w] << 4) & 0xF0F0F0F0u;
-        hi = x[c][w] & 0xF0F0F0F0u;
-      } else {
-        lo = (x[c][w] << SHIFT) & (0x0F0F0F0Fu << SHIFT);
-        hi = (x[c][w] >> (4 - SHIFT)) & (0x0F0F0F0Fu << SHIFT);
+      for (int w = 0; w < 4; ++w) {
+        // byte j of lo / hi = EB x (low / high nibble of byte j): the entry's byte offset
+        uint32_t lo, hi;
+        if constexpr (SHIFT == 4) {
+          lo = (x[c][w] << 4) & 0xF0F0F0F0u;
+          hi = x[c][w] & 0xF0F0F0F0u;
+        } else {
+          lo = (x[c][w] << SHIFT) & (0x0F0F0F0Fu << SHIFT);
+          hi = (x[c][w] >> (4 - SHIFT)) & (0x0F0F0F0Fu << SHIFT);
+        }
+        asm volatile("" : "+v"(lo), "+v"(hi));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const Entry<EW> el = ld_entry<EW>(tc, (lo >> (8 * j)) & 0xFFu);
+          const Entry<EW> eh = ld_entry<EW>(tc + 16 * EB, (hi >> (8 * j)) & 0xFFu);
+#pragma unroll
+          for (int q = 0; q < NQ; ++q)
+            acc[4 * w + j][q] = __builtin_amdgcn_bitop3_b32(acc[4 * w + j][q], el.w[q], eh.w[q], 0x96);
+        }
       }
-      asm volatile("" : "+v"(lo), "+v"(hi));
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const Entry<EW> el = ld_entry<EW>(tc, (lo >> (8 * j)) & 0xFFu);
-        const Entry<EW> eh = ld_entry<EW>(tc + 16 * EB, (hi >> (8 * j)) & 0xFFu);
+      for (int p = 0; p < 16; ++p)
 #pragma unroll
-        for (int q = 0; q < NQ; ++q)
-          acc[4 * w + j][q] = __builtin_amdgcn_bitop3_b32(acc[4 * w + j][q], el.w[q], eh.w[q], 0x96);
-      }
+        for (int q = 0; q < NQ; ++q) asm volatile("" : "+v"(acc[p][q]));
     }
+    if constexpr (MP > 0) {
+      dev::mac_row_k<MP>(accp, x[c], tab01 + c * MP, tab2 + c * MP);
 #pragma unroll
-    for (int p = 0; p < 16; ++p)
+      for (int r = 0; r < MP; ++r)
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) asm volatile("" : "+v"(acc[p][q]));
+        for (int w = 0; w < 4; ++w) asm volatile("" : "+v"(accp[r][w]));
+    }
     __builtin_amdgcn_sched_barrier(0);
   }
   constexpr bool kVer = MODE == MatVecMode::kVerify, kMix = MODE == MatVecMode::kStoreVerify;
+  const auto finish = [&](int r, const uint32_t (&o)[4]) {
+    uint8_t* p = out[r] + sbase + off;
+    const bool cmp = kVer || (kMix && r >= nstore);
+    const u32x4 v{o[0], o[1], o[2], o[3]};
+    if (cmp) {
+      const u32x4 d = v ^ (full ? dev::ld16<true>(p) : dev::ld_tail(p, rem));
+      diff |= d.x | d.y | d.z | d.w;
+    } else if (full) {
+      dev::st16_out<true>(p, v);
+    } else {
+      dev::st_tail(p, v, rem);
+    }
+  };
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
     uint32_t g[16];
@@ -178,32 +211,29 @@ __device__ __forceinline__ void lut_chunk(const char* T, const uint8_t* const* i
     uint32_t o[4][4];
     untranspose4(g, o);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = 4 * q + i;
-      if (r >= M) break;
-      uint8_t* p = out[r] + sbase + off;
-      const bool cmp = kVer || (kMix && r >= nstore);
-      const u32x4 v{o[i][0], o[i][1], o[i][2], o[i][3]};
-      if (cmp) {
-        const u32x4 d = v ^ (full ? dev::ld16<true>(p) : dev::ld_tail(p, rem));
-        diff |= d.x | d.y | d.z | d.w;
-      } else if (full) {
-        dev::st16_out<true>(p, v);
-      } else {
-        dev::st_tail(p, v, rem);
-      }
-    }
+    for (int i = 0; i < 4; ++i)
+      if (4 * q + i < ML) finish(4 * q + i, o[i]);
   }
+#pragma unroll
+  for (int r = 0; r < MP; ++r) finish(ML + r, accp[r]);
 }
 
 // Grid (tiles, stripes), 256 threads, one 4 KiB tile of every row per workgroup (GfArgs as the
 // fixed-K kernel: a.k == K, a.m == M, a.len < 4 GiB).
-template <int K, int M, MatVecMode MODE>
+template <int K, int M, int ML, MatVecMode MODE, int LA = CFSEC_LUT_LOOKAHEAD>
 __global__ __launch_bounds__(256) void gf_lut_kernel(const dev::GfArgs a) {
-  constexpr int EW = entry_words(M), NQ = (M + 3) / 4;
-  __shared__ __attribute__((aligned(16))) uint32_t T[K * 2 * 16 * EW];
-  __shared__ uint32_t pw[K * NQ * 8];
-  build_lut<K, M>(a.coef, T, pw);
+  constexpr int EW = entry_words(ML), NQ = (ML + 3) / 4, MP = M - ML;
+  __shared__ __attribute__((aligned(16))) uint32_t T[NQ > 0 ? K * 2 * 16 * EW : 4];
+  __shared__ uint32_t pw[NQ > 0 ? K * NQ * 8 : 1];
+  __shared__ u32x4 tab01[MP > 0 ? K * MP : 1];
+  __shared__ uint32_t tab2[MP > 0 ? K * MP : 1];
+  if constexpr (MP > 0) {
+    for (int i = threadIdx.x; i < K * MP; i += 256) {
+      const int c = i / MP, r = i - (i / MP) * MP;
+      dev::coef_tables(a.coef[(ML + r) * K + c], tab01[i], tab2[i]);
+    }
+  }
+  if constexpr (NQ > 0) build_lut<K, ML, K>(a.coef, T, pw);
   __syncthreads();
   const uint32_t stripe = blockIdx.y, tile = blockIdx.x;
   const size_t ts = a.sstride ? 0 : (size_t)stripe;
@@ -215,7 +245,8 @@ __global__ __launch_bounds__(256) void gf_lut_kernel(const dev::GfArgs a) {
   uint32_t diff = 0;
   if ((uint64_t)off < len) {
     const uint32_t rem = (uint64_t)off + 16 <= len ? 16u : (uint32_t)(len - off);
-    lut_chunk<K, M, MODE>(reinterpret_cast<const char*>(T), in, out, (int)a.nstore, sbase, off, rem, diff);
+    lut_chunk<K, M, ML, MODE, LA>(reinterpret_cast<const char*>(T), tab01, tab2, in, out, (int)a.nstore, sbase, off, rem,
+                              diff);
   }
   if constexpr (MODE == MatVecMode::kVerify || MODE == MatVecMode::kStoreVerify) {
     if (diff) atomicOr(a.flags + stripe, 1u);

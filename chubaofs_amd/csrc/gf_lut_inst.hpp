@@ -1,0 +1,28 @@
+// gf_lut_inst.hpp -- the launcher body of launch_lut_k<K> (included by gf_lut_k<K>.hip).
+#pragma once
+#include "gf_lut.hpp"
+#include "gf_lut_launch.hpp"
+
+namespace cfsec {
+namespace lutinst {
+
+template <int K, int M>
+hipError_t go(MatVecMode mode, const dev::GfArgs& a, dim3 grid, hipStream_t st) {
+  constexpr int ML = M <= 8 ? M : (M == 9 ? 8 : M);
+  switch (mode) {
+    case MatVecMode::kStore:
+      hipLaunchKernelGGL((lut::gf_lut_kernel<K, M, ML, MatVecMode::kStore>), grid, dim3(256), 0, st, a);
+      break;
+    case MatVecMode::kVerify:
+      hipLaunchKernelGGL((lut::gf_lut_kernel<K, M, ML, MatVecMode::kVerify>), grid, dim3(256), 0, st, a);
+      break;
+    case MatVecMode::kStoreVerify:
+      hipLaunchKernelGGL((lut::gf_lut_kernel<K, M, ML, MatVecMode::kStoreVerify>), grid, dim3(256), 0, st, a);
+      break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace lutinst
+}  // namespace cfsec

@@ -1,0 +1,39 @@
+// gf_lut_launch.hpp -- the lookup-product kernels (gf_lut.hpp) behind launch_matvec: which (k, m)
+// take them, and their launchers (instantiated per k in gf_lut_k<K>.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "gf_device.hpp"
+#include "kernels.hpp"
+
+namespace cfsec {
+
+// Outputs the lookups carry for a k x m product (the rest take the v_perm product in the same
+// kernel), or 0 when the shape keeps the v_perm / dyadic kernels.  Measured against them on the
+// same stripes (tools/lut_probe.hip, profiles/r03/lut_probe*.txt): EC15P12 encode 116 -> 94 us,
+// verify 118 -> 89; EC12P9 encode 73 -> 63 (8 lookups + 1 v_perm row).  EC12P4 stays on its 4x4-
+// dyadic kernel: faster in the probe (135 vs 141 us) but slower in the bench's rotated batches
+// (0.659 vs 0.685 of 8 TB/s, profiles/r03/bench_lut_ab.txt); EC16P20(L2) and EC6P10(L2) stay on
+// their dyadic kernels, and so do the narrow shapes of other k.
+inline int lut_outputs(int k, int m) {
+  if (k == 12 && m >= 5 && m <= 9) return m <= 8 ? m : 8;
+  if (k == 15 && m >= 5 && m <= 12) return m == 9 ? 8 : m;
+  return 0;
+}
+
+template <int K>
+hipError_t launch_lut_k(int m, MatVecMode mode, const dev::GfArgs& a, dim3 grid, hipStream_t st);
+template <>
+hipError_t launch_lut_k<12>(int, MatVecMode, const dev::GfArgs&, dim3, hipStream_t);
+template <>
+hipError_t launch_lut_k<15>(int, MatVecMode, const dev::GfArgs&, dim3, hipStream_t);
+
+inline hipError_t launch_lut(int k, int m, MatVecMode mode, const dev::GfArgs& a, dim3 grid, hipStream_t st) {
+  switch (k) {
+    case 12: return launch_lut_k<12>(m, mode, a, grid, st);
+    case 15: return launch_lut_k<15>(m, mode, a, grid, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace cfsec

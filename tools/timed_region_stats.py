@@ -22,7 +22,7 @@ def main():
     line = [l for l in open(bench_out) if l.startswith("{")][-1]
     b = json.loads(line)
     first, last = b["roofline"]["timed_dispatches"]
-    want = "gf_dy_kernel<12, 4, 4, (cfsec::MatVecMode)0, 0>".replace(" ", "")
+    want = b["roofline"].get("kernel_match", "gf_dy_kernel<12, 4, 4, (cfsec::MatVecMode)0, 0>").replace(" ", "")
     rows = []
     for f in glob.glob(os.path.join(tdir, "**", "*kernel_trace.csv"), recursive=True):
         with open(f) as fh:
