@@ -54,10 +54,9 @@ ERASED = [0, 1, 2, 3]
 NBATCH = 3  # batches rotated through the step (no Infinity-Cache reuse between launches)
 HBM_PEAK_GBPS = 8000.0  # MI355X spec (MI355X_MICROARCH.md)
 CPU_SHARE = 16  # host CPUs leased with one GPU on the bench pool
-# Both step launches (encode, reconstruct of {0,1,2,3}) are 12 -> 4 row products: the lookup-product
-# kernel (csrc/gf_lut.hpp), or with CFSEC_LUT=0 the 4x4-dyadic v_perm kernel (A/B)
-LUT = os.environ.get("CFSEC_LUT", "1") != "0"
-KERNEL = "gf_lut_kernel<12, 4, 4, (cfsec::MatVecMode)0" if LUT else "gf_dy_kernel<12, 4, 4, (cfsec::MatVecMode)0, 0>"
+# Both step launches (encode, reconstruct of {0,1,2,3}) are 12 -> 4 row products on the 4x4-dyadic
+# kernel (the lookup-product kernel is 4 % behind on this shape: profiles/r03/bench_lut_ab.txt)
+KERNEL = "gf_dy_kernel<12, 4, 4, (cfsec::MatVecMode)0, 0>"
 
 
 def parse():
@@ -433,8 +432,7 @@ def main():
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
             "traffic": None if traffic is None else int(traffic),
-            "kernel": ("gf_lut_kernel<12, 4, 4, kStore> (encode and reconstruct launches: lookup-product kernel)" if LUT
-                       else "gf_dy_kernel<12, 4, 4, kStore, 0> (encode and reconstruct launches: both matrices are 4x4-dyadic)"),
+            "kernel": "gf_dy_kernel<12, 4, 4, kStore, 0> (encode and reconstruct launches: both matrices are 4x4-dyadic)",
             "kernel_match": KERNEL,
             "algorithmic_bytes_per_launch": launch_bytes,
             "avg_launch_ms": round(avg_ms, 4),
@@ -675,6 +673,8 @@ def other_configs(args, torch, dev, stream, cpu):
     golden bytes afterwards, so a kernel that writes nothing fails).  C4 / C5 report both the
     synchronous batch calls a caller makes (planning, launches, sync) and the asynchronous calls
     (cfsec_ec_*_batch_async) on one stream, with their kernel-only time from per-call HIP events."""
+    import zlib
+
     import numpy as np
 
     from chubaofs_amd import _lib, codemode as cm, ec, reedsolomon
@@ -894,11 +894,30 @@ def other_configs(args, torch, dev, stream, cpu):
         _lib.check(e5._L.cfsec_ec_reconstruct_batch_async(e5._h, bm.arr, tot5, nb5, bad5, off5, 1, st5,
                                                           fl5.data_ptr(), None, stream.cuda_stream))
 
+    # the same tasklet returning the rebuilt shards' checksums (blobnode's ShardCrc32 of each repaired
+    # shard, work_shard_recover.go:335-342): device words [bid][shard], written on the stream
+    cw5 = torch.zeros((NBATCH, nb5 * tot5), dtype=torch.int32, device=dev)
+
+    def rep5c(i):
+        bm = bm5[i % NBATCH]
+        _lib.check(e5._L.cfsec_ec_reconstruct_batch_async(e5._h, bm.arr, tot5, nb5, bad5, off5, 1, st5,
+                                                          fl5.data_ptr(), ctypes.c_void_p(cw5[i % NBATCH].data_ptr()),
+                                                          stream.cuda_stream))
+
     zero5 = lambda: b5[:, :, er5, :].zero_()
     rs = gated_calls(torch, stream, rep5, NBATCH, secs, zero5, check5, sync_call=True)
     assert list(st5) == [0] * nb5
     ra = gated_calls(torch, stream, rep5a, NBATCH, secs, zero5, check5, sync_call=False)
     assert list(st5) == [0] * nb5 and not bool(fl5.any().item()), "C5: Verify failed"
+    rc = gated_calls(torch, stream, rep5c, NBATCH, secs, zero5, check5, sync_call=False)
+    assert list(st5) == [0] * nb5 and not bool(fl5.any().item()), "C5: Verify failed (crc run)"
+    # the words against zlib on the golden rebuilt rows (every bid of batch 0), 0 for the others
+    w5 = cw5[0].cpu().numpy().view(np.uint32).reshape(nb5, tot5)
+    g5h = gold5[0].cpu().numpy()
+    for bid in range(nb5):
+        for i in range(tot5):
+            want = zlib.crc32(g5h[bid, i].tobytes()) & 0xFFFFFFFF if i in er5 else 0
+            assert int(w5[bid, i]) == want, f"C5 checksum of bid {bid} shard {i}"
     # per bid, one pass: reads 16 inputs + the 16 other global parities and the 2 local parities
     # it checks, writes 2 data + 2 parity rows (the local Verify rides in the global pass: the
     # separate AZ-local pass would re-read 2 x 19 shards)
@@ -911,6 +930,11 @@ def other_configs(args, torch, dev, stream, cpu):
           "async_data_GBps": round(N5 * S5 * nb5 * ra["calls_per_s"] / 1e9, 1),
           "kernel_ms": round(ra["kernel_ms_per_call"], 4),
           "kernel_roofline_frac": frac(alg5 * nb5, ra["kernel_ms_per_call"]),
+          "with_crc_kernel_ms": round(rc["kernel_ms_per_call"], 4),
+          "with_crc_over_kernel": round(rc["kernel_ms_per_call"] / ra["kernel_ms_per_call"], 3),
+          "with_crc_note": ("cfsec_ec_reconstruct_batch_async with the rebuilt shards' checksums (256 words per "
+                            "call, checked against zlib on the golden rows): device time per call, and its ratio "
+                            "to the call without checksums"),
           "algorithmic_bytes_per_bid": alg5,
           "timing": ("data_GBps / roofline_frac: synchronous cfsec_ec_reconstruct_batch calls (planning + launches + "
                      "sync); async_*: cfsec_ec_reconstruct_batch_async back to back on one stream; kernel_*: per-call "
@@ -956,7 +980,7 @@ def other_configs(args, torch, dev, stream, cpu):
                               "saturated": {"value": round(N5 * S5 * sat5 / 1e9, 3), "unit": "GB/s", "cores": callers,
                                             "sample": f"{callers} single-threaded callers, one bid each"}}
     out["C5_EC16P20L2_repair_tasklet"] = c5
-    del bm5, b5, gold5
+    del bm5, b5, gold5, cw5
     return out
 
 

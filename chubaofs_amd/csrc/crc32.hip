@@ -10,6 +10,7 @@
 // reduction and one multiply by x^(8(S - e)) to the shard end, then atomicXor into the shard's
 // word.  `fin` (crc32_shift_ones(S), or 0 for the raw word) is folded in by workgroup 0.
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "gf_crc.hpp"
@@ -23,7 +24,11 @@ using crcdev::kMaxGroups;
 using crcdev::kTabWords;
 using crcdev::kTile;
 using dev::u32x4;
-constexpr int kSlots = 160;
+// Argument block: the fixed fields, then a flexible area of words holding the group constants
+// gconst[0 .. ng) (x^(8(len - e_g)) mod P, the same for every shard) followed by the shard pointers
+// and their output words: a launch carries as many shards as fit beside its ng constants (256 shards
+// at ng = 16: a repair tasklet's rebuilt rows in one launch).
+constexpr int kFlexWords = 800;
 
 struct __attribute__((aligned(16))) CrcArgs {
   uint64_t len;
@@ -31,12 +36,16 @@ struct __attribute__((aligned(16))) CrcArgs {
   uint32_t tiles, tpw;
   uint32_t* out;
   const uint32_t* tabs;
-  uint32_t fin, pad;
-  const uint8_t* ptr[kSlots];
-  uint32_t idx[kSlots];          // output word of shard i
-  uint32_t gconst[kMaxGroups];   // x^(8(len - e_g)) mod P
+  uint32_t fin, ng;              // ng: workgroups per shard (group constants in flex[0 .. ng))
+  uint32_t pw, iw;               // word offsets of the pointer (8-byte) and index arrays in flex
+  uint32_t pad[2];
+  uint32_t flex[kFlexWords];
 };
 static_assert(sizeof(CrcArgs) <= 3584, "kernel argument block must stay below 4 KiB");
+
+__device__ __forceinline__ const uint8_t* shard_ptr(const CrcArgs& a, uint32_t i) {
+  return reinterpret_cast<const uint8_t* const*>(a.flex + a.pw)[i];
+}
 
 __device__ __forceinline__ void piece(const uint8_t* p, uint64_t len, uint32_t off, uint32_t (&d)[4]) {
   if ((uint64_t)off + dev::kLaneBytes <= len) {
@@ -49,22 +58,31 @@ __device__ __forceinline__ void piece(const uint8_t* p, uint64_t len, uint32_t o
   }
 }
 
+// The loads of CFSEC_CRC_AHEAD tiles are issued before any of them is folded (each thread's pieces
+// are independent loads; only the fold is a chain), so short runs -- a repair tasklet's 256 rebuilt
+// shards of 64 tiles, 8 per workgroup -- keep 8 loads per thread in flight instead of one.
+#ifndef CFSEC_CRC_AHEAD
+#define CFSEC_CRC_AHEAD 8
+#endif
 __global__ __launch_bounds__(256) void crc32_horner_kernel(const CrcArgs a) {
+  constexpr int A = CFSEC_CRC_AHEAD;
   __shared__ uint32_t ct[crcdev::kOnlyTabWords];
   __shared__ uint32_t red[4];
   for (int i = threadIdx.x; i < crcdev::kOnlyTabWords; i += 256) ct[i] = a.tabs[crcdev::kOnlyTabBase + i];
   __syncthreads();
   const uint32_t g = blockIdx.x, sh = blockIdx.y;
-  const uint8_t* p = a.sstride ? a.ptr[0] + (int64_t)sh * a.sstride : a.ptr[sh];
+  const uint8_t* p = a.sstride ? shard_ptr(a, 0) + (int64_t)sh * a.sstride : shard_ptr(a, sh);
   const uint32_t t0 = g * a.tpw, t1 = min(t0 + a.tpw, a.tiles);
   const uint32_t lanepos = threadIdx.x * dev::kLaneBytes;
-  uint32_t R = 0, cur[4], nxt[4];
-  piece(p, a.len, t0 * kTile + lanepos, cur);
-  for (uint32_t t = t0; t < t1; ++t) {
-    if (t + 1 < t1) piece(p, a.len, (t + 1) * kTile + lanepos, nxt);
-    R = crcdev::only_step(ct, R, cur);
+  uint32_t R = 0;
+  for (uint32_t t = t0; t < t1; t += A) {
+    uint32_t buf[A][4];
 #pragma unroll
-    for (int w = 0; w < 4; ++w) cur[w] = nxt[w];
+    for (int k = 0; k < A; ++k)
+      if (t + k < t1) piece(p, a.len, (t + k) * kTile + lanepos, buf[k]);
+#pragma unroll
+    for (int k = 0; k < A; ++k)
+      if (t + k < t1) R = crcdev::only_step(ct, R, buf[k]);
   }
   const u32x4* basis = reinterpret_cast<const u32x4*>(a.tabs + kTabWords + threadIdx.x * 32);
   uint32_t o = 0;
@@ -81,10 +99,17 @@ __global__ __launch_bounds__(256) void crc32_horner_kernel(const CrcArgs a) {
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = o;
   __syncthreads();
   if (threadIdx.x == 0) {
-    uint32_t v = crcdev::mulmod(a.gconst[g], red[0] ^ red[1] ^ red[2] ^ red[3]);
+    uint32_t v = crcdev::mulmod(a.flex[g], red[0] ^ red[1] ^ red[2] ^ red[3]);
     if (g == 0) v ^= a.fin;
-    atomicXor(a.out + (a.sstride ? a.idx[0] + sh : a.idx[sh]), v);
+    const uint32_t* idx = a.flex + a.iw;
+    atomicXor(a.out + (a.sstride ? idx[0] + sh : idx[sh]), v);
   }
+}
+
+// CFSEC_CRC32_GROUPS_PROBE: re-read on every launch (A/B of the workgroup count in one process)
+uint32_t probe_groups() {
+  const char* v = std::getenv("CFSEC_CRC32_GROUPS_PROBE");
+  return v && *v ? (uint32_t)std::strtoul(v, nullptr, 10) : 0u;
 }
 
 }  // namespace
@@ -103,27 +128,40 @@ hipError_t launch_crc32_to(const uint8_t* const* ptrs, size_t len, int n, uint32
   for (int i = 1; i < n && stride; ++i)
     if (at(i) - at(0) != stride * i || (idx && idx[i] != idx[0] + (uint32_t)i)) stride = 0;
   if (n > 65535) stride = 0;
-  const int per_launch = stride ? n : kSlots;
-  // ~2048 workgroups in all, each keeping >= 1 tile
-  const uint32_t want = std::max<uint32_t>(1, 2048u / (uint32_t)n);
+  // ~4096 workgroups in all, but each folding >= 16 tiles: its fixed cost (the 32-word alignment
+  // basis of every thread, 32 KiB from L2, and the step table) must not outweigh its tiles.  Round 3,
+  // event-timed (tools/crc_pass_probe.hip, profiles/r03/crc_pass.txt): a tasklet's 256 rebuilt rows
+  // of 64 tiles 21 us at 4 workgroups per row vs 34 us at 16; 128 rows of 1366 tiles 126 us at 32
+  // per row (5.67 TB/s) vs 132-134 at 8-16.  Then as many shards per launch as fit beside the group
+  // constants.
+  const uint32_t total = probe_groups() ? probe_groups() : 4096u;
+  const uint32_t want = std::max<uint32_t>(1, std::min<uint32_t>(total / (uint32_t)n, tiles / 16));
   uint32_t groups = std::min<uint32_t>({tiles, want, (uint32_t)kMaxGroups});
   const uint32_t tpw = (tiles + groups - 1) / groups;
   groups = (tiles + tpw - 1) / tpw;
+  const uint32_t pw = (groups + 1) & ~1u;                       // pointers 8-byte aligned
+  const int slots = (int)((kFlexWords - pw) / 3);              // 2 words of pointer + 1 of index
+  const int per_launch = stride ? n : std::min(n, slots);
   a.len = len;
   a.sstride = stride;
   a.tiles = tiles;
   a.tpw = tpw;
   a.out = out;
   a.fin = fin;
+  a.ng = groups;
+  a.pw = pw;
+  a.iw = pw + 2 * (uint32_t)(stride ? 1 : per_launch);
   for (uint32_t g = 0; g < groups; ++g) {
     const int64_t end = (int64_t)std::min<uint64_t>((uint64_t)(g + 1) * tpw, tiles) * kTile;
-    a.gconst[g] = crc_xpow(8 * ((int64_t)len - end));
+    a.flex[g] = crc_xpow(8 * ((int64_t)len - end));
   }
   for (int s0 = 0; s0 < n; s0 += per_launch) {
     const int ns = std::min(per_launch, n - s0);
-    for (int s = 0; s < std::min(ns, kSlots); ++s) {
-      a.ptr[s] = ptrs[s0 + s];
-      a.idx[s] = idx ? idx[s0 + s] : (uint32_t)(s0 + s);
+    const uint8_t** pp = reinterpret_cast<const uint8_t**>(a.flex + a.pw);
+    uint32_t* ip = a.flex + a.iw;
+    for (int s = 0; s < (stride ? 1 : ns); ++s) {
+      pp[s] = ptrs[s0 + s];
+      ip[s] = idx ? idx[s0 + s] : (uint32_t)(s0 + s);
     }
     hipLaunchKernelGGL(crc32_horner_kernel, dim3(groups, (unsigned)ns), dim3(256), 0, stream, a);
     e = hipGetLastError();

@@ -17,8 +17,9 @@ from oracle import oracle as O
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
-# fused: (12,4) (6,6) (8,1) (18,1) (16,4); fallback: (6,10) (10,4) (16,20)
-SHAPES = [(12, 4), (6, 6), (8, 1), (18, 1), (16, 4), (6, 10), (10, 4), (16, 20)]
+# (12, 4) (8, 1) (16, 4) (6, 3) (8, 2) (16, 3) (12, 1): the lookup-product fused kernel (m <= 4, k <= 16);
+# (6, 6) (18, 1): the v_perm fused kernels; (6, 10) (10, 4) (16, 20): product + standalone CRC
+SHAPES = [(12, 4), (6, 6), (8, 1), (18, 1), (16, 4), (6, 10), (10, 4), (16, 20), (6, 3), (8, 2), (16, 3), (12, 1)]
 SIZES = [1, 15, 16, 17, 4095, 4096, 4097, 8191, 65539, 174763]
 
 
