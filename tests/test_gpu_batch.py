@@ -22,7 +22,8 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 MOCK_SIZES = [1024, 2048, 0, 512, 23, 65, 12]  # worker_for_test.go:79-83
-RS_MODES = [(6, 6), (12, 4), (15, 12), (16, 20), (10, 4), (3, 3), (40, 4)]  # k = 40: compared rows over > 32 inputs
+RS_MODES = [(6, 6), (12, 4), (15, 12), (12, 9), (16, 20), (10, 4), (3, 3), (40, 4)]  # k = 40: compared rows over > 32 inputs;
+# (15, 12), (12, 9): the lookup-product kernels (gf_lut.hpp)
 
 
 def gen_mock_bytes(letter, size):
