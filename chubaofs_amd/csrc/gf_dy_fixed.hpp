@@ -6,8 +6,12 @@
 
 namespace cfsec {
 
+#ifndef CFSEC_DY_WPE
+#define CFSEC_DY_WPE 1  // amdgpu_waves_per_eu floor (1: the compiler's choice)
+#endif
 template <int K, int M, int B, MatVecMode MODE, int E>
-__global__ __launch_bounds__((dev::DyShape<M - E, B>::kThreadsPerWg)) void gf_dy_kernel(const dev::GfArgs a) {
+__global__ __launch_bounds__((dev::DyShape<M - E, B>::kThreadsPerWg))
+__attribute__((amdgpu_waves_per_eu(CFSEC_DY_WPE, 8))) void gf_dy_kernel(const dev::GfArgs a) {
   dev::matvec_dy<K, M, B, MODE, true, true, 64, E>(a);
 }
 
