@@ -385,6 +385,42 @@ def main():
         assert torch.equal(batch[b, :, :, :S], golden[b]), f"batch {b} differs from the golden codeword after the timed steps"
     gate = {"zeroed_before_timed": {str(b): op for b, op in sorted(first.items())}, "rows_equal_golden": True}
 
+    # Strong scaling: the same nst-stripe total split over the ranks -- each codes the
+    # first ceil(nst / world) stripes of its batches -- timed like the headline (barrier + sync on both
+    # sides, max over ranks).  At N = 1 it is the headline's work; the driver's curve is the weak one.
+    per_rank = max(1, -(-nst // world))
+    strong_steps = max(NBATCH, args.steps // NBATCH * NBATCH)
+
+    def strong_step(i):
+        enc.encode_batch(ptrs[i % NBATCH], S, per_rank, stream=stream)
+        enc.reconstruct_batch(ptrs[(i + 2) % NBATCH], S, per_rank, ERASED, stream=stream)
+
+    with torch.cuda.stream(stream):
+        for i in range(NBATCH):
+            strong_step(i)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    ts0 = time.perf_counter()
+    with torch.cuda.stream(stream):
+        for i in range(strong_steps):
+            strong_step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    st_el = time.perf_counter() - ts0
+    if world > 1:
+        t = torch.tensor([st_el], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        st_el = float(t.item())
+    for b in range(NBATCH):
+        assert torch.equal(batch[b, :, :, :S], golden[b]), f"batch {b} differs from the golden codeword (strong run)"
+    strong = {"total_stripes": per_rank * world, "stripes_per_gpu": per_rank, "steps": strong_steps,
+              "value": round(2 * K_DATA * S * per_rank * world * strong_steps / st_el / 1e9, 2), "unit": "GB/s",
+              "ms_per_step": round(st_el / strong_steps * 1e3, 4),
+              "note": ("fixed total work (BASELINE configs[2] strong scaling): the 8-stripe batch split over the "
+                       "GPUs, same step as the headline; rows checked against the golden codeword afterwards")}
+
     data_bytes = K_DATA * S * nst
     launch_bytes = (K_DATA + M_PARITY) * S * nst  # algorithmic bytes per launch (read 12S + write 4S)
     achieved = launch_bytes / (avg_ms * 1e-3) / 1e9
@@ -446,6 +482,7 @@ def main():
                            "between two launches over the same batch, so the 256 MB Infinity Cache serves no reuse"),
         },
         "gate": gate,
+        "strong_scaling": strong,
         "cpu_baseline": cpu,
     }
     out.update(extra)
