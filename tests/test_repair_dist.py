@@ -187,3 +187,61 @@ def test_repair_gpu_lrc(mode, erased, strategy, nccl_world1):
     for b in range(nb):
         for q, e in enumerate(sorted(erased)):
             assert np.array_equal(got[b, q], full[b][e]), (b, e)
+
+
+def _gpu_worker(rank, world, port, strategy, mode):
+    """One rank of a world-N repair on the box's one GPU (gloo transport: RCCL refuses two ranks on
+    one device): this rank holds the shards repair.owned() assigns it, the exchange moves the
+    survivors' bytes between ranks, the decode runs on the GPU, and every rebuilt row this rank owns
+    must equal the shard the encoder produced."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        if mode == "EC16P20":
+            from chubaofs_amd import reedsolomon
+            k, total, erased = 16, 36, [0, 1, 16, 17]
+            enc = reedsolomon.New(k, total - k, device=0)
+        else:
+            from chubaofs_amd import codemode as cm, ec
+            t = cm.GetTactic(getattr(cm, mode))
+            enc = ec.NewEncoder(ec.Config(CodeMode=t, EnableVerify=False), device=0)
+            k, total = t.N, t.N + t.M + t.L
+            erased = [0, t.N + 1, t.N + t.M + 1]  # data, global parity, local parity
+        nb, S_ = 3, 65536 + 13
+        g = torch.Generator(device="cuda")
+        g.manual_seed(777)  # every rank builds the same stripes, keeps the rows it owns
+        full = torch.zeros((nb, total, S_), dtype=torch.uint8, device="cuda")
+        full[:, :k] = torch.randint(0, 256, (nb, k, S_), generator=g, device="cuda", dtype=torch.uint8)
+        if mode == "EC16P20":
+            enc.encode_batch([full[b, i].data_ptr() for b in range(nb) for i in range(total)], S_, nb)
+        else:
+            for b in range(nb):
+                sh = [full[b, i] for i in range(total)]
+                enc.Encode(sh)
+        torch.cuda.synchronize()
+        mine = repair.owned(rank, total, world)
+        local = full[:, mine].clone()
+        for q, i in enumerate(mine):
+            if i in erased:
+                local[:, q] = 0
+        out = repair.repair_batch(enc, local, erased, rank, world, strategy=strategy)
+        torch.cuda.synchronize()
+        mine_er = [e for e in sorted(erased) if repair.owner(e, world) == rank]
+        assert out.shape == (nb, len(mine_er), S_)
+        for q, e in enumerate(mine_er):
+            assert torch.equal(out[:, q], full[:, e]), (rank, e)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("strategy", ["columns", "allgather"])
+@pytest.mark.parametrize("mode", ["EC16P20", "EC16P20L2", "EC6P10L2"])
+def test_repair_gpu_multi_rank_shared_device(world, strategy, mode):
+    """repair_batch at world 2 and 3 end to end on the GPU -- exchange, then the decode of every
+    rank's column slice (or of the gathered rows) -- the path the 8-GPU repair runs, rehearsed with
+    all ranks on the box's one GPU."""
+    mp.spawn(_gpu_worker, args=(world, free_port(), strategy, mode), nprocs=world, join=True)
