@@ -221,20 +221,31 @@ func (e *Engine) Verify(shards [][]byte) (bool, error) {
 	return ok[0] != 0, err
 }
 
-// prepareMissing gives every zero-length shard a buffer of the shard size, as
-// KRS/reedsolomon.go:1514-1518 does (reuse cap, else a 64-byte aligned allocation).
-func prepareMissing(shards [][]byte) {
-	size := 0
-	for _, s := range shards {
+// prepareMissing gives the shards KRS's reconstruct rebuilds a buffer of the shard size when their
+// capacity is short, as KRS/reedsolomon.go:1514-1518 and :1539-1543 do (reuse cap, else a 64-byte
+// aligned allocation) -- and only those: nothing when the stripe is complete (or, for
+// ReconstructData, its data is), nothing when too few shards are present (ErrTooFewShards comes
+// first, :1418-1441), and no parity shard for ReconstructData.  The C side writes into cap only.
+func prepareMissing(shards [][]byte, dataShards int, dataOnly bool) {
+	size, present, dataPresent := 0, 0, 0
+	for i, s := range shards {
 		if len(s) != 0 {
-			size = len(s)
-			break
+			if size == 0 {
+				size = len(s)
+			}
+			present++
+			if i < dataShards {
+				dataPresent++
+			}
 		}
 	}
-	if size == 0 {
+	if size == 0 || present == len(shards) || present < dataShards || (dataOnly && dataPresent == dataShards) {
 		return
 	}
 	for i, s := range shards {
+		if dataOnly && i >= dataShards {
+			break
+		}
 		if len(s) == 0 && cap(s) < size {
 			shards[i] = reedsolomon.AllocAligned(1, size)[0][:0]
 		}
@@ -273,7 +284,7 @@ func (e *Engine) reconstruct(shards [][]byte, dataOnly bool) error {
 		}
 		return err
 	}
-	prepareMissing(shards)
+	prepareMissing(shards, e.dataShards, dataOnly)
 	return toError(callVec(shards, func(v *C.cfsec_shard, n C.int) C.int {
 		if dataOnly {
 			return C.cfsec_rs_reconstruct_data(e.h, v, n, C.CFSEC_MEM_HOST, nil)

@@ -143,7 +143,13 @@ func (e *ECEncoder) reconstruct(shards [][]byte, badIdx []int, dataOnly bool) er
 			shards[i] = shards[i][:0]
 		}
 	}
-	reserve(shards)
+	if e.tactic.L == 0 {
+		// RS modes: the engine's Reconstruct allocates only the shards it rebuilds (encoder.go:139-151)
+		prepareMissing(shards, e.tactic.N, dataOnly)
+	} else {
+		// LRC modes: fillFullShards (encoder.go:199-210) gives every zero-length shard the size first
+		reserve(shards)
+	}
 	return ecError(callVec(shards, func(v *C.cfsec_shard, n C.int) C.int {
 		if dataOnly {
 			return C.cfsec_ec_reconstruct_data(e.h, v, n, bp, C.int(len(b)), C.CFSEC_MEM_HOST, nil)
