@@ -224,7 +224,8 @@ hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
         const dim3 grid((unsigned)(ltiles * ns));
         hipError_t e;
         if (lut) {
-          const dim3 lgrid((unsigned)((llen + 4095) / 4096), (unsigned)ns);  // 4 KiB tiles
+          const size_t lt = lut_tile_bytes(kc);
+          const dim3 lgrid((unsigned)((llen + lt - 1) / lt), (unsigned)ns);
           e = launch_lut(kc, mc, mode, a, lgrid, stream);
           if (e != hipSuccess) return e;
           continue;

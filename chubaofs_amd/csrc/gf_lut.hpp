@@ -93,10 +93,11 @@ __device__ __forceinline__ Entry<EW> ld_entry(const char* T, uint32_t off) {
   return e;
 }
 
-// o[i][w] byte b = byte i of g[4w + b]: 4 outputs x 16 bytes from the byte-transposed words.
-__device__ __forceinline__ void untranspose4(const uint32_t (&g)[16], uint32_t (&o)[4][4]) {
+// o[i][w] byte b = byte i of g[4w + b]: 4 outputs x 4 LW bytes from the byte-transposed words.
+template <int LW = 4>
+__device__ __forceinline__ void untranspose4(const uint32_t (&g)[4 * LW], uint32_t (&o)[4][LW]) {
 #pragma unroll
-  for (int w = 0; w < 4; ++w) {
+  for (int w = 0; w < LW; ++w) {
     const uint32_t a = g[4 * w], b = g[4 * w + 1], c = g[4 * w + 2], d = g[4 * w + 3];
     const uint32_t ab_lo = __builtin_amdgcn_perm(b, a, 0x05010400u), cd_lo = __builtin_amdgcn_perm(d, c, 0x05010400u);
     const uint32_t ab_hi = __builtin_amdgcn_perm(b, a, 0x07030602u), cd_hi = __builtin_amdgcn_perm(d, c, 0x07030602u);
@@ -118,33 +119,35 @@ __device__ __forceinline__ void untranspose4(const uint32_t (&g)[16], uint32_t (
 // tools/lds_rate.hip) and the VALU ~13 cycles for 8 outputs, the v_perm product ~4.7 VALU cycles
 // per output.  MODE: kStore (outputs written), kVerify (compared: diff), kStoreVerify (rows < nstore
 // written, the rest compared).
-template <int K, int M, int ML, MatVecMode MODE, int LA = CFSEC_LUT_LOOKAHEAD>
+template <int K, int M, int ML, MatVecMode MODE, int LA = CFSEC_LUT_LOOKAHEAD, int LW = 4>
 __device__ __forceinline__ void lut_chunk(const char* T, const u32x4* tab01, const uint32_t* tab2,
                                           const uint8_t* const* in, uint8_t* const* out, int nstore, int64_t sbase,
                                           uint32_t off, uint32_t rem, uint32_t& diff) {
   constexpr int EW = entry_words(ML), NQ = (ML + 3) / 4, EB = 4 * EW, MP = M - ML;
   constexpr int D = LA < K ? LA : K;
   constexpr int SHIFT = EW == 1 ? 2 : (EW == 2 ? 3 : 4);  // log2 of the entry bytes
-  const bool full = rem >= 16;
-  uint32_t acc[16][NQ > 0 ? NQ : 1];
-  uint32_t accp[MP > 0 ? MP : 1][4];
+  constexpr int NP = 4 * LW;                              // bytes per lane chunk
+  const bool full = rem >= (uint32_t)NP;
+  uint32_t acc[NP][NQ > 0 ? NQ : 1];
+  uint32_t accp[MP > 0 ? MP : 1][LW];
 #pragma unroll
-  for (int p = 0; p < 16; ++p)
+  for (int p = 0; p < NP; ++p)
 #pragma unroll
     for (int q = 0; q < NQ; ++q) acc[p][q] = 0u;
 #pragma unroll
   for (int r = 0; r < MP; ++r)
 #pragma unroll
-    for (int w = 0; w < 4; ++w) accp[r][w] = 0u;
-  uint32_t x[K][4];
+    for (int w = 0; w < LW; ++w) accp[r][w] = 0u;
+  uint32_t x[K][LW];
   const auto load = [&](int c) {
-    u32x4 v;
-    if (full) v = dev::ld16<true>(in[c] + sbase + off);
-    else v = dev::ld_tail(in[c] + sbase + off, rem);
-    x[c][0] = v.x;
-    x[c][1] = v.y;
-    x[c][2] = v.z;
-    x[c][3] = v.w;
+    if (full) {
+      dev::ld_chunk<LW, true>(in[c] + sbase + off, x[c]);
+    } else {
+      const u32x4 v = dev::ld_tail(in[c] + sbase + off, rem);
+      const uint32_t t[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int w = 0; w < LW; ++w) x[c][w] = t[w];
+    }
   };
 #pragma unroll
   for (int c = 0; c < D; ++c) load(c);
@@ -155,7 +158,7 @@ __device__ __forceinline__ void lut_chunk(const char* T, const u32x4* tab01, con
     if constexpr (NQ > 0) {
       const char* tc = T + c * 2 * 16 * EB;
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {
+      for (int w = 0; w < LW; ++w) {
         // byte j of lo / hi = EB x (low / high nibble of byte j): the entry's byte offset
         uint32_t lo, hi;
         if constexpr (SHIFT == 4) {
@@ -176,40 +179,52 @@ __device__ __forceinline__ void lut_chunk(const char* T, const u32x4* tab01, con
         }
       }
 #pragma unroll
-      for (int p = 0; p < 16; ++p)
+      for (int p = 0; p < NP; ++p)
 #pragma unroll
         for (int q = 0; q < NQ; ++q) asm volatile("" : "+v"(acc[p][q]));
     }
     if constexpr (MP > 0) {
-      dev::mac_row_k<MP>(accp, x[c], tab01 + c * MP, tab2 + c * MP);
+      dev::mac_row_k<MP, LW>(accp, x[c], tab01 + c * MP, tab2 + c * MP);
 #pragma unroll
       for (int r = 0; r < MP; ++r)
 #pragma unroll
-        for (int w = 0; w < 4; ++w) asm volatile("" : "+v"(accp[r][w]));
+        for (int w = 0; w < LW; ++w) asm volatile("" : "+v"(accp[r][w]));
     }
     __builtin_amdgcn_sched_barrier(0);
   }
   constexpr bool kVer = MODE == MatVecMode::kVerify, kMix = MODE == MatVecMode::kStoreVerify;
-  const auto finish = [&](int r, const uint32_t (&o)[4]) {
+  const auto finish = [&](int r, const uint32_t (&o)[LW]) {
     uint8_t* p = out[r] + sbase + off;
     const bool cmp = kVer || (kMix && r >= nstore);
-    const u32x4 v{o[0], o[1], o[2], o[3]};
-    if (cmp) {
-      const u32x4 d = v ^ (full ? dev::ld16<true>(p) : dev::ld_tail(p, rem));
-      diff |= d.x | d.y | d.z | d.w;
-    } else if (full) {
-      dev::st16_out<true>(p, v);
+    if (full) {
+      if (cmp) {
+        uint32_t y[LW];
+        dev::ld_chunk<LW, true>(p, y);
+#pragma unroll
+        for (int w = 0; w < LW; ++w) diff |= o[w] ^ y[w];
+      } else {
+        dev::st_chunk<LW, true>(p, o);
+      }
     } else {
-      dev::st_tail(p, v, rem);
+      uint32_t t[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int w = 0; w < LW; ++w) t[w] = o[w];
+      const u32x4 v{t[0], t[1], t[2], t[3]};
+      if (cmp) {
+        const u32x4 d = v ^ dev::ld_tail(p, rem);
+        diff |= d.x | d.y | d.z | d.w;
+      } else {
+        dev::st_tail(p, v, rem);
+      }
     }
   };
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
-    uint32_t g[16];
+    uint32_t g[NP];
 #pragma unroll
-    for (int p = 0; p < 16; ++p) g[p] = acc[p][q];
-    uint32_t o[4][4];
-    untranspose4(g, o);
+    for (int p = 0; p < NP; ++p) g[p] = acc[p][q];
+    uint32_t o[4][LW];
+    untranspose4<LW>(g, o);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       if (4 * q + i < ML) finish(4 * q + i, o[i]);
@@ -218,9 +233,9 @@ __device__ __forceinline__ void lut_chunk(const char* T, const u32x4* tab01, con
   for (int r = 0; r < MP; ++r) finish(ML + r, accp[r]);
 }
 
-// Grid (tiles, stripes), 256 threads, one 4 KiB tile of every row per workgroup (GfArgs as the
+// Grid (tiles, stripes), 256 threads, one tile (256 lanes x 4 LW bytes) of every row per workgroup (GfArgs as the
 // fixed-K kernel: a.k == K, a.m == M, a.len < 4 GiB).
-template <int K, int M, int ML, MatVecMode MODE, int LA = CFSEC_LUT_LOOKAHEAD>
+template <int K, int M, int ML, MatVecMode MODE, int LA = CFSEC_LUT_LOOKAHEAD, int LW = 4>
 __global__ __launch_bounds__(256) void gf_lut_kernel(const dev::GfArgs a) {
   constexpr int EW = entry_words(ML), NQ = (ML + 3) / 4, MP = M - ML;
   __shared__ __attribute__((aligned(16))) uint32_t T[NQ > 0 ? K * 2 * 16 * EW : 4];
@@ -240,12 +255,13 @@ __global__ __launch_bounds__(256) void gf_lut_kernel(const dev::GfArgs a) {
   const int64_t sbase = (int64_t)stripe * a.sstride;
   const uint8_t* const* in = a.ptr + ts * K;
   uint8_t* const* out = const_cast<uint8_t* const*>(a.ptr + (size_t)a.tab * K + ts * M);
-  const uint32_t off = tile * 4096u + threadIdx.x * 16u;
+  constexpr uint32_t kLB = 4u * LW;  // bytes per lane chunk
+  const uint32_t off = tile * (256u * kLB) + threadIdx.x * kLB;
   const uint64_t len = dev::stripe_len(a, stripe);
   uint32_t diff = 0;
   if ((uint64_t)off < len) {
-    const uint32_t rem = (uint64_t)off + 16 <= len ? 16u : (uint32_t)(len - off);
-    lut_chunk<K, M, ML, MODE, LA>(reinterpret_cast<const char*>(T), tab01, tab2, in, out, (int)a.nstore, sbase, off, rem,
+    const uint32_t rem = (uint64_t)off + kLB <= len ? kLB : (uint32_t)(len - off);
+    lut_chunk<K, M, ML, MODE, LA, LW>(reinterpret_cast<const char*>(T), tab01, tab2, in, out, (int)a.nstore, sbase, off, rem,
                               diff);
   }
   if constexpr (MODE == MatVecMode::kVerify || MODE == MatVecMode::kStoreVerify) {

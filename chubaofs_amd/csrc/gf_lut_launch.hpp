@@ -21,6 +21,12 @@ inline int lut_outputs(int k, int m) {
   return 0;
 }
 
+// Lane chunk of the lookup kernel for k inputs: 8 bytes for k = 15 (EC15P12: 64 instead of 107 VGPRs,
+// 8 waves per SIMD instead of 4; encode 96 -> 81 us, verify unchanged: profiles/r03/lut_probe4.txt),
+// 16 bytes otherwise (EC12P9: no difference).  The launch grid's tiles are 256 lanes of it.
+constexpr int lut_lane_dwords(int k) { return k == 15 ? 2 : 4; }
+constexpr size_t lut_tile_bytes(int k) { return size_t(256) * 4 * lut_lane_dwords(k); }
+
 template <int K>
 hipError_t launch_lut_k(int m, MatVecMode mode, const dev::GfArgs& a, dim3 grid, hipStream_t st);
 template <>

@@ -25,7 +25,7 @@
 
 using namespace cfsec;
 
-template <int K, int M, int ML, int LA = 2>
+template <int K, int M, int ML, int LA = 2, int LW = 4>
 void run_case(const char* name, size_t S, int nst) {
   Matrix mat;
   build_matrix(K, K + M, mat);
@@ -73,7 +73,7 @@ void run_case(const char* name, size_t S, int nst) {
     for (int c = 0; c < K; ++c) a.coef[r * K + c] = coef[(size_t)r * K + c];
   for (int c = 0; c < K; ++c) a.ptr[c] = buf + c * pitch;
   for (int r = 0; r < M; ++r) a.ptr[K + r] = buf + (K + r) * pitch;
-  const dim3 grid(a.tiles_per_stripe, (unsigned)nst);
+  const dim3 grid((unsigned)((S + 1024 * LW - 1) / (1024 * LW)), (unsigned)nst);
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
@@ -90,7 +90,7 @@ void run_case(const char* name, size_t S, int nst) {
   };
   const double us_lib = time([&] { CK(launch_matvec(job, 0)); });
   const double us_lut =
-      time([&] { hipLaunchKernelGGL((lut::gf_lut_kernel<K, M, ML, MatVecMode::kStore, LA>), grid, dim3(256), 0, 0, a); });
+      time([&] { hipLaunchKernelGGL((lut::gf_lut_kernel<K, M, ML, MatVecMode::kStore, LA, LW>), grid, dim3(256), 0, 0, a); });
   CK(hipDeviceSynchronize());
   std::vector<uint8_t> a1(bytes), a2(bytes);
   CK(hipMemcpy(a1.data(), buf, bytes, hipMemcpyDeviceToHost));
@@ -103,7 +103,7 @@ void run_case(const char* name, size_t S, int nst) {
   CK(hipMemset(flags, 0, 4 * nst));
   const double vus_lib = time([&] { CK(launch_matvec(vjob, 0)); });
   const double vus_lut =
-      time([&] { hipLaunchKernelGGL((lut::gf_lut_kernel<K, M, ML, MatVecMode::kVerify, LA>), grid, dim3(256), 0, 0, a); });
+      time([&] { hipLaunchKernelGGL((lut::gf_lut_kernel<K, M, ML, MatVecMode::kVerify, LA, LW>), grid, dim3(256), 0, 0, a); });
   std::vector<uint32_t> fl(nst);
   CK(hipMemcpy(fl.data(), flags, 4 * nst, hipMemcpyDeviceToHost));
   for (uint32_t f : fl) same = same && f == 0;
@@ -114,13 +114,13 @@ void run_case(const char* name, size_t S, int nst) {
   byte ^= 0x40;
   CK(hipMemcpy(buf + at, &byte, 1, hipMemcpyHostToDevice));
   CK(hipMemset(flags, 0, 4 * nst));
-  hipLaunchKernelGGL((lut::gf_lut_kernel<K, M, ML, MatVecMode::kVerify, LA>), grid, dim3(256), 0, 0, a);
+  hipLaunchKernelGGL((lut::gf_lut_kernel<K, M, ML, MatVecMode::kVerify, LA, LW>), grid, dim3(256), 0, 0, a);
   CK(hipMemcpy(fl.data(), flags, 4 * nst, hipMemcpyDeviceToHost));
   for (int s = 0; s < nst; ++s) same = same && fl[s] == (s == nst - 1 ? 1u : 0u);
   const double alg = (double)(K + M) * S * nst;
   const auto pct = [&](double us) { return alg / (us * 1e-6) / 8e12 * 100; };
-  std::printf("%-22s k=%2d m=%2d ml=%2d la=%2d  encode lib %7.1f us (%4.1f %%)  lut %7.1f us (%4.1f %%)   verify lib %7.1f (%4.1f %%)  lut %7.1f (%4.1f %%)  %s\n",
-              name, K, M, ML, LA, us_lib, pct(us_lib), us_lut, pct(us_lut), vus_lib, pct(vus_lib), vus_lut, pct(vus_lut),
+  std::printf("%-22s k=%2d m=%2d ml=%2d la=%2d lw=%d  encode lib %7.1f us (%4.1f %%)  lut %7.1f us (%4.1f %%)   verify lib %7.1f (%4.1f %%)  lut %7.1f (%4.1f %%)  %s\n",
+              name, K, M, ML, LA, LW, us_lib, pct(us_lib), us_lut, pct(us_lut), vus_lib, pct(vus_lib), vus_lut, pct(vus_lut),
               same ? "bytes+flags equal" : "DIFFER");
   CK(hipFree(buf));
   CK(hipFree(ref));
@@ -128,19 +128,17 @@ void run_case(const char* name, size_t S, int nst) {
 }
 
 int main() {
-  run_case<15, 12, 12, 2>("EC15P12", 349526, 32);
-  run_case<15, 12, 12, 4>("EC15P12", 349526, 32);
-  run_case<15, 12, 12, 6>("EC15P12", 349526, 32);
-  run_case<15, 12, 12, 8>("EC15P12", 349526, 32);
-  run_case<12, 9, 8, 2>("EC12P9", 349526, 32);
-  run_case<12, 9, 8, 4>("EC12P9", 349526, 32);
-  run_case<12, 9, 8, 6>("EC12P9", 349526, 32);
-  run_case<12, 9, 8, 8>("EC12P9", 349526, 32);
-  run_case<16, 16, 16, 2>("16x16 (EC16P20 top)", 262144, 64);
-  run_case<16, 16, 16, 4>("16x16 (EC16P20 top)", 262144, 64);
-  run_case<16, 20, 16, 4>("EC16P20 global", 262144, 64);
-  run_case<16, 22, 16, 4>("EC16P20L2 fused", 262144, 64);
-  run_case<6, 12, 8, 4>("EC6P10L2 fused", 699051, 32);
-  run_case<15, 12, 12, 2>("EC15P12", 349526, 32);
+  run_case<15, 12, 12, 2, 4>("EC15P12", 349526, 32);
+  run_case<15, 12, 12, 2, 2>("EC15P12", 349526, 32);
+  run_case<15, 12, 12, 4, 2>("EC15P12", 349526, 32);
+  run_case<12, 9, 8, 2, 4>("EC12P9", 349526, 32);
+  run_case<12, 9, 8, 2, 2>("EC12P9", 349526, 32);
+  run_case<12, 9, 8, 4, 2>("EC12P9", 349526, 32);
+  run_case<16, 16, 16, 2, 4>("16x16 (EC16P20 top)", 262144, 64);
+  run_case<16, 16, 16, 2, 2>("16x16 (EC16P20 top)", 262144, 64);
+  run_case<16, 20, 16, 2, 2>("EC16P20 global", 262144, 64);
+  run_case<16, 22, 16, 2, 2>("EC16P20L2 fused", 262144, 64);
+  run_case<6, 12, 8, 2, 2>("EC6P10L2 fused", 699051, 32);
+  run_case<15, 12, 12, 2, 4>("EC15P12", 349526, 32);
   return 0;
 }
