@@ -28,8 +28,8 @@
 //
 // Kernel families, first match wins:
 //   lookup-product (gf_lut.hpp): the products of each input byte with a whole column from two LDS
-//                table reads, for the shapes lut_outputs() names (EC12P4 / EC12P9 / EC15P12 and
-//                their repairs); CFSEC_LUT=0 disables (A/B)
+//                table reads, for the shapes lut_outputs() names (EC12P9, EC15P12, EC16P20(L2)
+//                repairs of 5-16 shards, non-dyadic k = 6 products); CFSEC_LUT=0 disables (A/B)
 //   16x16-dyadic (gf_dyadic16.hpp): EC16P20's 20 parity rows
 //   dyadic-block (gf_dyadic.hpp): 4x4 / 2x2 dyadic matrices (code-mode encodes, coset-aligned
 //                repairs, fused LRC encodes with 2 plain rows)
@@ -168,16 +168,16 @@ hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
         const char* v = std::getenv("CFSEC_LUT");
         return !(v && v[0] == '0');
       }();
-      const bool lut = kLut && fixed && lut_outputs(kc, mc) > 0;
       DyPlan dy{0, 0};
       bool dy16 = false;
-      if (fixed && !lut && r0 == 0 && mc == job.m && mode != MatVecMode::kStoreVerify) {
+      if (fixed && r0 == 0 && mc == job.m && mode != MatVecMode::kStoreVerify) {
         std::vector<uint8_t> sub((size_t)mc * kc);
         for (int r = 0; r < mc; ++r)
           for (int c = 0; c < kc; ++c) sub[(size_t)r * kc + c] = job.coef[(size_t)r * job.k + c];
         dy16 = dyadic16_plan(sub.data(), mc, kc);
         if (!dy16) dy = dyadic_plan(sub.data(), mc, kc);
       }
+      const bool lut = kLut && fixed && lut_outputs(kc, mc, dy16 || dy.B != 0) > 0;
       const size_t tile = fixed ? size_t(256) * 4 * dev::fixed_lane_dwords(kc, mc)
                                 : size_t(threads / sh.OS) * dev::kLaneBytes * (verify ? kVerifyW : kStoreW);
       const int per_stripe = kc + mc;

@@ -56,6 +56,8 @@ int main() {
       {"EC16P20 global encode", 16, 20, 262144, 64},
       {"EC16P20L2 fused encode", 16, 22, 262144, 64},
       {"EC16P20L2 repair 4 erased", 16, 4, 262144, 64},
+      {"EC16P20 repair 8 rows", 16, 8, 262144, 64},
+      {"EC16P20 repair 16 rows", 16, 16, 262144, 64},
       {"EC15P12 encode", 15, 12, 349526, 32},
       {"EC16P4 encode", 16, 4, 262144, 64},
       {"EC12P9 encode", 12, 9, 349526, 32},

@@ -25,13 +25,15 @@
 
 using namespace cfsec;
 
-template <int K, int M, int ML, int LA = 2, int LW = 4>
+// PERM: the m rows are parity rows 7r mod 20 of the k + 20 code (no dyadic block structure left), as
+// a repair's non-coset-aligned rows are; else parity rows 0..m-1.
+template <int K, int M, int ML, int LA = 2, int LW = 4, bool PERM = false>
 void run_case(const char* name, size_t S, int nst) {
   Matrix mat;
-  build_matrix(K, K + M, mat);
+  build_matrix(K, K + (PERM ? 20 : M), mat);
   std::vector<uint8_t> coef((size_t)M * K);
   for (int r = 0; r < M; ++r)
-    for (int c = 0; c < K; ++c) coef[(size_t)r * K + c] = mat.at(K + r, c);
+    for (int c = 0; c < K; ++c) coef[(size_t)r * K + c] = mat.at(K + (PERM ? (7 * r) % 20 : r), c);
   const size_t pitch = (S + 255) / 256 * 256, per = pitch * (K + M), bytes = per * nst;
   uint8_t *buf, *ref;
   uint32_t* flags;
@@ -128,17 +130,17 @@ void run_case(const char* name, size_t S, int nst) {
 }
 
 int main() {
-  run_case<15, 12, 12, 2, 4>("EC15P12", 349526, 32);
-  run_case<15, 12, 12, 2, 2>("EC15P12", 349526, 32);
-  run_case<15, 12, 12, 4, 2>("EC15P12", 349526, 32);
-  run_case<12, 9, 8, 2, 4>("EC12P9", 349526, 32);
+  run_case<16, 5, 5, 2, 2, true>("16x5 non-dyadic", 262144, 64);
+  run_case<16, 8, 8, 2, 2, true>("16x8 non-dyadic", 262144, 64);
+  run_case<16, 8, 8, 2, 2>("16x8 dyadic", 262144, 64);
+  run_case<16, 12, 12, 2, 2, true>("16x12 non-dyadic", 262144, 64);
+  run_case<16, 12, 12, 2, 2>("16x12 dyadic", 262144, 64);
+  run_case<16, 16, 16, 2, 2, true>("16x16 non-dyadic", 262144, 64);
+  run_case<16, 16, 16, 2, 2>("16x16 dyadic", 262144, 64);
+  run_case<12, 8, 8, 2, 4>("12x8 dyadic", 349526, 32);
+  run_case<12, 8, 8, 2, 2>("12x8 dyadic", 349526, 32);
   run_case<12, 9, 8, 2, 2>("EC12P9", 349526, 32);
-  run_case<12, 9, 8, 4, 2>("EC12P9", 349526, 32);
-  run_case<16, 16, 16, 2, 4>("16x16 (EC16P20 top)", 262144, 64);
-  run_case<16, 16, 16, 2, 2>("16x16 (EC16P20 top)", 262144, 64);
-  run_case<16, 20, 16, 2, 2>("EC16P20 global", 262144, 64);
-  run_case<16, 22, 16, 2, 2>("EC16P20L2 fused", 262144, 64);
-  run_case<6, 12, 8, 2, 2>("EC6P10L2 fused", 699051, 32);
-  run_case<15, 12, 12, 2, 4>("EC15P12", 349526, 32);
+  run_case<6, 10, 8, 2, 2, true>("6x10 non-dyadic", 699051, 32);
+  run_case<6, 8, 8, 2, 2, true>("6x8 non-dyadic", 699051, 32);
   return 0;
 }
