@@ -130,17 +130,13 @@ void run_case(const char* name, size_t S, int nst) {
 }
 
 int main() {
-  run_case<16, 5, 5, 2, 2, true>("16x5 non-dyadic", 262144, 64);
-  run_case<16, 8, 8, 2, 2, true>("16x8 non-dyadic", 262144, 64);
-  run_case<16, 8, 8, 2, 2>("16x8 dyadic", 262144, 64);
-  run_case<16, 12, 12, 2, 2, true>("16x12 non-dyadic", 262144, 64);
-  run_case<16, 12, 12, 2, 2>("16x12 dyadic", 262144, 64);
-  run_case<16, 16, 16, 2, 2, true>("16x16 non-dyadic", 262144, 64);
-  run_case<16, 16, 16, 2, 2>("16x16 dyadic", 262144, 64);
-  run_case<12, 8, 8, 2, 4>("12x8 dyadic", 349526, 32);
-  run_case<12, 8, 8, 2, 2>("12x8 dyadic", 349526, 32);
-  run_case<12, 9, 8, 2, 2>("EC12P9", 349526, 32);
-  run_case<6, 10, 8, 2, 2, true>("6x10 non-dyadic", 699051, 32);
-  run_case<6, 8, 8, 2, 2, true>("6x8 non-dyadic", 699051, 32);
+  run_case<6, 6, 6, 2, 2>("EC6P6 (dyadic lib)", 174763, 256);
+  run_case<6, 6, 6, 4, 2>("EC6P6 (dyadic lib)", 174763, 256);
+  run_case<6, 10, 10, 2, 2>("EC6P10 (dyadic lib)", 699051, 32);
+  run_case<6, 12, 12, 2, 2>("6x12 (EC6P10L2 fused)", 699051, 32);
+  run_case<6, 12, 8, 2, 2>("6x12 (EC6P10L2 fused)", 699051, 32);
+  run_case<16, 20, 16, 4, 2>("EC16P20 global", 262144, 64);
+  run_case<12, 4, 4, 2, 2>("EC12P4 64MiB", 5592406, 8);
+  run_case<6, 6, 6, 2, 2>("EC6P6 (dyadic lib)", 174763, 256);
   return 0;
 }
