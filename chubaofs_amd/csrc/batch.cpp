@@ -201,6 +201,8 @@ bool fused_crc_group(const Group& g, uint32_t* dcrc, size_t nwords, const std::m
   job.out = g.out.data();
   job.mode = MatVecMode::kStore;
   *st = hip_status(launch_matvec_crc(job, dcrc + t0->crc_word, (int)cs, slot.data(), s), "launch_matvec_crc(batch)");
+  if (std::getenv("CFSEC_TRACE_BATCH"))  // which groups fused, for tests
+    std::fprintf(stderr,"cfsec batch: fused crc group k=%d m=%d tasks=%zu len=%llu\n", k, m, nt, (unsigned long long)len);
   return true;
 }
 
@@ -734,8 +736,9 @@ Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceCont
     }
     return CFSEC_OK;
   };
-  std::map<int, int> tasks_per_owner;  // a bid with several tasks keeps the separate checksum pass
-  for (StripeTask* t : tasks) ++tasks_per_owner[t->owner];
+  std::map<int, int> tasks_per_owner;  // a bid with several checksummed tasks keeps the separate pass
+  for (StripeTask* t : tasks)          // (EnableVerify's compare task writes no words: not counted)
+    if (t->crc) ++tasks_per_owner[t->owner];
   int next_flag = 0;
   std::vector<std::pair<StripeTask*, int>> flags;  // (task, flag word)
   const auto record = [&](const std::vector<Group>& groups) {

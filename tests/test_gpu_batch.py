@@ -670,3 +670,83 @@ def test_ec_reconstruct_batch_async_crc():
     for b, (_, shards) in enumerate(want):
         for i in range(total):
             assert got[b][i] == (crc_of(shards[i]) if i in bads[b] else 0), (b, i)
+
+
+@pytest.mark.parametrize("gap", [False, True])
+@pytest.mark.parametrize("memory", ["host", "device"])
+@pytest.mark.parametrize("mode", [cm.EC12P4, cm.EC6P6, cm.EC6P10L2])
+def test_ec_batch_crc_uniform_groups(mode, memory, gap, monkeypatch, capfd):
+    """The batch calls' checksums when a group holds many equal-length tasks -- the case the fused
+    product + CRC launch takes (batch.cpp fused_crc_group: one task per bid, one checksum-word
+    stride); with gap, a failed bid in the middle breaks the stride and the separate pass runs.
+    Reconstruct: a corrupted bid fails Verify after the fused launch wrote its words (they read 0)."""
+    monkeypatch.setenv("CFSEC_TRACE_BATCH", "1")
+    from chubaofs_amd import ec
+    t = cm.GetTactic(mode)
+    total = t.N + t.M + t.L
+    size = 65536
+    rs = t.L == 0
+    # encode
+    enc = ec.NewEncoder(ec.Config(CodeMode=t, EnableVerify=True), device=0)
+    orc = ECOracle.from_tactic(t, enable_verify=True)
+    stripes, want, exp = [], [], []
+    for b in range(6):
+        src = [gen_mock_bytes(b * 7 + i, size) for i in range(t.N)] + \
+              [np.zeros(size, np.uint8) for _ in range(total - t.N)]
+        if gap and b == 2:
+            src[1] = src[1][:-1].copy()  # shard size mismatch: the bid fails before any launch
+        ref = [Slice.of(x) for x in src]
+        exp.append(orc.encode(ref))
+        want.append([x.view().copy() for x in ref])
+        stripes.append(to_mem(src, memory))
+    capfd.readouterr()
+    st, crcs = enc.EncodeBatch(stripes, crcs=True)
+    err = capfd.readouterr().err
+    assert st == exp
+    assert (exp[2] != 0) == gap
+    for b in range(6):
+        for i in range(total):
+            assert np.array_equal(host(stripes[b][i]), want[b][i]), (b, i)
+            assert crcs[b][i] == (crc_of(want[b][i]) if exp[b] == 0 else 0), (b, i)
+    fused = "fused crc group k=%d m=%d tasks=6" % (t.N, t.M)
+    if rs and memory == "device" and not gap:
+        assert fused in err, err
+    if gap:
+        assert "tasks=6" not in err and "tasks=5" not in err, err
+    # reconstruct: the same bad set everywhere (one plan, one group).  With a parity of slack the plan
+    # also compares the survivors (Verify's rows: not a plain store, the separate pass runs) and bid 3
+    # is corrupted; with exactly M erasures nothing is left to compare and the group fuses.
+    enc = ec_new(mode)
+    for slack in ([1, 0] if rs else [1]):
+        bad = list(range(t.M - slack)) if rs else [0, total - 1]
+        bids, bads, wantr = [], [], []
+        for b in range(6):
+            good = ec_full_codeword(enc, t, size, 50 + b)
+            src = [x.copy() for x in good]
+            bb = list(bad)
+            if b == 3 and slack:
+                src[total - 1 if rs else t.N][size // 3] ^= 0x21
+            if gap and b == 1:
+                bb = list(range(t.M + t.L + 1))  # too many erasures: no task for this bid
+            wantr.append(sequential(enc, src, bb))
+            work = to_mem(src, memory)
+            for i in bb:
+                if memory == "device":
+                    work[i].zero_()
+                else:
+                    work[i][:] = 0
+            bids.append(work)
+            bads.append(bb)
+        capfd.readouterr()
+        st, crcs = enc.ReconstructBatch(bids, bads, crcs=True)
+        err = capfd.readouterr().err
+        assert (wantr[3][0] != 0) == bool(slack)
+        for b, (e, shards) in enumerate(wantr):
+            assert st[b] == e, (b, st[b], e)
+            for i in range(total):
+                assert np.array_equal(host(bids[b][i]), shards[i]), (b, i)
+                assert crcs[b][i] == (crc_of(shards[i]) if e == 0 and i in bads[b] else 0), (b, i)
+        if not slack and memory == "device" and not gap:
+            assert "fused crc group k=%d m=%d tasks=6" % (t.N, t.M) in err, err
+        if slack or gap:
+            assert "fused crc group" not in err, err
