@@ -160,7 +160,8 @@ hipError_t launch_group_run(const Group& g, size_t t0, size_t t1, uint32_t* dfla
 // (no index remap, no other task of the same bid writing that bid's words) runs as one fused launch:
 // the shards are checksummed from the registers the product already holds, instead of a second pass
 // that reads every row again (EC12P4 8 x 64 MiB: 130 + 123 us -> ~180 us).  Returns false when the
-// group does not qualify (then the product and the separate pass run as before).
+// group does not qualify (then the product and the separate pass run as before).  The words are
+// zeroed by run_device already (the launch skips its own memset).
 bool fused_crc_group(const Group& g, uint32_t* dcrc, size_t nwords, const std::map<int, int>& tasks_per_owner,
                      hipStream_t s, Status* st) {
   static const bool kOn = [] {  // CFSEC_BATCH_FUSED_CRC=0: the separate pass always (A/B)
@@ -200,7 +201,8 @@ bool fused_crc_group(const Group& g, uint32_t* dcrc, size_t nwords, const std::m
   job.in = g.in.data();
   job.out = g.out.data();
   job.mode = MatVecMode::kStore;
-  *st = hip_status(launch_matvec_crc(job, dcrc + t0->crc_word, (int)cs, slot.data(), s), "launch_matvec_crc(batch)");
+  *st = hip_status(launch_matvec_crc(job, dcrc + t0->crc_word, (int)cs, slot.data(), s, false),
+                   "launch_matvec_crc(batch)");
   if (std::getenv("CFSEC_TRACE_BATCH"))  // which groups fused, for tests
     std::fprintf(stderr,"cfsec batch: fused crc group k=%d m=%d tasks=%zu len=%llu\n", k, m, nt, (unsigned long long)len);
   return true;
@@ -708,6 +710,9 @@ Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceCont
     return e;
   };
   if (mem == CFSEC_MEM_DEVICE && !async) st = ctx->order_after_default(ws);
+  // Zeroed inline on lane 0: a memset on lane 1 beside the first products, waited for by the first
+  // checksum launch, measured slower (C5 +26 instead of +14 us, EC12P4 fused encode + CRC 246
+  // instead of 224 us: the cross-stream wait costs more than the 10 KiB fill it hides).
   if (st == CFSEC_OK && sums) st = hip_status(hipMemsetAsync(dcrc, 0, crc->n * 4, lane[0]), "hipMemsetAsync(crc)");
   if (st == CFSEC_OK && nlanes > 1) st = join(0, 1);
   // crc32.ChecksumIEEE of the rows the tasks of a launched part name, on the part's stream, from the

@@ -195,7 +195,7 @@ bool matvec_crc_supported(int k, int m, size_t len) {
 uint32_t crc32_shift_ones(size_t len) { return mulmod(xpow(8 * (int64_t)len), 0xFFFFFFFFu) ^ 0xFFFFFFFFu; }
 
 hipError_t launch_matvec_crc(const MatVecJob& job, uint32_t* crc, int crc_stride, const int* slot,
-                             hipStream_t stream) {
+                             hipStream_t stream, bool zero) {
   if (job.mode != MatVecMode::kStore || !matvec_crc_supported(job.k, job.m, job.len) || !crc || !slot ||
       crc_stride <= 0 || crc_stride > 256 || job.nstripes < 0 || !job.coef || !job.in || !job.out)
     return hipErrorInvalidValue;
@@ -205,7 +205,8 @@ hipError_t launch_matvec_crc(const MatVecJob& job, uint32_t* crc, int crc_stride
     const bool want = i >= k || cin;
     if (want && (slot[i] < 0 || slot[i] >= crc_stride)) return hipErrorInvalidValue;
   }
-  hipError_t e = hipMemsetAsync(crc, 0, sizeof(uint32_t) * (size_t)crc_stride * job.nstripes, stream);
+  hipError_t e = zero ? hipMemsetAsync(crc, 0, sizeof(uint32_t) * (size_t)crc_stride * job.nstripes, stream)
+                      : hipSuccess;
   if (e != hipSuccess || job.nstripes == 0 || job.len == 0) return e;
 
   GfCrcArgs a{};

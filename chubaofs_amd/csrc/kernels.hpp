@@ -85,10 +85,11 @@ hipError_t launch_crc32_to(const uint8_t* const* ptrs, size_t len, int n, uint32
 // into the product kernel (gf_crc.hpp): row i of the product (inputs 0..k-1, then outputs) has its
 // checksum in device word crc[s * crc_stride + slot[i]] of stripe s.  slot[0] < 0 skips the inputs
 // (checksum the outputs only).  Every word of crc[0 .. nstripes*crc_stride) is zeroed first, so
-// words no row maps to read 0.  Only for matvec_crc_supported shapes (k in {6,8,12,16,18}, m <= 6).
+// words no row maps to read 0 (zero = false: the caller zeroed them; the kernel XORs into them).
+// Only for matvec_crc_supported shapes (k in {6,8,12,16,18}, m <= 6).
 bool matvec_crc_supported(int k, int m, size_t len);
 hipError_t launch_matvec_crc(const MatVecJob& job, uint32_t* crc, int crc_stride, const int* slot,
-                             hipStream_t stream);
+                             hipStream_t stream, bool zero = true);
 // shift(~0, len) ^ ~0: XOR it into a raw (zero-preset) CRC of len bytes to get crc32.ChecksumIEEE.
 uint32_t crc32_shift_ones(size_t len);
 

@@ -129,7 +129,14 @@ void run_case(const char* name, size_t S, int nst) {
   CK(hipFree(flags));
 }
 
-int main() {
+int main(int argc, char** argv) {
+  if (argc > 1 && std::strcmp(argv[1], "c5") == 0) {  // C5's row count: 16 inputs, 4 + 18 outputs
+    run_case<16, 16, 16, 2, 2, true>("16x16 (perm rows)", 262144, 64);
+    run_case<16, 22, 16, 2, 2, true>("16x22 hybrid 16+6", 262144, 64);
+    run_case<16, 20, 16, 2, 2, true>("16x20 hybrid 16+4", 262144, 64);
+    run_case<16, 18, 16, 2, 2, true>("16x18 hybrid 16+2", 262144, 64);
+    return 0;
+  }
   run_case<6, 6, 6, 2, 2>("EC6P6 (dyadic lib)", 174763, 256);
   run_case<6, 6, 6, 4, 2>("EC6P6 (dyadic lib)", 174763, 256);
   run_case<6, 10, 10, 2, 2>("EC6P10 (dyadic lib)", 699051, 32);
