@@ -60,6 +60,7 @@ struct Group {
   std::vector<uint64_t> lens;
   std::vector<uint8_t*> hout;      // plan->dy16: [tasks * (nd + 20)] its output rows
   int flag0 = 0;                   // first flag word
+  uint32_t* direct = nullptr;      // or: task i's Verify word is direct[i] (consecutive items' words)
 };
 
 hipError_t launch_group_run(const Group& g, size_t t0, size_t t1, uint32_t* dflags, hipStream_t s);
@@ -116,7 +117,7 @@ hipError_t launch_group_run(const Group& g, size_t t0, size_t t1, uint32_t* dfla
     for (size_t t = t0; t < t1; ++t) uniform = uniform && g.lens[t] == g.lens[t0];
     job.lens = uniform ? nullptr : g.lens.data() + t0;
     job.len = g.lens[t0];
-    job.flags = dflags + g.flag0 + t0;
+    job.flags = g.direct ? g.direct + t0 : dflags + g.flag0 + t0;
     return launch_dy16_repair(job, s);
   }
   MatVecJob job;
@@ -132,7 +133,7 @@ hipError_t launch_group_run(const Group& g, size_t t0, size_t t1, uint32_t* dfla
   for (size_t t = t0; t < t1; ++t) uniform = uniform && g.lens[t] == g.lens[t0];
   job.lens = uniform ? nullptr : g.lens.data() + t0;
   job.len = g.lens[t0];
-  job.flags = dflags + g.flag0 + t0;
+  job.flags = g.direct ? g.direct + t0 : dflags + g.flag0 + t0;
   job.mode = MatVecMode::kStoreVerify;
   job.nstore = g.plan->nstore;
   if (job.m <= kLaunchMaxRows || job.nstore == 0 || job.nstore == job.m) return launch_matvec(job, s);
@@ -745,10 +746,32 @@ Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceCont
   for (StripeTask* t : tasks)          // (EnableVerify's compare task writes no words: not counted)
     if (t->crc) ++tasks_per_owner[t->owner];
   int next_flag = 0;
-  std::vector<std::pair<StripeTask*, int>> flags;  // (task, flag word)
+  // Verify flags.  A group whose tasks belong to consecutive items writes each mismatch straight
+  // into the items' words -- the caller's device array (asynchronous) or the pinned host words,
+  // zeroed here first (synchronous) -- so no gather launch follows it (C4 / C5: one tasklet group,
+  // -4 us of device time per call).  Other groups use per-task words and the gather.
+  // CFSEC_BATCH_DIRECT_FLAGS=0: the gather always (A/B).
+  static const bool kDirect = [] {
+    const char* v = std::getenv("CFSEC_BATCH_DIRECT_FLAGS");
+    return !(v && v[0] == '0');
+  }();
+  uint32_t* fdirect = checks && kDirect ? (async ? async->flags : ws->hflags_dev) : nullptr;
+  if (fdirect && !async)
+    for (StripeTask* t : tasks) ws->hflags[t->owner] = 0;
+  const auto route = [&](std::vector<Group>& groups) {
+    if (!fdirect) return;
+    for (Group& gr : groups) {
+      if (gr.plan->out.size() <= (size_t)gr.plan->nstore) continue;  // nothing compared
+      bool consecutive = true;
+      for (size_t i = 1; i < gr.tasks.size() && consecutive; ++i)
+        consecutive = gr.tasks[i]->owner == gr.tasks[0]->owner + (int)i;
+      if (consecutive) gr.direct = fdirect + gr.tasks[0]->owner;
+    }
+  };
+  std::vector<std::pair<StripeTask*, int>> flags;  // (task, flag word; -1: written directly)
   const auto record = [&](const std::vector<Group>& groups) {
     for (const Group& gr : groups)
-      for (size_t i = 0; i < gr.tasks.size(); ++i) flags.emplace_back(gr.tasks[i], gr.flag0 + (int)i);
+      for (size_t i = 0; i < gr.tasks.size(); ++i) flags.emplace_back(gr.tasks[i], gr.direct ? -1 : gr.flag0 + (int)i);
   };
   int chunk = 0;
   tm.reset(new HostTimer("    group + launch"));
@@ -768,6 +791,7 @@ Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceCont
         return mem == CFSEC_MEM_DEVICE ? (const uint8_t*)t->shards[idx].data : (const uint8_t*)alias[{t, idx}];
       };
       std::vector<Group> groups = make_groups(dph, &next_flag, dptr);
+      route(groups);
       std::set<const StripeTask*> fused;  // tasks whose checksums a fused product + CRC launch took
       for (const Group& gr : groups) {
         if (st != CFSEC_OK) break;
@@ -824,6 +848,7 @@ Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceCont
       }
       const auto sptr = [&](const StripeTask* t, int idx) { return (const uint8_t*)slot[{t, idx}]; };
       std::vector<Group> groups = make_groups(part, &next_flag, sptr);
+      route(groups);
       for (const Group& gr : groups)
         if (st == CFSEC_OK) st = hip_status(launch_group(gr, ws->bflags, s), "launch_matvec(batch)");
       record(groups);
@@ -846,12 +871,13 @@ Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceCont
   if (st == CFSEC_OK && checks) {
     std::vector<std::pair<int, int>> pairs;
     for (auto& f : flags)
-      if (f.first->plan->out.size() > (size_t)f.first->plan->nstore) pairs.emplace_back(f.first->owner, f.second);
+      if (f.second >= 0 && f.first->plan->out.size() > (size_t)f.first->plan->nstore)
+        pairs.emplace_back(f.first->owner, f.second);
     std::sort(pairs.begin(), pairs.end());
     std::vector<int> item(pairs.size()), word(pairs.size());
     for (size_t i = 0; i < pairs.size(); ++i) item[i] = pairs[i].first, word[i] = pairs[i].second;
     st = hip_status(launch_flag_gather(ws->bflags, async ? async->flags : ws->hflags_dev, item.data(), word.data(),
-                                       (int)pairs.size(), async != nullptr, lane[0]),
+                                       (int)pairs.size(), async != nullptr || fdirect != nullptr, lane[0]),
                     "launch_flag_gather");
   }
   if (st != CFSEC_OK) ws->bflags_clean = false;  // some task words may be left set: memset on reuse

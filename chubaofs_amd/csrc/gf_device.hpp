@@ -69,6 +69,14 @@ __device__ __forceinline__ bool row_compared(const GfArgs& a, int r) {
   else return false;
 }
 
+// A Verify mismatch in stripe s: flags[s] = 1.  The words only ever hold 0 or 1, so a store is the
+// OR the semantics ask for (no read-modify-write), and it may target pinned host words directly
+// (batch.cpp: a synchronous batch's per-item flags, no gather launch), where an atomic RMW would
+// need PCIe atomics.
+__device__ __forceinline__ void set_flag(uint32_t* flags, uint32_t s) {
+  __hip_atomic_store(flags + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef u32x4 u32x4_ua __attribute__((aligned(1)));  // shard rows may start at any byte
 
@@ -511,7 +519,7 @@ __device__ __forceinline__ void matvec_k(const GfArgs& a) {
       lane_tail<M, MT, MODE>(a, tab01, tab2, in, out, og, (size_t)sbase + off, len - off, diff);
   }
   if constexpr (MODE == MatVecMode::kVerify || MODE == MatVecMode::kStoreVerify) {
-    if (diff) atomicOr(a.flags + stripe, 1u);
+    if (diff) dev::set_flag(a.flags, stripe);
   }
 }
 
@@ -569,7 +577,7 @@ __device__ __forceinline__ void matvec(const GfArgs& a) {
     }
     if constexpr (MODE == MatVecMode::kVerify || MODE == MatVecMode::kStoreVerify) {
       if (diff) {
-        atomicOr(a.flags + stripe, 1u);
+        dev::set_flag(a.flags, stripe);
         diff = 0;
       }
     }

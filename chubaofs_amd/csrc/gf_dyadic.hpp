@@ -343,7 +343,7 @@ __device__ __forceinline__ void matvec_dy(const GfArgs& a) {
     }
   }
   if constexpr (kVer) {
-    if (diff) atomicOr(a.flags + stripe, 1u);
+    if (diff) dev::set_flag(a.flags, stripe);
   }
 }
 

@@ -245,7 +245,7 @@ __device__ __forceinline__ void matvec_dy16(const GfArgs& a) {
     });
   }
   if constexpr (kVer) {
-    if (diff) atomicOr(a.flags + stripe, 1u);
+    if (diff) dev::set_flag(a.flags, stripe);
   }
 }
 
@@ -345,7 +345,7 @@ __device__ __forceinline__ void repair_dy16(const GfArgs& a) {
       if ((pstore >> r) & 1u) st_lane<W>(p, full, rem, v);
     });
   }
-  if (diff) atomicOr(a.flags + stripe, 1u);
+  if (diff) dev::set_flag(a.flags, stripe);
 }
 
 }  // namespace dev

@@ -265,7 +265,7 @@ __global__ __launch_bounds__(256) void gf_lut_kernel(const dev::GfArgs a) {
                               diff);
   }
   if constexpr (MODE == MatVecMode::kVerify || MODE == MatVecMode::kStoreVerify) {
-    if (diff) atomicOr(a.flags + stripe, 1u);
+    if (diff) dev::set_flag(a.flags, stripe);
   }
 }
 
