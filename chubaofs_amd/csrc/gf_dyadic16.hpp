@@ -84,10 +84,13 @@ __device__ __forceinline__ void ld_lane(const uint8_t* p, bool full, size_t rem,
   }
 }
 
+#ifndef CFSEC_DY16_ST_NT
+#define CFSEC_DY16_ST_NT 1  // non-temporal output stores (0: plain, the A/B of tools/dy16_st_ab.sh)
+#endif
 template <int W>
 __device__ __forceinline__ void st_lane(uint8_t* p, bool full, size_t rem, const uint32_t (&x)[W]) {
   if (full) {
-    st_chunk<W, true>(p, x);
+    st_chunk<W, (bool)CFSEC_DY16_ST_NT>(p, x);
   } else {
     u32x4 v{0u, 0u, 0u, 0u};
 #pragma unroll
