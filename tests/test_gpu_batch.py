@@ -750,3 +750,50 @@ def test_ec_batch_crc_uniform_groups(mode, memory, gap, monkeypatch, capfd):
             assert "fused crc group k=%d m=%d tasks=6" % (t.N, t.M) in err, err
         if slack or gap:
             assert "fused crc group" not in err, err
+
+
+@pytest.mark.parametrize("call", ["sync", "async"])
+@pytest.mark.parametrize("mode", [cm.EC12P4, cm.EC16P20L2])
+def test_verify_flags_direct_and_gathered(mode, call):
+    """Verify verdicts by both routes of batch.cpp: bids 0, 2, 4 share one erasure set and 1, 3, 5
+    another (each group's items are not consecutive: per-task words + the gather launch), 6 and 7 a
+    third (consecutive: the kernel writes the items' words directly).  Bids 2 and 7 are corrupted.
+    Asynchronous flags accumulate: bid 5's word preset to 1 stays 1 (engine.hpp AsyncOut)."""
+    t = cm.GetTactic(mode)
+    enc = ec_new(mode)
+    total = t.N + t.M + t.L
+    sets = ([[0, 5], [1, 13], [2, 3]] if mode == cm.EC12P4 else [[0, 17], [3, 20], [0, 1, 16, 17]])
+    plan = [0, 1, 0, 1, 0, 1, 2, 2]
+    bids, bads, want = [], [], []
+    for b, p in enumerate(plan):
+        size = 65536
+        good = ec_full_codeword(enc, t, size, 200 + b)
+        bad = list(sets[p])
+        src = [x.copy() for x in good]
+        if b in (2, 7):
+            cand = [i for i in range(t.N, t.N + t.M) if i not in bad]
+            src[cand[-1]][size // 5] ^= 0x81
+        want.append(sequential(enc, src, bad))
+        work = to_mem(src, "device")
+        for i in bad:
+            work[i].zero_()
+        bids.append(work)
+        bads.append(bad)
+    assert want[2][0] != 0 and want[7][0] != 0
+    if call == "sync":
+        st = enc.ReconstructBatch(bids, bads)
+        got = list(st)
+    else:
+        flags = torch.zeros(len(bids), dtype=torch.int32, device="cuda")
+        flags[5] = 1
+        torch.cuda.synchronize()
+        st = enc.ReconstructBatchAsync(bids, bads, flags=flags)
+        torch.cuda.synchronize()
+        fl = flags.cpu().numpy()
+        assert fl[5] == 1
+        got = [ErrVerify if (s == 0 and fl[b] and b != 5) else s for b, s in enumerate(st)]
+        assert [int(v) for v in fl] == [int(b in (2, 5, 7)) for b in range(len(bids))], fl
+    for b, (exp, shards) in enumerate(want):
+        assert got[b] == exp, (cm.Name(mode), call, b, got[b], exp)
+        for i in range(total):
+            assert np.array_equal(host(bids[b][i]), shards[i]), (b, i)
