@@ -431,6 +431,7 @@ def main():
         extra = secondary(args, torch, enc, batch, ptrs, stream, S, nst, pitch, dev, launch_bytes, data_bytes)
         del batch, golden
         torch.cuda.empty_cache()
+        extra["C5_multi_gpu_repair"] = multi_gpu_repair(args, torch, dev, rank, world)
         extra["configs"] = other_configs(args, torch, dev, stream, cpu=(world == 1 and rank == 0 and not args.no_cpu))
         extra["host_path"] = host_path(args, torch, dev, world)
 
@@ -616,6 +617,116 @@ def host_path(args, torch, dev, world):
                      "per_gpu_data_GBps": round(nst * K * S * reps / dt / 1e9, 2), "n_gpus": world}
         del stripes, buf
     return out
+
+
+# ----------------------------------------------------------------- BASELINE configs[4] over N GPUs
+def multi_gpu_repair(args, torch, dev, rank, world):
+    """BASELINE.json configs[4]: an EC16P20L2 repair tasklet (64 bids x S = 262,144, bad {0,1,16,17})
+    whose shards are spread over the job's GPUs -- shard i of every bid on rank i % N -- repaired by
+    chubaofs_amd/repair.py: all_to_all of every survivor's column slice over RCCL (xGMI), the
+    reference's Reconstruct + Verify per bid on each rank's columns (blobnode/work_shard_recover.go:
+    751-760), all_reduce of the per-bid status, all_to_all of the rebuilt slices back to their owners.
+    Gate: the bad rows are zeroed in every rank's shards before the timed calls, and after them every
+    rebuilt row equals the golden row, every bid's status is OK.  value = the tasklet's data bytes
+    (16 * S * 64) per call / call time (barrier + sync both sides, max over ranks); at N = 1 the
+    exchange is a local copy."""
+    from chubaofs_amd import codemode as cm, ec, repair
+
+    t5 = cm.GetTactic(cm.EC16P20L2)
+    n, N5, nb, S = t5.N + t5.M + t5.L, t5.N, 64, 262144
+    bad = [0, 1, 16, 17]
+    enc = ec.NewEncoder(ec.Config(CodeMode=t5, EnableVerify=False), device=dev.index)
+    # every rank builds the same tasklet (same seed) and keeps the shards it owns
+    g = torch.Generator(device=dev)
+    g.manual_seed(0xC5)
+    full = torch.empty((nb, n, S), dtype=torch.uint8, device=dev)
+    full[:, :N5] = torch.randint(0, 256, (nb, N5, S), generator=g, device=dev, dtype=torch.uint8)
+    st = enc.EncodeBatchAsync([[full[b, i] for i in range(n)] for b in range(nb)])
+    assert st == [0] * nb
+    torch.cuda.synchronize()
+    mine = repair.owned(rank, n, world)
+    local = full[:, mine].contiguous()
+    mine_bad = [e for e in bad if repair.owner(e, world) == rank]
+    golden = full[:, mine_bad].clone()
+    del full
+    torch.cuda.empty_cache()
+    for q, i in enumerate(mine):
+        if i in bad:
+            local[:, q].zero_()
+    backend = torch.distributed.get_backend() if world > 1 else "none (world 1: local copies)"
+
+    def call(timer=None, crcs=False):
+        return repair.repair_batch(enc, local, bad, rank, world, crcs=crcs, timer=timer)
+
+    for _ in range(2):
+        call()
+    torch.cuda.synchronize()
+    steps = max(5, args.steps // 2)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    outs = [call() for _ in range(steps)]
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+        el = float(tt.item())
+    # gate: every bid of every timed call verified OK (the fused pass recomputes all parities from the
+    # rebuilt data rows and compares the 18 stored ones), and the rebuilt rows, written in place into
+    # the zeroed rows of `local`, equal the golden rows
+    for r in outs:
+        assert r.status == [0] * nb, "C5 multi-GPU repair: a bid failed"
+    assert outs[-1].index == mine_bad and torch.equal(outs[-1].rows, golden), "C5 multi-GPU repair: rebuilt rows differ"
+    del outs
+    # phase breakdown (HIP events on this rank's stream) and the checksummed form, averaged
+    phases, reps = {}, 5
+    for _ in range(reps):
+        tm = {}
+        call(timer=tm)
+        for k_, v in tm.items():
+            phases[k_] = phases.get(k_, 0.0) + v / reps
+    tc0 = time.perf_counter()
+    rc = None
+    for _ in range(reps):
+        rc = call(crcs=True)
+    torch.cuda.synchronize()
+    crc_ms = (time.perf_counter() - tc0) / reps * 1e3
+    gh = golden.cpu().numpy()
+    import zlib
+    for q in range(len(mine_bad)):
+        for b in (0, nb - 1):
+            assert int(rc.crcs[b, q]) == zlib.crc32(gh[b, q].tobytes()) & 0xFFFFFFFF, "C5 multi-GPU checksum"
+    st_ = rc.stats
+    data = N5 * S * nb
+    ph = {k_: torch.tensor([v], dtype=torch.float64, device=dev) for k_, v in phases.items()}
+    if world > 1:
+        for v in ph.values():
+            torch.distributed.all_reduce(v, op=torch.distributed.ReduceOp.MAX)
+    ph = {k_: round(float(v.item()), 4) for k_, v in ph.items()}
+    xbytes = st_.get("exchange_bytes_received", 0)
+    return {
+        "workload": (f"EC16P20L2 repair tasklet, {nb} bids x S={S}, bad {{0,1,16,17}}, shard i of every bid on "
+                     f"rank i % {world}; column-split Reconstruct + Verify per bid (repair.py 'columns')"),
+        "world": world, "backend": backend,
+        "data_GBps": round(data * steps / el / 1e9, 2),
+        "ms_per_tasklet": round(el / steps * 1e3, 4),
+        "phases_ms_max_over_ranks": ph,
+        "exchange_bytes_received_per_rank": xbytes,
+        "exchange_bytes_sent_per_rank": st_.get("exchange_bytes_sent", 0),
+        "return_bytes_received_per_rank": st_.get("return_bytes_received", 0),
+        "exchange_GBps_per_rank": round(xbytes / (ph["exchange_ms"] * 1e-3) / 1e9, 2) if ph.get("exchange_ms") else None,
+        "rows_shipped_per_bid": st_.get("rows_shipped"), "columns_per_rank": st_.get("columns"),
+        "with_crc_ms_per_tasklet": round(crc_ms, 4),
+        "timing": ("data_GBps: tasklets back to back, barrier + sync both sides, max over ranks; phases: HIP events "
+                   "around the forward exchange, the decode and the return exchange + status reduction (mean of "
+                   f"{reps}, max over ranks); with_crc: the call returning the rebuilt shards' checksums (zlib-checked)"),
+        "gate": ("bad rows zeroed before the timed calls; every bid of every call verified OK; the rebuilt rows "
+                 "(in place in each rank's shards) equal the golden rows afterwards"),
+    }
 
 
 # ----------------------------------------------------------------- BASELINE configs 1, 4, 5
@@ -977,8 +1088,7 @@ def other_configs(args, torch, dev, stream, cpu):
                      "sync); async_*: cfsec_ec_reconstruct_batch_async back to back on one stream; kernel_*: per-call "
                      "HIP event pairs around the async calls"),
           "gate": "rows {0,1,16,17} zeroed before the timed calls, equal to the golden after (sync and async runs)",
-          "multi_gpu_note": "the RCCL exchange of survivors spread over 8 GPUs is chubaofs_amd/repair.py (gloo-tested; "
-                            "not run by this 1-GPU bench)"}
+          "multi_gpu_note": "the same tasklet with its shards spread over the job's GPUs: C5_multi_gpu_repair"}
     if cpu:
         G5 = O.build_matrix(N5, N5 + t5.M)
         l5 = (N5 + t5.M) // t5.AZCount

@@ -128,6 +128,8 @@ SIGNATURES = {
     "cfsec_ec_encode_batch_contig": ([_V, _V, _S, _S, _S, _I, _I, _I, _V, _V], _I),
     "cfsec_ec_reconstruct_batch_contig": ([_V, _V, _V, _V, _I, _I, _V, _V, _I, _I, _V, _V], _I),
     "cfsec_crc32_ieee_batch": ([_V, _S, _I, _V, _I, _V], _I),
+    "cfsec_crc32_combine": ([ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int64], ctypes.c_uint32),
+    "cfsec_crc32_shift": ([_V, _I, ctypes.c_int64], _I),
     "cfsec_host_alloc": ([_S, _P(_V)], _I),
     "cfsec_host_free": ([_V], _I),
     "cfsec_crc32block_encode_size": ([ctypes.c_int64, ctypes.c_int64], ctypes.c_int64),

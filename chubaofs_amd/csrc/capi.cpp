@@ -10,6 +10,8 @@
 
 namespace cfsec {
 const char* last_error_cstr();
+uint32_t crc_xpow(int64_t e);                   // gf_crc.hip: x^e mod P
+uint32_t crc_mulmod(uint32_t a, uint32_t b);  // a * b mod P
 }
 
 using cfsec::ECEncoder;
@@ -171,7 +173,7 @@ int crc32block_call(bool encode, const uint8_t* src, int64_t src_len, int64_t si
 
 extern "C" {
 
-const char* cfsec_version(void) { return "cfsec 0.3.0 (gfx950)"; }
+const char* cfsec_version(void) { return "cfsec 0.4.0 (gfx950)"; }
 
 const char* cfsec_last_error(void) { return cfsec::last_error_cstr(); }
 
@@ -563,6 +565,22 @@ int cfsec_crc32_ieee_batch(uint8_t* const* ptrs, size_t shard_size, int n, uint3
     ctx->release(ws);
     return st;
   });
+}
+
+// Checksums of concatenations (host arithmetic in GF(2)[x] mod P, gf_crc.hip's xpow / mulmod):
+// ChecksumIEEE(A || B) = ChecksumIEEE(A) * x^(8|B|) ^ ChecksumIEEE(B) -- the init and final XORs of
+// the two halves cancel (zlib's crc32_combine identity).
+uint32_t cfsec_crc32_combine(uint32_t crc1, uint32_t crc2, int64_t len2) {
+  if (len2 <= 0) return crc1 ^ crc2;
+  return cfsec::crc_mulmod(cfsec::crc_xpow(8 * len2), crc1) ^ crc2;
+}
+
+int cfsec_crc32_shift(uint32_t* words, int n, int64_t nbytes) {
+  if ((!words && n > 0) || n < 0 || nbytes < 0) return CFSEC_ERR_INVALID_ARG;
+  if (nbytes == 0) return CFSEC_OK;
+  const uint32_t xp = cfsec::crc_xpow(8 * nbytes);
+  for (int i = 0; i < n; ++i) words[i] = cfsec::crc_mulmod(xp, words[i]);
+  return CFSEC_OK;
 }
 
 // ---------------- crc32block ----------------

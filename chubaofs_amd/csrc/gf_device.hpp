@@ -148,16 +148,19 @@ __device__ __forceinline__ void st_tail(uint8_t* p, u32x4 v, size_t rem) {
     if ((size_t)i < rem) p[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
 }
 
-// Full lane chunks of LW dwords (16 or 8 bytes) for the fixed-K and 16x16-dyadic kernels.
+// Full lane chunks of LW dwords (16, 8 or 4 bytes) for the fixed-K and 16x16-dyadic kernels.
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef u32x2 u32x2_ua __attribute__((aligned(1)));
+typedef uint32_t u32_ua __attribute__((aligned(1)));
 
 template <int LW, bool NT>
 __device__ __forceinline__ void ld_chunk(const uint8_t* p, uint32_t (&x)[LW]) {
-  static_assert(LW == 2 || LW == 4, "lane chunk of 2 or 4 dwords");
+  static_assert(LW == 1 || LW == 2 || LW == 4, "lane chunk of 1, 2 or 4 dwords");
   if constexpr (LW == 4) {
     const u32x4 v = ld16<NT>(p);
     x[0] = v.x, x[1] = v.y, x[2] = v.z, x[3] = v.w;
+  } else if constexpr (LW == 1) {
+    x[0] = NT ? __builtin_nontemporal_load(reinterpret_cast<const u32_ua*>(p)) : *reinterpret_cast<const u32_ua*>(p);
   } else {
     const u32x2 v = NT ? __builtin_nontemporal_load(reinterpret_cast<const u32x2_ua*>(p))
                        : *reinterpret_cast<const u32x2_ua*>(p);
@@ -169,6 +172,9 @@ template <int LW, bool NTS>
 __device__ __forceinline__ void st_chunk(uint8_t* p, const uint32_t (&x)[LW]) {
   if constexpr (LW == 4) {
     st16_out<NTS>(p, u32x4{x[0], x[1], x[2], x[3]});
+  } else if constexpr (LW == 1) {
+    if constexpr (NTS) asm volatile("global_store_dword %0, %1, off nt" ::"v"(p), "v"(x[0]) : "memory");
+    else *reinterpret_cast<u32_ua*>(p) = x[0];
   } else if constexpr (NTS) {
     asm volatile("global_store_dwordx2 %0, %1, off nt" ::"v"(p), "v"(u32x2{x[0], x[1]}) : "memory");
   } else {

@@ -2,11 +2,20 @@
 // and the EC16P20L2 fused encode, the same 20 rows + 2 local rows); see gf_dyadic16.hpp.  The local
 // rows share the 4x4 row block's registers and take one input column at a time (pairs of columns
 // needed 256 VGPRs + AGPRs: 1 wave/SIMD; this form 214-217, 2 waves/SIMD like EC16P20's 178-201).
-#include "gf_dyadic16.hpp"
+#include <cstdlib>
+#include <cstring>
+
+#include "gf_dyadic16f.hpp"
 #include "gf_launch.hpp"
 
 #ifndef CFSEC_DY16_W
-#define CFSEC_DY16_W 2  // dwords per lane: 8-byte lane chunks
+#define CFSEC_DY16_W 2  // dwords per lane: 8-byte lane chunks (byte-form kernels)
+#endif
+#ifndef CFSEC_DY16F_W
+#define CFSEC_DY16F_W 1  // field-form kernels (gf_dyadic16f.hpp): 4-byte lane chunks
+#endif
+#ifndef CFSEC_DY16F_TPW
+#define CFSEC_DY16F_TPW 1  // field-form kernels: tiles per workgroup (2: the loop hoists the row pointers, SGPR spills)
 #endif
 
 namespace cfsec {
@@ -16,9 +25,32 @@ __global__ __launch_bounds__(256) void gf_dy16_kernel(const dev::GfArgs a) {
   dev::matvec_dy16<M, R4, E, MODE, true, W>(a);
 }
 
+template <int M, int R4, int E, MatVecMode MODE>
+__global__ __launch_bounds__(256) void gf_dy16f_kernel(const dev::GfArgs a) {
+  dev::matvec_dy16f<M, R4, E, MODE, true, CFSEC_DY16F_W, CFSEC_DY16F_TPW>(a);
+}
+
 namespace {
+// CFSEC_DY16F=0: the byte-form kernels (A/B); default: the field-form ones
+bool use_fields() {
+  static const bool on = [] {
+    const char* v = std::getenv("CFSEC_DY16F");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
 template <int M, int R4, int E, int W>
 hipError_t launch_one(MatVecMode mode, const dev::GfArgs& a, unsigned ns, hipStream_t st) {
+  if (use_fields()) {
+    constexpr uint64_t ftile = 256 * 4 * CFSEC_DY16F_W * CFSEC_DY16F_TPW;
+    const unsigned ft = (unsigned)((a.len + ftile - 1) / ftile);
+    if (mode == MatVecMode::kVerify)
+      hipLaunchKernelGGL((gf_dy16f_kernel<M, R4, E, MatVecMode::kVerify>), dim3(ft, ns), dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((gf_dy16f_kernel<M, R4, E, MatVecMode::kStore>), dim3(ft, ns), dim3(256), 0, st, a);
+    return hipGetLastError();
+  }
   constexpr uint64_t tile = 256 * 4 * W;
   const unsigned tiles = (unsigned)((a.len + tile - 1) / tile);
   if (mode == MatVecMode::kVerify)
@@ -32,6 +64,41 @@ hipError_t launch_one(MatVecMode mode, const dev::GfArgs& a, unsigned ns, hipStr
 template <int ND, int E>
 __global__ __launch_bounds__(256) void gf_dy16_repair_kernel(const dev::GfArgs a) {
   dev::repair_dy16<ND, E, true, CFSEC_DY16_W>(a);
+}
+
+template <int ND, int E>
+__global__ __launch_bounds__(256) void gf_dy16f_repair_kernel(const dev::GfArgs a) {
+  dev::repair_dy16f<ND, E, true, CFSEC_DY16F_W, CFSEC_DY16F_TPW>(a);
+}
+
+template <int E>
+hipError_t launch_repair_f(int nd, const dev::GfArgs& a, dim3 grid, hipStream_t st) {
+  switch (nd) {
+    case 0: hipLaunchKernelGGL((gf_dy16f_repair_kernel<0, E>), grid, dim3(256), 0, st, a); break;
+    case 1: hipLaunchKernelGGL((gf_dy16f_repair_kernel<1, E>), grid, dim3(256), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((gf_dy16f_repair_kernel<2, E>), grid, dim3(256), 0, st, a); break;
+    case 3: hipLaunchKernelGGL((gf_dy16f_repair_kernel<3, E>), grid, dim3(256), 0, st, a); break;
+    case 4: hipLaunchKernelGGL((gf_dy16f_repair_kernel<4, E>), grid, dim3(256), 0, st, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// The field-form repair's argument block from the byte-form one: inputs in data-row slots (slot i
+// = data row i when present, else the parity input standing in for missing row j), decode
+// coefficients permuted to slot order, src[j] = the data row of missing row j.
+void to_slot_order(int nd, int ne, const dev::GfArgs& a, dev::GfArgs& f) {
+  std::memcpy(&f, &a, sizeof(dev::GfArgs));
+  int col[16];
+  for (int i = 0; i < 16; ++i) {
+    const int s = a.src[i];
+    col[i] = s < 16 ? s : (16 - nd) + (s - 16);
+    if (s >= 16) f.src[s - 16] = (uint8_t)i;
+  }
+  for (int j = 0; j < nd; ++j)
+    for (int i = 0; i < 16; ++i) f.coef[(20 + ne + j) * 16 + i] = a.coef[(20 + ne + j) * 16 + col[i]];
+  for (uint32_t s = 0; s < a.tab; ++s)
+    for (int i = 0; i < 16; ++i) f.ptr[s * 16 + i] = a.ptr[s * 16 + col[i]];
 }
 
 template <int E>
@@ -49,6 +116,17 @@ hipError_t launch_repair_e(int nd, const dev::GfArgs& a, dim3 grid, hipStream_t 
 
 // ne extra rows: 0, or 2 (EC16P20L2's local parities checked in the global pass)
 hipError_t launch_dy16_repair_args(int nd, int ne, const dev::GfArgs& a, unsigned ns, hipStream_t st) {
+  if (use_fields()) {
+    constexpr uint64_t ftile = 256 * 4 * CFSEC_DY16F_W * CFSEC_DY16F_TPW;
+    const dim3 fgrid((unsigned)((a.len + ftile - 1) / ftile), ns);
+    static thread_local dev::GfArgs f;
+    to_slot_order(nd, ne, a, f);
+    switch (ne) {
+      case 0: return launch_repair_f<0>(nd, f, fgrid, st);
+      case 2: return launch_repair_f<2>(nd, f, fgrid, st);
+      default: return hipErrorInvalidValue;
+    }
+  }
   constexpr uint64_t tile = 256 * 4 * CFSEC_DY16_W;
   const dim3 grid((unsigned)((a.len + tile - 1) / tile), ns);
   switch (ne) {

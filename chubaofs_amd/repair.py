@@ -1,41 +1,52 @@
 """Distributed stripe repair across the GPUs of one node (BASELINE config 5).
 
-Reference: blobnode repairs a batch of bids serially -- download the surviving shards over
-HTTP, `encoder.Reconstruct(blobShards, badIdx)`, `encoder.Verify` -- in
-blobstore/blobnode/work_shard_recover.go:690-771.  Here the surviving shards of a repair batch
-already sit in HBM on the GPUs that own them and the only exchange is over xGMI through RCCL
-(torch.distributed "nccl" backend).
+Reference: blobnode repairs a tasklet bid by bid -- download the surviving shards over HTTP, then
+per bid `encoder.Reconstruct(blobShards, badIdx)` followed by `encoder.Verify(blobShards)`, failing
+the bid with errBidCanNotRecover / errEcVerifyFailed (blobstore/blobnode/work_shard_recover.go:
+706-771).  Here the shards of a tasklet already sit in HBM on the GPUs that own them and the only
+exchange is over xGMI through RCCL (torch.distributed "nccl" backend).
 
-Ownership: shard i of every bid lives on rank `i % world`.  Rank r holds `local`, a uint8
-tensor [nbids, n_owned(r), S] with its shards in index order.
+Ownership: shard i of every bid lives on rank `i % world`.  Rank r holds `local`, a uint8 tensor
+[nbids, n_owned(r), S] with its shards in index order (the bad ones' rows included: they are the
+buffers the rebuilt bytes go to, exactly blobnode's `getShardBuf` of a bad shard).
 
-Two exchange strategies, both followed by one fused reconstruct launch per rank:
+Every step of the reference's per-bid repair is byte-column local -- GF(2^8) products act on each
+byte position on its own, a Verify is false when any column mismatches, and every other status
+(checkShards, ErrTooFewShards, the LRC local passes) depends only on the lengths and the bad sets --
+so the default "columns" strategy cuts the shard length into one byte range per rank:
 
-* "columns" (default): rank r rebuilds byte columns [c_r, c_r + L_r) of every erased shard of
-  every bid.  One all_to_all_single sends each survivor's column slice to the rank that decodes
-  it (a rank receives n_surv * S / world bytes per bid, not n_surv * S), and a second one
-  returns each rebuilt slice to the erased shard's owner.
-* "allgather": all_gather of every needed survivor (every rank receives all of them); the owner
-  of each erased shard rebuilds it whole.  Moves world/2x more bytes; kept for comparison.
+  1. all_to_all_single: every shard a bid's Reconstruct or Verify reads (every shard that is not bad
+     in every bid) sends its column slice [c_r, c_r + L_r) to rank r != its owner -- (shards read) *
+     S / world bytes per rank and bid, not (shards read) * S; a rank's own shards stay in place;
+  2. rank r runs the reference's repair on its columns: cfsec_ec_reconstruct_batch_async with Verify
+     (one fused Reconstruct + Verify pass per bid on the GPU; LRC bids with a bad local shard take the
+     global then the AZ-local passes) over a shard table pointing into `local` and the receive
+     buffer, per-bid planning status + per-bid Verify flag;
+  3. all_reduce(MAX) of [status, flag] per bid: a bid fails when its columns fail anywhere;
+  4. all_to_all_single returns each rebuilt slice to the bad shard's owner, which writes it into its
+     `local` rows (its own columns were rebuilt there in step 2).
 
-Only the first k surviving shards in index order are needed: the reference decodes from exactly
-those (KRS/reedsolomon.go:1453-1465), so the exchange ships only them.
+The per-bid result is what cfsec_ec_reconstruct_batch returns on one GPU for the whole bid:
+ErrVerify where Verify is false, the Reconstruct error, or OK.  With crcs=True the rebuilt shards'
+crc32.ChecksumIEEE (blobnode's ShardCrc32 of a repaired shard, work_shard_recover.go:335-342) are
+combined from the column slices' checksums (cfsec_crc32_shift: x^(8 * bytes after the slice)).
 
-LRC modes (an ec.Encoder, e.g. EC16P20L2): the erased set may hold local parities too; the
-survivors are the first N present *global* shards (lrcencoder.go:156-160 reconstructs the global
-stripe first) and every erased shard -- data, global or local parity -- is one row over them
-(cfsec_ec_repair_rows; a local parity through its AZ's local engine over the rebuilt AZ), so the
-decode stays one launch (cfsec_ec_matvec_batch) and the exchange is unchanged.  For a consistent
-stripe this equals the reference's global-then-local Reconstruct; the reference's local pass
-would read the AZ's stored shards, which this exchange does not ship.
+"allgather" (kept for comparison): all_gather of every shard read; every rank then repairs every bid
+whole (world x the decode work, world/2 x the exchange bytes of "columns").
 """
 from __future__ import annotations
 
-from dataclasses import dataclass
-from typing import Callable, List
+import ctypes
+from dataclasses import dataclass, field
+from typing import List, Optional
 
+import numpy as np
 import torch
 import torch.distributed as dist
+
+from . import _lib
+
+SHARD_DTYPE = np.dtype([("data", "<u8"), ("len", "<u8"), ("cap", "<u8")])  # cfsec_shard
 
 
 def owner(i: int, world: int) -> int:
@@ -60,163 +71,338 @@ def column_split(S: int, world: int, align: int = 256):
 
 @dataclass
 class RepairPlan:
-    k: int
-    total: int
-    erased: List[int]
-    survivors: List[int]  # first k present, index order
+    """The shape of one tasklet repair, identical on every rank (a function of the code mode and the
+    bad sets only).
+
+    bad[b]: bid b's bad shard indices (blobnode's recoverIdxOfStripe, work_shard_recover.go:715-718).
+    rebuilt: shards bad in some bid, index order -- the rows the repair returns to their owners.
+    shipped: shards some bid's Reconstruct or Verify reads (present in at least one bid), index order.
+    slots:   the other shards (bad in every bid): no bytes cross the exchange, a rank decodes into them.
+    """
+
+    n: int
+    bad: List[List[int]]
+    rebuilt: List[int]
+    shipped: List[int]
+    slots: List[int]
+    verify: bool = True
 
     @staticmethod
-    def make(k: int, total: int, erased, nglobal: int = None) -> "RepairPlan":
-        """nglobal: the survivors come from shards [0, nglobal) (LRC: the global stripe)."""
-        er = sorted(set(int(e) for e in erased))
-        surv = [i for i in range(total if nglobal is None else nglobal) if i not in er][:k]
-        if len(surv) < k:
-            from ._lib import ErrTooFewShards
-            raise ErrTooFewShards("ErrTooFewShards")
-        return RepairPlan(k, total, er, surv)
+    def make(n: int, nbids: int, bad, verify: bool = True) -> "RepairPlan":
+        if len(bad) and isinstance(bad[0], (list, tuple, np.ndarray)):
+            per = [sorted(set(int(i) for i in b)) for b in bad]
+            if len(per) != nbids:
+                raise ValueError("one bad-index list per bid")
+        else:
+            per = [sorted(set(int(i) for i in bad))] * nbids
+        for b in per:
+            for i in b:
+                if not 0 <= i < n:
+                    raise IndexError(f"bad shard index {i} out of range [0, {n})")  # the reference panics
+        union = sorted(set().union(*per)) if per else []
+        every = sorted(set(per[0]).intersection(*per[1:])) if per else []
+        shipped = [i for i in range(n) if i not in every]
+        return RepairPlan(n, per, union, shipped, every, verify)
+
+    def order(self, world: int) -> List[int]:
+        """Row order of a rank's work buffer: the shipped shards grouped by owner rank (so each source
+        rank's block is contiguous in the all_to_all), then the slots."""
+        return sorted(self.shipped, key=lambda i: (owner(i, world), i)) + list(self.slots)
 
 
-# ---------------------------------------------------------------- exchange ("columns")
-def gather_columns(local: torch.Tensor, plan: RepairPlan, rank: int, world: int, group=None):
-    """all_to_all_single: rank r receives columns [c_r, c_r+L_r) of every needed survivor of
-    every bid.  Returns (recv, layout) with recv viewed per source rank as
-    [nbids, n_needed_from_src, L_r] blocks, concatenated in source-rank order; layout[i] =
-    (byte offset of survivor i's row for bid 0, row stride between bids)."""
-    nb, S = local.shape[0], local.shape[2]
-    cols = column_split(S, world)
-    mine = owned(rank, plan.total, world)
-    need_from = [[i for i in owned(j, plan.total, world) if i in plan.survivors] for j in range(world)]
-    # send: for each destination r, my needed survivors' column slice [c_r, c_r+L_r)
-    sel = [mine.index(i) for i in need_from[rank]]
-    sends, send_sizes = [], []
-    for r in range(world):
-        c, L = cols[r]
-        blk = local[:, sel, c:c + L].contiguous() if sel and L else local.new_empty(0)
-        sends.append(blk.reshape(-1))
-        send_sizes.append(blk.numel())
-    L_me = cols[rank][1]
-    recv_sizes = [nb * len(need_from[j]) * L_me for j in range(world)]
-    sendbuf = torch.cat(sends) if sends else local.new_empty(0)
-    recv = local.new_empty(sum(recv_sizes))
-    dist.all_to_all_single(recv, sendbuf, recv_sizes, send_sizes, group=group)
-    layout, off = {}, 0
-    for j in range(world):
-        for p, i in enumerate(need_from[j]):
-            layout[i] = (off + p * L_me, len(need_from[j]) * L_me)
-        off += recv_sizes[j]
-    return recv, layout
+@dataclass
+class RepairResult:
+    """The outcome on one rank.  The rebuilt bytes are written in place into the caller's `local`
+    (blobnode's setShardBuf of each recovered shard, work_shard_recover.go:762-769); `rows` gathers the
+    rows of `index` from it."""
+
+    local: torch.Tensor = field(repr=False)
+    index: List[int]              # the shards this rank owns that are bad in some bid (index order)
+    status: List[int]             # per bid: cfsec status (0 OK, 10 ErrVerify, or the Reconstruct error)
+    crcs: Optional[np.ndarray] = None  # [nbids, len(index)] uint32: ChecksumIEEE of rows the bid rebuilt
+    stats: dict = field(default_factory=dict)
+    qpos: List[int] = field(default_factory=list, repr=False)  # position of index[k] in local's rows
+
+    @property
+    def rows(self) -> torch.Tensor:
+        """[nbids, len(index), S]: this rank's rebuilt shards (for a bid where a shard is not bad, its
+        own bytes)."""
+        if not self.qpos:
+            return self.local.new_empty((self.local.shape[0], 0, self.local.shape[2]))
+        return self.local[:, self.qpos]
 
 
-def scatter_columns(rebuilt: torch.Tensor, plan: RepairPlan, rank: int, world: int, S: int, group=None):
-    """Inverse exchange: rebuilt [nbids, n_erased, L_rank] column slices go to each erased shard's
-    owner.  Returns [nbids, n_erased_owned(rank), S] with the whole rebuilt rows this rank owns
-    (erased shards in index order)."""
-    nb = rebuilt.shape[0]
-    cols = column_split(S, world)
-    mine_er = [e for e in plan.erased if owner(e, world) == rank]
-    sends, send_sizes = [], []
-    for o in range(world):
-        idx = [q for q, e in enumerate(plan.erased) if owner(e, world) == o]
-        blk = rebuilt[:, idx, :].contiguous() if idx else rebuilt.new_empty(0)
-        sends.append(blk.reshape(-1))
-        send_sizes.append(blk.numel())
-    recv_sizes = [nb * len(mine_er) * cols[r][1] for r in range(world)]
-    recv = rebuilt.new_empty(sum(recv_sizes))
-    dist.all_to_all_single(recv, torch.cat(sends), recv_sizes, send_sizes, group=group)
-    out = rebuilt.new_empty((nb, len(mine_er), S))
-    off = 0
-    for r in range(world):
-        c, L = cols[r]
-        if recv_sizes[r]:
-            out[:, :, c:c + L] = recv[off:off + recv_sizes[r]].view(nb, len(mine_er), L)
-        off += recv_sizes[r]
-    return out
+def _shard_table(nbids: int, n: int, addr: np.ndarray, length: int):
+    """A cfsec_shard array of nbids * n entries {addr, length, length} (every shard full length: the
+    bad ones are named by bad_idx, as blobnode passes them)."""
+    t = np.zeros(max(nbids * n, 1), SHARD_DTYPE)
+    t["data"][:nbids * n] = addr.reshape(-1)
+    t["len"][:nbids * n] = length
+    t["cap"][:nbids * n] = length
+    return t
 
 
-# ---------------------------------------------------------------- exchange ("allgather")
-def gather_all(local: torch.Tensor, plan: RepairPlan, rank: int, world: int, group=None):
-    """all_gather of every rank's needed survivors (padded to the largest count).  Returns
-    (buf [world, nbids, maxn, S], layout) with layout[i] = (src rank, position)."""
-    need_from = [[i for i in owned(j, plan.total, world) if i in plan.survivors] for j in range(world)]
-    maxn = max(len(x) for x in need_from)
-    mine = owned(rank, plan.total, world)
-    nb, S = local.shape[0], local.shape[2]
-    mine_blk = local.new_zeros((nb, maxn, S))
-    sel = [mine.index(i) for i in need_from[rank]]
-    if sel:
-        mine_blk[:, :len(sel)] = local[:, sel]
-    buf = local.new_empty((world, nb, maxn, S))
-    dist.all_gather_into_tensor(buf.view(-1), mine_blk.view(-1), group=group)
-    layout = {i: (j, p) for j in range(world) for p, i in enumerate(need_from[j])}
-    return buf, layout
+def _bad_arrays(plan: RepairPlan):
+    flat = [i for b in plan.bad for i in b]
+    off = [0]
+    for b in plan.bad:
+        off.append(off[-1] + len(b))
+    return (ctypes.c_int * max(len(flat), 1))(*flat), (ctypes.c_int * len(off))(*off)
 
 
-# ---------------------------------------------------------------- end to end (GPU)
-def repair_batch(enc, local: torch.Tensor, erased, rank: int, world: int, strategy: str = "columns",
-                 group=None, stream=None) -> torch.Tensor:
-    """Rebuild `erased` shards of every bid of a batch whose shards are spread over `world` GPUs.
+def _repair_call(enc, plan: RepairPlan, table: np.ndarray, nbids: int, flags: torch.Tensor,
+                 words: Optional[torch.Tensor], stream) -> List[int]:
+    """cfsec_ec_reconstruct_batch_async over the shard table: per-bid planning status now, Verify
+    flags (and checksums) on the stream."""
+    bad, off = _bad_arrays(plan)
+    status = (ctypes.c_int * max(nbids, 1))()
+    L = enc._L
+    st = L.cfsec_ec_reconstruct_batch_async(
+        enc._h, table.ctypes.data_as(_lib.P_SHARD), plan.n, nbids, bad, off, int(plan.verify), status,
+        flags.data_ptr(), None if words is None else words.data_ptr(), stream)
+    _lib.check(st)
+    return [int(status[b]) for b in range(nbids)]
 
-    enc: reedsolomon.ReedSolomon for (k, total-k), or an ec.Encoder (RS or LRC code mode), on this
-    rank's device.  Returns the rebuilt rows this rank owns, [nbids, n_erased_owned(rank), S],
-    erased shards in index order."""
-    if hasattr(enc, "repair_rows"):  # ec.Encoder
-        t = enc.CodeMode
-        plan = RepairPlan.make(t.N, t.N + t.M + t.L, erased, nglobal=t.N + t.M)
-    else:
-        plan = RepairPlan.make(enc.data_shards, enc.total_shards, erased)
-    nb, S = local.shape[0], local.shape[2]
-    er = plan.erased
+
+def _crc_shift(words: np.ndarray, nbytes: int) -> np.ndarray:
+    w = np.ascontiguousarray(words, dtype=np.uint32).copy()
+    _lib.check(_lib.lib().cfsec_crc32_shift(w.ctypes.data, w.size, int(nbytes)))
+    return w
+
+
+def _a2a(recv: torch.Tensor, send: torch.Tensor, rsizes, ssizes, world: int, group):
+    if world == 1:
+        if recv.numel():
+            recv.copy_(send)
+        return
+    dist.all_to_all_single(recv, send, rsizes, ssizes, group=group)
+
+
+def _max_reduce(t: torch.Tensor, world: int, group):
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+
+
+class _Marks:
+    """Phase marks of one repair: HIP events on the current stream (read after a synchronise), or the
+    host clock for CPU tensors (the gloo tests)."""
+
+    def __init__(self, timer, dev):
+        self.timer, self.cuda = timer, dev.type == "cuda"
+        self.dev, self.t = dev, {}
+
+    def mark(self, name):
+        if self.timer is None:
+            return
+        if self.cuda:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(torch.cuda.current_stream(self.dev))
+            self.t[name] = e
+        else:
+            import time
+            self.t[name] = time.perf_counter()
+
+    def finish(self):
+        if self.timer is None:
+            return
+        if self.cuda:
+            torch.cuda.synchronize(self.dev)
+            d = lambda a, b: self.t[a].elapsed_time(self.t[b])
+        else:
+            d = lambda a, b: (self.t[b] - self.t[a]) * 1e3
+        self.timer.update(exchange_ms=d("t0", "sent"), decode_ms=d("sent", "decoded"),
+                          return_ms=d("decoded", "returned"), total_ms=d("t0", "returned"))
+
+
+def gpu_decode(enc, plan: RepairPlan, row, L: int, flags: torch.Tensor, words: Optional[torch.Tensor]) -> None:
+    """Step 2 on this rank's GPU: the reference's per-bid Reconstruct + Verify over the [nbids, L] rows
+    row(i) (shard i of every bid), rebuilt rows written in place.  flags[0] receives the per-bid
+    planning status, flags[1] the Verify flags (on the stream), words the rebuilt rows' checksums."""
+    nb = flags.shape[1]
+    addr = np.empty((nb, plan.n), np.uint64)
+    bids = np.arange(nb, dtype=np.uint64)
+    for i in range(plan.n):
+        r = row(i)  # [nb, L] with its rows contiguous, any stride between bids
+        assert r.shape == (nb, L) and (L == 0 or r.stride(1) == 1)
+        addr[:, i] = np.uint64(r.data_ptr()) + bids * np.uint64(r.stride(0))
+    status = _repair_call(enc, plan, _shard_table(nb, plan.n, addr, L), nb, flags[1], words,
+                          torch.cuda.current_stream(flags.device).cuda_stream)
+    if any(status):
+        flags[0].copy_(torch.tensor(status, dtype=torch.int32))
+
+
+def _statuses(flags: torch.Tensor, S: int) -> List[int]:
+    st = flags.cpu().numpy()
+    if S == 0:
+        return [_lib.ErrShardNoData.status] * st.shape[1]  # checkShards on all-empty shards
+    return [int(st[0, b]) if st[0, b] else (_lib.ErrVerify.status if st[1, b] else 0) for b in range(st.shape[1])]
+
+
+# ---------------------------------------------------------------- the tasklet repair
+def repair_batch(enc, local: torch.Tensor, bad, rank: int, world: int, strategy: str = "columns",
+                 group=None, verify: bool = True, crcs: bool = False, timer: Optional[dict] = None,
+                 decode=gpu_decode) -> RepairResult:
+    """Repair a tasklet whose shards are spread over `world` GPUs (shard i on rank i % world).
+
+    enc: ec.Encoder (RS or LRC code mode) on this rank's device.  local: [nbids, n_owned, S] uint8 on
+    that device.  bad: one list of bad shard indices for every bid, or one list per bid.  Runs on
+    torch's current stream.  Returns this rank's rebuilt rows (every shard it owns that is bad in some
+    bid; for a bid where that shard is not bad, its own bytes), the per-bid status (identical on every
+    rank), and with crcs=True the rebuilt rows' checksums.  timer: a dict that receives the exchange,
+    decode and return times in ms (synchronises).  decode: step 2 (gpu_decode; the CPU tests pass the
+    oracle to check the exchange and the column split around it)."""
+    t = enc.CodeMode
+    n = t.N + t.M + t.L
+    nb, n_own, S = local.shape
+    mine = owned(rank, n, world)
+    if n_own != len(mine):
+        raise ValueError(f"rank {rank} holds {len(mine)} shards per bid, local has {n_own}")
+    plan = RepairPlan.make(n, nb, bad, verify)
     if strategy == "columns":
-        recv, layout = gather_columns(local, plan, rank, world, group)
-        L = column_split(S, world)[rank][1]
-        rebuilt = local.new_empty((nb, len(er), L))
-        if L:
-            _decode(enc, plan, nb, L, lambda i, b: recv.data_ptr() + layout[i][0] + b * layout[i][1],
-                    lambda e, b: rebuilt.data_ptr() + (b * len(er) + er.index(e)) * L, stream)
-        return scatter_columns(rebuilt, plan, rank, world, S, group)
+        return _repair_columns(enc, local, plan, rank, world, group, crcs, timer, decode)
     if strategy == "allgather":
-        buf, layout = gather_all(local, plan, rank, world, group)
-        mine_er = [e for e in er if owner(e, world) == rank]
-        out = local.new_empty((nb, len(mine_er), S))
-        if mine_er:
-            maxn = buf.shape[2]
-            # every erased row is rebuilt (the decode must not treat any as a survivor); the rows
-            # other ranks own land in a scratch row
-            scratch = local.new_empty((nb, S))
-
-            def dst(e, b):
-                if e in mine_er:
-                    return out.data_ptr() + (b * len(mine_er) + mine_er.index(e)) * S
-                return scratch.data_ptr() + b * S
-
-            _decode(enc, plan, nb, S,
-                    lambda i, b: buf.data_ptr() + ((layout[i][0] * nb + b) * maxn + layout[i][1]) * S,
-                    dst, stream)
-        return out
+        return _repair_allgather(enc, local, plan, rank, world, group, crcs, timer, decode)
     raise ValueError(strategy)
 
 
-def _decode(enc, plan: RepairPlan, nb: int, L: int, src: Callable, dst: Callable, stream):
-    """One fused reconstruct launch over all bids: a full shard-pointer table per bid with the
-    survivors at their exchange addresses and the erased rows at their output slots.  Present
-    rows past the first k survivors are never read; they reuse a survivor's address.  With an
-    ec.Encoder: the erased shards' rows over the survivors, one product launch."""
-    if hasattr(enc, "repair_rows"):
-        ins, rows = enc.repair_rows(plan.erased, plan.erased)
-        assert ins == plan.survivors, (ins, plan.survivors)
-        ptrs = []
-        for b in range(nb):
-            ptrs += [src(i, b) for i in ins]
-            ptrs += [dst(e, b) for e in plan.erased]
-        enc.matvec_batch(rows, ptrs, L, nb, stream=stream)
-        return
-    ptrs = []
-    for b in range(nb):
-        for i in range(plan.total):
-            if i in plan.erased:
-                ptrs.append(dst(i, b))
-            elif i in plan.survivors:
-                ptrs.append(src(i, b))
-            else:
-                ptrs.append(src(plan.survivors[0], b))
-    enc.reconstruct_batch(ptrs, L, nb, plan.erased, stream=stream)
+def _repair_columns(enc, local, plan: RepairPlan, rank, world, group, crcs, timer, decode) -> RepairResult:
+    nb, n_own, S = local.shape
+    n = plan.n
+    dev = local.device
+    marks = _Marks(timer, dev)
+    cols = column_split(S, world)
+    c_me, L_me = cols[rank]
+    mine = owned(rank, n, world)
+    qof = {i: q for q, i in enumerate(mine)}
+    # shipped shards by owner; a source's block in the receive buffer is [nb, n_from[j], L_me]
+    ship_by = [[i for i in plan.shipped if owner(i, world) == j] for j in range(world)]
+    sel = [qof[i] for i in ship_by[rank]]
+    n_me = len(sel)
+    marks.mark("t0")
+    # 1. forward exchange: to rank r != rank, my shipped shards' columns [c_r, c_r + L_r) as [nb, n_me, L_r]
+    fsend = [0 if r == rank else n_me * nb * cols[r][1] for r in range(world)]
+    frecv = [0 if j == rank else len(ship_by[j]) * nb * L_me for j in range(world)]
+    if world > 1:
+        send = local.new_empty(sum(fsend))
+        src = local if sel == list(range(n_own)) else local[:, sel]
+        o = 0
+        for r in range(world):
+            if fsend[r]:
+                c, L = cols[r]
+                send[o:o + fsend[r]].view(nb, n_me, L).copy_(src[:, :, c:c + L])
+            o += fsend[r]
+        recv = local.new_empty(sum(frecv))
+        _a2a(recv, send, frecv, fsend, world, group)
+        del send
+    else:
+        recv = local.new_empty(0)
+    # where shard i's columns live on this rank: in place in `local` (mine), the receive buffer
+    # (others' shipped shards) or a slot (others' shards bad in every bid)
+    view, o = {}, 0
+    for j in range(world):
+        if j == rank or not frecv[j]:
+            continue
+        blk = recv[o:o + frecv[j]].view(nb, len(ship_by[j]), L_me)
+        for p, i in enumerate(ship_by[j]):
+            view[i] = blk[:, p]
+        o += frecv[j]
+    others_slots = [i for i in plan.slots if owner(i, world) != rank]
+    slots = local.new_empty((nb, len(others_slots), L_me))
+    for p, i in enumerate(others_slots):
+        view[i] = slots[:, p]
+    for i in mine:
+        view[i] = local[:, qof[i], c_me:c_me + L_me]
+    marks.mark("sent")
+    # 2. the reference's Reconstruct + Verify of every bid, on this rank's columns
+    flags = torch.zeros((2, nb), dtype=torch.int32, device=dev)  # [planning status, Verify flag]
+    words = torch.zeros(nb * n, dtype=torch.int32, device=dev) if crcs else None
+    if L_me:
+        decode(enc, plan, lambda i: view[i], L_me, flags, words)
+    marks.mark("decoded")
+    # 3. a bid fails when its columns fail on any rank
+    _max_reduce(flags, world, group)
+    # 4. return exchange: the rebuilt rows' columns to their owners, [nb, n_rebuilt(owner), L_me]
+    out_idx = [e for e in plan.rebuilt if owner(e, world) == rank]
+    reb_by = [[e for e in plan.rebuilt if owner(e, world) == o_] for o_ in range(world)]
+    rsend = [0 if o_ == rank else len(reb_by[o_]) * nb * L_me for o_ in range(world)]
+    rrecv = [0 if r == rank else len(out_idx) * nb * cols[r][1] for r in range(world)]
+    if world > 1 and (sum(rsend) or sum(rrecv)):
+        send = local.new_empty(sum(rsend))
+        o = 0
+        for o_ in range(world):
+            if rsend[o_]:
+                blk = send[o:o + rsend[o_]].view(nb, len(reb_by[o_]), L_me)
+                for p, e in enumerate(reb_by[o_]):
+                    blk[:, p] = view[e]
+            o += rsend[o_]
+        recv = local.new_empty(sum(rrecv))
+        _a2a(recv, send, rrecv, rsend, world, group)
+        o = 0
+        for r in range(world):
+            if rrecv[r]:
+                c, L = cols[r]
+                blk = recv[o:o + rrecv[r]].view(nb, len(out_idx), L)
+                for p, e in enumerate(out_idx):
+                    local[:, qof[e], c:c + L] = blk[:, p]
+            o += rrecv[r]
+    marks.mark("returned")
+    res = RepairResult(local, out_idx, _statuses(flags, S), qpos=[qof[e] for e in out_idx])
+    if crcs:
+        # ChecksumIEEE(row) = XOR over ranks of ChecksumIEEE(slice_r) * x^(8 * bytes after slice_r)
+        w = _crc_shift(words.cpu().numpy().view(np.uint32), S - c_me - L_me) if L_me else np.zeros(nb * n, np.uint32)
+        if world > 1:
+            wt = torch.from_numpy(w.view(np.int32)).to(dev)
+            allw = torch.empty((world, nb * n), dtype=torch.int32, device=dev)
+            dist.all_gather_into_tensor(allw.view(-1), wt, group=group)
+            w = np.bitwise_xor.reduce(allw.cpu().numpy().view(np.uint32), axis=0)
+        w = w.reshape(nb, n)
+        res.crcs = np.stack([w[:, e] for e in out_idx], axis=1) if out_idx else np.zeros((nb, 0), np.uint32)
+    res.stats = {"exchange_bytes_sent": int(sum(fsend)), "exchange_bytes_received": int(sum(frecv)),
+                 "return_bytes_received": int(sum(rrecv)), "rows_shipped": len(plan.shipped), "columns": L_me}
+    marks.finish()
+    return res
+
+
+def _repair_allgather(enc, local, plan: RepairPlan, rank, world, group, crcs, timer, decode) -> RepairResult:
+    nb, _, S = local.shape
+    n = plan.n
+    dev = local.device
+    marks = _Marks(timer, dev)
+    mine = owned(rank, n, world)
+    ship_by = [[i for i in plan.shipped if owner(i, world) == j] for j in range(world)]
+    maxn = max(len(x) for x in ship_by)
+    marks.mark("t0")
+    blk = local.new_zeros((maxn, nb, S))
+    for p, i in enumerate(ship_by[rank]):
+        blk[p] = local[:, mine.index(i)]
+    buf = local.new_empty((world, maxn, nb, S))
+    if world > 1:
+        dist.all_gather_into_tensor(buf.view(-1), blk.view(-1), group=group)
+    else:
+        buf[0] = blk
+    del blk
+    slots = local.new_empty((len(plan.slots), nb, S))
+    marks.mark("sent")
+    where = {i: (j, p) for j in range(world) for p, i in enumerate(ship_by[j])}
+
+    def row(i):
+        if i in where:
+            return buf[where[i][0], where[i][1]]
+        return slots[plan.slots.index(i)]
+
+    flags = torch.zeros((2, nb), dtype=torch.int32, device=dev)
+    words = torch.zeros(nb * n, dtype=torch.int32, device=dev) if crcs else None
+    if S:
+        decode(enc, plan, row, S, flags, words)
+    marks.mark("decoded")
+    out_idx = [e for e in plan.rebuilt if owner(e, world) == rank]
+    for e in out_idx:
+        local[:, mine.index(e)] = row(e)
+    marks.mark("returned")
+    res = RepairResult(local, out_idx, _statuses(flags, S), qpos=[mine.index(e) for e in out_idx])
+    if crcs:
+        w = words.cpu().numpy().view(np.uint32).reshape(nb, n)
+        res.crcs = np.stack([w[:, e] for e in out_idx], axis=1) if out_idx else np.zeros((nb, 0), np.uint32)
+    res.stats = {"exchange_bytes_received": int((world - 1) * maxn * nb * S), "rows_shipped": len(plan.shipped)}
+    marks.finish()
+    return res

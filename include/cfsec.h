@@ -87,7 +87,7 @@ typedef struct cfsec_ec cfsec_ec;
 /* ---------------- library ---------------- */
 /* "cfsec MAJOR.MINOR.PATCH (gfx950)".  ABI history: 0.2.0 inserted src_len into
  * cfsec_crc32block_decode / cfsec_crc32block_decode_batch (callers built against 0.1.0 must be
- * rebuilt); 0.3.0 adds entry points only. */
+ * rebuilt); 0.3.0 and 0.4.0 add entry points only. */
 const char* cfsec_version(void);
 /* Message for the last CFSEC_ERR_DEVICE on this thread ("" if none). */
 const char* cfsec_last_error(void);
@@ -314,6 +314,15 @@ int cfsec_host_free(void* p);
 /* crc32.ChecksumIEEE of each device shard; out: host array of n uint32. Synchronous. */
 int cfsec_crc32_ieee_batch(uint8_t* const* ptrs, size_t shard_size, int n, uint32_t* out,
                            int device, void* stream);
+
+/* Checksums of concatenations (host only, no device).  cfsec_crc32_combine: crc32.ChecksumIEEE(A || B)
+ * from crc1 = ChecksumIEEE(A), crc2 = ChecksumIEEE(B) and len2 = |B| (zlib's crc32_combine).
+ * cfsec_crc32_shift: words[i] <- words[i] * x^(8 nbytes) mod P, i.e. the term a byte range's checksum
+ * contributes to the checksum of a longer run that continues for nbytes more bytes: the checksum of a
+ * shard cut into column slices is the XOR of its slices' shifted checksums (the multi-GPU repair's
+ * rebuilt shards, chubaofs_amd/repair.py; blobnode's ShardCrc32, blobnode/work_shard_recover.go:335-342). */
+uint32_t cfsec_crc32_combine(uint32_t crc1, uint32_t crc2, int64_t len2);
+int cfsec_crc32_shift(uint32_t* words, int n, int64_t nbytes);
 
 /* ---------------- crc32block framing (blobstore/common/crc32block) ---------------- */
 /* A framed object is a run of block_len-byte blocks (default 64 KiB; block_len a positive multiple
