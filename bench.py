@@ -432,6 +432,8 @@ def main():
         del batch, golden
         torch.cuda.empty_cache()
         extra["C5_multi_gpu_repair"] = multi_gpu_repair(args, torch, dev, rank, world)
+        extra["segment_reconstruct_data"] = segment_latency(args, torch, dev,
+                                                            cpu=(world == 1 and rank == 0 and not args.no_cpu))
         extra["configs"] = other_configs(args, torch, dev, stream, cpu=(world == 1 and rank == 0 and not args.no_cpu))
         extra["host_path"] = host_path(args, torch, dev, world)
 
@@ -530,6 +532,31 @@ def secondary(args, torch, enc, batch, ptrs, stream, S, nst, pitch, dev, launch_
     total = K_DATA + M_PARITY
     crcs = torch.zeros(nst * total, dtype=torch.int32, device=dev)
     crc_ms = timed(lambda b: enc.encode_crc_batch(ptrs[b], S, nst, crcs.data_ptr(), stream=stream))
+    # The same through the ec seam access calls (ec.Encoder EncodeBatch with checksums, asynchronous
+    # form on the stream): planning + the fused kernel where the group qualifies
+    from chubaofs_amd import _lib, codemode as cm, ec
+    from chubaofs_amd._shards import BatchMarshal
+    e12 = ec.NewEncoder(ec.Config(CodeMode=cm.GetTactic(cm.EC12P4), EnableVerify=False), device=dev.index)
+    bms = [BatchMarshal([[batch[b, s, i, :S] for i in range(total)] for s in range(nst)], total) for b in range(NBATCH)]
+    est = (ctypes.c_int * nst)()
+    ecrc = torch.zeros(nst * total, dtype=torch.int32, device=dev)
+
+    def ec_crc(b):
+        _lib.check(e12._L.cfsec_ec_encode_batch_async(e12._h, bms[b].arr, total, nst, est, None,
+                                                      ctypes.c_void_p(ecrc.data_ptr()), stream.cuda_stream))
+
+    ec_crc_ms = timed(ec_crc)
+    ec_crc(0)
+    torch.cuda.synchronize()
+    assert list(est) == [0] * nst
+    import zlib
+    w = ecrc.cpu().numpy().view("uint32").reshape(nst, total)
+    for s_ in (0, nst - 1):
+        for i in (0, K_DATA, total - 1):
+            assert int(w[s_, i]) == zlib.crc32(batch[0, s_, i, :S].cpu().numpy().tobytes()) & 0xFFFFFFFF, "ec seam crc"
+    out.update({"ec_seam_encode_crc_ms": round(ec_crc_ms, 4),
+                "ec_seam_encode_crc_roofline_frac": frac(launch_bytes, ec_crc_ms)})
+    del bms, ecrc
     out.update({
         "encode_data_GBps": rate(data_bytes, enc_ms), "encode_roofline_frac": frac(launch_bytes, enc_ms),
         "reconstruct_data_GBps": rate(data_bytes, rec_ms), "reconstruct_roofline_frac": frac(launch_bytes, rec_ms),
@@ -729,6 +756,93 @@ def multi_gpu_repair(args, torch, dev, rank, world):
     }
 
 
+# ----------------------------------------------------------------- segment ReconstructData latency
+def segment_latency(args, torch, dev, cpu):
+    """access's degraded read of a byte range (access/stream_get.go:420-427): ReconstructData over
+    every shard's segment [off, off + seg) of a blob with two data shards bad, one call per read --
+    a latency path.  Per-call wall time (median of repeated calls) for segments in pageable host
+    memory (what a Go caller has), page-locked host memory (cfsec_host_alloc) and HBM, with the
+    klauspost-strategy CPU port on the same segment (4 threads as the reference with GFNI, and 1).
+    `gpu_wins_from_bytes` per mode: the smallest measured segment size at which the GPU call beats
+    the CPU port -- below it a caller should decode on the CPU."""
+    import numpy as np
+
+    from chubaofs_amd import _lib, codemode as cm, ec
+    out = {"workload": ("ReconstructData of one segment per shard at offset 4096 inside a 64 MiB blob, bad data "
+                        "shards {0, 1}; median of repeated calls"), "modes": {}}
+    reps = 40
+    if cpu:
+        from oracle import oracle as O
+
+    def med(fn, n=reps):
+        fn()
+        ts = []
+        for _ in range(n):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        ts.sort()
+        return ts[len(ts) // 2] * 1e6
+
+    for name, mode in (("EC6P6", cm.EC6P6), ("EC12P4", cm.EC12P4)):
+        t = cm.GetTactic(mode)
+        N, n = t.N, t.N + t.M
+        enc = ec.NewEncoder(ec.Config(CodeMode=t, EnableVerify=False), device=dev.index)
+        rows = {}
+        for seg in (4096, 65536, 1 << 20):
+            off = 4096
+            S = off + seg
+            rng = np.random.default_rng(seg + N)
+            full = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(N)] + [np.zeros(S, np.uint8) for _ in range(t.M)]
+            enc.Encode(full)
+            gold = [x[off:off + seg].copy() for x in full]
+            bad = [0, 1]
+            r = {}
+            pin = _lib.pinned_empty(n * seg)
+            pinned = [pin[i * seg:(i + 1) * seg] for i in range(n)]
+            devt = [torch.from_numpy(g.copy()).to(dev) for g in gold]
+            for kind in ("pageable", "pinned", "device"):
+                if kind == "pageable":
+                    segs = [x[off:off + seg] for x in full]
+                elif kind == "pinned":
+                    for i in range(n):
+                        pinned[i][:] = gold[i]
+                    segs = list(pinned)
+                else:
+                    segs = list(devt)
+
+                def call():
+                    v = list(segs)
+                    enc.ReconstructData(v, bad)
+                    if kind == "device":
+                        torch.cuda.synchronize()
+
+                r[kind + "_us"] = round(med(call), 1)
+                got = [np.asarray(x.cpu().numpy() if kind == "device" else x) for x in segs[:N]]
+                assert all(np.array_equal(got[i], gold[i]) for i in range(N)), f"segment {name} {seg} {kind}"
+            if cpu:
+                G = O.build_matrix(N, n)
+                valid = [i for i in range(n) if i not in bad][:N]
+                err, dec = O.invert(G[valid])
+                assert err == 0
+                ins = [gold[i] for i in valid]
+                outs = [np.zeros(seg, np.uint8) for _ in bad]
+                for thr in (4, 1):
+                    r[f"cpu_port_{thr}t_us"] = round(med(lambda: O.simd_code(dec[bad], ins, outs, thr)), 1)
+                assert all(np.array_equal(outs[j], gold[b]) for j, b in enumerate(bad))
+            rows[str(seg)] = r
+            del pin, pinned, devt
+        wins = {}
+        if cpu:
+            for kind in ("pageable", "pinned", "device"):
+                w = [int(s) for s, r in rows.items() if r[kind + "_us"] < r["cpu_port_4t_us"]]
+                wins[kind] = min(w) if w else None
+        out["modes"][name] = {"by_segment_bytes": rows, "gpu_wins_from_bytes": wins}
+    out["note"] = ("gpu_wins_from_bytes: smallest measured segment where the GPU call (wall, incl. staging and "
+                   "sync) beats the 4-thread CPU port; None: the CPU port wins at every measured size")
+    return out
+
+
 # ----------------------------------------------------------------- BASELINE configs 1, 4, 5
 def cpu_rate(fn, seconds):
     """Calls of fn per second over ~seconds (after one warm call)."""
@@ -923,13 +1037,32 @@ def other_configs(args, torch, dev, stream, cpu):
     assert list(st4) == [0] * nb4
     ra = gated_calls(torch, stream, enc4a, NBATCH, secs, zero4(par4), check4(par4), sync_call=False)
     assert list(st4) == [0] * nb4
+    # access's Put checksums every shard of the encoded blob (stream_put.go:249-253): the same calls
+    # returning all 18 checksums per blob
+    cw4 = torch.zeros((NBATCH, nb4 * tot4), dtype=torch.int32, device=dev)
+
+    def enc4c(i):
+        bm = bms[i % NBATCH]
+        _lib.check(e4._L.cfsec_ec_encode_batch_async(e4._h, bm.arr, tot4, nb4, st4, None,
+                                                     ctypes.c_void_p(cw4[i % NBATCH].data_ptr()), stream.cuda_stream))
+
+    rc4 = gated_calls(torch, stream, enc4c, NBATCH, secs, zero4(par4), check4(par4), sync_call=False)
+    assert list(st4) == [0] * nb4
+    w4 = cw4[0].cpu().numpy().view(np.uint32).reshape(nb4, tot4)
+    g4h = gold4[0].cpu().numpy()
+    for s_ in (0, nb4 - 1):
+        for i in range(tot4):
+            assert int(w4[s_, i]) == zlib.crc32(g4h[s_, i].tobytes()) & 0xFFFFFFFF, f"C4 checksum {s_} {i}"
     enc_bytes = tot4 * S4 * nb4
     c4 = {"workload": f"EC6P10L2 fused LRC encode (global + 2 local parities in one pass), {nb4} blobs of 4 MiB (S={S4})",
           "encode_data_GBps": round(N * S4 * nb4 * rs["calls_per_s"] / 1e9, 1),
           "encode_roofline_frac": round(enc_bytes * rs["calls_per_s"] / 1e9 / HBM_PEAK_GBPS, 4),
           "encode_async_data_GBps": round(N * S4 * nb4 * ra["calls_per_s"] / 1e9, 1),
           "encode_kernel_ms": round(ra["kernel_ms_per_call"], 4),
-          "encode_kernel_roofline_frac": frac(enc_bytes, ra["kernel_ms_per_call"])}
+          "encode_kernel_roofline_frac": frac(enc_bytes, ra["kernel_ms_per_call"]),
+          "encode_crc_kernel_ms": round(rc4["kernel_ms_per_call"], 4),
+          "encode_crc_kernel_roofline_frac": frac(enc_bytes, rc4["kernel_ms_per_call"]),
+          "encode_crc_over_kernel": round(rc4["kernel_ms_per_call"] / ra["kernel_ms_per_call"], 3)}
     # AZ-local repair: AZ0's local stripe (8 + 1 shards) per blob, local index 0 lost
     idx0, _, _ = t4.LocalStripeInAZ(0)
     lsz = len(idx0)
@@ -962,6 +1095,18 @@ def other_configs(args, torch, dev, stream, cpu):
                           "launch + sync); *_async_*: cfsec_ec_*_batch_async back to back on one stream; "
                           "*_kernel_*: per-call HIP event pairs around the async calls (device time only)"),
                "gate": "rows each timed call writes zeroed before, equal to the golden after (sync and async runs)"})
+    # the floor under any synchronous call: one trivial kernel launched and waited for (HIP launch +
+    # completion latency), the part of a synchronous call's time no host-side planning cache removes
+    tiny = torch.zeros(64, dtype=torch.int32, device=dev)
+    fl = []
+    for _ in range(200):
+        t0 = time.perf_counter()
+        tiny.add_(1)
+        torch.cuda.synchronize()
+        fl.append(time.perf_counter() - t0)
+    fl.sort()
+    c4["sync_floor_us"] = round(fl[len(fl) // 2] * 1e6, 1)
+    c4["local_repair_sync_call_us"] = round(1e6 / rs["calls_per_s"], 1)
     if cpu:
         G = O.build_matrix(N, N + M)
         Lm = O.build_matrix(lsz - 1, lsz)

@@ -174,10 +174,10 @@ bool fused_crc_group(const Group& g, uint32_t* dcrc, size_t nwords, const std::m
   const size_t nt = g.tasks.size();
   if (!kOn || p.dy16 || p.nstore != m || m == 0 || nt == 0) return false;
   const uint64_t len = g.lens[0];
-  if (len == 0 || !matvec_crc_supported(k, m, len)) return false;
+  if (len == 0 || !matvec_crc_supported(k, m, len, p.rows.v.data())) return false;
   const StripeTask* t0 = g.tasks[0];
   const int mode = t0->crc;  // 2: inputs and outputs, 1: the stored outputs only
-  if (mode == 0) return false;
+  if (mode == 0 || (m > 6 && mode != 2)) return false;  // m = 12 (EC6P10L2 encode): every shard checksummed
   int64_t cs = 0;
   for (size_t i = 0; i < nt; ++i) {
     const StripeTask* t = g.tasks[i];

@@ -876,7 +876,7 @@ Status RSEngine::reconstruct_batch(uint8_t* const* ptrs, size_t S, int nstripes,
 // CRC kernel over the same shards (one more read of each).
 static Status matvec_with_crc(const MatVecJob& job, uint8_t* const* ptrs, int total, const std::vector<int>& slot,
                               size_t S, uint32_t* crcs, hipStream_t stream) {
-  if (matvec_crc_supported(job.k, job.m, S))
+  if (matvec_crc_supported(job.k, job.m, S, job.coef))
     return hip_status(launch_matvec_crc(job, crcs, total, slot.data(), stream), "launch_matvec_crc");
   Status st = hip_status(launch_matvec(job, stream), "launch_matvec");
   if (st != CFSEC_OK) return st;
@@ -1232,17 +1232,22 @@ Status LrcEncoder::reconstruct(cfsec_shard* shards, int n, const int* bad, int n
       local_bad[idc].push_back(b - N - M - L / AZ * idc + (N + M) / AZ);
     }
   }
+  // task.Run (util/task/task.go:43-73) runs every AZ's local pass to the end and returns the first
+  // error sent; the AZs are disjoint, so running them in AZ order and keeping the lowest AZ's error
+  // gives the same bytes (the reference's pick among several failing AZs is scheduling-dependent,
+  // oracle/ec_oracle.py takes the lowest AZ as well).
+  Status first = CFSEC_OK;
   for (auto& kv : local_bad) {
     // Go copies the slice headers into a fresh [][]byte (lrcencoder.go:236-243); the
     // rebuilt bytes land in the shared buffers, the caller's headers keep their length.
     std::vector<cfsec_shard> ls;
     for (int g : shards_in_idc(kv.first)) ls.push_back(shards[g]);
     st = init_bad_shards(ls.data(), (int)ls.size(), kv.second);
-    if (st != CFSEC_OK) return st;
-    st = local_->reconstruct(ls.data(), (int)ls.size(), false, mem, s);
-    if (st != CFSEC_OK) return st;
+    if (st == CFSEC_OK) st = local_->reconstruct(ls.data(), (int)ls.size(), false, mem, s);
+    if (st == CFSEC_ERR_DEVICE) return st;  // the device failed: nothing further is meaningful
+    if (first == CFSEC_OK) first = st;
   }
-  return CFSEC_OK;
+  return first;
 }
 
 Status LrcEncoder::reconstruct_data(cfsec_shard* shards, int n, const int* bad, int nbad, int mem,

@@ -186,17 +186,24 @@ hipError_t launch_crc(int k, int m, const GfCrcArgs& a, dim3 grid, hipStream_t s
 
 }  // namespace
 
-bool matvec_crc_supported(int k, int m, size_t len) {
-  // the fused kernels exist for the input counts of the code modes of SURVEY §8
+bool matvec_crc_supported(int k, int m, size_t len, const uint8_t* coef) {
+  // the fused kernels exist for the input counts of the code modes of SURVEY §8, m <= 6 outputs, and
+  // EC6P10L2's fused encode (6 x (10 dyadic + 2 local) rows)
   const bool crc_k = k == 6 || k == 8 || k == 12 || k == 16 || k == 18;
-  return crc_k && m >= 1 && m <= crcdev::kMaxM && len <= 0xFFFFFFFFull - crcdev::kTile;
+  if (!crc_k || m < 1 || len > 0xFFFFFFFFull - crcdev::kTile) return false;
+  if (m <= 6) return true;
+  if (k == 6 && m == 12 && coef) {
+    const DyPlan dp = dyadic_plan(coef, m, k);
+    return dp.B == 2 && dp.E == 2;
+  }
+  return false;
 }
 
 uint32_t crc32_shift_ones(size_t len) { return mulmod(xpow(8 * (int64_t)len), 0xFFFFFFFFu) ^ 0xFFFFFFFFu; }
 
 hipError_t launch_matvec_crc(const MatVecJob& job, uint32_t* crc, int crc_stride, const int* slot,
                              hipStream_t stream, bool zero) {
-  if (job.mode != MatVecMode::kStore || !matvec_crc_supported(job.k, job.m, job.len) || !crc || !slot ||
+  if (job.mode != MatVecMode::kStore || !matvec_crc_supported(job.k, job.m, job.len, job.coef) || !crc || !slot ||
       crc_stride <= 0 || crc_stride > 256 || job.nstripes < 0 || !job.coef || !job.in || !job.out)
     return hipErrorInvalidValue;
   const int k = job.k, m = job.m;
@@ -220,11 +227,16 @@ hipError_t launch_matvec_crc(const MatVecJob& job, uint32_t* crc, int crc_stride
     for (int c = 0; c < k; ++c) a.coef[r * k + c] = job.coef[(size_t)r * k + c];
   // matrices of dyadic blocks the v_perm kernel has a reduced-product form for: 4 outputs of 4x4
   // blocks (EC12P4 / EC16P4 encode, coset-aligned repairs), 6 x 6 of 2x2 blocks (EC6P6 encode)
-  const DyPlan dp = (m == 4 && k % 4 == 0) || (m == 6 && k == 6) ? dyadic_plan(a.coef, m, k) : DyPlan{0, 0};
+  const DyPlan dp = (m == 4 && k % 4 == 0) || (k == 6 && (m == 6 || m == 12)) ? dyadic_plan(a.coef, m, k)
+                                                                             : DyPlan{0, 0};
 #ifndef CFSEC_CRC_DY2
 #define CFSEC_CRC_DY2 1  // A/B switch for the 2x2 form
 #endif
   int dy = dp.E == 0 && ((dp.B == 4 && m == 4) || (CFSEC_CRC_DY2 && dp.B == 2 && m == 6 && k == 6)) ? dp.B : 0;
+  if (k == 6 && m == 12 && dp.B == 2 && dp.E == 2) {  // EC6P10L2 fused encode + its 18 checksums
+    if (!cin) return hipErrorInvalidValue;             // (the only form instantiated: inputs checksummed)
+    dy = 2;
+  }
   // m <= 4, k <= 16: the lookup-product kernel (gf_crc_lds_kernel; CFSEC_CRC_LDS=0 keeps the v_perm
   // kernels for A/B): EC12P4 8 x 64 MiB encode + 16 checksums 225-230 -> 200 us
   // (profiles/r03/crc_lds_ab*.txt)

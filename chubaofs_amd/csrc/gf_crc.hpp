@@ -36,7 +36,7 @@ using dev::u32x4;
 
 constexpr uint32_t kPoly = 0xEDB88320u;
 constexpr int kTile = 4096;            // bytes per row per tile: 256 threads x 16 B
-constexpr int kMaxK = 18, kMaxM = 6, kPtrSlots = 96, kMaxGroups = 384;
+constexpr int kMaxK = 18, kMaxM = 12, kPtrSlots = 96, kMaxGroups = 384;  // m = 12: EC6P10L2's fused encode
 constexpr int kByteTabWords = 20 * 256;  // F0..F15: bytes of a 16-B piece;  G0..G3: register bytes
 constexpr int kNibTabWords = 40 * 16;    // N0..N31: nibbles of a 16-B piece;  H0..H7: register nibbles
 constexpr int kFiveFields = 7;           // per 32-bit word: six 5-bit fields + one 2-bit field
@@ -298,22 +298,34 @@ __device__ __forceinline__ void crc_tile(uint64_t len, const u32x4* tab01, const
 // column block ahead, the CRC step of each block's input rows after its product.  The kernel is
 // VALU-issue-bound (§4.1 of DESIGN.md), so fewer products pay even at 3 waves per SIMD (144 VGPRs):
 // EC12P4 8 x 64 MiB encode + CRC 242 -> 224 us (profiles/r02/fused_crc_ab.txt).
-template <int K, int M, int B, bool CIN>
+// E > 0: the last E of the M rows are plain rows over the inputs (the local parities of the fused
+// EC6P10L2 encode: 10 dyadic global rows + 2 local rows, every one of its 18 shards checksummed as
+// access's Put does, stream_put.go:249-253), on the loaded inputs of each column block.
+template <int K, int M, int B, bool CIN, int E = 0>
 __device__ __forceinline__ void crc_tile_dy(uint64_t len, const u32x4* tab01, const uint32_t* tab2,
                                             const uint32_t* ct, const uint8_t* const (&row)[K + M],
                                             uint32_t off, uint32_t (&R)[(CIN ? K : 0) + M]) {
-  constexpr int RO = CIN ? K : 0, KB = K / B, MB = M / B, NC = dev::Dy<B>::NC;
-  static_assert(K % B == 0 && M % B == 0 && (B == 2 || (B == 4 && M == 4)), "dyadic shape");
+  constexpr int MD = M - E;
+  constexpr int RO = CIN ? K : 0, KB = K / B, MB = MD / B, NC = dev::Dy<B>::NC, ND = MB * KB * NC;
+  static_assert(K % B == 0 && MD % B == 0 && (B == 2 || (B == 4 && M == 4 && E == 0)), "dyadic shape");
+  static_assert(E == 0 || B == 2, "plain rows ride along the 2x2-dyadic product");
   uint32_t acc[M][4];
 #pragma unroll
   for (int r = 0; r < M; ++r)
 #pragma unroll
     for (int w = 0; w < 4; ++w) acc[r][w] = 0u;
   const auto product = [&](int cb, uint32_t (&xs)[B][4]) {
-    if constexpr (B == 4)
+    if constexpr (B == 4) {
       dev::dy_col4<1, true>(acc, xs[0], xs[1], xs[2], xs[3], tab01 + cb * NC, tab2 + cb * NC, KB * NC);
-    else
-      dev::dy_col2<MB, true>(acc, xs[0], xs[1], tab01 + cb * NC, tab2 + cb * NC, KB * NC);
+    } else {
+      dev::dy_col2<MB, true>(reinterpret_cast<uint32_t(&)[MD][4]>(acc), xs[0], xs[1], tab01 + cb * NC,
+                             tab2 + cb * NC, KB * NC);
+      if constexpr (E > 0) {
+        const int c = B * cb;
+        dev::mac_pair_k<E>(reinterpret_cast<uint32_t(&)[E][4]>(acc[MD]), xs[0], xs[1], tab01 + ND + c * E,
+                           tab2 + ND + c * E, tab01 + ND + (c + 1) * E, tab2 + ND + (c + 1) * E);
+      }
+    }
   };
   if ((uint64_t)off + dev::kLaneBytes <= len) {
     uint32_t x[K][4];
@@ -409,9 +421,10 @@ __device__ __forceinline__ void crc_epilogue(const GfCrcArgs& a, const uint32_t 
   }
 }
 
-// DY: a.coef is M x K made of DY x DY dyadic blocks (checked by the launcher; 0: plain product); the
-// register allocation aims at 4 waves per SIMD, 3 for the dyadic products
-template <int K, int M, bool CIN, int DY>
+// DY: a.coef is M x K made of DY x DY dyadic blocks (checked by the launcher; 0: plain product),
+// the last E rows plain (DY = 2 only); the register allocation aims at 4 waves per SIMD, 3 for the
+// dyadic products
+template <int K, int M, bool CIN, int DY, int E = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DY ? 3 : 4, 8))) void gf_crc_kernel(const GfCrcArgs a) {
   constexpr int NR = (CIN ? K : 0) + M;  // checksummed rows
   __shared__ u32x4 tab01[K * M];
@@ -419,8 +432,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DY ? 3 : 4,
   __shared__ uint32_t ct[kFusedTabWords];
   __shared__ uint32_t red[4][NR];
   constexpr bool kDy = DY != 0;
-  if constexpr (kDy) dev::build_dy_tables<K, M, (DY ? DY : 1), M / (DY ? DY : 1), 0>(a.coef, tab01, tab2);
-  else dev::build_tables<M>(K, M, a.coef, tab01, tab2);
+  if constexpr (kDy)
+    dev::build_dy_tables<K, M - E, (DY ? DY : 1), (M - E) / (DY ? DY : 1), E>(a.coef, tab01, tab2);
+  else
+    dev::build_tables<M>(K, M, a.coef, tab01, tab2);
   for (int i = threadIdx.x; i < kFusedTabWords; i += 256) ct[i] = a.tabs[kFusedTabBase + i];
   __syncthreads();
 
@@ -444,7 +459,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DY ? 3 : 4,
     const uint32_t off = t * kTile + lanepos;
     // the next tile is full for this thread: its first rows are fetched during this one
     const bool next = t + 1 < t1 && (uint64_t)off + kTile + dev::kLaneBytes <= a.len;
-    if constexpr (kDy) crc_tile_dy<K, M, DY, CIN>(a.len, tab01, tab2, ct, row, off, R);
+    if constexpr (kDy) crc_tile_dy<K, M, DY, CIN, E>(a.len, tab01, tab2, ct, row, off, R);
     else crc_tile<K, M, CIN>(a.len, tab01, tab2, ct, row, off, pre, next, x, R);
     pre = next && (uint64_t)off + dev::kLaneBytes <= a.len;
   }
@@ -800,6 +815,12 @@ hipError_t launch_crc_k(int m, const GfCrcArgs& a, dim3 grid, hipStream_t st, in
     if (dy == 2 && m == 6) {
       hipLaunchKernelGGL((gf_crc_kernel<K, 6, CIN, 2>), grid, dim3(256), 0, st, a);
       return hipGetLastError();
+    }
+    if constexpr (CIN) {
+      if (dy == 2 && m == 12) {  // EC6P10L2 fused encode (every shard checksummed): 10 dyadic + 2 local rows
+        hipLaunchKernelGGL((gf_crc_kernel<K, 12, CIN, 2, 2>), grid, dim3(256), 0, st, a);
+        return hipGetLastError();
+      }
     }
   }
   if (dy) return hipErrorInvalidValue;

@@ -31,14 +31,17 @@ __global__ __launch_bounds__(256) void gf_dy16f_kernel(const dev::GfArgs a) {
 }
 
 namespace {
-// CFSEC_DY16F=0: the byte-form kernels (A/B); default: the field-form ones
-bool use_fields() {
-  static const bool on = [] {
+// The 16x16-dyadic kernel forms (A/B): CFSEC_DY16F=1 the field-form kernels (gf_dyadic16f.hpp),
+// 2 the byte-form repair with inputs in data-row slots (default), 0 the byte-form kernels as in
+// round 3
+int dy16_form() {
+  static const int f = [] {
     const char* v = std::getenv("CFSEC_DY16F");
-    return !(v && v[0] == '0');
+    return v && *v ? std::atoi(v) : 2;
   }();
-  return on;
+  return f;
 }
+bool use_fields() { return dy16_form() == 1; }
 
 template <int M, int R4, int E, int W>
 hipError_t launch_one(MatVecMode mode, const dev::GfArgs& a, unsigned ns, hipStream_t st) {
@@ -101,6 +104,24 @@ void to_slot_order(int nd, int ne, const dev::GfArgs& a, dev::GfArgs& f) {
     for (int i = 0; i < 16; ++i) f.ptr[s * 16 + i] = a.ptr[s * 16 + col[i]];
 }
 
+template <int ND, int E>
+__global__ __launch_bounds__(256) void gf_dy16s_repair_kernel(const dev::GfArgs a) {
+  dev::repair_dy16<ND, E, true, CFSEC_DY16_W, true>(a);
+}
+
+template <int E>
+hipError_t launch_repair_s(int nd, const dev::GfArgs& a, dim3 grid, hipStream_t st) {
+  switch (nd) {
+    case 0: hipLaunchKernelGGL((gf_dy16s_repair_kernel<0, E>), grid, dim3(256), 0, st, a); break;
+    case 1: hipLaunchKernelGGL((gf_dy16s_repair_kernel<1, E>), grid, dim3(256), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((gf_dy16s_repair_kernel<2, E>), grid, dim3(256), 0, st, a); break;
+    case 3: hipLaunchKernelGGL((gf_dy16s_repair_kernel<3, E>), grid, dim3(256), 0, st, a); break;
+    case 4: hipLaunchKernelGGL((gf_dy16s_repair_kernel<4, E>), grid, dim3(256), 0, st, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 template <int E>
 hipError_t launch_repair_e(int nd, const dev::GfArgs& a, dim3 grid, hipStream_t st) {
   switch (nd) {
@@ -129,6 +150,15 @@ hipError_t launch_dy16_repair_args(int nd, int ne, const dev::GfArgs& a, unsigne
   }
   constexpr uint64_t tile = 256 * 4 * CFSEC_DY16_W;
   const dim3 grid((unsigned)((a.len + tile - 1) / tile), ns);
+  if (dy16_form() == 2) {
+    static thread_local dev::GfArgs f;
+    to_slot_order(nd, ne, a, f);
+    switch (ne) {
+      case 0: return launch_repair_s<0>(nd, f, grid, st);
+      case 2: return launch_repair_s<2>(nd, f, grid, st);
+      default: return hipErrorInvalidValue;
+    }
+  }
   switch (ne) {
     case 0: return launch_repair_e<0>(nd, a, grid, st);
     case 2: return launch_repair_e<2>(nd, a, grid, st);

@@ -266,7 +266,12 @@ __device__ __forceinline__ void matvec_dy16(const GfArgs& a) {
 // ptr per stripe: the 16 inputs, then ND + 20 + E outputs (the missing data rows, parity rows
 // 0..19, the extra rows); src[i] = the input slot of data row i, or 16 + j for missing data row j;
 // pstore / pcmp: parity (bits 0..19) and extra (20..) rows stored / compared.
-template <int ND, int E, bool PIN = true, int W = 2>
+// SLOTS: the inputs come in data-row slots (slot i = data row i when present, else the parity row
+// standing in for a missing one; the decode rows' coefficients in slot order; src[j] = the data row
+// of missing row j, gf_dy16.hip to_slot_order): missing row j then replaces its slot's input through
+// one uniform branch, where the run-time permutation of the first-16-present order costs v_cndmask
+// selects on every data row (~100 VALU ops per dword column, PMC: profiles/r04).
+template <int ND, int E, bool PIN = true, int W = 2, bool SLOTS = false>
 __device__ __forceinline__ void repair_dy16(const GfArgs& a) {
   constexpr int K = 16, NDY = kDy16Leaves + 36 + K * E, NT = NDY + K * (ND > 0 ? ND : 1), MO = ND + 20 + E;
   constexpr uint32_t kLane = 4 * W;
@@ -314,21 +319,38 @@ __device__ __forceinline__ void repair_dy16(const GfArgs& a) {
       }
 #pragma unroll
       for (int j = 0; j < ND; ++j) st_lane<W>(out[j] + sbase + off, full, rem, rec[j]);
-      // the data rows in order, in place: data row i is input slot i - (missing rows below i),
-      // so from the top down no slot is overwritten before it is read
+      if constexpr (SLOTS) {
+        // missing row j replaces the parity input in its slot: a uniform branch (the asm keeps it
+        // one -- as a select it costs W v_cndmask per slot)
 #pragma unroll
-      for (int i = K - 1; i >= 0; --i) {
-        const uint32_t s = a.src[i];
+        for (int j = 0; j < ND; ++j) {
+          const uint32_t m = a.src[j];
 #pragma unroll
-        for (int d = 0; d <= ND; ++d)
-          if (i - d >= 0 && s == (uint32_t)(i - d))
+          for (int i = 0; i < K; ++i) {
+            if (m == (uint32_t)i) {
+              asm volatile("" ::: "memory");
 #pragma unroll
-            for (int w = 0; w < W; ++w) x[i][w] = x[i - d][w];
+              for (int w = 0; w < W; ++w) x[i][w] = rec[j][w];
+            }
+          }
+        }
+      } else {
+        // the data rows in order, in place: data row i is input slot i - (missing rows below i),
+        // so from the top down no slot is overwritten before it is read
 #pragma unroll
-        for (int j = 0; j < ND; ++j)
-          if (s == (uint32_t)(K + j))
+        for (int i = K - 1; i >= 0; --i) {
+          const uint32_t s = a.src[i];
 #pragma unroll
-            for (int w = 0; w < W; ++w) x[i][w] = rec[j][w];
+          for (int d = 0; d <= ND; ++d)
+            if (i - d >= 0 && s == (uint32_t)(i - d))
+#pragma unroll
+              for (int w = 0; w < W; ++w) x[i][w] = x[i - d][w];
+#pragma unroll
+          for (int j = 0; j < ND; ++j)
+            if (s == (uint32_t)(K + j))
+#pragma unroll
+              for (int w = 0; w < W; ++w) x[i][w] = rec[j][w];
+        }
       }
       sb();
     }
@@ -341,7 +363,10 @@ __device__ __forceinline__ void repair_dy16(const GfArgs& a) {
       uint8_t* p = out[ND + r] + sbase + off;
       const bool cmp = (pcmp >> r) & 1u;
       uint32_t y[W];
-      ld_lane<W>(cmp ? p : spare, full, rem, y);
+      if constexpr (SLOTS)  // the row base chosen on the scalar unit, then the lane offset
+        ld_lane<W>((cmp ? (const uint8_t*)out[ND + r] : in[0]) + sbase + off, full, rem, y);
+      else
+        ld_lane<W>(cmp ? p : spare, full, rem, y);
       const uint32_t msk = cmp ? ~0u : 0u;
 #pragma unroll
       for (int w = 0; w < W; ++w) diff |= (y[w] ^ v[w]) & msk;

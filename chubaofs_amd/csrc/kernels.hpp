@@ -86,8 +86,9 @@ hipError_t launch_crc32_to(const uint8_t* const* ptrs, size_t len, int n, uint32
 // checksum in device word crc[s * crc_stride + slot[i]] of stripe s.  slot[0] < 0 skips the inputs
 // (checksum the outputs only).  Every word of crc[0 .. nstripes*crc_stride) is zeroed first, so
 // words no row maps to read 0 (zero = false: the caller zeroed them; the kernel XORs into them).
-// Only for matvec_crc_supported shapes (k in {6,8,12,16,18}, m <= 6).
-bool matvec_crc_supported(int k, int m, size_t len);
+// Only for matvec_crc_supported shapes (k in {6,8,12,16,18}, m <= 6; and k = 6, m = 12 when coef is
+// EC6P10L2's fused LRC matrix: 10 rows of 2x2 dyadic blocks + 2 plain rows).
+bool matvec_crc_supported(int k, int m, size_t len, const uint8_t* coef = nullptr);
 hipError_t launch_matvec_crc(const MatVecJob& job, uint32_t* crc, int crc_stride, const int* slot,
                              hipStream_t stream, bool zero = true);
 // shift(~0, len) ^ ~0: XOR it into a raw (zero-preset) CRC of len bytes to get crc32.ChecksumIEEE.

@@ -9,10 +9,12 @@
 //
 // Go releases.  CubeFS builds with Go 1.17 (go.mod:3, docker/Dockerfile:1), whose cgo rules forbid a
 // C array holding Go pointers.  So every call first looks for the one-allocation layout that
-// ec.Buffer and Split produce (stripeOf: shard i at base + i*stride) and passes that stripe as a
-// single pointer to the cfsec_*_contig entry points -- legal on every Go release.  Any other shard
-// vector goes through callVec: with Go >= 1.21 the buffers are pinned (runtime.Pinner, vec_pin.go),
-// before that they are staged through C memory (vec_copy.go).
+// ec.Buffer and Split produce (stripeOf: shard i at base + i*stride, inside one buffer registered
+// with RegisterBuffer or allocated by HostAlloc) and passes that stripe as a single pointer to the
+// cfsec_*_contig entry points -- legal on every Go release.  Any other shard vector goes through
+// callVec: shards in HostAlloc memory are C memory and go into the C array as they are; Go memory is
+// pinned with Go >= 1.21 (runtime.Pinner, vec_pin.go) and staged through C memory before that
+// (vec_copy.go).
 //
 // Source only: this container has no Go toolchain, so the package is not built or
 // tested here (see INTEGRATION.md for the build line and the test plan).
@@ -37,8 +39,10 @@ import (
 )
 
 // stripeOf reports whether every shard is size bytes at one stride from the first (ec.Buffer's
-// layout, common/ec/buf.go:83-84, which encoder.Split carves): then the stripe crosses the C ABI as
-// its base pointer alone (cfsec_*_contig).
+// layout, common/ec/buf.go:83-84, which encoder.Split carves) inside one registered allocation
+// (regions.go: RegisterBuffer, HostAlloc): then the stripe crosses the C ABI as its base pointer
+// alone (cfsec_*_contig).  Shards that only happen to sit at one stride are not enough -- cgo lets C
+// reach the allocation a pointer points into, nothing beyond it.
 func stripeOf(shards [][]byte) (base *C.uint8_t, size, stride int, ok bool) {
 	if len(shards) == 0 || len(shards[0]) == 0 {
 		return nil, 0, 0, false
@@ -56,6 +60,9 @@ func stripeOf(shards [][]byte) (base *C.uint8_t, size, stride int, ok bool) {
 		if len(s) != size || uintptr(unsafe.Pointer(&s[0])) != p0+uintptr(i*stride) {
 			return nil, 0, 0, false
 		}
+	}
+	if _, one := regionOf(p0, (len(shards)-1)*stride+size); !one {
+		return nil, 0, 0, false
 	}
 	return (*C.uint8_t)(unsafe.Pointer(&shards[0][0])), size, stride, true
 }
@@ -96,6 +103,9 @@ func stripeOfMissing(shards [][]byte) (base *C.uint8_t, size, stride int, missin
 		if addr[i] != addr[0]+uintptr(i*stride) {
 			return nil, 0, 0, nil, false
 		}
+	}
+	if _, one := regionOf(addr[0], (len(shards)-1)*stride+size); !one {
+		return nil, 0, 0, nil, false
 	}
 	return (*C.uint8_t)(unsafe.Pointer(addr[0])), size, stride, missing, true
 }
@@ -188,7 +198,10 @@ func (e *Engine) EncodeCRC(shards [][]byte) ([]uint32, error) {
 
 // HostAlloc returns size bytes of page-locked C memory (cfsec_host_alloc) as a byte slice: the
 // allocation hook for resourcepool.NewMemPoolWith (common/resourcepool/mempool.go:60), so
-// ec.Buffer shards are coded in place over PCIe.  Release it with HostFree.
+// ec.Buffer shards are coded in place over PCIe, and for blobnode's shard buffers
+// (blobnode/base/workutils/buf_pool.go:26-29).  The block is registered as one region (regions.go):
+// its stripes take the one-pointer entry points and its shards sit in C arrays without staging or
+// pinning on every Go release.  Release it with HostFree.
 func HostAlloc(size int) ([]byte, error) {
 	if size <= 0 {
 		return nil, nil
@@ -197,7 +210,9 @@ func HostAlloc(size int) ([]byte, error) {
 	if err := toError(C.cfsec_host_alloc(C.size_t(size), &p)); err != nil {
 		return nil, err
 	}
-	return unsafe.Slice((*byte)(p), size), nil
+	b := unsafe.Slice((*byte)(p), size)
+	addRegion(b, true)
+	return b, nil
 }
 
 // HostFree releases a slice from HostAlloc.
@@ -205,6 +220,7 @@ func HostFree(b []byte) error {
 	if cap(b) == 0 {
 		return nil
 	}
+	removeRegion(b)
 	return toError(C.cfsec_host_free(unsafe.Pointer(&b[:1][0])))
 }
 

@@ -134,8 +134,10 @@ func (e *ECEncoder) reconstruct(shards [][]byte, badIdx []int, dataOnly bool) er
 	// blobnode and access hand over full-length shards of one ec.Buffer with the broken ones named
 	// in badIdx: one pointer, rebuilt in place
 	if base, size, stride, ok := stripeOf(shards); ok {
-		return ecError(C.cfsec_ec_reconstruct_contig(e.h, base, C.size_t(size), C.size_t(stride), C.int(len(shards)),
+		err := ecError(C.cfsec_ec_reconstruct_contig(e.h, base, C.size_t(size), C.size_t(stride), C.int(len(shards)),
 			bp, C.int(len(b)), donly, C.CFSEC_MEM_HOST, nil))
+		e.contigHeaders(shards, badIdx, dataOnly, err != nil)
+		return err
 	}
 	// initBadShards (encoder.go:182-188) happens in C; a bad shard keeps its buffer as capacity
 	for _, i := range badIdx {
@@ -156,6 +158,25 @@ func (e *ECEncoder) reconstruct(shards [][]byte, badIdx []int, dataOnly bool) er
 		}
 		return C.cfsec_ec_reconstruct(e.h, v, n, bp, C.int(len(b)), C.CFSEC_MEM_HOST, nil)
 	}))
+}
+
+// contigHeaders leaves the Go headers of a contiguous-stripe reconstruct (rebuilt in place in C,
+// every header still the shard size) as the reference leaves them: initBadShards (encoder.go:
+// 182-188) cuts every bad global shard to len 0 and the engine's Reconstruct restores the ones it
+// rebuilds -- so a bad parity shard of ReconstructData (encoder.go:146-151, lrcencoder.go:188-201)
+// and every bad global shard of a failed call keep len 0.  LRC local shards are rebuilt through
+// header copies (lrcencoder.go:172-178, 236-243): the caller's keep their length.  A contiguous
+// stripe has one shard size, so a failed call failed in the global pass (ErrTooFewShards).
+func (e *ECEncoder) contigHeaders(shards [][]byte, badIdx []int, dataOnly, failed bool) {
+	N, M := e.tactic.N, e.tactic.M
+	for _, i := range badIdx {
+		if i < 0 || i >= len(shards) || (e.tactic.L != 0 && i >= N+M) {
+			continue
+		}
+		if failed || (dataOnly && i >= N) {
+			shards[i] = shards[i][:0]
+		}
+	}
 }
 
 func (e *ECEncoder) Reconstruct(shards [][]byte, badIdx []int) error {

@@ -32,7 +32,9 @@ func callVec(shards [][]byte, fn func(*C.cfsec_shard, C.int) C.int) C.int {
 		elems[i] = C.cfsec_shard{data: nil, len: C.size_t(len(s)), cap: C.size_t(cap(s))}
 		if cap(s) > 0 {
 			p := &s[:cap(s)][0]
-			pin.Pin(p)
+			if !inCMem(s) { // HostAlloc memory is C memory: nothing to pin
+				pin.Pin(p)
+			}
 			elems[i].data = (*C.uint8_t)(unsafe.Pointer(p))
 		}
 	}

@@ -171,6 +171,39 @@ int main(int argc, char** argv) {
   for (int b = 0; b < 3; ++b) rec("batch_after", bb[b], T * bs[b]);
   rec("batch_status", bst, sizeof bst);
 
+  /* ---- blobnode's tasklet with per-shard buffers (ShardsBuf, work_shard_recover.go:711-716) from
+   * cfsec_host_alloc: a non-contiguous vector of page-locked shards, which the Go 1.17 shim passes
+   * as a C array of C pointers with no staging (vec_copy.go) -- coded in place over PCIe ---- */
+  {
+    enum { NB = 2 };
+    const size_t PS = 6000 + 3;
+    uint8_t* ps[NB][64];
+    cfsec_shard psh[NB * 64];
+    for (int b = 0; b < NB; ++b)
+      for (int i = 0; i < LT; ++i) {
+        CHECK(cfsec_host_alloc(PS, (void**)&ps[b][i]));
+        for (size_t j = 0; j < PS; ++j) ps[b][i][j] = i < t.n ? sm_byte() : 0;
+        psh[b * LT + i] = (cfsec_shard){ps[b][i], PS, PS};
+      }
+    for (int b = 0; b < NB; ++b) CHECK(cfsec_ec_encode(lrc, psh + b * LT, LT, CFSEC_MEM_HOST, NULL));
+    for (int b = 0; b < NB; ++b)
+      for (int i = 0; i < LT; ++i) rec("pv_good", ps[b][i], PS);
+    const int pb[] = {0, 7, 16, 3, 17};
+    const int po[] = {0, 3, 5};
+    for (int b = 0; b < NB; ++b)
+      for (int j = po[b]; j < po[b + 1]; ++j) memset(ps[b][pb[j]], 0x3C, PS);
+    ps[1][9][11] ^= 0x80; /* bid 1: a corrupted surviving global parity -> ErrVerify */
+    int pst[NB] = {-1, -1};
+    uint32_t pcrc[NB * 64];
+    CHECK(cfsec_ec_reconstruct_batch_crc(lrc, psh, LT, NB, pb, po, 1, CFSEC_MEM_HOST, pst, pcrc));
+    for (int b = 0; b < NB; ++b)
+      for (int i = 0; i < LT; ++i) rec("pv_after", ps[b][i], PS);
+    rec("pv_st", pst, sizeof pst);
+    rec("pv_crc", pcrc, sizeof(uint32_t) * NB * LT);
+    for (int b = 0; b < NB; ++b)
+      for (int i = 0; i < LT; ++i) CHECK(cfsec_host_free(ps[b][i]));
+  }
+
   /* ---- contiguous stripes (ec.Buffer layout): the Go 1.17 cgo path, one pointer per call ---- */
   {
     /* EC6P10L2 stripe of 4097-byte shards at stride 4100 inside one pageable allocation */

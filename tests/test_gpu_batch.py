@@ -708,8 +708,8 @@ def test_ec_batch_crc_uniform_groups(mode, memory, gap, monkeypatch, capfd):
         for i in range(total):
             assert np.array_equal(host(stripes[b][i]), want[b][i]), (b, i)
             assert crcs[b][i] == (crc_of(want[b][i]) if exp[b] == 0 else 0), (b, i)
-    fused = "fused crc group k=%d m=%d tasks=6" % (t.N, t.M)
-    if rs and memory == "device" and not gap:
+    fused = "fused crc group k=%d m=%d tasks=6" % (t.N, t.M + t.L)
+    if memory == "device" and not gap:  # EC6P10L2: the 6 x (10 + 2) fused LRC encode + 18 checksums
         assert fused in err, err
     if gap:
         assert "tasks=6" not in err and "tasks=5" not in err, err

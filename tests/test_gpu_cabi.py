@@ -178,3 +178,32 @@ def test_contiguous_stripes(run):
             shard = good[o + i * S:o + (i + 1) * S]
             assert int(crc[b, i]) == ((zlib.crc32(shard.tobytes()) & 0xFFFFFFFF) if i in bad else 0), (b, i)
     assert as_int(run["ct_err_overlap"][0]) == _lib.ErrInvalidArg.status
+
+
+def test_tasklet_of_separate_pinned_shards(run):
+    """blobnode's tasklet with every shard its own cfsec_host_alloc block (the ShardsBuf layout the
+    Go 1.17 shim passes without copies): cfsec_ec_reconstruct_batch_crc over EC6P10L2 bids with bad
+    {0, 7, 16} and {3, 17}, bid 1 with a corrupted surviving global parity -- statuses, rebuilt bytes
+    and checksums against the ec oracle and zlib."""
+    from chubaofs_amd import codemode as cm
+    from oracle.ec_oracle import ECOracle, Slice
+    t = cm.GetTactic(cm.EC6P10L2)
+    LT = t.N + t.M + t.L
+    good = run["pv_good"]
+    after = run["pv_after"]
+    st = list(np.frombuffer(run["pv_st"][0].tobytes(), np.int32))
+    crc = np.frombuffer(run["pv_crc"][0].tobytes(), np.uint32).reshape(2, LT)
+    orc = ECOracle.from_tactic(t)
+    for b, bad in enumerate([[0, 7, 16], [3, 17]]):
+        sh = [Slice.of(good[b * LT + i]) for i in range(LT)]
+        for i in bad:
+            sh[i].buf[:] = 0x3C
+        if b == 1:
+            sh[9].buf[11] ^= 0x80
+        want = orc.repair(sh, bad)
+        assert st[b] == want, (b, st)
+        for i in range(LT):
+            assert np.array_equal(after[b * LT + i], sh[i].view()), (b, i)
+            if want == 0:
+                assert int(crc[b, i]) == ((zlib.crc32(sh[i].view().tobytes()) & 0xFFFFFFFF) if i in bad else 0), (b, i)
+    assert st == [0, _lib.ErrVerify.status]

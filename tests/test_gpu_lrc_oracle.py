@@ -197,3 +197,38 @@ def test_c4_c5_sizes(memory):
     for kinds in ([], [("flip", 36)], [("flip", 37)], [("flip", 35)], [("flip", 5)]):
         run_case(cm.EC16P20L2, "reconstruct", damage(t5, good, r, kinds), [0, 1, 16, 17], memory)
         run_case(cm.EC16P20L2, "verify", damage(t5, good, r, kinds), [], memory)
+
+
+@pytest.mark.parametrize("memory", ["host", "device"])
+@pytest.mark.parametrize("mode", [cm.EC6P6L9, cm.EC6P8L10])
+def test_local_pass_failure_runs_every_az(mode, memory):
+    """lrcencoder.go:173-184 hands every AZ's local Reconstruct to task.Run, which runs them all and
+    returns the first error: when AZ 0's local pass fails (another local parity of AZ 0 has the wrong
+    length: ErrShardSize) AZ 1's bad local parity is still rebuilt.  Single call and the tasklet
+    batch, both against the ec oracle (status, lengths and bytes)."""
+    t = cm.GetTactic(mode)
+    N, M, L, AZ = t.N, t.M, t.L, t.AZCount
+    lpa = L // AZ
+    az0, az1 = N + M, N + M + lpa  # first local parity of AZ 0 and of AZ 1
+    r = random.Random(mode)
+    good = codeword(t, 2049, 77)
+    cases = [
+        ([("len", az0 + 1), ("flip", az1)], [az0, az1]),   # AZ 0 fails, AZ 1 rebuilt
+        ([("len", az1 + 1), ("flip", az0)], [az0, az1]),   # AZ 1 fails, AZ 0 rebuilt
+        ([("len", az0 + 1), ("len", az1 + 1)], [az0, az1]),  # both fail: AZ 0's error
+        ([("flip", az1)], [az0, az1]),                      # both rebuilt
+    ]
+    for kinds, bad in cases:
+        run_case(mode, "reconstruct", damage(t, good, r, kinds), bad, memory)
+    # the tasklet form: the same bids in one cfsec_ec_reconstruct_batch (Reconstruct + Verify per bid)
+    enc = new(mode, False)
+    bids = [damage(t, good, random.Random(i), kinds) for i, (kinds, _) in enumerate(cases)]
+    want = [to_oracle(b) for b in bids]
+    orc = ECOracle.from_tactic(t)
+    exp = [orc.repair(w, bad) for w, (_, bad) in zip(want, cases)]
+    work = [to_mem(b, memory) for b in bids]
+    st = enc.ReconstructBatch(work, [bad for _, bad in cases], verify=True)
+    assert st == exp, (cm.Name(mode), st, exp)
+    for b, (wk, w) in enumerate(zip(work, want)):
+        if exp[b] in (0, _lib.ErrVerify.status):
+            assert_same(wk, w, (cm.Name(mode), "batch", b))
