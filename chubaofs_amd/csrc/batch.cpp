@@ -61,6 +61,8 @@ struct Group {
   std::vector<uint8_t*> hout;      // plan->dy16: [tasks * (nd + 20)] its output rows
   int flag0 = 0;                   // first flag word
   uint32_t* direct = nullptr;      // or: task i's Verify word is direct[i] (consecutive items' words)
+  uint32_t* zero_words = nullptr;  // dy16: the call's checksum words, zeroed by the group's first launch
+  uint32_t nzero = 0;
 };
 
 hipError_t launch_group_run(const Group& g, size_t t0, size_t t1, uint32_t* dflags, hipStream_t s);
@@ -118,6 +120,10 @@ hipError_t launch_group_run(const Group& g, size_t t0, size_t t1, uint32_t* dfla
     job.lens = uniform ? nullptr : g.lens.data() + t0;
     job.len = g.lens[t0];
     job.flags = g.direct ? g.direct + t0 : dflags + g.flag0 + t0;
+    if (t0 == 0) {
+      job.zero_words = g.zero_words;
+      job.nzero = g.nzero;
+    }
     return launch_dy16_repair(job, s);
   }
   MatVecJob job;
@@ -713,8 +719,16 @@ Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceCont
   if (mem == CFSEC_MEM_DEVICE && !async) st = ctx->order_after_default(ws);
   // Zeroed inline on lane 0: a memset on lane 1 beside the first products, waited for by the first
   // checksum launch, measured slower (C5 +26 instead of +14 us, EC12P4 fused encode + CRC 246
-  // instead of 224 us: the cross-stream wait costs more than the 10 KiB fill it hides).
-  if (st == CFSEC_OK && sums) st = hip_status(hipMemsetAsync(dcrc, 0, crc->n * 4, lane[0]), "hipMemsetAsync(crc)");
+  // instead of 224 us: the cross-stream wait costs more than the 10 KiB fill it hides).  When the
+  // first launch is a 16x16-dyadic repair (C5's tasklet) its workgroup (0, 0) zeroes the words and
+  // the memset launch goes (zero_first below).
+  bool zero_first = false;
+  if (sums && nlanes == 1 && nphase == 1 && !direct.empty()) {
+    const StripeTask* t0 = direct.front();
+    zero_first = t0->plan->dy16 && t0->phase == 0 && crc->n <= 0xFFFFFFFFu;
+  }
+  if (st == CFSEC_OK && sums && !zero_first)
+    st = hip_status(hipMemsetAsync(dcrc, 0, crc->n * 4, lane[0]), "hipMemsetAsync(crc)");
   if (st == CFSEC_OK && nlanes > 1) st = join(0, 1);
   // crc32.ChecksumIEEE of the rows the tasks of a launched part name, on the part's stream, from the
   // same device addresses the product used (staged rows before their lane is reused)
@@ -792,6 +806,15 @@ Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceCont
       };
       std::vector<Group> groups = make_groups(dph, &next_flag, dptr);
       route(groups);
+      if (zero_first) {  // make_groups keeps first-appearance order: groups[0] holds direct.front()
+        if (!groups.empty() && groups[0].plan->dy16) {
+          groups[0].zero_words = dcrc;
+          groups[0].nzero = (uint32_t)crc->n;
+        } else {
+          st = hip_status(hipMemsetAsync(dcrc, 0, crc->n * 4, lane[0]), "hipMemsetAsync(crc)");
+        }
+        zero_first = false;
+      }
       std::set<const StripeTask*> fused;  // tasks whose checksums a fused product + CRC launch took
       for (const Group& gr : groups) {
         if (st != CFSEC_OK) break;
@@ -962,7 +985,9 @@ Status ECEncoder::reconstruct_batch(cfsec_shard* shards, int n, int nbids, const
   std::vector<int> st(stripes.size());
   Status rc;
   if (verify && engine_->k() > kLaunchMaxRows) {
-    if (crc) return CFSEC_ERR_NOT_SUPPORTED;
+    // the single-stripe path is synchronous on its own streams: not for the checksummed or the
+    // asynchronous forms (no code mode of SURVEY §8 has more than 16 inputs)
+    if (crc || async) return CFSEC_ERR_NOT_SUPPORTED;
     rc = engine_->reconstruct_stripes(stripes.data(), (int)stripes.size(), mem, verify, st.data());
   } else {
     PlanStore store;
@@ -991,7 +1016,7 @@ Status LrcEncoder::reconstruct_batch(cfsec_shard* shards, int n, int nbids, cons
   const int N = t_.n, M = t_.m, L = t_.l, AZ = t_.az_count;
   const int lsz = (N + M + L) / AZ;
   if (verify && std::max(N, local_->k()) > kLaunchMaxRows) {
-    if (crc) return CFSEC_ERR_NOT_SUPPORTED;
+    if (crc || async) return CFSEC_ERR_NOT_SUPPORTED;  // synchronous bid-by-bid path only
     // compared rows over more than one launch's inputs: the single calls, bid by bid (each takes
     // its own concurrency slot)
     for (int b = 0; b < nbids; ++b) {
@@ -1167,7 +1192,7 @@ Status ECEncoder::encode_batch(cfsec_shard* shards, int n, int nstripes, int mem
   Slot slot(pool_.get());
   const int k = engine_->k(), m = engine_->m(), tot = k + m;
   if (enable_verify_ && k > kLaunchMaxRows) {  // compared rows over more inputs than one launch carries
-    if (crc) return CFSEC_ERR_NOT_SUPPORTED;
+    if (crc || async) return CFSEC_ERR_NOT_SUPPORTED;  // synchronous stripe-by-stripe path only
     std::vector<cfsec_shard*> stripes;
     std::vector<int> pos;
     for (int s = 0; s < nstripes; ++s) {
@@ -1229,7 +1254,7 @@ Status LrcEncoder::encode_batch(cfsec_shard* shards, int n, int nstripes, int me
   const int N = t_.n, M = t_.m, L = t_.l;
   Slot slot(pool_.get());
   if (enable_verify_ && N > kLaunchMaxRows) {  // the fused Verify's rows exceed one compare launch
-    if (crc) return CFSEC_ERR_NOT_SUPPORTED;
+    if (crc || async) return CFSEC_ERR_NOT_SUPPORTED;  // synchronous stripe-by-stripe path only
     for (int s = 0; s < nstripes; ++s) {
       status[s] = n != N + M + L ? CFSEC_ERR_INVALID_SHARDS
                                  : encode_stripe(shards + (size_t)s * n, n, mem, async ? async->stream : nullptr);

@@ -121,6 +121,7 @@ DeviceContext* DeviceContext::get(int device, int slot) {
 
 Status DeviceContext::acquire(size_t bytes, size_t nflags, Workspace** out, size_t nbflags, size_t ncrc) {
   Workspace* ws = nullptr;
+  bool wait = false;
   {
     std::lock_guard<std::mutex> l(mu_);
     // a workspace an asynchronous call returned is free once its stream has passed the call
@@ -144,10 +145,24 @@ Status DeviceContext::acquire(size_t bytes, size_t nflags, Workspace** out, size
     if (best != free_.end()) {
       ws = *best;
       free_.erase(best);
+    } else if (all_.size() >= kMaxWorkspaces && !free_.empty()) {
+      // every free workspace is still pending on an asynchronous call's stream: wait for the
+      // oldest one instead of growing without bound (each holds streams, events, pinned words)
+      ws = free_.front();
+      free_.erase(free_.begin());
+      wait = true;
     } else {
       all_.emplace_back(new Workspace());
       ws = all_.back().get();
     }
+  }
+  if (wait) {
+    if (hipEventSynchronize(ws->done) != hipSuccess) {
+      (void)hipGetLastError();
+      DeviceGuard dg(device_);
+      (void)hipDeviceSynchronize();
+    }
+    ws->pending = false;
   }
   DeviceGuard g(device_);
   if (!g.ok()) {

@@ -105,7 +105,10 @@ class DeviceContext {
   int device_;
   std::mutex mu_;
   std::vector<std::unique_ptr<Workspace>> all_;
-  std::vector<Workspace*> free_;
+  std::vector<Workspace*> free_;  // release order: the front was released first
+  // beyond this many workspaces an acquire with every free one still pending (asynchronous calls
+  // queued without a sync) waits for the oldest instead of allocating another
+  static constexpr size_t kMaxWorkspaces = 64;
 };
 
 // Makes `device` current for the scope, restoring the caller's device after.

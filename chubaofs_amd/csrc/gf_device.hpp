@@ -49,6 +49,8 @@ struct __attribute__((aligned(16))) GfArgs {
   uint16_t nstore;                 // kStoreVerify: outputs [0, nstore) are stored, [nstore, m) compared
   uint16_t varlen;                 // nonzero: per-stripe lengths in slen[]
   uint32_t pstore, pcmp;           // repair_dy16: parity rows stored / compared
+  uint32_t* zw;                    // repair_dy16: nzw words workgroup (0, 0) zeroes (checksum words)
+  uint32_t nzw;
   uint8_t src[16];                 // repair_dy16: input slot of data row i (16 + j: missing row j)
   uint8_t coef[kMaxM * kMaxK];    // m x k, row stride k
   uint32_t slen[kLenSlots];

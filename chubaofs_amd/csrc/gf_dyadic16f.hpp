@@ -268,6 +268,8 @@ __device__ __forceinline__ void repair_dy16f(const GfArgs& a) {
     coef_tables(a.coef[(20 + E + i % ND) * K + i / ND], tab01[NDY + i], tab2[NDY + i]);
   __syncthreads();
 
+  if (a.zw && blockIdx.x == 0 && blockIdx.y == 0)  // the batch's checksum words (gf_device.hpp GfArgs)
+    for (uint32_t i = threadIdx.x; i < a.nzw; i += blockDim.x) a.zw[i] = 0u;
   const uint32_t stripe = blockIdx.y;
   const size_t ts = a.sstride ? 0 : (size_t)stripe;
   const int64_t sbase = (int64_t)stripe * a.sstride;

@@ -357,6 +357,8 @@ hipError_t launch_dy16_repair(const Dy16RepairJob& job, hipStream_t stream) {
   a.nstore = 0;
   a.pstore = job.pstore;
   a.pcmp = job.pcmp;
+  a.zw = job.zero_words;
+  a.nzw = job.nzero;
   std::memcpy(a.src, job.src, 16);
   std::memcpy(a.coef, job.coef, (size_t)(20 + ne + nd) * 16);
   for (int s0 = 0; s0 < job.nstripes; s0 += per) {
@@ -382,6 +384,8 @@ hipError_t launch_dy16_repair(const Dy16RepairJob& job, hipStream_t stream) {
     }
     const hipError_t e = launch_dy16_repair_args(nd, ne, a, (unsigned)ns, stream);
     if (e != hipSuccess) return e;
+    a.zw = nullptr;  // the first launch zeroed them
+    a.nzw = 0;
   }
   return hipSuccess;
 }

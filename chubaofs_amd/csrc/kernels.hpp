@@ -51,6 +51,8 @@ struct Dy16RepairJob {
   const uint8_t* const* in = nullptr;  // host [nstripes * 16]: the first 16 present rows
   uint8_t* const* out = nullptr;       // host [nstripes * (nd + 20 + e)]: missing data rows, parity 0..19, extras
   uint32_t* flags = nullptr;           // device [nstripes]
+  uint32_t* zero_words = nullptr;      // device: nzero words the first launch zeroes (a batch's checksum
+  uint32_t nzero = 0;                  // words, XOR-accumulated by the checksum pass that follows)
 };
 hipError_t launch_dy16_repair(const Dy16RepairJob& job, hipStream_t stream);
 

@@ -242,8 +242,9 @@ int cfsec_ec_reconstruct_batch_crc(cfsec_ec* h, cfsec_shard* shards, int n, int 
  * (CFSEC_ERR_VERIFY of the synchronous call).  Missing shards' lengths are set at return, as in the
  * synchronous call; the bytes are there when the stream gets there.  The library keeps no caller
  * pointer after the call returns (the shard pointers are copied into the kernel arguments).  Shapes
- * the kernels cannot compare in one pass (more than 32 inputs with Verify, an LRC stripe whose
- * local shard has another length) run synchronously on `stream` and report ErrVerify in status[b].
+ * the kernels cannot compare in one pass: more than 32 inputs with Verify (no code mode has them)
+ * return CFSEC_ERR_NOT_SUPPORTED -- use the synchronous call; an LRC stripe whose local shard has
+ * another length runs synchronously on `stream` and reports ErrVerify in status[b].
  * crcs (device, nbids * n / nstripes * n words, may be NULL): the checksums of the _crc forms,
  * written on the stream (zeroed by the call first); a flagged or failed item's words are
  * meaningless. */

@@ -797,3 +797,24 @@ def test_verify_flags_direct_and_gathered(mode, call):
         assert got[b] == exp, (cm.Name(mode), call, b, got[b], exp)
         for i in range(total):
             assert np.array_equal(host(bids[b][i]), shards[i]), (b, i)
+
+
+def test_async_over_32_inputs_not_supported():
+    """A Verify over more than 32 inputs takes the synchronous stripe-by-stripe path, which cannot
+    honour an asynchronous call's stream: the _async forms return ErrNotSupported for it (no code
+    mode has more than 16 inputs; a custom 40 + 4 tactic reaches it), the synchronous call works."""
+    from chubaofs_amd import ec
+    from chubaofs_amd.codemode import Tactic
+    t = Tactic(40, 4, 0, 1, 42, 0, 0)
+    enc = ec.NewEncoder(ec.Config(CodeMode=t, EnableVerify=True), device=0)
+    S = 4096
+    good = [gen_mock_bytes(i, S) for i in range(40)] + [np.zeros(S, np.uint8) for _ in range(4)]
+    assert enc.EncodeBatch([[x.copy() for x in good]]) == [0]
+    dev = [torch.from_numpy(x.copy()).cuda() for x in good]
+    flags = torch.zeros(1, dtype=torch.int32, device="cuda")
+    with pytest.raises(_lib.ErrNotSupported):
+        enc.EncodeBatchAsync([dev], flags=flags)
+    with pytest.raises(_lib.ErrNotSupported):
+        enc.ReconstructBatchAsync([dev], [[0]], flags=flags)
+    st = enc.ReconstructBatch([[x.copy() for x in good]], [[0]])
+    assert st == [0]

@@ -3,6 +3,7 @@
 # (W = 1), and the field form at W = 2 (probes_bin/f2); then VALU instruction counts per form.
 set -e
 mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/test_gpu_batch.py tests/test_gpu_lrc_oracle.py tests/test_repair_dist.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r4_dy16_tests.log 2>&1
 out=gpurun_out/r4_dy16_ab2.txt
 for rep in 1 2; do
   for v in 0 2 1; do
