@@ -483,7 +483,7 @@ void RSEngine::plan_reconstruct_tasks(cfsec_shard* const* stripes, int nst, bool
   tasks->reserve(tasks->size() + (size_t)nst);
   // batches mostly repeat one erasure pattern: the previous stripe's plan is checked first
   std::vector<bool> present(total()), last_present;
-  std::unique_ptr<StripePlan>* last_plan = nullptr;
+  const StripePlan* last_plan = nullptr;
   for (int s = 0; s < nst; ++s) {
     status[s] = CFSEC_OK;
     cfsec_shard* sh = stripes[s];
@@ -507,24 +507,18 @@ void RSEngine::plan_reconstruct_tasks(cfsec_shard* const* stripes, int nst, bool
     // plans are keyed by the present shards, plus whether the extra rows ride along
     present.push_back(fx);
     if (!last_plan || present != last_present) {
-      last_plan = &store->by_pattern[present];
-      last_present = present;
-    }
-    auto& plan = *last_plan;
-    if (!plan) {
-      plan.reset(new StripePlan());
       present.pop_back();
-      st = plan_stripe(present, verify, plan.get(), fx ? extra : nullptr);
+      last_plan = cached_plan(present, fx, verify, fx ? extra : nullptr, store, &st);
       present.push_back(fx);
-      if (st != CFSEC_OK) {
-        store->by_pattern.erase(present);
+      last_present = present;
+      if (!last_plan) {
         present.pop_back();
-        last_plan = nullptr;
         status[s] = st;
         continue;
       }
     }
     present.pop_back();
+    const StripePlan* plan = last_plan;
     for (int r = 0; r < plan->nstore && st == CFSEC_OK; ++r)
       if (!sh[plan->out[r]].data || sh[plan->out[r]].cap < S) st = CFSEC_ERR_INVALID_ARG;
     for (int c : plan->in)
@@ -536,12 +530,12 @@ void RSEngine::plan_reconstruct_tasks(cfsec_shard* const* stripes, int nst, bool
     }
     // KRS/reedsolomon.go:1514-1518: shards[i] = shards[i][0:S]
     for (int r = 0; r < plan->nstore; ++r) sh[plan->out[r]].len = S;
-    const StripePlan* use = plan.get();
+    const StripePlan* use = plan;
     if (split_verify(*plan)) {
       // Verify as a second pass over the whole stripe with the encoding matrix instead of compared
       // rows in the reconstruct pass: the compared rows (parity_row x dec over the k inputs) have
       // no structure, the parity rows over the data do (dyadic kernels)
-      StripePlan*& so = store_only[plan.get()];
+      StripePlan*& so = store_only[plan];
       if (!so) {
         StripePlan cut = *plan;
         cut.dy16.reset();
@@ -564,6 +558,26 @@ void RSEngine::plan_reconstruct_tasks(cfsec_shard* const* stripes, int nst, bool
     }
     if (!use->out.empty()) tasks->push_back(StripeTask{sh, use, S, &status[s], 0, phase, owner0 + s});
   }
+}
+
+const StripePlan* RSEngine::cached_plan(const std::vector<bool>& present, bool fx, bool verify,
+                                        const ExtraRows* extra, PlanStore* store, Status* st) {
+  std::vector<bool> key = present;
+  key.push_back(fx);
+  key.push_back(verify);
+  {
+    std::lock_guard<std::mutex> l(plan_mu_);
+    auto it = plan_cache_.find(key);
+    if (it != plan_cache_.end()) return it->second.get();
+  }
+  std::unique_ptr<StripePlan> p(new StripePlan());
+  *st = plan_stripe(present, verify, p.get(), extra);
+  if (*st != CFSEC_OK) return nullptr;
+  std::lock_guard<std::mutex> l(plan_mu_);
+  auto it = plan_cache_.find(key);  // another caller may have planned it meanwhile
+  if (it != plan_cache_.end()) return it->second.get();
+  if (plan_cache_.size() < kMaxCachedPlans) return plan_cache_.emplace(std::move(key), std::move(p)).first->second.get();
+  return store->add(*p);
 }
 
 bool RSEngine::split_verify(const StripePlan& p) const {

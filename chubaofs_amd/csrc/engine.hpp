@@ -322,6 +322,14 @@ class RSEngine {
   Matrix mat_;     // total x k
   Matrix parity_;  // m x k (r.parity, KRS/reedsolomon.go:568-571)
   InversionCache tree_;
+  // Reconstruct plans across calls (blobnode's tasklets repeat one erasure pattern call after call):
+  // key = the present shards + [extra rows fused] + [verify]; a cached plan is never changed or
+  // freed, so concurrent callers share it.  Beyond kMaxCachedPlans patterns a call keeps its own.
+  std::mutex plan_mu_;
+  std::map<std::vector<bool>, std::unique_ptr<StripePlan>> plan_cache_;
+  static constexpr size_t kMaxCachedPlans = 4096;
+  const StripePlan* cached_plan(const std::vector<bool>& present, bool fx, bool verify, const ExtraRows* extra,
+                                PlanStore* store, Status* st);
   DeviceContext* ctx_ = nullptr;
   std::vector<DeviceContext*> devs_;  // batch devices, ctx_ first
   Status run_device(std::vector<StripeTask*>& tasks, int mem, DeviceContext* ctx, const AsyncOut* async,

@@ -104,9 +104,12 @@ void to_slot_order(int nd, int ne, const dev::GfArgs& a, dev::GfArgs& f) {
     for (int i = 0; i < 16; ++i) f.ptr[s * 16 + i] = a.ptr[s * 16 + col[i]];
 }
 
+#ifndef CFSEC_DY16_PF
+#define CFSEC_DY16_PF 1  // compared rows of the 16x16 block loaded before it (repair_dy16 PF)
+#endif
 template <int ND, int E>
 __global__ __launch_bounds__(256) void gf_dy16s_repair_kernel(const dev::GfArgs a) {
-  dev::repair_dy16<ND, E, true, CFSEC_DY16_W, true>(a);
+  dev::repair_dy16<ND, E, true, CFSEC_DY16_W, true, (bool)CFSEC_DY16_PF>(a);
 }
 
 template <int E>

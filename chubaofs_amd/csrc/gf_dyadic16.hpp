@@ -103,8 +103,14 @@ __device__ __forceinline__ void st_lane(uint8_t* p, bool full, size_t rem, const
 // input chunks x (clobbered), each handed to put(r, chunk) as soon as it is final.  Rows 16.. (the
 // 4x4 row blocks, then the E plain rows) come first, from the original inputs, one group at a time
 // in acc[16..]; then the 16x16 block into acc[0..15].
-template <int R4, int E, bool PIN, int W, class Put>
-__device__ __forceinline__ void dy16_rows(uint32_t (&x)[16][W], const u32x4* tab01, const uint32_t* tab2, Put&& put) {
+struct NoHook {
+  __device__ __forceinline__ void operator()() const {}
+};
+
+// hook() runs after rows 16.. and before the 16x16 block (repair_dy16: the compared rows' loads)
+template <int R4, int E, bool PIN, int W, class Put, class Hook = NoHook>
+__device__ __forceinline__ void dy16_rows(uint32_t (&x)[16][W], const u32x4* tab01, const uint32_t* tab2, Put&& put,
+                                          Hook&& hook = Hook()) {
   constexpr int K = 16, N4 = R4 * 4 * 9;
   constexpr int NA = 16 + (4 * R4 > E ? 4 * R4 : E);
   uint32_t acc[NA][W];
@@ -150,6 +156,7 @@ __device__ __forceinline__ void dy16_rows(uint32_t (&x)[16][W], const u32x4* tab
     for (int e = 0; e < E; ++e) put(16 + 4 * R4 + e, acc[16 + e]);
     sb();
   }
+  hook();
   // the 16x16 block: S = X + Y into x[0..7]
 #pragma unroll
   for (int j = 0; j < 8; ++j)
@@ -271,7 +278,9 @@ __device__ __forceinline__ void matvec_dy16(const GfArgs& a) {
 // of missing row j, gf_dy16.hip to_slot_order): missing row j then replaces its slot's input through
 // one uniform branch, where the run-time permutation of the first-16-present order costs v_cndmask
 // selects on every data row (~100 VALU ops per dword column, PMC: profiles/r04).
-template <int ND, int E, bool PIN = true, int W = 2, bool SLOTS = false>
+// PF: the compared rows of the 16x16 block are loaded before the block is computed (else each when
+// its row is final, all 16 at the end of the block: their latency exposed once per lane chunk).
+template <int ND, int E, bool PIN = true, int W = 2, bool SLOTS = false, bool PF = false>
 __device__ __forceinline__ void repair_dy16(const GfArgs& a) {
   constexpr int K = 16, NDY = kDy16Leaves + 36 + K * E, NT = NDY + K * (ND > 0 ? ND : 1), MO = ND + 20 + E;
   constexpr uint32_t kLane = 4 * W;
@@ -358,22 +367,39 @@ __device__ __forceinline__ void repair_dy16(const GfArgs& a) {
     }
     const uint32_t pstore = a.pstore, pcmp = a.pcmp;
     const uint8_t* spare = in[0] + sbase + off;  // just read: what rows not compared load instead
-    dy16_rows<1, E, PIN, W>(x, tab01, tab2, [&](int r, const uint32_t (&v)[W]) {
+    uint32_t yb[PF ? 16 : 1][W];                 // PF: the 16x16 block's compared rows
+    const auto load_cmp = [&](int r, uint32_t (&y)[W]) {
       // every row loads (its own chunk if compared, else the input chunk above, a cache hit) and
       // the mask picks: no branch around the loads, so the compiler issues a group of them before
       // the first wait (a branch per row exposed one load latency per compared row: +45 % time)
-      uint8_t* p = out[ND + r] + sbase + off;
       const bool cmp = (pcmp >> r) & 1u;
-      uint32_t y[W];
       if constexpr (SLOTS)  // the row base chosen on the scalar unit, then the lane offset
         ld_lane<W>((cmp ? (const uint8_t*)out[ND + r] : in[0]) + sbase + off, full, rem, y);
       else
-        ld_lane<W>(cmp ? p : spare, full, rem, y);
-      const uint32_t msk = cmp ? ~0u : 0u;
+        ld_lane<W>(cmp ? (const uint8_t*)out[ND + r] + sbase + off : spare, full, rem, y);
+    };
+    dy16_rows<1, E, PIN, W>(
+        x, tab01, tab2,
+        [&](int r, const uint32_t (&v)[W]) {
+          uint8_t* p = out[ND + r] + sbase + off;
+          uint32_t y[W];
+          if (PF && r < 16) {
 #pragma unroll
-      for (int w = 0; w < W; ++w) diff |= (y[w] ^ v[w]) & msk;
-      if ((pstore >> r) & 1u) st_lane<W>(p, full, rem, v);
-    });
+            for (int w = 0; w < W; ++w) y[w] = yb[PF ? r : 0][w];
+          } else {
+            load_cmp(r, y);
+          }
+          const uint32_t msk = ((pcmp >> r) & 1u) ? ~0u : 0u;
+#pragma unroll
+          for (int w = 0; w < W; ++w) diff |= (y[w] ^ v[w]) & msk;
+          if ((pstore >> r) & 1u) st_lane<W>(p, full, rem, v);
+        },
+        [&]() {
+          if constexpr (PF) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) load_cmp(r, yb[r]);
+          }
+        });
   }
   if (diff) dev::set_flag(a.flags, stripe);
 }
