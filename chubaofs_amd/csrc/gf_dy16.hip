@@ -5,17 +5,11 @@
 #include <cstdlib>
 #include <cstring>
 
-#include "gf_dyadic16f.hpp"
+#include "gf_dyadic16.hpp"
 #include "gf_launch.hpp"
 
 #ifndef CFSEC_DY16_W
 #define CFSEC_DY16_W 2  // dwords per lane: 8-byte lane chunks (byte-form kernels)
-#endif
-#ifndef CFSEC_DY16F_W
-#define CFSEC_DY16F_W 1  // field-form kernels (gf_dyadic16f.hpp): 4-byte lane chunks
-#endif
-#ifndef CFSEC_DY16F_TPW
-#define CFSEC_DY16F_TPW 1  // field-form kernels: tiles per workgroup (2: the loop hoists the row pointers, SGPR spills)
 #endif
 
 namespace cfsec {
@@ -25,15 +19,9 @@ __global__ __launch_bounds__(256) void gf_dy16_kernel(const dev::GfArgs a) {
   dev::matvec_dy16<M, R4, E, MODE, true, W>(a);
 }
 
-template <int M, int R4, int E, MatVecMode MODE>
-__global__ __launch_bounds__(256) void gf_dy16f_kernel(const dev::GfArgs a) {
-  dev::matvec_dy16f<M, R4, E, MODE, true, CFSEC_DY16F_W, CFSEC_DY16F_TPW>(a);
-}
-
 namespace {
-// The 16x16-dyadic kernel forms (A/B): CFSEC_DY16F=1 the field-form kernels (gf_dyadic16f.hpp),
-// 2 the byte-form repair with inputs in data-row slots (default), 0 the byte-form kernels as in
-// round 3
+// The 16x16-dyadic repair (A/B): CFSEC_DY16F=0 the round-3 form (inputs in first-present order,
+// data rows permuted with selects), default the inputs in data-row slots
 int dy16_form() {
   static const int f = [] {
     const char* v = std::getenv("CFSEC_DY16F");
@@ -41,19 +29,9 @@ int dy16_form() {
   }();
   return f;
 }
-bool use_fields() { return dy16_form() == 1; }
 
 template <int M, int R4, int E, int W>
 hipError_t launch_one(MatVecMode mode, const dev::GfArgs& a, unsigned ns, hipStream_t st) {
-  if (use_fields()) {
-    constexpr uint64_t ftile = 256 * 4 * CFSEC_DY16F_W * CFSEC_DY16F_TPW;
-    const unsigned ft = (unsigned)((a.len + ftile - 1) / ftile);
-    if (mode == MatVecMode::kVerify)
-      hipLaunchKernelGGL((gf_dy16f_kernel<M, R4, E, MatVecMode::kVerify>), dim3(ft, ns), dim3(256), 0, st, a);
-    else
-      hipLaunchKernelGGL((gf_dy16f_kernel<M, R4, E, MatVecMode::kStore>), dim3(ft, ns), dim3(256), 0, st, a);
-    return hipGetLastError();
-  }
   constexpr uint64_t tile = 256 * 4 * W;
   const unsigned tiles = (unsigned)((a.len + tile - 1) / tile);
   if (mode == MatVecMode::kVerify)
@@ -69,28 +47,10 @@ __global__ __launch_bounds__(256) void gf_dy16_repair_kernel(const dev::GfArgs a
   dev::repair_dy16<ND, E, true, CFSEC_DY16_W>(a);
 }
 
-template <int ND, int E>
-__global__ __launch_bounds__(256) void gf_dy16f_repair_kernel(const dev::GfArgs a) {
-  dev::repair_dy16f<ND, E, true, CFSEC_DY16F_W, CFSEC_DY16F_TPW>(a);
-}
-
-template <int E>
-hipError_t launch_repair_f(int nd, const dev::GfArgs& a, dim3 grid, hipStream_t st) {
-  switch (nd) {
-    case 0: hipLaunchKernelGGL((gf_dy16f_repair_kernel<0, E>), grid, dim3(256), 0, st, a); break;
-    case 1: hipLaunchKernelGGL((gf_dy16f_repair_kernel<1, E>), grid, dim3(256), 0, st, a); break;
-    case 2: hipLaunchKernelGGL((gf_dy16f_repair_kernel<2, E>), grid, dim3(256), 0, st, a); break;
-    case 3: hipLaunchKernelGGL((gf_dy16f_repair_kernel<3, E>), grid, dim3(256), 0, st, a); break;
-    case 4: hipLaunchKernelGGL((gf_dy16f_repair_kernel<4, E>), grid, dim3(256), 0, st, a); break;
-    default: return hipErrorInvalidValue;
-  }
-  return hipGetLastError();
-}
-
-// The field-form repair's argument block from the byte-form one: inputs in data-row slots (slot i
-// = data row i when present, else the parity input standing in for missing row j), decode
+// The slot-ordered repair's argument block from the first-present one: inputs in data-row slots
+// (slot i = data row i when present, else the parity input standing in for missing row j), decode
 // coefficients permuted to slot order, src[j] = the data row of missing row j.
-void to_slot_order(int nd, int ne, const dev::GfArgs& a, dev::GfArgs& f) {
+static void to_slot_order(int nd, int ne, const dev::GfArgs& a, dev::GfArgs& f) {
   std::memcpy(&f, &a, sizeof(dev::GfArgs));
   int col[16];
   for (int i = 0; i < 16; ++i) {
@@ -105,10 +65,16 @@ void to_slot_order(int nd, int ne, const dev::GfArgs& a, dev::GfArgs& f) {
 }
 
 #ifndef CFSEC_DY16_PF
-#define CFSEC_DY16_PF 1  // compared rows of the 16x16 block loaded before it (repair_dy16 PF)
+// compared rows of the 16x16 block loaded before it (repair_dy16 PF): 152 VGPRs, 3 waves per SIMD,
+// C5 201-203 vs 190 us per call without (profiles/r04/dy16_pf_ab.txt)
+#define CFSEC_DY16_PF 0
+#endif
+#ifndef CFSEC_DY16_WPE
+#define CFSEC_DY16_WPE 4  // waves per SIMD the repair kernel's registers aim at (probes: 5)
 #endif
 template <int ND, int E>
-__global__ __launch_bounds__(256) void gf_dy16s_repair_kernel(const dev::GfArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CFSEC_DY16_WPE, 8))) void gf_dy16s_repair_kernel(
+    const dev::GfArgs a) {
   dev::repair_dy16<ND, E, true, CFSEC_DY16_W, true, (bool)CFSEC_DY16_PF>(a);
 }
 
@@ -140,17 +106,6 @@ hipError_t launch_repair_e(int nd, const dev::GfArgs& a, dim3 grid, hipStream_t 
 
 // ne extra rows: 0, or 2 (EC16P20L2's local parities checked in the global pass)
 hipError_t launch_dy16_repair_args(int nd, int ne, const dev::GfArgs& a, unsigned ns, hipStream_t st) {
-  if (use_fields()) {
-    constexpr uint64_t ftile = 256 * 4 * CFSEC_DY16F_W * CFSEC_DY16F_TPW;
-    const dim3 fgrid((unsigned)((a.len + ftile - 1) / ftile), ns);
-    static thread_local dev::GfArgs f;
-    to_slot_order(nd, ne, a, f);
-    switch (ne) {
-      case 0: return launch_repair_f<0>(nd, f, fgrid, st);
-      case 2: return launch_repair_f<2>(nd, f, fgrid, st);
-      default: return hipErrorInvalidValue;
-    }
-  }
   constexpr uint64_t tile = 256 * 4 * CFSEC_DY16_W;
   const dim3 grid((unsigned)((a.len + tile - 1) / tile), ns);
   if (dy16_form() == 2) {
