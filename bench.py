@@ -835,11 +835,13 @@ def segment_latency(args, torch, dev, cpu):
         wins = {}
         if cpu:
             for kind in ("pageable", "pinned", "device"):
-                w = [int(s) for s, r in rows.items() if r[kind + "_us"] < r["cpu_port_4t_us"]]
+                w = [int(s) for s, r in rows.items()
+                     if r[kind + "_us"] < min(r["cpu_port_4t_us"], r["cpu_port_1t_us"])]
                 wins[kind] = min(w) if w else None
         out["modes"][name] = {"by_segment_bytes": rows, "gpu_wins_from_bytes": wins}
     out["note"] = ("gpu_wins_from_bytes: smallest measured segment where the GPU call (wall, incl. staging and "
-                   "sync) beats the 4-thread CPU port; None: the CPU port wins at every measured size")
+                   "sync) beats the faster of the CPU port's 1- and 4-thread calls; None: the CPU port wins at every "
+                   "measured size")
     return out
 
 

@@ -214,17 +214,24 @@ class _Marks:
                           return_ms=d("decoded", "returned"), total_ms=d("t0", "returned"))
 
 
-def gpu_decode(enc, plan: RepairPlan, row, L: int, flags: torch.Tensor, words: Optional[torch.Tensor]) -> None:
+def gpu_decode(enc, plan: RepairPlan, row, L: int, flags: torch.Tensor, words: Optional[torch.Tensor],
+               geom=None) -> None:
     """Step 2 on this rank's GPU: the reference's per-bid Reconstruct + Verify over the [nbids, L] rows
-    row(i) (shard i of every bid), rebuilt rows written in place.  flags[0] receives the per-bid
-    planning status, flags[1] the Verify flags (on the stream), words the rebuilt rows' checksums."""
+    of every shard (row(i): a view with its rows contiguous; geom: (base addresses, bid strides) of
+    the same rows as two uint64 arrays, which spares the views), rebuilt rows written in place.
+    flags[0] receives the per-bid planning status, flags[1] the Verify flags (on the stream), words
+    the rebuilt rows' checksums."""
     nb = flags.shape[1]
-    addr = np.empty((nb, plan.n), np.uint64)
-    bids = np.arange(nb, dtype=np.uint64)
-    for i in range(plan.n):
-        r = row(i)  # [nb, L] with its rows contiguous, any stride between bids
-        assert r.shape == (nb, L) and (L == 0 or r.stride(1) == 1)
-        addr[:, i] = np.uint64(r.data_ptr()) + bids * np.uint64(r.stride(0))
+    if geom is None:
+        base = np.empty(plan.n, np.uint64)
+        stride = np.empty(plan.n, np.uint64)
+        for i in range(plan.n):
+            r = row(i)
+            assert r.shape == (nb, L) and (L == 0 or r.stride(1) == 1)
+            base[i], stride[i] = r.data_ptr(), r.stride(0)
+    else:
+        base, stride = geom
+    addr = base[None, :] + np.arange(nb, dtype=np.uint64)[:, None] * stride[None, :]
     status = _repair_call(enc, plan, _shard_table(nb, plan.n, addr, L), nb, flags[1], words,
                           torch.cuda.current_stream(flags.device).cuda_stream)
     if any(status):
@@ -297,27 +304,34 @@ def _repair_columns(enc, local, plan: RepairPlan, rank, world, group, crcs, time
     else:
         recv = local.new_empty(0)
     # where shard i's columns live on this rank: in place in `local` (mine), the receive buffer
-    # (others' shipped shards) or a slot (others' shards bad in every bid)
-    view, o = {}, 0
-    for j in range(world):
-        if j == rank or not frecv[j]:
-            continue
-        blk = recv[o:o + frecv[j]].view(nb, len(ship_by[j]), L_me)
-        for p, i in enumerate(ship_by[j]):
-            view[i] = blk[:, p]
-        o += frecv[j]
+    # (others' shipped shards, [nb, n_from, L_me] per source) or a slot (others' shards bad in every
+    # bid) -- as (tensor, row, bid stride) and as plain addresses for the shard table
     others_slots = [i for i in plan.slots if owner(i, world) != rank]
     slots = local.new_empty((nb, len(others_slots), L_me))
+    where, o = {}, 0
+    for j in range(world):
+        if j == rank:
+            continue
+        for p, i in enumerate(ship_by[j]):
+            where[i] = (recv, o + p * L_me, len(ship_by[j]) * L_me)
+        o += frecv[j]
     for p, i in enumerate(others_slots):
-        view[i] = slots[:, p]
+        where[i] = (slots, p * L_me, len(others_slots) * L_me)
     for i in mine:
-        view[i] = local[:, qof[i], c_me:c_me + L_me]
+        where[i] = (local, qof[i] * S + c_me, n_own * S)
+    base = np.array([where[i][0].data_ptr() + where[i][1] for i in range(n)], np.uint64)
+    bstride = np.array([where[i][2] for i in range(n)], np.uint64)
+
+    def view(i):
+        t_, o_, st_ = where[i]
+        return t_.view(-1).as_strided((nb, L_me), (st_, 1), t_.storage_offset() + o_)
+
     marks.mark("sent")
     # 2. the reference's Reconstruct + Verify of every bid, on this rank's columns
     flags = torch.zeros((2, nb), dtype=torch.int32, device=dev)  # [planning status, Verify flag]
     words = torch.zeros(nb * n, dtype=torch.int32, device=dev) if crcs else None
     if L_me:
-        decode(enc, plan, lambda i: view[i], L_me, flags, words)
+        decode(enc, plan, view, L_me, flags, words, geom=(base, bstride))
     marks.mark("decoded")
     # 3. a bid fails when its columns fail on any rank
     _max_reduce(flags, world, group)
@@ -333,7 +347,7 @@ def _repair_columns(enc, local, plan: RepairPlan, rank, world, group, crcs, time
             if rsend[o_]:
                 blk = send[o:o + rsend[o_]].view(nb, len(reb_by[o_]), L_me)
                 for p, e in enumerate(reb_by[o_]):
-                    blk[:, p] = view[e]
+                    blk[:, p] = view(e)
             o += rsend[o_]
         recv = local.new_empty(sum(rrecv))
         _a2a(recv, send, rrecv, rsend, world, group)
