@@ -925,7 +925,7 @@ Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceCont
   }
   tm.reset(new HostTimer("    sync"));
   for (int l = 0; l < nlanes; ++l) {
-    const Status sync = hip_status(hipStreamSynchronize(lane[l]), "hipStreamSynchronize");
+    const Status sync = ctx->finish(ws, lane[l]);
     if (st == CFSEC_OK) st = sync;
   }
   tm.reset();

@@ -1,4 +1,6 @@
 // engine.cpp -- RSEngine / ECEncoder / LrcEncoder host logic (see engine.hpp).
+#include <chrono>
+
 #include "engine.hpp"
 
 #include <algorithm>
@@ -254,6 +256,45 @@ void DeviceContext::release(Workspace* ws) {
   free_.push_back(ws);
 }
 
+Status DeviceContext::finish(Workspace* ws, hipStream_t stream) {
+  static const bool kPoll = [] {  // CFSEC_SYNC_POLL=0: hipStreamSynchronize always (A/B)
+    const char* v = std::getenv("CFSEC_SYNC_POLL");
+    return !(v && v[0] == '0');
+  }();
+  const auto blocking = [&] { return hip_status(hipStreamSynchronize(stream), "hipStreamSynchronize"); };
+  if (!kPoll) return blocking();
+  if (!ws->hmark) {
+    void* h = nullptr;
+    if (hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+      (void)hipGetLastError();
+      return blocking();
+    }
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      (void)hipHostFree(h);
+      return blocking();
+    }
+    ws->hmark = static_cast<uint32_t*>(h);
+    ws->dmark = static_cast<uint32_t*>(d);
+    __atomic_store_n(ws->hmark, 0u, __ATOMIC_RELEASE);
+    ws->seq = 0;
+  }
+  const uint32_t seq = ++ws->seq;
+  if (hipStreamWriteValue32(stream, ws->dmark, seq, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    return blocking();
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t spin = 0;; ++spin) {
+    if (__atomic_load_n(ws->hmark, __ATOMIC_ACQUIRE) == seq) return CFSEC_OK;
+    __builtin_ia32_pause();
+    if ((spin & 1023u) == 1023u &&
+        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() > kSpinLimitUs)
+      return blocking();
+  }
+}
+
 void DeviceContext::release_after(Workspace* ws, hipStream_t stream) {
   // if the record fails the stream's work is unknown: wait for the device before reuse
   if (hipEventRecord(ws->done, stream) != hipSuccess) {
@@ -449,7 +490,7 @@ Status RSEngine::run(const Matrix& rows, const std::vector<cfsec_shard*>& ins,
   if (st == CFSEC_OK && host && !verify)
     for (int r = 0; r < nout && st == CFSEC_OK; ++r)
       st = hip_status(hipMemcpyAsync(outs[r]->data, dout[r], S, hipMemcpyDeviceToHost, s), "hipMemcpyAsync D2H");
-  const Status sync = hip_status(hipStreamSynchronize(s), "hipStreamSynchronize");
+  const Status sync = ctx_->finish(ws, s);
   if (st == CFSEC_OK) st = sync;
   if (st == CFSEC_OK && verify && ok) *ok = ws->hflags[0] == 0;
   ctx_->release(ws);
@@ -545,7 +586,7 @@ Status RSEngine::run_host(const Matrix& rows, const std::vector<cfsec_shard*>& i
   if (st == CFSEC_OK && verify)
     st = hip_status(hipMemcpyAsync(ws->hflags, ws->dflags, 4, hipMemcpyDeviceToHost, lane[0]), "hipMemcpyAsync D2H");
   for (int l = 0; l < nlanes; ++l) {
-    const Status sync = hip_status(hipStreamSynchronize(lane[l]), "hipStreamSynchronize");
+    const Status sync = ctx_->finish(ws, lane[l]);
     if (st == CFSEC_OK) st = sync;
   }
   if (st == CFSEC_OK && verify && ok) *ok = ws->hflags[0] == 0;
@@ -623,7 +664,7 @@ Status RSEngine::encode_crc(cfsec_shard* shards, int n, int mem, hipStream_t str
       st = hip_status(hipMemcpyAsync(shards[r].data, dptr[r], S, hipMemcpyDeviceToHost, s), "hipMemcpyAsync D2H");
   if (st == CFSEC_OK)
     st = hip_status(hipMemcpyAsync(ws->hflags, ws->dflags, 4 * (size_t)n, hipMemcpyDeviceToHost, s), "hipMemcpyAsync D2H");
-  const Status sync = hip_status(hipStreamSynchronize(s), "hipStreamSynchronize");
+  const Status sync = ctx_->finish(ws, s);
   if (st == CFSEC_OK) st = sync;
   if (st == CFSEC_OK) std::memcpy(crcs, ws->hflags, 4 * (size_t)n);
   ctx_->release(ws);

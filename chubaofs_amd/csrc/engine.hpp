@@ -85,7 +85,19 @@ class DeviceContext {
     uint32_t* dcrc = nullptr;
     uint32_t* hcrc = nullptr;
     size_t ncrc = 0;
+    // finish(): a pinned, coherent word the stream writes after its work, polled by the caller
+    uint32_t* hmark = nullptr;
+    uint32_t* dmark = nullptr;
+    uint32_t seq = 0;
   };
+  // Wait for everything queued on `stream` so far (a synchronous call's end): the stream writes a
+  // sequence number into ws's pinned marker word after its work (hipStreamWriteValue32) and the
+  // caller polls it, which returns as soon as the GPU gets there -- hipStreamSynchronize's
+  // completion-signal wait returned ~15-20 us later (C4 / C5 calls, profiles/r04).  Falls back to
+  // hipStreamSynchronize when the marker cannot be written, and after kSpinLimitUs of polling (a
+  // long host batch, a fault: the runtime then reports the error).
+  Status finish(Workspace* ws, hipStream_t stream);
+  static constexpr double kSpinLimitUs = 20000.0;
   // Order ws->stream after the work already queued on the legacy default stream (and, by that
   // stream's semantics, on every blocking stream of the device): a device-memory call made
   // without a caller stream must not read its input before the kernel that produced it ran.
