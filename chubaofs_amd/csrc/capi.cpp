@@ -155,7 +155,7 @@ int crc32block_call(bool encode, const uint8_t* src, int64_t src_len, int64_t si
                              "hipMemcpyAsync D2H");
     if (st == CFSEC_OK)
       st = cfsec::hip_status(hipMemcpyAsync(ws->hflags, ws->dflags, 8, hipMemcpyDeviceToHost, s), "hipMemcpyAsync D2H");
-    const int sync = cfsec::hip_status(hipStreamSynchronize(s), "hipStreamSynchronize");
+    const int sync = ctx->finish(ws, s);
     if (st == CFSEC_OK) st = sync;
     if (st == CFSEC_OK) {
       if (encode && shard_crc) *shard_crc = ws->hflags[1];
@@ -558,7 +558,7 @@ int cfsec_crc32_ieee_batch(uint8_t* const* ptrs, size_t shard_size, int n, uint3
     if (st == CFSEC_OK)
       st = cfsec::hip_status(hipMemcpyAsync(ws->hflags, ws->dflags, 4 * (size_t)n, hipMemcpyDeviceToHost, s),
                              "hipMemcpyAsync D2H");
-    const int sync = cfsec::hip_status(hipStreamSynchronize(s), "hipStreamSynchronize");
+    const int sync = ctx->finish(ws, s);
     if (st == CFSEC_OK) st = sync;
     if (st == CFSEC_OK)
       for (int i = 0; i < n; ++i) out[i] = cfsec::crc32_finalize(ws->hflags[i], shard_size);
