@@ -126,6 +126,7 @@ type Engine struct {
 	h            *C.cfsec_rs
 	dataShards   int
 	parityShards int
+	cpu          reedsolomon.Encoder // Split / Join only (host bookkeeping)
 }
 
 var _ reedsolomon.Encoder = (*Engine)(nil)
@@ -171,7 +172,12 @@ func New(dataShards, parityShards int) (*Engine, error) {
 	if err := toError(C.cfsec_rs_new(C.int(dataShards), C.int(parityShards), -1, &h)); err != nil {
 		return nil, err
 	}
-	e := &Engine{h: h, dataShards: dataShards, parityShards: parityShards}
+	cpu, err := reedsolomon.New(dataShards, parityShards)
+	if err != nil {
+		C.cfsec_rs_free(h)
+		return nil, err
+	}
+	e := &Engine{h: h, dataShards: dataShards, parityShards: parityShards, cpu: cpu}
 	runtime.SetFinalizer(e, func(e *Engine) { C.cfsec_rs_free(e.h) })
 	return e, nil
 }
@@ -313,90 +319,13 @@ func (e *Engine) Reconstruct(shards [][]byte) error { return e.reconstruct(shard
 
 func (e *Engine) ReconstructData(shards [][]byte) error { return e.reconstruct(shards, true) }
 
-// Split is host bookkeeping (KRS/reedsolomon.go:1574-1632) and stays in Go: the shards are views
-// into data (its spare capacity zeroed and used), the tail in AllocAligned padding, each capped at
-// the shard size as the reference's three-index slices are.
-func (e *Engine) Split(data []byte) ([][]byte, error) {
-	total := e.dataShards + e.parityShards
-	if len(data) == 0 {
-		return nil, reedsolomon.ErrShortData
-	}
-	if total == 1 {
-		return [][]byte{data}, nil
-	}
-	dataLen := len(data)
-	per := (dataLen + e.dataShards - 1) / e.dataShards
-	need := total * per
-	if cap(data) > len(data) {
-		if cap(data) > need {
-			data = data[:need]
-		} else {
-			data = data[:cap(data)]
-		}
-		for i := dataLen; i < len(data); i++ {
-			data[i] = 0
-		}
-	}
-	var padding [][]byte
-	if len(data) < need {
-		full := len(data) / per
-		padding = reedsolomon.AllocAligned(total-full, per)
-		if dataLen > per*full {
-			rest := data[per*full : dataLen]
-			for i := range padding {
-				if len(rest) == 0 {
-					break
-				}
-				rest = rest[copy(padding[i], rest):]
-			}
-		}
-	}
-	out := make([][]byte, total)
-	i := 0
-	for ; i < total && len(data) >= per; i++ {
-		out[i] = data[:per:per]
-		data = data[per:]
-	}
-	for j := 0; i+j < total; j++ {
-		out[i+j] = padding[0]
-		padding = padding[1:]
-	}
-	return out, nil
-}
+// Split and Join are host bookkeeping with no coding in them, so they are klauspost's own
+// (KRS/reedsolomon.go:1574-1632, 1646-1684) on a CPU engine of the same shape: the shard views,
+// the AllocAligned padding and the io.Writer's write pattern are the reference's by construction.
+func (e *Engine) Split(data []byte) ([][]byte, error) { return e.cpu.Split(data) }
 
-// Join is pure host bookkeeping (KRS/reedsolomon.go:1646-1684); it stays in Go so the
-// io.Writer sees exactly the reference's write pattern.
 func (e *Engine) Join(dst io.Writer, shards [][]byte, outSize int) error {
-	if len(shards) < e.dataShards {
-		return reedsolomon.ErrTooFewShards
-	}
-	shards = shards[:e.dataShards]
-	size := 0
-	for _, shard := range shards {
-		if shard == nil {
-			return reedsolomon.ErrReconstructRequired
-		}
-		size += len(shard)
-		if size >= outSize {
-			break
-		}
-	}
-	if size < outSize {
-		return reedsolomon.ErrShortData
-	}
-	write := outSize
-	for _, shard := range shards {
-		if write < len(shard) {
-			_, err := dst.Write(shard[:write])
-			return err
-		}
-		n, err := dst.Write(shard)
-		if err != nil {
-			return err
-		}
-		write -= n
-	}
-	return nil
+	return e.cpu.Join(dst, shards, outSize)
 }
 
 func (e *Engine) EncodeIdx(dataShard []byte, idx int, parity [][]byte) error {

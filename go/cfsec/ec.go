@@ -447,18 +447,16 @@ func (e *ECEncoder) Split(data []byte) ([][]byte, error) {
 	if err != nil || e.tactic.L == 0 {
 		return shards, err
 	}
-	// lrcencoder.go:203-222: the local shards follow in the same buffer when it has room
-	shardN, shardLen := len(shards), len(shards[0])
-	if cap(data) >= (e.tactic.L+shardN)*shardLen {
-		if cap(data) > len(data) {
-			data = data[:cap(data)]
-		}
-		for i := 0; i < e.tactic.L; i++ {
-			shards = append(shards, data[(shardN+i)*shardLen:(shardN+i+1)*shardLen])
-		}
-	} else {
-		for i := 0; i < e.tactic.L; i++ {
-			shards = append(shards, make([]byte, shardLen))
+	// lrcencoder.go:203-222: the L local shards take the next L shard-sized pieces of data's
+	// capacity when all of them fit there, else fresh zeroed buffers
+	n, size := len(shards), len(shards[0])
+	room := cap(data) >= (n+e.tactic.L)*size
+	whole := data[:cap(data)]
+	for i := n; i < n+e.tactic.L; i++ {
+		if room {
+			shards = append(shards, whole[i*size:(i+1)*size])
+		} else {
+			shards = append(shards, make([]byte, size))
 		}
 	}
 	return shards, nil
