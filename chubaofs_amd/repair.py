@@ -37,6 +37,7 @@ whole (world x the decode work, world/2 x the exchange bytes of "columns").
 from __future__ import annotations
 
 import ctypes
+import functools
 from dataclasses import dataclass, field
 from typing import List, Optional
 
@@ -69,10 +70,10 @@ def column_split(S: int, world: int, align: int = 256):
     return out
 
 
-@dataclass
+@dataclass(eq=False)
 class RepairPlan:
     """The shape of one tasklet repair, identical on every rank (a function of the code mode and the
-    bad sets only).
+    bad sets only).  Plans are cached per bad-set pattern (`make`) and must not be mutated.
 
     bad[b]: bid b's bad shard indices (blobnode's recoverIdxOfStripe, work_shard_recover.go:715-718).
     rebuilt: shards bad in some bid, index order -- the rows the repair returns to their owners.
@@ -86,28 +87,38 @@ class RepairPlan:
     shipped: List[int]
     slots: List[int]
     verify: bool = True
+    _c: object = field(default=None, repr=False)  # the bad sets as C arrays (_bad_arrays)
 
     @staticmethod
     def make(n: int, nbids: int, bad, verify: bool = True) -> "RepairPlan":
         if len(bad) and isinstance(bad[0], (list, tuple, np.ndarray)):
-            per = [sorted(set(int(i) for i in b)) for b in bad]
-            if len(per) != nbids:
+            if len(bad) != nbids:
                 raise ValueError("one bad-index list per bid")
+            key = tuple(tuple(int(i) for i in b) for b in bad)
         else:
-            per = [sorted(set(int(i) for i in bad))] * nbids
-        for b in per:
-            for i in b:
-                if not 0 <= i < n:
-                    raise IndexError(f"bad shard index {i} out of range [0, {n})")  # the reference panics
-        union = sorted(set().union(*per)) if per else []
-        every = sorted(set(per[0]).intersection(*per[1:])) if per else []
-        shipped = [i for i in range(n) if i not in every]
-        return RepairPlan(n, per, union, shipped, every, verify)
+            key = tuple(int(i) for i in bad)
+        return _make_plan(n, nbids, key, bool(verify))
 
     def order(self, world: int) -> List[int]:
         """Row order of a rank's work buffer: the shipped shards grouped by owner rank (so each source
         rank's block is contiguous in the all_to_all), then the slots."""
         return sorted(self.shipped, key=lambda i: (owner(i, world), i)) + list(self.slots)
+
+
+@functools.lru_cache(maxsize=256)
+def _make_plan(n: int, nbids: int, key: tuple, verify: bool) -> RepairPlan:
+    if key and isinstance(key[0], tuple):
+        per = [sorted(set(b)) for b in key]
+    else:
+        per = [sorted(set(key))] * nbids
+    for b in per:
+        for i in b:
+            if not 0 <= i < n:
+                raise IndexError(f"bad shard index {i} out of range [0, {n})")  # the reference panics
+    union = sorted(set().union(*per)) if per else []
+    every = sorted(set(per[0]).intersection(*per[1:])) if per else []
+    shipped = [i for i in range(n) if i not in every]
+    return RepairPlan(n, per, union, shipped, every, verify)
 
 
 @dataclass
@@ -143,11 +154,13 @@ def _shard_table(nbids: int, n: int, addr: np.ndarray, length: int):
 
 
 def _bad_arrays(plan: RepairPlan):
-    flat = [i for b in plan.bad for i in b]
-    off = [0]
-    for b in plan.bad:
-        off.append(off[-1] + len(b))
-    return (ctypes.c_int * max(len(flat), 1))(*flat), (ctypes.c_int * len(off))(*off)
+    if plan._c is None:
+        flat = [i for b in plan.bad for i in b]
+        off = [0]
+        for b in plan.bad:
+            off.append(off[-1] + len(b))
+        plan._c = (ctypes.c_int * max(len(flat), 1))(*flat), (ctypes.c_int * len(off))(*off)
+    return plan._c
 
 
 def _repair_call(enc, plan: RepairPlan, table: np.ndarray, nbids: int, flags: torch.Tensor,
@@ -215,23 +228,25 @@ class _Marks:
 
 
 def gpu_decode(enc, plan: RepairPlan, row, L: int, flags: torch.Tensor, words: Optional[torch.Tensor],
-               geom=None) -> None:
+               geom=None, addr=None) -> None:
     """Step 2 on this rank's GPU: the reference's per-bid Reconstruct + Verify over the [nbids, L] rows
     of every shard (row(i): a view with its rows contiguous; geom: (base addresses, bid strides) of
-    the same rows as two uint64 arrays, which spares the views), rebuilt rows written in place.
+    the same rows as two uint64 arrays, which spares the views; addr: the [nbids, n] row addresses
+    themselves), rebuilt rows written in place.
     flags[0] receives the per-bid planning status, flags[1] the Verify flags (on the stream), words
     the rebuilt rows' checksums."""
     nb = flags.shape[1]
-    if geom is None:
-        base = np.empty(plan.n, np.uint64)
-        stride = np.empty(plan.n, np.uint64)
-        for i in range(plan.n):
-            r = row(i)
-            assert r.shape == (nb, L) and (L == 0 or r.stride(1) == 1)
-            base[i], stride[i] = r.data_ptr(), r.stride(0)
-    else:
-        base, stride = geom
-    addr = base[None, :] + np.arange(nb, dtype=np.uint64)[:, None] * stride[None, :]
+    if addr is None:
+        if geom is None:
+            base = np.empty(plan.n, np.uint64)
+            stride = np.empty(plan.n, np.uint64)
+            for i in range(plan.n):
+                r = row(i)
+                assert r.shape == (nb, L) and (L == 0 or r.stride(1) == 1)
+                base[i], stride[i] = r.data_ptr(), r.stride(0)
+        else:
+            base, stride = geom
+        addr = base[None, :] + np.arange(nb, dtype=np.uint64)[:, None] * stride[None, :]
     status = _repair_call(enc, plan, _shard_table(nb, plan.n, addr, L), nb, flags[1], words,
                           torch.cuda.current_stream(flags.device).cuda_stream)
     if any(status):
@@ -242,7 +257,7 @@ def _statuses(flags: torch.Tensor, S: int) -> List[int]:
     st = flags.cpu().numpy()
     if S == 0:
         return [_lib.ErrShardNoData.status] * st.shape[1]  # checkShards on all-empty shards
-    return [int(st[0, b]) if st[0, b] else (_lib.ErrVerify.status if st[1, b] else 0) for b in range(st.shape[1])]
+    return np.where(st[0] != 0, st[0], np.where(st[1] != 0, _lib.ErrVerify.status, 0)).tolist()
 
 
 # ---------------------------------------------------------------- the tasklet repair
@@ -261,9 +276,8 @@ def repair_batch(enc, local: torch.Tensor, bad, rank: int, world: int, strategy:
     t = enc.CodeMode
     n = t.N + t.M + t.L
     nb, n_own, S = local.shape
-    mine = owned(rank, n, world)
-    if n_own != len(mine):
-        raise ValueError(f"rank {rank} holds {len(mine)} shards per bid, local has {n_own}")
+    if n_own != len(range(rank, n, world)):  # owned(rank, n, world)
+        raise ValueError(f"rank {rank} holds {len(range(rank, n, world))} shards per bid, local has {n_own}")
     plan = RepairPlan.make(n, nb, bad, verify)
     if strategy == "columns":
         return _repair_columns(enc, local, plan, rank, world, group, crcs, timer, decode)
@@ -272,81 +286,124 @@ def repair_batch(enc, local: torch.Tensor, bad, rank: int, world: int, strategy:
     raise ValueError(strategy)
 
 
-def _repair_columns(enc, local, plan: RepairPlan, rank, world, group, crcs, timer, decode) -> RepairResult:
-    nb, n_own, S = local.shape
+@dataclass(eq=False)
+class _Columns:
+    """Everything about a columns repair that follows from (plan, S, world, rank, n_owned): the
+    column ranges, the exchange sizes and where every shard's columns sit on this rank -- `kind`
+    (0: in place in `local`, 1: the receive buffer, 2: a slot), a byte offset into that buffer and a
+    bid stride.  Cached, so a repeated pattern costs the host only the addresses of its buffers."""
+
+    cols: list
+    c_me: int
+    L_me: int
+    mine: List[int]
+    qof: dict
+    sel: List[int]
+    fsend: List[int]
+    frecv: List[int]
+    n_slots: int
+    kind: np.ndarray
+    off: np.ndarray
+    bstride: np.ndarray
+    rows_off: np.ndarray   # [nb, n] bid b's byte offset of shard i from its buffer's base
+    out_idx: List[int]
+    reb_by: List[List[int]]
+    rsend: List[int]
+    rrecv: List[int]
+
+
+@functools.lru_cache(maxsize=256)
+def _columns(plan: RepairPlan, nb: int, S: int, world: int, rank: int) -> _Columns:
     n = plan.n
-    dev = local.device
-    marks = _Marks(timer, dev)
     cols = column_split(S, world)
     c_me, L_me = cols[rank]
     mine = owned(rank, n, world)
+    n_own = len(mine)
     qof = {i: q for q, i in enumerate(mine)}
     # shipped shards by owner; a source's block in the receive buffer is [nb, n_from[j], L_me]
     ship_by = [[i for i in plan.shipped if owner(i, world) == j] for j in range(world)]
     sel = [qof[i] for i in ship_by[rank]]
     n_me = len(sel)
-    marks.mark("t0")
-    # 1. forward exchange: to rank r != rank, my shipped shards' columns [c_r, c_r + L_r) as [nb, n_me, L_r]
+    # to rank r != rank: my shipped shards' columns [c_r, c_r + L_r) as [nb, n_me, L_r]
     fsend = [0 if r == rank else n_me * nb * cols[r][1] for r in range(world)]
     frecv = [0 if j == rank else len(ship_by[j]) * nb * L_me for j in range(world)]
+    others_slots = [i for i in plan.slots if owner(i, world) != rank]
+    kind = np.zeros(n, np.int64)
+    off = np.zeros(n, np.uint64)
+    bstride = np.zeros(n, np.uint64)
+    o = 0
+    for j in range(world):
+        if j == rank:
+            continue
+        for p, i in enumerate(ship_by[j]):
+            kind[i], off[i], bstride[i] = 1, o + p * L_me, len(ship_by[j]) * L_me
+        o += frecv[j]
+    for p, i in enumerate(others_slots):
+        kind[i], off[i], bstride[i] = 2, p * L_me, len(others_slots) * L_me
+    for i in mine:
+        kind[i], off[i], bstride[i] = 0, qof[i] * S + c_me, n_own * S
+    rows_off = off[None, :] + np.arange(nb, dtype=np.uint64)[:, None] * bstride[None, :]
+    out_idx = [e for e in plan.rebuilt if owner(e, world) == rank]
+    reb_by = [[e for e in plan.rebuilt if owner(e, world) == o_] for o_ in range(world)]
+    rsend = [0 if o_ == rank else len(reb_by[o_]) * nb * L_me for o_ in range(world)]
+    rrecv = [0 if r == rank else len(out_idx) * nb * cols[r][1] for r in range(world)]
+    return _Columns(cols, c_me, L_me, mine, qof, sel, fsend, frecv, len(others_slots), kind, off, bstride,
+                    rows_off, out_idx, reb_by, rsend, rrecv)
+
+
+def _repair_columns(enc, local, plan: RepairPlan, rank, world, group, crcs, timer, decode) -> RepairResult:
+    nb, n_own, S = local.shape
+    n = plan.n
+    dev = local.device
+    marks = _Marks(timer, dev)
+    lay = _columns(plan, nb, S, world, rank)
+    cols, c_me, L_me, qof = lay.cols, lay.c_me, lay.L_me, lay.qof
+    marks.mark("t0")
+    # 1. forward exchange: to rank r != rank, my shipped shards' columns [c_r, c_r + L_r)
     if world > 1:
-        send = local.new_empty(sum(fsend))
-        src = local if sel == list(range(n_own)) else local[:, sel]
-        o = 0
+        send = local.new_empty(sum(lay.fsend))
+        src = local if lay.sel == list(range(n_own)) else local[:, lay.sel]
+        n_me, o = len(lay.sel), 0
         for r in range(world):
-            if fsend[r]:
+            if lay.fsend[r]:
                 c, L = cols[r]
-                send[o:o + fsend[r]].view(nb, n_me, L).copy_(src[:, :, c:c + L])
-            o += fsend[r]
-        recv = local.new_empty(sum(frecv))
-        _a2a(recv, send, frecv, fsend, world, group)
+                send[o:o + lay.fsend[r]].view(nb, n_me, L).copy_(src[:, :, c:c + L])
+            o += lay.fsend[r]
+        recv = local.new_empty(sum(lay.frecv))
+        _a2a(recv, send, lay.frecv, lay.fsend, world, group)
         del send
     else:
         recv = local.new_empty(0)
     # where shard i's columns live on this rank: in place in `local` (mine), the receive buffer
     # (others' shipped shards, [nb, n_from, L_me] per source) or a slot (others' shards bad in every
-    # bid) -- as (tensor, row, bid stride) and as plain addresses for the shard table
-    others_slots = [i for i in plan.slots if owner(i, world) != rank]
-    slots = local.new_empty((nb, len(others_slots), L_me))
-    where, o = {}, 0
-    for j in range(world):
-        if j == rank:
-            continue
-        for p, i in enumerate(ship_by[j]):
-            where[i] = (recv, o + p * L_me, len(ship_by[j]) * L_me)
-        o += frecv[j]
-    for p, i in enumerate(others_slots):
-        where[i] = (slots, p * L_me, len(others_slots) * L_me)
-    for i in mine:
-        where[i] = (local, qof[i] * S + c_me, n_own * S)
-    base = np.array([where[i][0].data_ptr() + where[i][1] for i in range(n)], np.uint64)
-    bstride = np.array([where[i][2] for i in range(n)], np.uint64)
+    # bid)
+    slots = local.new_empty((nb, lay.n_slots, L_me))
+    bufs = (local, recv, slots)
+    ptrs = np.array([t_.data_ptr() for t_ in bufs], np.uint64)
 
     def view(i):
-        t_, o_, st_ = where[i]
-        return t_.view(-1).as_strided((nb, L_me), (st_, 1), t_.storage_offset() + o_)
+        t_ = bufs[lay.kind[i]]
+        return t_.view(-1).as_strided((nb, L_me), (int(lay.bstride[i]), 1), t_.storage_offset() + int(lay.off[i]))
 
     marks.mark("sent")
     # 2. the reference's Reconstruct + Verify of every bid, on this rank's columns
     flags = torch.zeros((2, nb), dtype=torch.int32, device=dev)  # [planning status, Verify flag]
     words = torch.zeros(nb * n, dtype=torch.int32, device=dev) if crcs else None
     if L_me:
-        decode(enc, plan, view, L_me, flags, words, geom=(base, bstride))
+        decode(enc, plan, view, L_me, flags, words, geom=(ptrs[lay.kind] + lay.off, lay.bstride),
+               addr=ptrs[lay.kind][None, :] + lay.rows_off)
     marks.mark("decoded")
     # 3. a bid fails when its columns fail on any rank
     _max_reduce(flags, world, group)
     # 4. return exchange: the rebuilt rows' columns to their owners, [nb, n_rebuilt(owner), L_me]
-    out_idx = [e for e in plan.rebuilt if owner(e, world) == rank]
-    reb_by = [[e for e in plan.rebuilt if owner(e, world) == o_] for o_ in range(world)]
-    rsend = [0 if o_ == rank else len(reb_by[o_]) * nb * L_me for o_ in range(world)]
-    rrecv = [0 if r == rank else len(out_idx) * nb * cols[r][1] for r in range(world)]
+    out_idx, rsend, rrecv = lay.out_idx, lay.rsend, lay.rrecv
     if world > 1 and (sum(rsend) or sum(rrecv)):
         send = local.new_empty(sum(rsend))
         o = 0
         for o_ in range(world):
             if rsend[o_]:
-                blk = send[o:o + rsend[o_]].view(nb, len(reb_by[o_]), L_me)
-                for p, e in enumerate(reb_by[o_]):
+                blk = send[o:o + rsend[o_]].view(nb, len(lay.reb_by[o_]), L_me)
+                for p, e in enumerate(lay.reb_by[o_]):
                     blk[:, p] = view(e)
             o += rsend[o_]
         recv = local.new_empty(sum(rrecv))
@@ -370,8 +427,8 @@ def _repair_columns(enc, local, plan: RepairPlan, rank, world, group, crcs, time
             dist.all_gather_into_tensor(allw.view(-1), wt, group=group)
             w = np.bitwise_xor.reduce(allw.cpu().numpy().view(np.uint32), axis=0)
         w = w.reshape(nb, n)
-        res.crcs = np.stack([w[:, e] for e in out_idx], axis=1) if out_idx else np.zeros((nb, 0), np.uint32)
-    res.stats = {"exchange_bytes_sent": int(sum(fsend)), "exchange_bytes_received": int(sum(frecv)),
+        res.crcs = w[:, out_idx].copy() if out_idx else np.zeros((nb, 0), np.uint32)
+    res.stats = {"exchange_bytes_sent": int(sum(lay.fsend)), "exchange_bytes_received": int(sum(lay.frecv)),
                  "return_bytes_received": int(sum(rrecv)), "rows_shipped": len(plan.shipped), "columns": L_me}
     marks.finish()
     return res

@@ -81,7 +81,7 @@ def oracle_repair(mode, full, per):
     return st, out, crc
 
 
-def oracle_decode(enc, plan, row, L, flags, words, geom=None):
+def oracle_decode(enc, plan, row, L, flags, words, geom=None, addr=None):
     """Step 2 with the oracle (CPU tests only): ECOracle.repair of every bid's column slices."""
     t = enc.CodeMode
     o = ECOracle.from_tactic(t)
