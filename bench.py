@@ -232,6 +232,15 @@ def cpu_saturated(S, prow, drows, seconds, callers):
 
 
 # ----------------------------------------------------------------- GPU
+def leg(fn):
+    try:
+        return fn()
+    except Exception as e:  # noqa: BLE001 -- reported in the JSON line, with the traceback on stderr
+        import traceback
+        traceback.print_exc()
+        return {"error": f"{type(e).__name__}: {e}"}
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ and not args.pmc_child:
@@ -431,11 +440,14 @@ def main():
         extra = secondary(args, torch, enc, batch, ptrs, stream, S, nst, pitch, dev, launch_bytes, data_bytes)
         del batch, golden
         torch.cuda.empty_cache()
-        extra["C5_multi_gpu_repair"] = multi_gpu_repair(args, torch, dev, rank, world)
-        extra["segment_reconstruct_data"] = segment_latency(args, torch, dev,
-                                                            cpu=(world == 1 and rank == 0 and not args.no_cpu))
-        extra["configs"] = other_configs(args, torch, dev, stream, cpu=(world == 1 and rank == 0 and not args.no_cpu))
-        extra["host_path"] = host_path(args, torch, dev, world)
+        cpu_here = world == 1 and rank == 0 and not args.no_cpu
+        # the secondary legs run after the headline is measured and gated: an exception in one (every
+        # rank runs the same code on the same shapes, so it raises on all of them) is recorded in its
+        # field instead of costing the job its headline line
+        extra["C5_multi_gpu_repair"] = leg(lambda: multi_gpu_repair(args, torch, dev, rank, world))
+        extra["segment_reconstruct_data"] = leg(lambda: segment_latency(args, torch, dev, cpu=cpu_here))
+        extra["configs"] = leg(lambda: other_configs(args, torch, dev, stream, cpu=cpu_here))
+        extra["host_path"] = leg(lambda: host_path(args, torch, dev, world))
 
     if rank != 0:
         if world > 1:
