@@ -176,6 +176,19 @@ def test_repair_oracle_decoder_world1():
             check_result(res, 0, 1, c["mode"], full, per, *want)
 
 
+def test_cached_layout_follows_the_buffers():
+    """Plans and column layouts are cached per bad-set pattern, never per buffer: repeated calls on
+    fresh tensors (other addresses, other bytes) each repair their own tasklet."""
+    c = CASES["EC16P20L2"]
+    enc = types.SimpleNamespace(CodeMode=cm.GetTactic(c["mode"]))
+    assert repair.RepairPlan.make(38, 4, c["bad"]) is repair.RepairPlan.make(38, 4, list(c["bad"]))
+    for seed in (5, 6, 7):
+        full, per = make_tasklet(c["mode"], c["nb"], c["S"], seed, c["bad"], c["corrupt"])
+        want = oracle_repair(c["mode"], full, per)
+        res = repair.repair_batch(enc, torch.from_numpy(full.copy()), per, 0, 1, crcs=True, decode=oracle_decode)
+        check_result(res, 0, 1, c["mode"], full, per, *want)
+
+
 def test_column_split_covers_exactly():
     for S_, w in [(1000, 2), (1000, 3), (262144, 8), (5, 8), (5592406, 8)]:
         cols = repair.column_split(S_, w)
