@@ -1,0 +1,149 @@
+// bs_probe.hip -- bit-sliced EC16P20L2 parity (dev probe, round 4).
+//
+// The 22 parity rows of EC16P20L2 (20 global + 2 AZ-local, over the 16 data rows) from the
+// generated XOR network (tools/bs_net_ec16p20l2.hpp): each lane holds 32 bytes of
+// every data row as 8 bit planes (an 8x8 bit transpose per byte lane: 3 swap stages), runs the
+// network row by row and transposes each output row back.  Same tasklet shape as the library's
+// EC16P20L2 fused encode in tools/gf_shapes (64 stripes x S = 262,144), three batches in rotation;
+// stripe 0 and stripe 63 checked against a scalar GF product on the host.
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 bs_probe.hip -o bs_probe
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "bs_net_ec16p20l2.hpp"
+
+#define CK(x)                                                                          \
+  do {                                                                                 \
+    hipError_t e_ = (x);                                                               \
+    if (e_ != hipSuccess) {                                                            \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      exit(1);                                                                         \
+    }                                                                                  \
+  } while (0)
+
+constexpr int K = 16, M = 22, ROWS = K + M, NB = 64, NT = 3;
+constexpr size_t S = 262144;
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void swapmove(uint32_t& a, uint32_t& b, int s, uint32_t m) {
+  const uint32_t t = ((a >> s) ^ b) & m;
+  b ^= t;
+  a ^= t << s;
+}
+
+// 8 dwords (32 bytes) <-> 8 bit planes; an involution
+__device__ __forceinline__ void transpose8(uint32_t* w) {
+#pragma unroll
+  for (int i = 0; i < 8; i += 2) swapmove(w[i], w[i + 1], 1, 0x55555555u);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    if (!(i & 2)) swapmove(w[i], w[i + 2], 2, 0x33333333u);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) swapmove(w[i], w[i + 4], 4, 0x0F0F0F0Fu);
+}
+
+__device__ __forceinline__ u32x4 ld16nt(const uint8_t* p) {
+  return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+}
+__device__ __forceinline__ void st16nt(uint8_t* p, u32x4 v) {
+  __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+}
+
+template <int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void bs_encode(uint8_t* base) {
+  const uint32_t stripe = blockIdx.y;
+  const size_t off = ((size_t)blockIdx.x * 256 + threadIdx.x) * 32;
+  uint8_t* row0 = base + (size_t)stripe * ROWS * S;
+  uint32_t x[128];
+#pragma unroll
+  for (int c = 0; c < K; ++c) {
+    const u32x4 a = ld16nt(row0 + c * S + off), b = ld16nt(row0 + c * S + off + 16);
+    x[8 * c + 0] = a.x; x[8 * c + 1] = a.y; x[8 * c + 2] = a.z; x[8 * c + 3] = a.w;
+    x[8 * c + 4] = b.x; x[8 * c + 5] = b.y; x[8 * c + 6] = b.z; x[8 * c + 7] = b.w;
+  }
+#pragma unroll
+  for (int c = 0; c < K; ++c) transpose8(&x[8 * c]);
+  cfsec::dev::bs_net_ec16p20l2(x, [&](int r, uint32_t (&o)[8]) {
+    transpose8(o);
+    uint8_t* p = row0 + (size_t)(K + r) * S + off;
+    st16nt(p, u32x4{o[0], o[1], o[2], o[3]});
+    st16nt(p + 16, u32x4{o[4], o[5], o[6], o[7]});
+  });
+}
+
+__global__ void fill(uint32_t* p, size_t n, uint32_t seed) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    uint32_t v = (uint32_t)i * 2654435761u ^ seed;
+    v ^= v >> 15; v *= 0x2c1b3c6du; v ^= v >> 12;
+    p[i] = v;
+  }
+}
+
+static uint8_t gmul(uint8_t a, uint8_t b) {
+  uint8_t p = 0;
+  while (b) {
+    if (b & 1) p ^= a;
+    a = (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1D : 0));
+    b >>= 1;
+  }
+  return p;
+}
+
+template <int WPE>
+static double run(std::vector<uint8_t*>& bufs, int reps) {
+  const dim3 grid((unsigned)(S / (256 * 32)), NB);
+  for (int i = 0; i < 6; ++i) hipLaunchKernelGGL((bs_encode<WPE>), grid, dim3(256), 0, 0, bufs[i % NT]);
+  CK(hipDeviceSynchronize());
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  CK(hipEventRecord(e0, 0));
+  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((bs_encode<WPE>), grid, dim3(256), 0, 0, bufs[i % NT]);
+  CK(hipEventRecord(e1, 0));
+  CK(hipEventSynchronize(e1));
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  return ms * 1e3 / reps;
+}
+
+int main() {
+  std::vector<uint8_t*> bufs(NT);
+  const size_t bytes = (size_t)NB * ROWS * S;
+  for (int t = 0; t < NT; ++t) {
+    CK(hipMalloc(&bufs[t], bytes));
+    fill<<<4096, 256>>>((uint32_t*)bufs[t], bytes / 4, 0x9E3779B9u * (t + 1));
+  }
+  CK(hipDeviceSynchronize());
+  // correctness: batch 0, stripes 0 and NB-1, every parity byte
+  const dim3 grid((unsigned)(S / (256 * 32)), NB);
+  hipLaunchKernelGGL((bs_encode<2>), grid, dim3(256), 0, 0, bufs[0]);
+  CK(hipDeviceSynchronize());
+  std::vector<uint8_t> h((size_t)ROWS * S);
+  long bad = 0;
+  for (int st : {0, NB - 1}) {
+    CK(hipMemcpy(h.data(), bufs[0] + (size_t)st * ROWS * S, h.size(), hipMemcpyDeviceToHost));
+    for (int r = 0; r < M; ++r)
+      for (size_t i = 0; i < S; ++i) {
+        uint8_t v = 0;
+        for (int c = 0; c < K; ++c) v ^= gmul(cfsec::dev::kBsEc16p20l2Rows[r][c], h[(size_t)c * S + i]);
+        if (v != h[(size_t)(K + r) * S + i] && bad++ < 5)
+          printf("mismatch stripe %d row %d byte %zu: %02x vs %02x\n", st, r, i, h[(size_t)(K + r) * S + i], v);
+      }
+  }
+  printf("parity check: %s (%ld bad bytes)\n", bad ? "FAIL" : "ok", bad);
+  if (bad) return 1;
+  const double algo = (double)NB * ROWS * S;
+  for (int rep = 0; rep < 2; ++rep) {
+    double us = run<2>(bufs, 30);
+    printf("bs_encode 16->22 waves/EU 2: %8.1f us  %6.1f GB/s  %5.1f %% of 8 TB/s\n", us, algo / us / 1e3, algo / us / 8e4);
+    us = run<1>(bufs, 30);
+    printf("bs_encode 16->22 waves/EU 1: %8.1f us  %6.1f GB/s  %5.1f %% of 8 TB/s\n", us, algo / us / 1e3, algo / us / 8e4);
+  }
+  return 0;
+}

@@ -1,0 +1,189 @@
+#!/usr/bin/env python3
+"""Generate the bit-sliced XOR network of a fixed GF(2^8) parity matrix (dev tool, round 4).
+
+A byte product c*x over GF(2^8)/0x11D is GF(2)-linear in the bits of x: bit i of c*x is the XOR of
+the bits j of x where bit i of c*2^j is set.  With 32 bytes of a shard held as 8 bit planes (plane j
+= bit j of every byte), a whole parity row is therefore a fixed XOR network over the 8 * k input
+planes: no table lookups, no selectors.  This script writes that network for the EC16P20L2 parity
+(the 20 KRS global rows over 16 data rows, then the two AZ-local rows expressed over the data) as
+straight-line C++, one block per output row; common subexpressions are shared inside a row only
+(Paar's greedy pairing), which bounds the live temporaries to what one row needs.
+
+The matrix is built here with a plain restatement of KRS buildMatrix (vandermonde(k + m, k) times
+the inverse of its top k rows, reedsolomon.go:220-244) and of the CubeFS local rows
+(lrcencoder.go: the (18, 1) local code over an AZ's 8 data and 10 global parities).  Only the probe
+tools/bs_probe.hip uses the network (the library does not: measured no faster than the dyadic
+v_perm kernel, profiles/r04/bs_probe.txt).
+
+  python3 tools/gen_bs_net.py > tools/bs_net_ec16p20l2.hpp
+"""
+import sys
+
+import numpy as np
+
+EXP = [0] * 512
+LOG = [0] * 256
+_v = 1
+for _i in range(255):
+    EXP[_i] = _v
+    LOG[_v] = _i
+    _v <<= 1
+    if _v & 0x100:
+        _v ^= 0x11D
+for _i in range(255, 512):
+    EXP[_i] = EXP[_i - 255]
+
+
+def gmul(a, b):
+    return 0 if a == 0 or b == 0 else EXP[LOG[a] + LOG[b]]
+
+
+def gpow(a, n):
+    if n == 0:
+        return 1
+    return 0 if a == 0 else EXP[(LOG[a] * n) % 255]
+
+
+def inverse(M):
+    n = len(M)
+    A = [row[:] + [int(i == j) for j in range(n)] for i, row in enumerate(M)]
+    for c in range(n):
+        p = next(r for r in range(c, n) if A[r][c])
+        A[c], A[p] = A[p], A[c]
+        iv = EXP[255 - LOG[A[c][c]]]
+        A[c] = [gmul(iv, x) for x in A[c]]
+        for r in range(n):
+            if r != c and A[r][c]:
+                f = A[r][c]
+                A[r] = [x ^ gmul(f, y) for x, y in zip(A[r], A[c])]
+    return [row[n:] for row in A]
+
+
+def parity_rows(k, m):
+    V = [[gpow(r, c) for c in range(k)] for r in range(k + m)]
+    T = inverse(V[:k])
+    out = []
+    for r in range(k, k + m):
+        row = []
+        for c in range(k):
+            acc = 0
+            for t in range(k):
+                acc ^= gmul(V[r][t], T[t][c])
+            row.append(acc)
+        out.append(row)
+    return out
+
+
+def ec16p20l2_rows():
+    g = parity_rows(16, 20)
+    lc = parity_rows(18, 1)[0]
+    rows = [r[:] for r in g]
+    for a in range(2):  # AZ a: data 8a..8a+7, global parities 10a..10a+9, one local parity
+        row = [0] * 16
+        for t in range(8):
+            row[8 * a + t] ^= lc[t]
+        for t in range(10):
+            for c in range(16):
+                row[c] ^= gmul(lc[8 + t], g[10 * a + t][c])
+        rows.append(row)
+    return rows
+
+
+def bitmat(c):
+    """8x8 GF(2) matrix of x -> c*x: column j = bits of c * 2^j."""
+    M = np.zeros((8, 8), np.int32)
+    p = c
+    for j in range(8):
+        for i in range(8):
+            M[i, j] = (p >> i) & 1
+        p = gmul(p, 2)
+    return M
+
+
+def row_network(row):
+    """Paar's greedy CSE over one output row: 8 planes x 8k input planes."""
+    k = len(row)
+    B = np.concatenate([bitmat(c) for c in row], axis=1)  # 8 x 8k
+    n_in = B.shape[1]
+    temps = []
+    while True:
+        C = B.T @ B
+        np.fill_diagonal(C, 0)
+        i, j = np.unravel_index(np.argmax(C), C.shape)
+        if C[i, j] < 2:
+            break
+        col = B[:, i] & B[:, j]
+        B[:, i] -= col
+        B[:, j] -= col
+        B = np.concatenate([B, col[:, None]], axis=1)
+        temps.append((int(i), int(j)))
+    outs = [[int(s) for s in np.nonzero(B[o])[0]] for o in range(8)]
+    return n_in, temps, outs
+
+
+def emit_row(r, row, lines):
+    n_in, temps, outs = row_network(row)
+    name = lambda s: f"x[{s}]" if s < n_in else f"t{s - n_in}"
+    done = set()
+    body = []
+
+    def need(s):
+        if s < n_in or s in done:
+            return
+        a, b = temps[s - n_in]
+        need(a)
+        need(b)
+        done.add(s)
+        body.append(f"    const uint32_t {name(s)} = {name(a)} ^ {name(b)};")
+
+    ops = 0
+    for o, sig in enumerate(outs):
+        for s in sig:
+            need(s)
+        terms = [name(s) for s in sig]
+        if not terms:
+            expr = "0u"
+        else:
+            expr = terms[0]
+            rest = terms[1:]
+            while len(rest) >= 2:
+                expr = f"x3({expr}, {rest[0]}, {rest[1]})"
+                rest = rest[2:]
+                ops += 1
+            if rest:
+                expr = f"({expr} ^ {rest[0]})"
+                ops += 1
+        body.append(f"    o[{o}] = {expr};")
+    ops += len(temps)
+    lines.append(f"  {{  // row {r}: {len(temps)} shared pairs, {ops} VALU ops per 32-byte column")
+    lines += body
+    lines.append(f"    emit({r}, o);")
+    lines.append("    __builtin_amdgcn_sched_barrier(0);")
+    lines.append("  }")
+    return ops
+
+
+def main():
+    rows = ec16p20l2_rows()
+    lines = []
+    total = 0
+    for r, row in enumerate(rows):
+        total += emit_row(r, row, lines)
+    out = sys.stdout
+    out.write("// bs_net_ec16p20l2.hpp -- GENERATED by tools/gen_bs_net.py; do not edit.\n")
+    out.write("//\n// The EC16P20L2 parity (20 KRS global rows, then the 2 AZ-local rows over the data) as a\n")
+    out.write(f"// bit-sliced XOR network: {total} VALU ops per 32-byte column for all 22 rows.\n")
+    out.write("// x[8c + j]: bit plane j of data row c; emit(r, o) receives output row r's 8 planes.\n")
+    out.write("#pragma once\n#include <cstdint>\n\nnamespace cfsec {\nnamespace dev {\n\n")
+    out.write("constexpr uint8_t kBsEc16p20l2Rows[22][16] = {\n")
+    for row in rows:
+        out.write("    {" + ", ".join(f"0x{v:02x}" for v in row) + "},\n")
+    out.write("};\n\n")
+    out.write("template <class Emit>\n__device__ __forceinline__ void bs_net_ec16p20l2(const uint32_t (&x)[128], Emit&& emit) {\n")
+    out.write("  const auto x3 = [](uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); };\n")
+    out.write("  uint32_t o[8];\n")
+    out.write("\n".join(lines) + "\n}\n\n}  // namespace dev\n}  // namespace cfsec\n")
+
+
+if __name__ == "__main__":
+    main()
