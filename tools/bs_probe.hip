@@ -77,6 +77,129 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
   });
 }
 
+// Persistent form: one wave per SIMD (216 VGPRs), every wave prefetching its next tile's 16 input
+// rows straight into its own 32 KiB of LDS (global_load_lds_dwordx4, no VGPRs) while the network
+// runs on the current tile; the lane's 32 bytes of a row are bytes [16 lane, +16) and
+// [1024 + 16 lane, +16) of the wave's 2 KiB (each load instruction a contiguous 1 KiB).
+constexpr int kWaveTileBytes = 2048;
+__device__ __forceinline__ void glds16(const uint8_t* g, uint8_t* l) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+}
+constexpr unsigned waitcnt_vm(unsigned n) { return (n & 0xFu) | (0x7u << 4) | (0xFu << 8) | ((n >> 4) << 14); }
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void bs_encode_glds(uint8_t* base, uint32_t ntiles) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[4][K * kWaveTileBytes];
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint8_t* my = lds[wave];
+  const uint32_t tiles_per_stripe = (uint32_t)(S / kWaveTileBytes);
+  const uint32_t gw = blockIdx.x * 4 + wave, nw = gridDim.x * 4;
+  const auto prefetch = [&](uint32_t t) {
+    const uint32_t stripe = t / tiles_per_stripe;
+    const size_t off = (size_t)(t % tiles_per_stripe) * kWaveTileBytes + lane * 16;
+    const uint8_t* row0 = base + (size_t)stripe * ROWS * S;
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+      glds16(row0 + c * S + off, my + c * kWaveTileBytes);
+      glds16(row0 + c * S + off + 1024, my + c * kWaveTileBytes + 1024);
+    }
+  };
+  uint32_t t = gw;
+  if (t < ntiles) prefetch(t);
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));  // the first tile: nothing else in flight
+  for (; t < ntiles; t += nw) {
+    // this tile's 32 loads, issued before the previous tile's 44 stores (vmcnt retires in order):
+    // those stores may still fly
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm(44));
+    uint32_t x[128];
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+      const u32x4 a = *reinterpret_cast<const u32x4*>(my + c * kWaveTileBytes + lane * 16);
+      const u32x4 b = *reinterpret_cast<const u32x4*>(my + c * kWaveTileBytes + 1024 + lane * 16);
+      x[8 * c + 0] = a.x; x[8 * c + 1] = a.y; x[8 * c + 2] = a.z; x[8 * c + 3] = a.w;
+      x[8 * c + 4] = b.x; x[8 * c + 5] = b.y; x[8 * c + 6] = b.z; x[8 * c + 7] = b.w;
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the tile is in registers before the buffer is refilled
+    if (t + nw < ntiles) prefetch(t + nw);
+    const uint32_t stripe = t / tiles_per_stripe;
+    const size_t off = (size_t)(t % tiles_per_stripe) * kWaveTileBytes + lane * 16;
+    uint8_t* row0 = base + (size_t)stripe * ROWS * S;
+#pragma unroll
+    for (int c = 0; c < K; ++c) transpose8(&x[8 * c]);
+    cfsec::dev::bs_net_ec16p20l2(x, [&](int r, uint32_t (&o)[8]) {
+      transpose8(o);
+      uint8_t* p = row0 + (size_t)(K + r) * S + off;
+      st16nt(p, u32x4{o[0], o[1], o[2], o[3]});
+      st16nt(p + 1024, u32x4{o[4], o[5], o[6], o[7]});
+    });
+  }
+}
+
+// Two waves per SIMD: 8 waves per workgroup, 16 KiB of LDS each -- data rows 0-7 of the next tile
+// are prefetched into LDS (global_load_lds) while the network runs, rows 8-15 are loaded into
+// registers at the top of the tile (the other wave on the SIMD computes meanwhile).
+constexpr int kHalfRows = 8;
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void bs_encode_glds2(uint8_t* base, uint32_t ntiles) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[8][kHalfRows * kWaveTileBytes];
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint8_t* my = lds[wave];
+  const uint32_t tiles_per_stripe = (uint32_t)(S / kWaveTileBytes);
+  const uint32_t gw = blockIdx.x * 8 + wave, nw = gridDim.x * 8;
+  const auto where = [&](uint32_t t, const uint8_t*& row0, size_t& off) {
+    row0 = base + (size_t)(t / tiles_per_stripe) * ROWS * S;
+    off = (size_t)(t % tiles_per_stripe) * kWaveTileBytes + lane * 16;
+  };
+  const auto prefetch = [&](uint32_t t) {
+    const uint8_t* row0;
+    size_t off;
+    where(t, row0, off);
+#pragma unroll
+    for (int c = 0; c < kHalfRows; ++c) {
+      glds16(row0 + c * S + off, my + c * kWaveTileBytes);
+      glds16(row0 + c * S + off + 1024, my + c * kWaveTileBytes + 1024);
+    }
+  };
+  uint32_t t = gw;
+  if (t < ntiles) prefetch(t);
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+  for (; t < ntiles; t += nw) {
+    const uint8_t* row0c;
+    size_t off;
+    where(t, row0c, off);
+    uint8_t* row0 = const_cast<uint8_t*>(row0c);
+    uint32_t x[128];
+#pragma unroll
+    for (int c = kHalfRows; c < K; ++c) {
+      const u32x4 a = ld16nt(row0 + c * S + off), b = ld16nt(row0 + c * S + off + 1024);
+      x[8 * c + 0] = a.x; x[8 * c + 1] = a.y; x[8 * c + 2] = a.z; x[8 * c + 3] = a.w;
+      x[8 * c + 4] = b.x; x[8 * c + 5] = b.y; x[8 * c + 6] = b.z; x[8 * c + 7] = b.w;
+    }
+    // the prefetched rows: issued before the previous tile's 44 stores and these 16 loads
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm(60));
+#pragma unroll
+    for (int c = 0; c < kHalfRows; ++c) {
+      const u32x4 a = *reinterpret_cast<const u32x4*>(my + c * kWaveTileBytes + lane * 16);
+      const u32x4 b = *reinterpret_cast<const u32x4*>(my + c * kWaveTileBytes + 1024 + lane * 16);
+      x[8 * c + 0] = a.x; x[8 * c + 1] = a.y; x[8 * c + 2] = a.z; x[8 * c + 3] = a.w;
+      x[8 * c + 4] = b.x; x[8 * c + 5] = b.y; x[8 * c + 6] = b.z; x[8 * c + 7] = b.w;
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+#pragma unroll
+    for (int c = 0; c < kHalfRows; ++c) transpose8(&x[8 * c]);
+#pragma unroll
+    for (int c = kHalfRows; c < K; ++c) transpose8(&x[8 * c]);
+    __builtin_amdgcn_sched_barrier(0);
+    prefetch(t + nw < ntiles ? t + nw : t);  // branch-free (the last tile re-reads itself): no code sinks past it
+    __builtin_amdgcn_sched_barrier(0);
+    cfsec::dev::bs_net_ec16p20l2(x, [&](int r, uint32_t (&o)[8]) {
+      transpose8(o);
+      uint8_t* p = row0 + (size_t)(K + r) * S + off;
+      st16nt(p, u32x4{o[0], o[1], o[2], o[3]});
+      st16nt(p + 1024, u32x4{o[4], o[5], o[6], o[7]});
+    });
+  }
+}
+
 __global__ void fill(uint32_t* p, size_t n, uint32_t seed) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     uint32_t v = (uint32_t)i * 2654435761u ^ seed;
@@ -112,22 +235,50 @@ static double run(std::vector<uint8_t*>& bufs, int reps) {
   return ms * 1e3 / reps;
 }
 
-int main() {
-  std::vector<uint8_t*> bufs(NT);
-  const size_t bytes = (size_t)NB * ROWS * S;
-  for (int t = 0; t < NT; ++t) {
-    CK(hipMalloc(&bufs[t], bytes));
-    fill<<<4096, 256>>>((uint32_t*)bufs[t], bytes / 4, 0x9E3779B9u * (t + 1));
-  }
+static double run_glds(std::vector<uint8_t*>& bufs, int reps, int& grid_out) {
+  int dev = 0, ncu = 0;
+  CK(hipGetDevice(&dev));
+  CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  const uint32_t ntiles = (uint32_t)(NB * (S / kWaveTileBytes));
+  grid_out = ncu;
+  for (int i = 0; i < 6; ++i) hipLaunchKernelGGL(bs_encode_glds, dim3(ncu), dim3(256), 0, 0, bufs[i % NT], ntiles);
   CK(hipDeviceSynchronize());
-  // correctness: batch 0, stripes 0 and NB-1, every parity byte
-  const dim3 grid((unsigned)(S / (256 * 32)), NB);
-  hipLaunchKernelGGL((bs_encode<2>), grid, dim3(256), 0, 0, bufs[0]);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  CK(hipEventRecord(e0, 0));
+  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(bs_encode_glds, dim3(ncu), dim3(256), 0, 0, bufs[i % NT], ntiles);
+  CK(hipEventRecord(e1, 0));
+  CK(hipEventSynchronize(e1));
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  return ms * 1e3 / reps;
+}
+
+static double run_glds2(std::vector<uint8_t*>& bufs, int reps) {
+  int dev = 0, ncu = 0;
+  CK(hipGetDevice(&dev));
+  CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  const uint32_t ntiles = (uint32_t)(NB * (S / kWaveTileBytes));
+  for (int i = 0; i < 6; ++i) hipLaunchKernelGGL(bs_encode_glds2, dim3(ncu), dim3(512), 0, 0, bufs[i % NT], ntiles);
   CK(hipDeviceSynchronize());
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  CK(hipEventRecord(e0, 0));
+  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(bs_encode_glds2, dim3(ncu), dim3(512), 0, 0, bufs[i % NT], ntiles);
+  CK(hipEventRecord(e1, 0));
+  CK(hipEventSynchronize(e1));
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  return ms * 1e3 / reps;
+}
+
+static long check(uint8_t* buf) {
   std::vector<uint8_t> h((size_t)ROWS * S);
   long bad = 0;
-  for (int st : {0, NB - 1}) {
-    CK(hipMemcpy(h.data(), bufs[0] + (size_t)st * ROWS * S, h.size(), hipMemcpyDeviceToHost));
+  for (int st : {0, NB / 2, NB - 1}) {
+    CK(hipMemcpy(h.data(), buf + (size_t)st * ROWS * S, h.size(), hipMemcpyDeviceToHost));
     for (int r = 0; r < M; ++r)
       for (size_t i = 0; i < S; ++i) {
         uint8_t v = 0;
@@ -136,6 +287,29 @@ int main() {
           printf("mismatch stripe %d row %d byte %zu: %02x vs %02x\n", st, r, i, h[(size_t)(K + r) * S + i], v);
       }
   }
+  return bad;
+}
+
+int main() {
+  std::vector<uint8_t*> bufs(NT);
+  const size_t bytes = (size_t)NB * ROWS * S;
+  for (int t = 0; t < NT; ++t) {
+    CK(hipMalloc(&bufs[t], bytes));
+    fill<<<4096, 256>>>((uint32_t*)bufs[t], bytes / 4, 0x9E3779B9u * (t + 1));
+  }
+  CK(hipDeviceSynchronize());
+  // correctness: every parity byte of stripes 0, NB/2 and NB-1, both kernels
+  const dim3 grid((unsigned)(S / (256 * 32)), NB);
+  hipLaunchKernelGGL((bs_encode<2>), grid, dim3(256), 0, 0, bufs[0]);
+  CK(hipDeviceSynchronize());
+  long bad = check(bufs[0]);
+  CK(hipMemset(bufs[1], 0, 0));
+  int g = 0;
+  run_glds(bufs, 1, g);
+  for (int t = 0; t < NT; ++t) bad += check(bufs[t]);
+  for (int t = 0; t < NT; ++t) CK(hipMemset(bufs[t] + (size_t)K * S, 0, (size_t)M * S));  // stripe 0's parity
+  run_glds2(bufs, 1);
+  for (int t = 0; t < NT; ++t) bad += check(bufs[t]);
   printf("parity check: %s (%ld bad bytes)\n", bad ? "FAIL" : "ok", bad);
   if (bad) return 1;
   const double algo = (double)NB * ROWS * S;
@@ -144,6 +318,10 @@ int main() {
     printf("bs_encode 16->22 waves/EU 2: %8.1f us  %6.1f GB/s  %5.1f %% of 8 TB/s\n", us, algo / us / 1e3, algo / us / 8e4);
     us = run<1>(bufs, 30);
     printf("bs_encode 16->22 waves/EU 1: %8.1f us  %6.1f GB/s  %5.1f %% of 8 TB/s\n", us, algo / us / 1e3, algo / us / 8e4);
+    us = run_glds(bufs, 30, g);
+    printf("bs_encode_glds (%d x 256, LDS prefetch): %8.1f us  %6.1f GB/s  %5.1f %% of 8 TB/s\n", g, us, algo / us / 1e3, algo / us / 8e4);
+    us = run_glds2(bufs, 30);
+    printf("bs_encode_glds2 (8 waves, half LDS prefetch): %8.1f us  %6.1f GB/s  %5.1f %% of 8 TB/s\n", us, algo / us / 1e3, algo / us / 8e4);
   }
   return 0;
 }

@@ -144,23 +144,32 @@ def emit_row(r, row, lines):
         if not terms:
             expr = "0u"
         else:
+            # a balanced tree of 3-input XORs (depth log3 of the terms, not a serial chain)
+            while len(terms) > 1:
+                nxt = []
+                for i in range(0, len(terms), 3):
+                    g = terms[i:i + 3]
+                    if len(g) == 3:
+                        nxt.append(f"x3({g[0]}, {g[1]}, {g[2]})")
+                    elif len(g) == 2:
+                        nxt.append(f"({g[0]} ^ {g[1]})")
+                    else:
+                        nxt.append(g[0])
+                    ops += len(g) > 1
+                terms = nxt
             expr = terms[0]
-            rest = terms[1:]
-            while len(rest) >= 2:
-                expr = f"x3({expr}, {rest[0]}, {rest[1]})"
-                rest = rest[2:]
-                ops += 1
-            if rest:
-                expr = f"({expr} ^ {rest[0]})"
-                ops += 1
         body.append(f"    o[{o}] = {expr};")
     ops += len(temps)
     lines.append(f"  {{  // row {r}: {len(temps)} shared pairs, {ops} VALU ops per 32-byte column")
     lines += body
     lines.append(f"    emit({r}, o);")
-    lines.append("    __builtin_amdgcn_sched_barrier(0);")
+    if BARRIER:
+        lines.append("    __builtin_amdgcn_sched_barrier(0);")
     lines.append("  }")
     return ops
+
+
+BARRIER = "--no-barrier" not in sys.argv
 
 
 def main():
