@@ -122,6 +122,7 @@ def row_network(row):
 
 
 def emit_row(r, row, lines):
+    """Row r's network as a specialization bs_row_ec16p20l2<r>(x, o)."""
     n_in, temps, outs = row_network(row)
     name = lambda s: f"x[{s}]" if s < n_in else f"t{s - n_in}"
     done = set()
@@ -134,7 +135,7 @@ def emit_row(r, row, lines):
         need(a)
         need(b)
         done.add(s)
-        body.append(f"    const uint32_t {name(s)} = {name(a)} ^ {name(b)};")
+        body.append(f"  const uint32_t {name(s)} = {name(a)} ^ {name(b)};")
 
     ops = 0
     for o, sig in enumerate(outs):
@@ -150,7 +151,7 @@ def emit_row(r, row, lines):
                 for i in range(0, len(terms), 3):
                     g = terms[i:i + 3]
                     if len(g) == 3:
-                        nxt.append(f"x3({g[0]}, {g[1]}, {g[2]})")
+                        nxt.append(f"bs_x3({g[0]}, {g[1]}, {g[2]})")
                     elif len(g) == 2:
                         nxt.append(f"({g[0]} ^ {g[1]})")
                     else:
@@ -158,14 +159,13 @@ def emit_row(r, row, lines):
                     ops += len(g) > 1
                 terms = nxt
             expr = terms[0]
-        body.append(f"    o[{o}] = {expr};")
+        body.append(f"  o[{o}] = {expr};")
     ops += len(temps)
-    lines.append(f"  {{  // row {r}: {len(temps)} shared pairs, {ops} VALU ops per 32-byte column")
+    lines.append(f"// row {r}: {len(temps)} shared pairs, {ops} VALU ops per 32-byte column")
+    lines.append("template <>")
+    lines.append(f"__device__ __forceinline__ void bs_row_ec16p20l2<{r}>(const uint32_t (&x)[128], uint32_t (&o)[8]) {{")
     lines += body
-    lines.append(f"    emit({r}, o);")
-    if BARRIER:
-        lines.append("    __builtin_amdgcn_sched_barrier(0);")
-    lines.append("  }")
+    lines.append("}")
     return ops
 
 
@@ -182,16 +182,30 @@ def main():
     out.write("// bs_net_ec16p20l2.hpp -- GENERATED by tools/gen_bs_net.py; do not edit.\n")
     out.write("//\n// The EC16P20L2 parity (20 KRS global rows, then the 2 AZ-local rows over the data) as a\n")
     out.write(f"// bit-sliced XOR network: {total} VALU ops per 32-byte column for all 22 rows.\n")
-    out.write("// x[8c + j]: bit plane j of data row c; emit(r, o) receives output row r's 8 planes.\n")
+    out.write("// x[8c + j]: bit plane j of data row c; o: the output row's 8 planes.\n")
     out.write("#pragma once\n#include <cstdint>\n\nnamespace cfsec {\nnamespace dev {\n\n")
     out.write("constexpr uint8_t kBsEc16p20l2Rows[22][16] = {\n")
     for row in rows:
         out.write("    {" + ", ".join(f"0x{v:02x}" for v in row) + "},\n")
     out.write("};\n\n")
+    out.write("__device__ __forceinline__ uint32_t bs_x3(uint32_t a, uint32_t b, uint32_t c) {\n"
+              "  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);\n}\n\n")
+    out.write("template <int R>\n__device__ __forceinline__ void bs_row_ec16p20l2(const uint32_t (&x)[128], uint32_t (&o)[8]);\n\n")
+    out.write("\n".join(lines) + "\n\n")
+    out.write("// every row in order; emit(r, o) consumes row r's planes\n")
     out.write("template <class Emit>\n__device__ __forceinline__ void bs_net_ec16p20l2(const uint32_t (&x)[128], Emit&& emit) {\n")
-    out.write("  const auto x3 = [](uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); };\n")
-    out.write("  uint32_t o[8];\n")
-    out.write("\n".join(lines) + "\n}\n\n}  // namespace dev\n}  // namespace cfsec\n")
+    for r in range(len(rows)):
+        out.write(f"  {{\n    uint32_t o[8];\n    bs_row_ec16p20l2<{r}>(x, o);\n    emit({r}, o);\n")
+        if BARRIER:
+            out.write("    __builtin_amdgcn_sched_barrier(0);\n")
+        out.write("  }\n")
+    out.write("}\n\n")
+    out.write("// row r chosen at run time (uniform)\n")
+    out.write("__device__ __forceinline__ void bs_row_ec16p20l2_rt(int r, const uint32_t (&x)[128], uint32_t (&o)[8]) {\n  switch (r) {\n")
+    for r in range(len(rows)):
+        out.write(f"    case {r}: bs_row_ec16p20l2<{r}>(x, o); break;\n")
+    out.write("    default: for (int j = 0; j < 8; ++j) o[j] = 0u;\n  }\n}\n\n")
+    out.write("}  // namespace dev\n}  // namespace cfsec\n")
 
 
 if __name__ == "__main__":
