@@ -123,6 +123,19 @@ int64_t affine_stride(const MatVecJob& job, int c0, int kc, int r0, int mc) {
 
 }  // namespace
 
+// The bit-sliced EC16P20(L2) encode (gf_bs16.hip) for this launch: the network's matrix and
+// 16-byte aligned rows (global_load_lds and the 16-byte accesses); CFSEC_BS16=0 disables it (A/B).
+static const bool kBs16 = [] {
+  const char* v = std::getenv("CFSEC_BS16");
+  return !(v && v[0] == '0');
+}();
+static bool bs16_ok(const dev::GfArgs& a, int k, int m, int tab) {
+  if (!bs16_matches(a.coef, m, k) || (a.sstride & 15)) return false;
+  for (int i = 0; i < tab * (k + m); ++i)
+    if (reinterpret_cast<uintptr_t>(a.ptr[i]) & 15) return false;
+  return true;
+}
+
 hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
   using dev::kMaxK;
   using dev::kMaxM;
@@ -231,8 +244,27 @@ hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
           continue;
         }
         if (fixed && dy16) {
-          e = launch_dy16(mc, mode, a, (unsigned)ns, stream);
-          if (e != hipSuccess) return e;
+          // encodes whose rows are 16-byte aligned: the whole 2 KiB column runs through the
+          // bit-sliced network (gf_bs16.hip), the rest of each row through the dyadic kernel
+          const uint64_t full = mode == MatVecMode::kStore && !job.lens && kBs16 && bs16_ok(a, kc, mc, tab)
+                                    ? llen / kBs16Tile * kBs16Tile
+                                    : 0;
+          if (full) {
+            e = launch_bs16(mc, a, (unsigned)ns, full, stream);
+            if (e != hipSuccess) return e;
+          }
+          if (full < llen) {
+            const dev::GfArgs* ta = &a;
+            static thread_local dev::GfArgs tail;
+            if (full) {
+              std::memcpy(&tail, &a, sizeof(dev::GfArgs));
+              for (int i = 0; i < tab * (kc + mc); ++i) tail.ptr[i] = a.ptr[i] + full;
+              tail.len = llen - full;
+              ta = &tail;
+            }
+            e = launch_dy16(mc, mode, *ta, (unsigned)ns, stream);
+            if (e != hipSuccess) return e;
+          }
           continue;
         }
         if (fixed && dy.B) {

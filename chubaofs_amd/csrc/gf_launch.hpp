@@ -96,6 +96,13 @@ inline DyPlan dyadic_plan(const uint8_t* coef, int m, int k) {
 // encode's local parity).
 hipError_t launch_dy16(int m, MatVecMode mode, const dev::GfArgs& a, unsigned ns, hipStream_t st);
 
+// The bit-sliced EC16P20 / EC16P20L2 parity kernel (gf_bs16.hip): coef (m x 16, row stride 16) must
+// equal the network's constants (bs16_matches); launch_bs16 covers columns [0, len) of every stripe,
+// len a multiple of kBs16Tile, every row pointer (and sstride) 16-byte aligned.
+constexpr uint64_t kBs16Tile = 2048;
+bool bs16_matches(const uint8_t* coef, int m, int k);
+hipError_t launch_bs16(int m, const dev::GfArgs& a, unsigned ns, uint64_t len, hipStream_t st);
+
 // repair_dy16 on a GfArgs block (gf_dy16.hip); launch_dy16_repair (gf_kernels.hip) fills it.
 hipError_t launch_dy16_repair_args(int nd, int ne, const dev::GfArgs& a, unsigned ns, hipStream_t st);
 

@@ -232,3 +232,30 @@ def test_local_pass_failure_runs_every_az(mode, memory):
     for b, (wk, w) in enumerate(zip(work, want)):
         if exp[b] in (0, _lib.ErrVerify.status):
             assert_same(wk, w, (cm.Name(mode), "batch", b))
+
+
+@pytest.mark.parametrize("S", [2048, 2048 * 3 + 16, 262144 + 2048 + 48])
+def test_ec16p20l2_encode_bitsliced_column_runs(S):
+    """EC16P20L2's fused encode of 16-byte-aligned rows takes the bit-sliced network for the whole
+    2 KiB column runs and the dyadic kernel for the rest of each row (gf_bs16.hip; S = 2048: no
+    rest, S = 6160: 16 bytes of rest): every shard against the ec oracle, as single calls on
+    separate shard tensors and as a batch over one [bids, 38, S] buffer with stale parity."""
+    t = cm.GetTactic(cm.EC16P20L2)
+    n = t.N + t.M + t.L
+    good = [codeword(t, S, 70 + b) for b in range(3)]
+    for b in range(2):
+        arrs = [g.copy() for g in good[b]]
+        for a in arrs[t.N:]:
+            a[:] = 0xA5
+        run_case(cm.EC16P20L2, "encode", arrs, [], "device", verify_on=False)
+    buf = torch.empty((3, n, S), dtype=torch.uint8, device="cuda")
+    for b in range(3):
+        for i in range(n):
+            buf[b, i] = torch.from_numpy(good[b][i] if i < t.N else np.full(S, 0x5A, np.uint8))
+    assert buf.data_ptr() % 16 == 0 and (S % 16 == 0)
+    st = new(cm.EC16P20L2, False).EncodeBatch([[buf[b, i] for i in range(n)] for b in range(3)])
+    assert st == [0, 0, 0]
+    got = buf.cpu().numpy()
+    for b in range(3):
+        for i in range(n):
+            assert np.array_equal(got[b, i], good[b][i]), (S, b, i)

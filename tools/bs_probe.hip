@@ -1,13 +1,14 @@
 // bs_probe.hip -- bit-sliced EC16P20L2 parity (dev probe, round 4).
 //
 // The 22 parity rows of EC16P20L2 (20 global + 2 AZ-local, over the 16 data rows) from the
-// generated XOR network (tools/bs_net_ec16p20l2.hpp): each lane holds 32 bytes of
+// generated XOR network (chubaofs_amd/csrc/bs_net_ec16p20l2.hpp): each lane holds 32 bytes of
 // every data row as 8 bit planes (an 8x8 bit transpose per byte lane: 3 swap stages), runs the
 // network row by row and transposes each output row back.  Same tasklet shape as the library's
 // EC16P20L2 fused encode in tools/gf_shapes (64 stripes x S = 262,144), three batches in rotation;
 // stripe 0 and stripe 63 checked against a scalar GF product on the host.
 //
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 bs_probe.hip -o bs_probe
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../chubaofs_amd/csrc bs_probe.hip \
+//         -L../chubaofs_amd -lcfsec -Wl,-rpath,'$ORIGIN/../chubaofs_amd' -o bs_probe
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -16,6 +17,7 @@
 #include <vector>
 
 #include "bs_net_ec16p20l2.hpp"
+#include "kernels.hpp"
 
 #define CK(x)                                                                          \
   do {                                                                                 \
@@ -313,6 +315,47 @@ int main() {
   printf("parity check: %s (%ld bad bytes)\n", bad ? "FAIL" : "ok", bad);
   if (bad) return 1;
   const double algo = (double)NB * ROWS * S;
+  // the shipped launcher on the same tasklets (CFSEC_BS16 chooses its route)
+  std::vector<std::vector<const uint8_t*>> lin(NT);
+  std::vector<std::vector<uint8_t*>> lout(NT);
+  std::vector<cfsec::MatVecJob> jobs(NT);
+  for (int t = 0; t < NT; ++t) {
+    for (int b = 0; b < NB; ++b) {
+      for (int c = 0; c < K; ++c) lin[t].push_back(bufs[t] + ((size_t)b * ROWS + c) * S);
+      for (int r = 0; r < M; ++r) lout[t].push_back(bufs[t] + ((size_t)b * ROWS + K + r) * S);
+    }
+    cfsec::MatVecJob& j = jobs[t];
+    j.k = K;
+    j.m = M;
+    j.coef = &cfsec::dev::kBsEc16p20l2Rows[0][0];
+    j.len = S;
+    j.nstripes = NB;
+    j.in = lin[t].data();
+    j.out = lout[t].data();
+  }
+  const auto run_lib = [&](int reps) {
+    for (int i = 0; i < 6; ++i) CK(cfsec::launch_matvec(jobs[i % NT], 0));
+    CK(hipDeviceSynchronize());
+    hipEvent_t a0, a1;
+    CK(hipEventCreate(&a0));
+    CK(hipEventCreate(&a1));
+    CK(hipEventRecord(a0, 0));
+    for (int i = 0; i < reps; ++i) CK(cfsec::launch_matvec(jobs[i % NT], 0));
+    CK(hipEventRecord(a1, 0));
+    CK(hipEventSynchronize(a1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, a0, a1));
+    return ms * 1e3 / reps;
+  };
+  {
+    for (int t = 0; t < NT; ++t) CK(hipMemset(bufs[t] + (size_t)K * S, 0, (size_t)M * S));
+    run_lib(1);
+    CK(hipDeviceSynchronize());
+    long lb = 0;
+    for (int t = 0; t < NT; ++t) lb += check(bufs[t]);
+    printf("library launcher parity: %s (CFSEC_BS16=%s)\n", lb ? "FAIL" : "ok", getenv("CFSEC_BS16") ? getenv("CFSEC_BS16") : "default");
+    if (lb) return 1;
+  }
   for (int rep = 0; rep < 2; ++rep) {
     double us = run<2>(bufs, 30);
     printf("bs_encode 16->22 waves/EU 2: %8.1f us  %6.1f GB/s  %5.1f %% of 8 TB/s\n", us, algo / us / 1e3, algo / us / 8e4);
@@ -322,6 +365,9 @@ int main() {
     printf("bs_encode_glds (%d x 256, LDS prefetch): %8.1f us  %6.1f GB/s  %5.1f %% of 8 TB/s\n", g, us, algo / us / 1e3, algo / us / 8e4);
     us = run_glds2(bufs, 30);
     printf("bs_encode_glds2 (8 waves, half LDS prefetch): %8.1f us  %6.1f GB/s  %5.1f %% of 8 TB/s\n", us, algo / us / 1e3, algo / us / 8e4);
+    us = run_lib(30);
+    printf("library launch_matvec (22 x 16, CFSEC_BS16=%s): %8.1f us  %6.1f GB/s  %5.1f %% of 8 TB/s\n",
+           getenv("CFSEC_BS16") ? getenv("CFSEC_BS16") : "1", us, algo / us / 1e3, algo / us / 8e4);
   }
   return 0;
 }

@@ -1,7 +1,7 @@
 // bs_repair_probe.hip -- C5's repair pass in bit-sliced form (dev probe, round 4).
 //
 // The EC16P20L2 tasklet of BASELINE config 5 (64 bids x S = 262,144, rows {0,1,16,17} lost):
-// per bid, the reference's Reconstruct then Verify.  Bit-sliced form (tools/bs_net_ec16p20l2.hpp):
+// per bid, the reference's Reconstruct then Verify.  Bit-sliced form (chubaofs_amd/csrc/bs_net_ec16p20l2.hpp):
 //   1. the 16 input slots (present data rows in their slots, the first nd present parities standing
 //      in for the missing data rows) as bit planes; the stand-ins' planes set aside, their slots zeroed;
 //   2. syndromes: s_k = stored(p_k) ^ row p_k of the network over the present data;
@@ -15,7 +15,7 @@
 // row comes through a 3-deep LDS ring filled 2 compared rows ahead.  Every wait on those copies is a
 // conservative s_waitcnt (vector memory operations retire in issue order).
 //
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 bs_repair_probe.hip -o bs_repair_probe
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../chubaofs_amd/csrc bs_repair_probe.hip -o bs_repair_probe
 #include <hip/hip_runtime.h>
 
 #include <cstdio>

@@ -11,11 +11,11 @@ straight-line C++, one block per output row; common subexpressions are shared in
 
 The matrix is built here with a plain restatement of KRS buildMatrix (vandermonde(k + m, k) times
 the inverse of its top k rows, reedsolomon.go:220-244) and of the CubeFS local rows
-(lrcencoder.go: the (18, 1) local code over an AZ's 8 data and 10 global parities).  Only the probe
-tools/bs_probe.hip uses the network (the library does not: measured no faster than the dyadic
-v_perm kernel, profiles/r04/bs_probe.txt).
+(lrcencoder.go: the (18, 1) local code over an AZ's 8 data and 10 global parities); the library
+checks its engine's coefficients against these constants before it takes the network
+(gf_bs16.hip), and the probes tools/bs_probe.hip / bs_repair_probe.hip use it too.
 
-  python3 tools/gen_bs_net.py > tools/bs_net_ec16p20l2.hpp
+  python3 tools/gen_bs_net.py > chubaofs_amd/csrc/bs_net_ec16p20l2.hpp
 """
 import sys
 
@@ -192,10 +192,11 @@ def main():
               "  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);\n}\n\n")
     out.write("template <int R>\n__device__ __forceinline__ void bs_row_ec16p20l2(const uint32_t (&x)[128], uint32_t (&o)[8]);\n\n")
     out.write("\n".join(lines) + "\n\n")
-    out.write("// every row in order; emit(r, o) consumes row r's planes\n")
-    out.write("template <class Emit>\n__device__ __forceinline__ void bs_net_ec16p20l2(const uint32_t (&x)[128], Emit&& emit) {\n")
+    out.write("// rows 0 .. NR-1 in order (NR = 20: EC16P20's global parity; 22: with the local rows); emit(r, o)\n")
+    out.write("// consumes row r's planes\n")
+    out.write("template <int NR = 22, class Emit>\n__device__ __forceinline__ void bs_net_ec16p20l2(const uint32_t (&x)[128], Emit&& emit) {\n")
     for r in range(len(rows)):
-        out.write(f"  {{\n    uint32_t o[8];\n    bs_row_ec16p20l2<{r}>(x, o);\n    emit({r}, o);\n")
+        out.write(f"  if constexpr ({r} < NR) {{\n    uint32_t o[8];\n    bs_row_ec16p20l2<{r}>(x, o);\n    emit({r}, o);\n")
         if BARRIER:
             out.write("    __builtin_amdgcn_sched_barrier(0);\n")
         out.write("  }\n")
