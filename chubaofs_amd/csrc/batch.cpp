@@ -111,6 +111,11 @@ hipError_t launch_group_run(const Group& g, size_t t0, size_t t1, uint32_t* dfla
     std::memcpy(job.src, d->src, 16);
     job.pstore = d->pstore;
     job.pcmp = d->pcmp;
+    if (d->syn) {
+      job.syn = true;
+      std::memcpy(job.prow, d->prow, 4);
+      std::memcpy(job.ainv, d->ainv, 16);
+    }
     job.nstripes = (int)(t1 - t0);
     job.in = g.in.data() + t0 * 16;
     job.e = d->e;
@@ -398,6 +403,26 @@ void RSEngine::plan_dy16(const std::vector<bool>& present, const Matrix& dec, St
   std::memcpy(d->coef.v.data(), parity_.v.data(), 20 * 16);
   for (int q = 0; q < e; ++q) std::memcpy(d->coef.row(20 + q), extra->rows.row(q), 16);
   for (int q = 0; q < d->nd; ++q) std::memcpy(d->coef.row(20 + e + q), dec.row(d->rows[q]), 16);
+  // syndrome form: the inputs past the present data rows are the stand-in parities (first-present
+  // order); A[q][j] = parity row prow[q] at missing data column rows[j], invertible exactly when the
+  // decode is (block elimination of the 16 x 16 input matrix)
+  if (plan->in.size() == 16) {
+    bool ok = true;
+    Matrix A(d->nd, d->nd), Ai;
+    for (int q = 0; q < d->nd && ok; ++q) {
+      const int p = plan->in[16 - d->nd + q] - k_;
+      ok = p >= 0 && p < 20;
+      if (ok) {
+        d->prow[q] = (uint8_t)p;
+        for (int j = 0; j < d->nd; ++j) A.at(q, j) = parity_.at(p, d->rows[j]);
+      }
+    }
+    if (ok && (d->nd == 0 || mat_invert(A, Ai))) {
+      for (int j = 0; j < d->nd; ++j)
+        for (int q = 0; q < d->nd; ++q) d->ainv[j * 4 + q] = Ai.at(j, q);
+      d->syn = true;
+    }
+  }
   plan->dy16 = std::move(d);
 }
 

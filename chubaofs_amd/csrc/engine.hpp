@@ -163,6 +163,11 @@ struct Dy16Plan {
   uint8_t src[16] = {};
   uint32_t pstore = 0, pcmp = 0;
   Matrix coef;  // (20 + e + nd) x 16: parity matrix, extra rows, decode rows
+  // the syndrome form of the bit-sliced repair (gf_bs16.hip): parity row prow[q] stands in for
+  // missing data row rows[q]; the missing rows are ainv (nd x nd) times the stand-ins' syndromes
+  bool syn = false;
+  uint8_t prow[4] = {};
+  uint8_t ainv[16] = {};
 };
 
 // Rows beyond a code's own that a Reconstruct + Verify pass can check on the way: row j over the

@@ -11,9 +11,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <mutex>
 
 #include "bs_net_ec16p20l2.hpp"
 #include "gf_bitslice.hpp"
+#include "gf256.hpp"
 #include "gf_launch.hpp"
 
 namespace cfsec {
@@ -71,6 +73,162 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
   }
 }
 
+// Reconstruct + Verify of the 16 + 20 code (C5's repair pass) in the same form, the syndrome way:
+//   1. the 16 data slots as planes, a missing data row's slot loaded from a zero buffer;
+//   2. s_q = stored(prow[q]) ^ (row prow[q] of the network over the present data): the stand-in
+//      parities' syndromes, = A d with A the nd x nd block of the parity matrix at those rows and
+//      the missing columns;
+//   3. d = A^-1 s in byte form (v_perm products, tables from the host), stored, transposed and
+//      masked into their (zero) slots -- no register indexing;
+//   4. the full network: each parity (and extra) row stored (pstore), compared with its stored copy
+//      through a 3-deep LDS ring filled by global_load_lds 2 compared rows ahead (pcmp; a mismatch
+//      sets the stripe's flag), or skipped (the stand-ins, consistent by construction).
+// Slots 0-6 of the next tile are prefetched into LDS during the network, slots 7-15 and the
+// stand-ins load at the tile's top; 20 KiB of LDS per wave, 8 waves per CU.  C5's tasklet:
+// 158.7-161.6 us against 173.0 us for the dyadic repair kernel (profiles/r04/bs_probe.txt).
+struct BsRepairArgs {
+  uint8_t slot[4];      // missing data row q (its slot), q < nd <= kBsRepairMaxNd
+  uint8_t prow[4];      // the parity row standing in for it (input 16 - nd + q)
+  dev::u32x4 t01[16];   // A^-1 product tables, entry j * 4 + q (gf_device.hpp coef_tables layout)
+  uint32_t t2[16];
+  const uint8_t* zero;  // kBsWaveBytes of zeros
+};
+
+constexpr int kRepPrefetch = 7, kRepRing = 3;
+
+__device__ __forceinline__ void bs_mul_acc8(uint32_t* acc, const uint32_t* s0, const uint32_t* s1, const uint32_t* s2,
+                                            const dev::u32x4 q, uint32_t t2) {
+#pragma unroll
+  for (int w = 0; w < 8; ++w)
+    acc[w] = dev::bs_x3(acc[w], __builtin_amdgcn_perm(q.y, q.x, s0[w]), __builtin_amdgcn_perm(q.w, q.z, s1[w])) ^
+             __builtin_amdgcn_perm(0u, t2, s2[w]);
+}
+
+template <int M, int ND>
+__global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2, 2))) void gf_bs16_repair_kernel(
+    const dev::GfArgs a, const BsRepairArgs r, uint32_t tiles_per_stripe, uint32_t ntiles) {
+  using namespace dev;
+  constexpr int MO = ND + M;  // output rows per stripe: missing data rows, 20 parity rows, extras
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kBsWaves][(kRepPrefetch + kRepRing) * kBsWaveBytes];
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  uint8_t* pre = lds[wave];
+  uint8_t* ring = lds[wave] + kRepPrefetch * kBsWaveBytes;
+  const uint32_t nw = gridDim.x * kBsWaves;
+  if (blockIdx.x == 0)  // the checksum words the pass after this one accumulates into
+    for (uint32_t i = threadIdx.x; i < a.nzw; i += blockDim.x) a.zw[i] = 0u;
+  // affine batches only (the launcher checks): row i of stripe s at ptr[i] + s * sstride
+  const auto input = [&](uint32_t s, int i, uint32_t c) -> const uint8_t* {
+    return a.ptr[i] + (int64_t)s * a.sstride + (size_t)c * kBsWaveBytes + lane * 16;
+  };
+  const auto output = [&](uint32_t s, int o, uint32_t c) -> uint8_t* {
+    return const_cast<uint8_t*>(a.ptr[kBsK + o]) + (int64_t)s * a.sstride + (size_t)c * kBsWaveBytes + lane * 16;
+  };
+  const auto slot_ptr = [&](uint32_t s, int i, uint32_t c) -> const uint8_t* {  // data row i, or zeros
+    const int src = a.src[i];
+    return src < kBsK ? input(s, src, c) : r.zero + lane * 16;
+  };
+  const auto prefetch = [&](uint32_t t) {
+    const uint32_t s = t / tiles_per_stripe, c = t % tiles_per_stripe;
+#pragma unroll
+    for (int i = 0; i < kRepPrefetch; ++i) bs_glds_row(slot_ptr(s, i, c), pre + i * kBsWaveBytes);
+  };
+  uint32_t t = blockIdx.x * kBsWaves + wave;
+  if (t >= ntiles) return;
+  prefetch(t);
+  __builtin_amdgcn_s_waitcnt(bs_waitcnt_vm(0));
+  for (; t < ntiles; t += nw) {
+    const uint32_t s = t / tiles_per_stripe, c = t % tiles_per_stripe;
+    uint32_t x[128];
+    uint32_t y[ND > 0 ? ND : 1][8];
+#pragma unroll
+    for (int i = kRepPrefetch; i < kBsK; ++i) bs_ld_row(slot_ptr(s, i, c), &x[8 * i]);
+#pragma unroll
+    for (int q = 0; q < ND; ++q) bs_ld_row(input(s, kBsK - ND + q, c), y[q]);
+    // the prefetched slots were issued before everything since (in-order retirement)
+    __builtin_amdgcn_s_waitcnt(bs_waitcnt_vm(2 * (kBsK - kRepPrefetch + ND)));
+#pragma unroll
+    for (int i = 0; i < kRepPrefetch; ++i) bs_lds_row(pre + i * kBsWaveBytes, lane, &x[8 * i]);
+    __builtin_amdgcn_s_waitcnt(kBsWaitLgkm0);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < kBsK; ++i) bs_transpose8(&x[8 * i]);
+    if constexpr (ND > 0) {
+      // 2. syndromes of the stand-ins over the present data (missing slots are zero planes)
+#pragma unroll
+      for (int q = 0; q < ND; ++q) {
+        bs_transpose8(y[q]);
+        uint32_t o[8];
+        bs_row_ec16p20l2_rt(r.prow[q], x, o);
+#pragma unroll
+        for (int w = 0; w < 8; ++w) y[q][w] ^= o[w];
+        bs_transpose8(y[q]);  // back to bytes
+      }
+      // 3. d = A^-1 s, stored, into its slot
+#pragma unroll
+      for (int j = 0; j < ND; ++j) {
+        uint32_t d[8];
+#pragma unroll
+        for (int w = 0; w < 8; ++w) d[w] = 0u;
+#pragma unroll
+        for (int q = 0; q < ND; ++q) {
+          uint32_t s0[8], s1[8], s2[8];
+#pragma unroll
+          for (int w = 0; w < 8; ++w) {
+            s0[w] = y[q][w] & 0x07070707u;
+            s1[w] = (y[q][w] >> 3) & 0x07070707u;
+            s2[w] = (y[q][w] >> 6) & 0x03030303u;
+          }
+          bs_mul_acc8(d, s0, s1, s2, r.t01[j * 4 + q], r.t2[j * 4 + q]);
+        }
+        bs_st_row(output(s, j, c), d);
+        bs_transpose8(d);
+#pragma unroll
+        for (int i = 0; i < kBsK; ++i) {
+          const uint32_t m = i == r.slot[j] ? ~0u : 0u;
+#pragma unroll
+          for (int w = 0; w < 8; ++w) x[8 * i + w] ^= d[w] & m;
+        }
+      }
+    }
+    // ring: the first two compared rows; then the next tile's slots
+    uint32_t pend = a.pcmp, q_issue = 0, q_read = 0;
+    const auto issue_ring = [&]() {
+      if (pend) {
+        const int p = __builtin_ctz(pend);
+        pend &= pend - 1;
+        bs_glds_row(output(s, ND + p, c), ring + (q_issue % kRepRing) * kBsWaveBytes);
+        ++q_issue;
+      }
+    };
+    issue_ring();
+    issue_ring();
+    __builtin_amdgcn_sched_barrier(0);
+    prefetch(t + nw < ntiles ? t + nw : t);
+    __builtin_amdgcn_sched_barrier(0);
+    uint32_t diff = 0;
+    bs_net_ec16p20l2<M>(x, [&](int p, uint32_t (&o)[8]) {
+      if (a.pstore >> p & 1) {
+        bs_transpose8(o);
+        bs_st_row(output(s, ND + p, c), o);
+      } else if (a.pcmp >> p & 1) {
+        // this row's copy; the next compared row's may still fly (anything issued between them is
+        // waited for too: retirement is in order)
+        if (q_issue - q_read > 1) __builtin_amdgcn_s_waitcnt(bs_waitcnt_vm(2));
+        else __builtin_amdgcn_s_waitcnt(bs_waitcnt_vm(0));
+        uint32_t v[8];
+        bs_lds_row(ring + (q_read % kRepRing) * kBsWaveBytes, lane, v);
+        __builtin_amdgcn_s_waitcnt(kBsWaitLgkm0);
+        ++q_read;
+        issue_ring();
+        bs_transpose8(v);
+#pragma unroll
+        for (int w = 0; w < 8; ++w) diff |= v[w] ^ o[w];
+      }
+    });
+    if (diff) set_flag(a.flags, s);
+  }
+}
+
 int cu_count() {
   static int n[64] = {};
   int dev = 0;
@@ -102,6 +260,82 @@ hipError_t launch_bs16(int m, const dev::GfArgs& a, unsigned ns, uint64_t len, h
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
+}
+
+namespace {
+// kBsWaveBytes of zeros on the current device (the missing slots' loads), allocated once
+const uint8_t* zero_tile() {
+  static std::mutex mu;
+  static const uint8_t* z[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  if (!z[dev]) {
+    void* p = nullptr;
+    if (hipMalloc(&p, dev::kBsWaveBytes) != hipSuccess) return nullptr;
+    if (hipMemset(p, 0, dev::kBsWaveBytes) != hipSuccess) {
+      (void)hipFree(p);
+      return nullptr;
+    }
+    z[dev] = static_cast<const uint8_t*>(p);
+  }
+  return z[dev];
+}
+
+void coef_tables_host(uint8_t c, dev::u32x4& t01, uint32_t& t2) {  // gf_device.hpp coef_tables
+  const GF& gf = GF::get();
+  uint32_t p[8];
+  p[0] = c;
+  for (int j = 1; j < 8; ++j) p[j] = gf.mul((uint8_t)p[j - 1], 2);
+  uint32_t t0lo = 0, t0hi = 0, t1lo = 0, t1hi = 0, tt2 = 0;
+  for (int e = 0; e < 8; ++e) {
+    const uint32_t v0 = ((e & 1) ? p[0] : 0u) ^ ((e & 2) ? p[1] : 0u) ^ ((e & 4) ? p[2] : 0u);
+    const uint32_t v1 = ((e & 1) ? p[3] : 0u) ^ ((e & 2) ? p[4] : 0u) ^ ((e & 4) ? p[5] : 0u);
+    if (e < 4) {
+      const uint32_t v2 = ((e & 1) ? p[6] : 0u) ^ ((e & 2) ? p[7] : 0u);
+      t0lo |= v0 << (8 * e);
+      t1lo |= v1 << (8 * e);
+      tt2 |= v2 << (8 * e);
+    } else {
+      t0hi |= v0 << (8 * (e - 4));
+      t1hi |= v1 << (8 * (e - 4));
+    }
+  }
+  t01 = dev::u32x4{t0lo, t0hi, t1lo, t1hi};
+  t2 = tt2;
+}
+
+template <int M>
+hipError_t launch_rep_m(int nd, const dev::GfArgs& a, const BsRepairArgs& r, unsigned grid, uint32_t tps,
+                        uint32_t nt, hipStream_t st) {
+  switch (nd) {
+    case 0: hipLaunchKernelGGL((gf_bs16_repair_kernel<M, 0>), dim3(grid), dim3(64 * kBsWaves), 0, st, a, r, tps, nt); break;
+    case 1: hipLaunchKernelGGL((gf_bs16_repair_kernel<M, 1>), dim3(grid), dim3(64 * kBsWaves), 0, st, a, r, tps, nt); break;
+    case 2: hipLaunchKernelGGL((gf_bs16_repair_kernel<M, 2>), dim3(grid), dim3(64 * kBsWaves), 0, st, a, r, tps, nt); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+}  // namespace
+
+hipError_t launch_bs16_repair(int nd, int ne, const uint8_t* missing, const uint8_t* prow, const uint8_t* ainv,
+                              const dev::GfArgs& a, unsigned ns, uint64_t len, hipStream_t st) {
+  const uint32_t tps = (uint32_t)(len / dev::kBsWaveBytes);
+  const uint64_t ntiles = (uint64_t)tps * ns;
+  if (nd < 0 || nd > kBsRepairMaxNd || (ne != 0 && ne != 2) || a.tab != 1 || tps == 0 || ntiles > 0xFFFFFFFFull ||
+      (len % dev::kBsWaveBytes) || (a.pcmp && !a.flags))
+    return hipErrorInvalidValue;
+  BsRepairArgs r{};
+  for (int q = 0; q < nd; ++q) {
+    r.slot[q] = missing[q];
+    r.prow[q] = prow[q];
+    for (int j = 0; j < nd; ++j) coef_tables_host(ainv[j * 4 + q], r.t01[j * 4 + q], r.t2[j * 4 + q]);
+  }
+  r.zero = zero_tile();
+  if (!r.zero) return hipErrorOutOfMemory;
+  const unsigned grid = (unsigned)std::min<uint64_t>((uint64_t)cu_count(), (ntiles + kBsWaves - 1) / kBsWaves);
+  return ne == 2 ? launch_rep_m<22>(nd, a, r, grid, tps, (uint32_t)ntiles, st)
+                 : launch_rep_m<20>(nd, a, r, grid, tps, (uint32_t)ntiles, st);
 }
 
 }  // namespace cfsec

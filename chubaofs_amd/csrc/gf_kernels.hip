@@ -129,11 +129,14 @@ static const bool kBs16 = [] {
   const char* v = std::getenv("CFSEC_BS16");
   return !(v && v[0] == '0');
 }();
-static bool bs16_ok(const dev::GfArgs& a, int k, int m, int tab) {
-  if (!bs16_matches(a.coef, m, k) || (a.sstride & 15)) return false;
-  for (int i = 0; i < tab * (k + m); ++i)
+static bool aligned16(const dev::GfArgs& a, int nptr) {
+  if (a.sstride & 15) return false;
+  for (int i = 0; i < nptr; ++i)
     if (reinterpret_cast<uintptr_t>(a.ptr[i]) & 15) return false;
   return true;
+}
+static bool bs16_ok(const dev::GfArgs& a, int k, int m, int tab) {
+  return bs16_matches(a.coef, m, k) && aligned16(a, tab * (k + m));
 }
 
 hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
@@ -414,8 +417,31 @@ hipError_t launch_dy16_repair(const Dy16RepairJob& job, hipStream_t stream) {
       for (int c = 0; c < 16; ++c) a.ptr[s * 16 + c] = job.in[(size_t)(s0 + s) * 16 + c];
       for (int r = 0; r < mo; ++r) a.ptr[tab * 16 + s * mo + r] = job.out[(size_t)(s0 + s) * mo + r];
     }
-    const hipError_t e = launch_dy16_repair_args(nd, ne, a, (unsigned)ns, stream);
-    if (e != hipSuccess) return e;
+    // the syndrome form of the bit-sliced network (gf_bs16.hip) for the whole 2 KiB column runs of
+    // 16-byte aligned rows, the dyadic repair kernel for the rest of each row
+    const uint64_t full = job.syn && kBs16 && nd <= kBsRepairMaxNd && tab == 1 && !job.lens &&
+                                  bs16_matches(job.coef, 20 + ne, 16) && aligned16(a, tab * (16 + mo))
+                              ? llen / kBs16Tile * kBs16Tile
+                              : 0;
+    if (full) {
+      uint8_t missing[4] = {};
+      for (int i = 0; i < 16; ++i)
+        if (job.src[i] >= 16) missing[job.src[i] - 16] = (uint8_t)i;
+      const hipError_t e = launch_bs16_repair(nd, ne, missing, job.prow, job.ainv, a, (unsigned)ns, full, stream);
+      if (e != hipSuccess) return e;
+    }
+    if (full < llen) {
+      const dev::GfArgs* ta = &a;
+      static thread_local dev::GfArgs tail;
+      if (full) {
+        std::memcpy(&tail, &a, sizeof(dev::GfArgs));
+        for (int i = 0; i < tab * (16 + mo); ++i) tail.ptr[i] = a.ptr[i] + full;
+        tail.len = llen - full;
+        ta = &tail;
+      }
+      const hipError_t e = launch_dy16_repair_args(nd, ne, *ta, (unsigned)ns, stream);
+      if (e != hipSuccess) return e;
+    }
     a.zw = nullptr;  // the first launch zeroed them
     a.nzw = 0;
   }

@@ -102,6 +102,13 @@ hipError_t launch_dy16(int m, MatVecMode mode, const dev::GfArgs& a, unsigned ns
 constexpr uint64_t kBs16Tile = 2048;
 bool bs16_matches(const uint8_t* coef, int m, int k);
 hipError_t launch_bs16(int m, const dev::GfArgs& a, unsigned ns, uint64_t len, hipStream_t st);
+// The same network for a repair_dy16 argument block (ne = 0 / 2 extra rows) of an affine batch (tab
+// == 1): missing[q] the data row of missing row q, prow[q] the parity row of input 16 - nd + q, ainv
+// (nd x nd, row stride 4) the inverse of those parity rows at the missing columns; columns [0, len),
+// len a multiple of kBs16Tile; nd <= kBsRepairMaxNd (3 and 4 missing data rows spill: dyadic kernel).
+constexpr int kBsRepairMaxNd = 2;
+hipError_t launch_bs16_repair(int nd, int ne, const uint8_t* missing, const uint8_t* prow, const uint8_t* ainv,
+                              const dev::GfArgs& a, unsigned ns, uint64_t len, hipStream_t st);
 
 // repair_dy16 on a GfArgs block (gf_dy16.hip); launch_dy16_repair (gf_kernels.hip) fills it.
 hipError_t launch_dy16_repair_args(int nd, int ne, const dev::GfArgs& a, unsigned ns, hipStream_t st);

@@ -53,6 +53,9 @@ struct Dy16RepairJob {
   uint32_t* flags = nullptr;           // device [nstripes]
   uint32_t* zero_words = nullptr;      // device: nzero words the first launch zeroes (a batch's checksum
   uint32_t nzero = 0;                  // words, XOR-accumulated by the checksum pass that follows)
+  bool syn = false;                    // the syndrome form below is set: the bit-sliced kernel may run
+  uint8_t prow[4] = {};                // input 16 - nd + q is parity row prow[q]
+  uint8_t ainv[16] = {};               // missing row j = sum_q ainv[j * 4 + q] * syndrome of prow[q]
 };
 hipError_t launch_dy16_repair(const Dy16RepairJob& job, hipStream_t stream);
 
