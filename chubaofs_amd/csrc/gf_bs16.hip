@@ -94,7 +94,26 @@ struct BsRepairArgs {
   const uint8_t* zero;  // kBsWaveBytes of zeros
 };
 
-constexpr int kRepPrefetch = 7, kRepRing = 3;
+#ifndef CFSEC_BS_PF
+#define CFSEC_BS_PF 7  // slots prefetched into LDS per wave (A/B)
+#endif
+#ifndef CFSEC_BS_RING
+#define CFSEC_BS_RING 3  // LDS ring of compared rows per wave (A/B)
+#endif
+#ifndef CFSEC_BS_REP_ST
+#define CFSEC_BS_REP_ST 0  // rebuilt rows: 0 non-temporal stores, 1 plain (the checksum pass may find them cached)
+#endif
+constexpr int kRepPrefetch = CFSEC_BS_PF, kRepRing = CFSEC_BS_RING;
+static_assert(kRepRing >= 3 || kRepRing == 2, "ring of 2 or more rows");
+
+__device__ __forceinline__ void bs_st_rebuilt(uint8_t* p, const uint32_t* o) {
+  if constexpr (CFSEC_BS_REP_ST) {
+    *reinterpret_cast<dev::u32x4*>(p) = dev::u32x4{o[0], o[1], o[2], o[3]};
+    *reinterpret_cast<dev::u32x4*>(p + 1024) = dev::u32x4{o[4], o[5], o[6], o[7]};
+  } else {
+    dev::bs_st_row(p, o);
+  }
+}
 
 __device__ __forceinline__ void bs_mul_acc8(uint32_t* acc, const uint32_t* s0, const uint32_t* s1, const uint32_t* s2,
                                             const dev::u32x4 q, uint32_t t2) {
@@ -180,7 +199,7 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
           }
           bs_mul_acc8(d, s0, s1, s2, r.t01[j * 4 + q], r.t2[j * 4 + q]);
         }
-        bs_st_row(output(s, j, c), d);
+        bs_st_rebuilt(output(s, j, c), d);
         bs_transpose8(d);
 #pragma unroll
         for (int i = 0; i < kBsK; ++i) {
@@ -209,7 +228,7 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
     bs_net_ec16p20l2<M>(x, [&](int p, uint32_t (&o)[8]) {
       if (a.pstore >> p & 1) {
         bs_transpose8(o);
-        bs_st_row(output(s, ND + p, c), o);
+        bs_st_rebuilt(output(s, ND + p, c), o);
       } else if (a.pcmp >> p & 1) {
         // this row's copy; the next compared row's may still fly (anything issued between them is
         // waited for too: retirement is in order)
