@@ -23,28 +23,31 @@ namespace cfsec {
 namespace {
 constexpr int kBsK = 16, kBsPrefetch = 8, kBsWaves = 8;
 
-template <int M>
-__global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2, 2))) void gf_bs16_kernel(
+// Encode: Net's K inputs -> its first M rows (K <= 16: 8 K input planes in registers)
+template <class Net, int M>
+__global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2, 2))) void gf_bs_kernel(
     const dev::GfArgs a, uint32_t tiles_per_stripe, uint32_t ntiles) {
   using namespace dev;
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kBsWaves][kBsPrefetch * kBsWaveBytes];
+  constexpr int K = Net::K, PF = K < kBsPrefetch ? K : kBsPrefetch;
+  constexpr int NW = 2 * (K - PF) + 2 * M;  // vector memory ops a tile issues after its prefetch
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kBsWaves][PF * kBsWaveBytes];
   // the wave index as a scalar: tiles, stripes and row pointers are then wave-uniform (scalar loads
   // of the pointer table, no vector memory operations besides the shard copies counted below)
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   uint8_t* pre = lds[wave];
   const uint32_t nw = gridDim.x * kBsWaves;
-  // row i of stripe s (inputs 0..15, then outputs), at the lane's first byte of column tile c
+  // row i of stripe s (inputs 0..K-1, then outputs), at the lane's first byte of column tile c
   const auto row = [&](uint32_t s, int i, uint32_t c) -> uint8_t* {
     const uint8_t* base;
-    if (i < kBsK) base = a.sstride ? a.ptr[i] + (int64_t)s * a.sstride : a.ptr[(size_t)s * kBsK + i];
-    else base = a.sstride ? a.ptr[kBsK + (i - kBsK)] + (int64_t)s * a.sstride
-                          : a.ptr[(size_t)a.tab * kBsK + (size_t)s * M + (i - kBsK)];
+    if (i < K) base = a.sstride ? a.ptr[i] + (int64_t)s * a.sstride : a.ptr[(size_t)s * K + i];
+    else base = a.sstride ? a.ptr[K + (i - K)] + (int64_t)s * a.sstride
+                          : a.ptr[(size_t)a.tab * K + (size_t)s * M + (i - K)];
     return const_cast<uint8_t*>(base) + (size_t)c * kBsWaveBytes + lane * 16;
   };
   const auto prefetch = [&](uint32_t t) {
     const uint32_t s = t / tiles_per_stripe, c = t % tiles_per_stripe;
 #pragma unroll
-    for (int i = 0; i < kBsPrefetch; ++i) bs_glds_row(row(s, i, c), pre + i * kBsWaveBytes);
+    for (int i = 0; i < PF; ++i) bs_glds_row(row(s, i, c), pre + i * kBsWaveBytes);
   };
   uint32_t t = blockIdx.x * kBsWaves + wave;
   if (t >= ntiles) return;  // no barrier in this kernel: idle waves leave at once
@@ -52,23 +55,23 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
   __builtin_amdgcn_s_waitcnt(bs_waitcnt_vm(0));
   for (; t < ntiles; t += nw) {
     const uint32_t s = t / tiles_per_stripe, c = t % tiles_per_stripe;
-    uint32_t x[128];
+    uint32_t x[8 * K];
 #pragma unroll
-    for (int i = kBsPrefetch; i < kBsK; ++i) bs_ld_row(row(s, i, c), &x[8 * i]);
-    // the prefetched rows were issued before the previous tile's stores and these 16 loads, and
-    // vector memory operations retire in issue order: at most 16 + 2 M may still be in flight
-    __builtin_amdgcn_s_waitcnt(bs_waitcnt_vm(2 * (kBsK - kBsPrefetch) + 2 * M > 63 ? 63 : 2 * (kBsK - kBsPrefetch) + 2 * M));
+    for (int i = PF; i < K; ++i) bs_ld_row(row(s, i, c), &x[8 * i]);
+    // the prefetched rows were issued before the previous tile's stores and these loads, and
+    // vector memory operations retire in issue order
+    __builtin_amdgcn_s_waitcnt(bs_waitcnt_vm(NW > 63 ? 63 : NW));
 #pragma unroll
-    for (int i = 0; i < kBsPrefetch; ++i) bs_lds_row(pre + i * kBsWaveBytes, lane, &x[8 * i]);
+    for (int i = 0; i < PF; ++i) bs_lds_row(pre + i * kBsWaveBytes, lane, &x[8 * i]);
     __builtin_amdgcn_s_waitcnt(kBsWaitLgkm0);
 #pragma unroll
-    for (int i = 0; i < kBsK; ++i) bs_transpose8(&x[8 * i]);
+    for (int i = 0; i < K; ++i) bs_transpose8(&x[8 * i]);
     __builtin_amdgcn_sched_barrier(0);
     prefetch(t + nw < ntiles ? t + nw : t);  // branch-free: nothing sinks below it (the last re-reads)
     __builtin_amdgcn_sched_barrier(0);
-    bs_net_ec16p20l2<M>(x, [&](int r, uint32_t (&o)[8]) {
+    Net::template net<M>(x, [&](int r, uint32_t (&o)[8]) {
       bs_transpose8(o);
-      bs_st_row(row(s, kBsK + r, c), o);
+      bs_st_row(row(s, K + r, c), o);
     });
   }
 }
@@ -260,25 +263,39 @@ int cu_count() {
 }
 }  // namespace
 
-bool bs16_matches(const uint8_t* coef, int m, int k) {
-  if (k != 16 || (m != 20 && m != 22)) return false;
-  for (int r = 0; r < m; ++r)
-    for (int c = 0; c < 16; ++c)
-      if (coef[(size_t)r * 16 + c] != dev::kBsEc16p20l2Rows[r][c]) return false;
+namespace {
+template <class Net>
+bool rows_match(const uint8_t* coef, int m) {
+  const uint8_t* w = Net::rows();
+  for (int i = 0; i < m * Net::K; ++i)
+    if (coef[i] != w[i]) return false;
   return true;
 }
 
-hipError_t launch_bs16(int m, const dev::GfArgs& a, unsigned ns, uint64_t len, hipStream_t st) {
+template <class Net, int M>
+hipError_t launch_net(const dev::GfArgs& a, unsigned grid, uint32_t tps, uint32_t nt, hipStream_t st) {
+  hipLaunchKernelGGL((gf_bs_kernel<Net, M>), dim3(grid), dim3(64 * kBsWaves), 0, st, a, tps, nt);
+  return hipGetLastError();
+}
+}  // namespace
+
+// EC15P12 / EC12P9 networks (tools/gen_bs_net.py ec15p12 | ec12p9) run 13-23 % slower than the
+// lookup-product kernel on their shapes (profiles/r04/bsk_ab.txt: 2-3 tiles per wave, and the row
+// tails need a second launch), so only the 16 + 20 code takes this route.
+bool bs_matches(const uint8_t* coef, int m, int k) {
+  if (k == 16 && (m == 20 || m == 22)) return rows_match<dev::BsEc16p20l2>(coef, m);
+  return false;
+}
+
+hipError_t launch_bs(int k, int m, const dev::GfArgs& a, unsigned ns, uint64_t len, hipStream_t st) {
   const uint32_t tps = (uint32_t)(len / dev::kBsWaveBytes);
   const uint64_t ntiles = (uint64_t)tps * ns;
   if (tps == 0 || ntiles > 0xFFFFFFFFull || (len % dev::kBsWaveBytes)) return hipErrorInvalidValue;
   const unsigned grid = (unsigned)std::min<uint64_t>((uint64_t)cu_count(), (ntiles + kBsWaves - 1) / kBsWaves);
-  switch (m) {
-    case 20: hipLaunchKernelGGL(gf_bs16_kernel<20>, dim3(grid), dim3(64 * kBsWaves), 0, st, a, tps, (uint32_t)ntiles); break;
-    case 22: hipLaunchKernelGGL(gf_bs16_kernel<22>, dim3(grid), dim3(64 * kBsWaves), 0, st, a, tps, (uint32_t)ntiles); break;
-    default: return hipErrorInvalidValue;
-  }
-  return hipGetLastError();
+  const uint32_t nt = (uint32_t)ntiles;
+  if (k == 16 && m == 20) return launch_net<dev::BsEc16p20l2, 20>(a, grid, tps, nt, st);
+  if (k == 16 && m == 22) return launch_net<dev::BsEc16p20l2, 22>(a, grid, tps, nt, st);
+  return hipErrorInvalidValue;
 }
 
 namespace {

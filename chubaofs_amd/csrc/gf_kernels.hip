@@ -135,8 +135,8 @@ static bool aligned16(const dev::GfArgs& a, int nptr) {
     if (reinterpret_cast<uintptr_t>(a.ptr[i]) & 15) return false;
   return true;
 }
-static bool bs16_ok(const dev::GfArgs& a, int k, int m, int tab) {
-  return bs16_matches(a.coef, m, k) && aligned16(a, tab * (k + m));
+static bool bs_ok(const dev::GfArgs& a, int k, int m, int tab) {
+  return bs_matches(a.coef, m, k) && aligned16(a, tab * (k + m));
 }
 
 hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
@@ -217,7 +217,7 @@ hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
           }
           if (llen == 0) continue;
         }
-        const size_t ltiles = (llen + tile - 1) / tile;
+        size_t ltiles = (llen + tile - 1) / tile;
         a.len = llen;
         a.k = (uint32_t)kc;
         a.m = (uint32_t)mc;
@@ -237,8 +237,25 @@ hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
           for (int r = 0; r < mc; ++r)
             a.ptr[tab * kc + s * mc + r] = job.out[(size_t)(s0 + s) * job.m + r0 + r];
         }
-        const dim3 grid((unsigned)(ltiles * ns));
         hipError_t e;
+        // encodes of the bit-sliced shapes (gf_bs16.hip: EC16P20, EC16P20L2's fused encode) with 16-byte
+        // aligned rows: the whole 2 KiB column runs through the network, the rest of each row through
+        // the kernel chosen below
+        const uint64_t full = mode == MatVecMode::kStore && !job.lens && kBs16 && c0 == 0 && r0 == 0 && kc == job.k &&
+                                      mc == job.m && bs_ok(a, kc, mc, tab)
+                                  ? llen / kBs16Tile * kBs16Tile
+                                  : 0;
+        if (full) {
+          e = launch_bs(kc, mc, a, (unsigned)ns, full, stream);
+          if (e != hipSuccess) return e;
+          if (full == llen) continue;
+          for (int i = 0; i < tab * (kc + mc); ++i) a.ptr[i] += full;
+          llen -= full;
+          ltiles = (llen + tile - 1) / tile;
+          a.len = llen;
+          a.tiles_per_stripe = (uint32_t)ltiles;
+        }
+        const dim3 grid((unsigned)(ltiles * ns));
         if (lut) {
           const size_t lt = lut_tile_bytes(kc);
           const dim3 lgrid((unsigned)((llen + lt - 1) / lt), (unsigned)ns);
@@ -247,27 +264,8 @@ hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
           continue;
         }
         if (fixed && dy16) {
-          // encodes whose rows are 16-byte aligned: the whole 2 KiB column runs through the
-          // bit-sliced network (gf_bs16.hip), the rest of each row through the dyadic kernel
-          const uint64_t full = mode == MatVecMode::kStore && !job.lens && kBs16 && bs16_ok(a, kc, mc, tab)
-                                    ? llen / kBs16Tile * kBs16Tile
-                                    : 0;
-          if (full) {
-            e = launch_bs16(mc, a, (unsigned)ns, full, stream);
-            if (e != hipSuccess) return e;
-          }
-          if (full < llen) {
-            const dev::GfArgs* ta = &a;
-            static thread_local dev::GfArgs tail;
-            if (full) {
-              std::memcpy(&tail, &a, sizeof(dev::GfArgs));
-              for (int i = 0; i < tab * (kc + mc); ++i) tail.ptr[i] = a.ptr[i] + full;
-              tail.len = llen - full;
-              ta = &tail;
-            }
-            e = launch_dy16(mc, mode, *ta, (unsigned)ns, stream);
-            if (e != hipSuccess) return e;
-          }
+          e = launch_dy16(mc, mode, a, (unsigned)ns, stream);
+          if (e != hipSuccess) return e;
           continue;
         }
         if (fixed && dy.B) {
@@ -420,7 +418,7 @@ hipError_t launch_dy16_repair(const Dy16RepairJob& job, hipStream_t stream) {
     // the syndrome form of the bit-sliced network (gf_bs16.hip) for the whole 2 KiB column runs of
     // 16-byte aligned rows, the dyadic repair kernel for the rest of each row
     const uint64_t full = job.syn && kBs16 && nd <= kBsRepairMaxNd && tab == 1 && !job.lens &&
-                                  bs16_matches(job.coef, 20 + ne, 16) && aligned16(a, tab * (16 + mo))
+                                  bs_matches(job.coef, 20 + ne, 16) && aligned16(a, tab * (16 + mo))
                               ? llen / kBs16Tile * kBs16Tile
                               : 0;
     if (full) {

@@ -96,12 +96,13 @@ inline DyPlan dyadic_plan(const uint8_t* coef, int m, int k) {
 // encode's local parity).
 hipError_t launch_dy16(int m, MatVecMode mode, const dev::GfArgs& a, unsigned ns, hipStream_t st);
 
-// The bit-sliced EC16P20 / EC16P20L2 parity kernel (gf_bs16.hip): coef (m x 16, row stride 16) must
-// equal the network's constants (bs16_matches); launch_bs16 covers columns [0, len) of every stripe,
-// len a multiple of kBs16Tile, every row pointer (and sstride) 16-byte aligned.
+// The bit-sliced parity kernels (gf_bs16.hip) for the fixed matrices of EC16P20 (k 16, m 20) and
+// EC16P20L2's fused encode (16, 22): coef (m x k, row stride k) must equal the network's constants
+// (bs_matches); launch_bs covers columns [0, len) of every stripe, len a multiple of kBs16Tile,
+// every row pointer (and sstride) 16-byte aligned.
 constexpr uint64_t kBs16Tile = 2048;
-bool bs16_matches(const uint8_t* coef, int m, int k);
-hipError_t launch_bs16(int m, const dev::GfArgs& a, unsigned ns, uint64_t len, hipStream_t st);
+bool bs_matches(const uint8_t* coef, int m, int k);
+hipError_t launch_bs(int k, int m, const dev::GfArgs& a, unsigned ns, uint64_t len, hipStream_t st);
 // The same network for a repair_dy16 argument block (ne = 0 / 2 extra rows) of an affine batch (tab
 // == 1): missing[q] the data row of missing row q, prow[q] the parity row of input 16 - nd + q, ainv
 // (nd x nd, row stride 4) the inverse of those parity rows at the missing columns; columns [0, len),

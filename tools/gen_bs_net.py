@@ -15,7 +15,8 @@ the inverse of its top k rows, reedsolomon.go:220-244) and of the CubeFS local r
 checks its engine's coefficients against these constants before it takes the network
 (gf_bs16.hip), and the probes tools/bs_probe.hip / bs_repair_probe.hip use it too.
 
-  python3 tools/gen_bs_net.py > chubaofs_amd/csrc/bs_net_ec16p20l2.hpp
+  python3 tools/gen_bs_net.py ec16p20l2 > chubaofs_amd/csrc/bs_net_ec16p20l2.hpp
+  python3 tools/gen_bs_net.py ec15p12 | ec12p9   (measured, not shipped: profiles/r04/bsk_ab.txt)
 """
 import sys
 
@@ -121,27 +122,28 @@ def row_network(row):
     return n_in, temps, outs
 
 
-def emit_row(r, row, lines):
-    """Row r's network as a specialization bs_row_ec16p20l2<r>(x, o)."""
+def emit_row(name, r, row, lines):
+    """Row r's network as a specialization bs_row_<name><r>(x, o)."""
     n_in, temps, outs = row_network(row)
-    name = lambda s: f"x[{s}]" if s < n_in else f"t{s - n_in}"
+    nx = n_in
+    tname = lambda s_: f"x[{s_}]" if s_ < n_in else f"t{s_ - n_in}"
     done = set()
     body = []
 
-    def need(s):
-        if s < n_in or s in done:
+    def need(s_):
+        if s_ < n_in or s_ in done:
             return
-        a, b = temps[s - n_in]
-        need(a)
-        need(b)
-        done.add(s)
-        body.append(f"  const uint32_t {name(s)} = {name(a)} ^ {name(b)};")
+        a_, b_ = temps[s_ - n_in]
+        need(a_)
+        need(b_)
+        done.add(s_)
+        body.append(f"  const uint32_t {tname(s_)} = {tname(a_)} ^ {tname(b_)};")
 
     ops = 0
     for o, sig in enumerate(outs):
-        for s in sig:
-            need(s)
-        terms = [name(s) for s in sig]
+        for s_ in sig:
+            need(s_)
+        terms = [tname(s_) for s_ in sig]
         if not terms:
             expr = "0u"
         else:
@@ -163,7 +165,7 @@ def emit_row(r, row, lines):
     ops += len(temps)
     lines.append(f"// row {r}: {len(temps)} shared pairs, {ops} VALU ops per 32-byte column")
     lines.append("template <>")
-    lines.append(f"__device__ __forceinline__ void bs_row_ec16p20l2<{r}>(const uint32_t (&x)[128], uint32_t (&o)[8]) {{")
+    lines.append(f"__device__ __forceinline__ void bs_row_{name}<{r}>(const uint32_t (&x)[{nx}], uint32_t (&o)[8]) {{")
     lines += body
     lines.append("}")
     return ops
@@ -171,41 +173,59 @@ def emit_row(r, row, lines):
 
 BARRIER = "--no-barrier" not in sys.argv
 
+CODES = {
+    # name: (title, rows, note on NR)
+    "ec16p20l2": ("The EC16P20L2 parity (20 KRS global rows, then the 2 AZ-local rows over the data)",
+                  ec16p20l2_rows, "NR = 20: EC16P20's global parity; 22: with the local rows"),
+    "ec15p12": ("The EC15P12 parity (KRS buildMatrix(15, 27) rows 15..26)", lambda: parity_rows(15, 12), "NR = 12"),
+    "ec12p9": ("The EC12P9 parity (KRS buildMatrix(12, 21) rows 12..20)", lambda: parity_rows(12, 9), "NR = 9"),
+}
+
 
 def main():
-    rows = ec16p20l2_rows()
+    code = next((a for a in sys.argv[1:] if not a.startswith("--")), "ec16p20l2")
+    title, make_rows, nr_note = CODES[code]
+    rows = make_rows()
+    m, k = len(rows), len(rows[0])
+    nx = 8 * k
     lines = []
     total = 0
     for r, row in enumerate(rows):
-        total += emit_row(r, row, lines)
+        total += emit_row(code, r, row, lines)
+    Name = "Bs" + code[0].upper() + code[1:]
     out = sys.stdout
-    out.write("// bs_net_ec16p20l2.hpp -- GENERATED by tools/gen_bs_net.py; do not edit.\n")
-    out.write("//\n// The EC16P20L2 parity (20 KRS global rows, then the 2 AZ-local rows over the data) as a\n")
-    out.write(f"// bit-sliced XOR network: {total} VALU ops per 32-byte column for all 22 rows.\n")
+    out.write(f"// bs_net_{code}.hpp -- GENERATED by tools/gen_bs_net.py {code}; do not edit.\n")
+    out.write(f"//\n// {title} as a\n")
+    out.write(f"// bit-sliced XOR network: {total} VALU ops per 32-byte column for all {m} rows.\n")
     out.write("// x[8c + j]: bit plane j of data row c; o: the output row's 8 planes.\n")
     out.write("#pragma once\n#include <cstdint>\n\nnamespace cfsec {\nnamespace dev {\n\n")
-    out.write("constexpr uint8_t kBsEc16p20l2Rows[22][16] = {\n")
+    out.write(f"constexpr uint8_t k{Name}Rows[{m}][{k}] = {{\n")
     for row in rows:
         out.write("    {" + ", ".join(f"0x{v:02x}" for v in row) + "},\n")
     out.write("};\n\n")
+    out.write("#ifndef CFSEC_BS_X3\n#define CFSEC_BS_X3\n")
     out.write("__device__ __forceinline__ uint32_t bs_x3(uint32_t a, uint32_t b, uint32_t c) {\n"
-              "  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);\n}\n\n")
-    out.write("template <int R>\n__device__ __forceinline__ void bs_row_ec16p20l2(const uint32_t (&x)[128], uint32_t (&o)[8]);\n\n")
+              "  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);\n}\n#endif\n\n")
+    out.write(f"template <int R>\n__device__ __forceinline__ void bs_row_{code}(const uint32_t (&x)[{nx}], uint32_t (&o)[8]);\n\n")
     out.write("\n".join(lines) + "\n\n")
-    out.write("// rows 0 .. NR-1 in order (NR = 20: EC16P20's global parity; 22: with the local rows); emit(r, o)\n")
-    out.write("// consumes row r's planes\n")
-    out.write("template <int NR = 22, class Emit>\n__device__ __forceinline__ void bs_net_ec16p20l2(const uint32_t (&x)[128], Emit&& emit) {\n")
-    for r in range(len(rows)):
-        out.write(f"  if constexpr ({r} < NR) {{\n    uint32_t o[8];\n    bs_row_ec16p20l2<{r}>(x, o);\n    emit({r}, o);\n")
+    out.write(f"// rows 0 .. NR-1 in order ({nr_note}); emit(r, o) consumes row r's planes\n")
+    out.write(f"template <int NR = {m}, class Emit>\n__device__ __forceinline__ void bs_net_{code}(const uint32_t (&x)[{nx}], Emit&& emit) {{\n")
+    for r in range(m):
+        out.write(f"  if constexpr ({r} < NR) {{\n    uint32_t o[8];\n    bs_row_{code}<{r}>(x, o);\n    emit({r}, o);\n")
         if BARRIER:
             out.write("    __builtin_amdgcn_sched_barrier(0);\n")
         out.write("  }\n")
     out.write("}\n\n")
     out.write("// row r chosen at run time (uniform)\n")
-    out.write("__device__ __forceinline__ void bs_row_ec16p20l2_rt(int r, const uint32_t (&x)[128], uint32_t (&o)[8]) {\n  switch (r) {\n")
-    for r in range(len(rows)):
-        out.write(f"    case {r}: bs_row_ec16p20l2<{r}>(x, o); break;\n")
+    out.write(f"__device__ __forceinline__ void bs_row_{code}_rt(int r, const uint32_t (&x)[{nx}], uint32_t (&o)[8]) {{\n  switch (r) {{\n")
+    for r in range(m):
+        out.write(f"    case {r}: bs_row_{code}<{r}>(x, o); break;\n")
     out.write("    default: for (int j = 0; j < 8; ++j) o[j] = 0u;\n  }\n}\n\n")
+    out.write(f"// the network as a type for the K-input kernels (gf_bs16.hip)\n")
+    out.write(f"struct {Name} {{\n  static constexpr int K = {k}, M = {m};\n")
+    out.write(f"  static const uint8_t* rows() {{ return &k{Name}Rows[0][0]; }}\n")
+    out.write(f"  template <int NR, class Emit>\n  __device__ static __forceinline__ void net(const uint32_t (&x)[{nx}], Emit&& emit) {{\n")
+    out.write(f"    bs_net_{code}<NR>(x, static_cast<Emit&&>(emit));\n  }}\n}};\n\n")
     out.write("}  // namespace dev\n}  // namespace cfsec\n")
 
 
