@@ -245,12 +245,30 @@ hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
                                       mc == job.m && bs_ok(a, kc, mc, tab)
                                   ? llen / kBs16Tile * kBs16Tile
                                   : 0;
-        if (full) {
-          e = launch_bs(kc, mc, a, (unsigned)ns, full, stream);
+        // Verify of the same shapes: the bit-sliced repair kernel with nothing missing, every row compared
+        const uint64_t vfull = mode == MatVecMode::kVerify && full == 0 && !job.lens && kBs16 && c0 == 0 &&
+                                       r0 == 0 && kc == 16 && kc == job.k && mc == job.m && tab == 1 &&
+                                       a.flags && bs_ok(a, kc, mc, tab)
+                                   ? llen / kBs16Tile * kBs16Tile
+                                   : 0;
+        if (vfull) {
+          a.pstore = 0;
+          a.pcmp = (1u << mc) - 1;
+          for (int i = 0; i < 16; ++i) a.src[i] = (uint8_t)i;
+          a.zw = nullptr;
+          a.nzw = 0;
+          e = launch_bs16_repair(0, mc - 20, nullptr, nullptr, nullptr, a, (unsigned)ns, vfull, stream);
           if (e != hipSuccess) return e;
-          if (full == llen) continue;
-          for (int i = 0; i < tab * (kc + mc); ++i) a.ptr[i] += full;
-          llen -= full;
+        }
+        if (full || vfull) {
+          if (full) {
+            e = launch_bs(kc, mc, a, (unsigned)ns, full, stream);
+            if (e != hipSuccess) return e;
+          }
+          const uint64_t done = full ? full : vfull;
+          if (done == llen) continue;
+          for (int i = 0; i < tab * (kc + mc); ++i) a.ptr[i] += done;
+          llen -= done;
           ltiles = (llen + tile - 1) / tile;
           a.len = llen;
           a.tiles_per_stripe = (uint32_t)ltiles;
