@@ -818,3 +818,44 @@ def test_async_over_32_inputs_not_supported():
         enc.ReconstructBatchAsync([dev], [[0]], flags=flags)
     st = enc.ReconstructBatch([[x.copy() for x in good]], [[0]])
     assert st == [0]
+
+
+@pytest.mark.parametrize("S", [4096, 262144 + 2048 + 48])
+def test_ec16p20l2_tasklet_bitsliced_repair(S):
+    """C5-shaped repairs through the bit-sliced repair kernel (gf_bs16.hip: aligned rows of one
+    [bids, 38, S] buffer, pairs of bids per erasure pattern so every group is one affine run; S =
+    264,240 leaves a 48-byte row tail to the dyadic kernel): nothing missing but parities ({16, 17}),
+    one and two missing data rows ({3, 20}, {0, 1, 16, 17}), the same with a corrupted compared parity
+    and a corrupted data row (Verify must fail), and three missing data rows (the dyadic kernel) --
+    statuses and every shard against the reference loop restated by the ec oracle."""
+    mode = cm.EC16P20L2
+    t = cm.GetTactic(mode)
+    n = t.N + t.M + t.L
+    enc = ec_new(mode)
+    patterns = [[16, 17], [3, 20], [0, 1, 16, 17], [0, 1, 16, 17], [5, 30], [0, 1, 2, 16]]
+    nb = 2 * len(patterns)
+    buf = torch.empty((nb, n, S), dtype=torch.uint8, device="cuda")
+    assert buf.data_ptr() % 16 == 0
+    rnd = random.Random(S)
+    bads, want = [], []
+    for b in range(nb):
+        good = ec_full_codeword(enc, t, S, 100 + b)
+        bad = patterns[b // 2]
+        work = [g.copy() for g in good]
+        for i in bad:
+            work[i][:] = 0
+        if b in (6, 7):  # a compared global parity (bid 6) / a present data row (bid 7) corrupted
+            j = 25 if b == 6 else 9
+            work[j][rnd.randrange(S)] ^= 1 + rnd.randrange(255)
+        if b == 9:  # a local parity corrupted
+            work[37][rnd.randrange(S)] ^= 0x11
+        want.append(sequential(enc, [w.copy() for w in work], bad))
+        buf[b] = torch.from_numpy(np.stack(work))
+        bads.append(bad)
+    status = enc.ReconstructBatch([[buf[b, i] for i in range(n)] for b in range(nb)], bads)
+    assert status == [w[0] for w in want], (status, [w[0] for w in want])
+    got = buf.cpu().numpy()
+    assert {w[0] for w in want} == {0, _lib.ErrVerify.status}
+    for b in range(nb):  # ErrVerify bids too: the reference's Reconstruct wrote them before Verify
+        for i in range(n):
+            assert np.array_equal(got[b, i], want[b][1][i]), (S, b, bads[b], i)
