@@ -106,6 +106,12 @@ struct BsRepairArgs {
 #ifndef CFSEC_BS_REP_ST
 #define CFSEC_BS_REP_ST 0  // rebuilt rows: 0 non-temporal stores, 1 plain (the checksum pass may find them cached)
 #endif
+#ifndef CFSEC_BS_SKIPZ
+#define CFSEC_BS_SKIPZ 1  // missing slots (zero planes) skip their transpose (A/B)
+#endif
+#ifndef CFSEC_BS_INS
+#define CFSEC_BS_INS 1  // a solved row into its slot: 0 masked XOR over every slot, 1 uniform branch (A/B)
+#endif
 constexpr int kRepPrefetch = CFSEC_BS_PF, kRepRing = CFSEC_BS_RING;
 static_assert(kRepRing >= 3 || kRepRing == 2, "ring of 2 or more rows");
 
@@ -173,17 +179,18 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
     __builtin_amdgcn_s_waitcnt(kBsWaitLgkm0);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int i = 0; i < kBsK; ++i) bs_transpose8(&x[8 * i]);
+    for (int i = 0; i < kBsK; ++i)
+      if (CFSEC_BS_SKIPZ == 0 || a.src[i] < kBsK) bs_transpose8(&x[8 * i]);  // a missing slot's zeros need none
     if constexpr (ND > 0) {
-      // 2. syndromes of the stand-ins over the present data (missing slots are zero planes)
+      // 2. syndromes of the stand-ins over the present data (missing slots are zero planes), in
+      // bytes: the row's planes transposed back and XOR-ed into the stored copy
 #pragma unroll
       for (int q = 0; q < ND; ++q) {
-        bs_transpose8(y[q]);
         uint32_t o[8];
         bs_row_ec16p20l2_rt(r.prow[q], x, o);
+        bs_transpose8(o);
 #pragma unroll
         for (int w = 0; w < 8; ++w) y[q][w] ^= o[w];
-        bs_transpose8(y[q]);  // back to bytes
       }
       // 3. d = A^-1 s, stored, into its slot
 #pragma unroll
@@ -206,9 +213,15 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
         bs_transpose8(d);
 #pragma unroll
         for (int i = 0; i < kBsK; ++i) {
-          const uint32_t m = i == r.slot[j] ? ~0u : 0u;
+          if constexpr (CFSEC_BS_INS == 1) {
+            if (i == r.slot[j])  // uniform: one slot's 8 moves
 #pragma unroll
-          for (int w = 0; w < 8; ++w) x[8 * i + w] ^= d[w] & m;
+              for (int w = 0; w < 8; ++w) x[8 * i + w] = d[w];
+          } else {
+            const uint32_t m = i == r.slot[j] ? ~0u : 0u;
+#pragma unroll
+            for (int w = 0; w < 8; ++w) x[8 * i + w] ^= d[w] & m;
+          }
         }
       }
     }

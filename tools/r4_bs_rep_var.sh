@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 out=gpurun_out/r4_bs_rep_var.txt
 : > $out
 cp chubaofs_amd/libcfsec.so gpurun_out/lib_default.so
-for v in default bs_st1 bs_pf6 default bs_st1; do
+for v in default bs_old default bs_old; do
   if [ $v = default ]; then cp gpurun_out/lib_default.so chubaofs_amd/libcfsec.so; else cp probes_bin/$v/libcfsec.so chubaofs_amd/libcfsec.so; fi
   echo "== $v" >> $out
   timeout -k 10 200 python tools/c5_crc_probe.py 2>/dev/null | grep -v amdgpu >> $out
