@@ -22,6 +22,21 @@ namespace cfsec {
 
 namespace {
 constexpr int kBsK = 16, kBsPrefetch = 8, kBsWaves = 8;
+// LDS-DMA cache policy (gf_bitslice.hpp bs_glds_row): encode default, repair non-temporal (A/B)
+#ifndef CFSEC_BS_ENC_GLDS
+#define CFSEC_BS_ENC_GLDS 0
+#endif
+#ifndef CFSEC_BS_REP_GLDS
+#define CFSEC_BS_REP_GLDS 2
+#endif
+#ifndef CFSEC_BS_ENC_LDNT
+#define CFSEC_BS_ENC_LDNT 1  // register loads of the rows not prefetched: non-temporal (A/B)
+#endif
+#ifndef CFSEC_BS_REP_LDNT
+#define CFSEC_BS_REP_LDNT 1
+#endif
+constexpr int kBsEncGlds = CFSEC_BS_ENC_GLDS, kBsRepGlds = CFSEC_BS_REP_GLDS;
+constexpr bool kBsEncLdNt = CFSEC_BS_ENC_LDNT, kBsRepLdNt = CFSEC_BS_REP_LDNT;
 
 // Encode: Net's K inputs -> its first M rows (K <= 16: 8 K input planes in registers)
 template <class Net, int M>
@@ -47,7 +62,7 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
   const auto prefetch = [&](uint32_t t) {
     const uint32_t s = t / tiles_per_stripe, c = t % tiles_per_stripe;
 #pragma unroll
-    for (int i = 0; i < PF; ++i) bs_glds_row(row(s, i, c), pre + i * kBsWaveBytes);
+    for (int i = 0; i < PF; ++i) bs_glds_row<kBsEncGlds>(row(s, i, c), pre + i * kBsWaveBytes);
   };
   uint32_t t = blockIdx.x * kBsWaves + wave;
   if (t >= ntiles) return;  // no barrier in this kernel: idle waves leave at once
@@ -57,7 +72,7 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
     const uint32_t s = t / tiles_per_stripe, c = t % tiles_per_stripe;
     uint32_t x[8 * K];
 #pragma unroll
-    for (int i = PF; i < K; ++i) bs_ld_row(row(s, i, c), &x[8 * i]);
+    for (int i = PF; i < K; ++i) bs_ld_row<kBsEncLdNt>(row(s, i, c), &x[8 * i]);
     // the prefetched rows were issued before the previous tile's stores and these loads, and
     // vector memory operations retire in issue order
     __builtin_amdgcn_s_waitcnt(bs_waitcnt_vm(NW > 63 ? 63 : NW));
@@ -158,7 +173,7 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
   const auto prefetch = [&](uint32_t t) {
     const uint32_t s = t / tiles_per_stripe, c = t % tiles_per_stripe;
 #pragma unroll
-    for (int i = 0; i < kRepPrefetch; ++i) bs_glds_row(slot_ptr(s, i, c), pre + i * kBsWaveBytes);
+    for (int i = 0; i < kRepPrefetch; ++i) bs_glds_row<kBsRepGlds>(slot_ptr(s, i, c), pre + i * kBsWaveBytes);
   };
   uint32_t t = blockIdx.x * kBsWaves + wave;
   if (t >= ntiles) return;
@@ -169,9 +184,9 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
     uint32_t x[128];
     uint32_t y[ND > 0 ? ND : 1][8];
 #pragma unroll
-    for (int i = kRepPrefetch; i < kBsK; ++i) bs_ld_row(slot_ptr(s, i, c), &x[8 * i]);
+    for (int i = kRepPrefetch; i < kBsK; ++i) bs_ld_row<kBsRepLdNt>(slot_ptr(s, i, c), &x[8 * i]);
 #pragma unroll
-    for (int q = 0; q < ND; ++q) bs_ld_row(input(s, kBsK - ND + q, c), y[q]);
+    for (int q = 0; q < ND; ++q) bs_ld_row<kBsRepLdNt>(input(s, kBsK - ND + q, c), y[q]);
     // the prefetched slots were issued before everything since (in-order retirement)
     __builtin_amdgcn_s_waitcnt(bs_waitcnt_vm(2 * (kBsK - kRepPrefetch + ND)));
 #pragma unroll
@@ -231,7 +246,7 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
       if (pend) {
         const int p = __builtin_ctz(pend);
         pend &= pend - 1;
-        bs_glds_row(output(s, ND + p, c), ring + (q_issue % kRepRing) * kBsWaveBytes);
+        bs_glds_row<kBsRepGlds>(output(s, ND + p, c), ring + (q_issue % kRepRing) * kBsWaveBytes);
         ++q_issue;
       }
     };
