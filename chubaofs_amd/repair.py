@@ -310,6 +310,14 @@ class _Columns:
     reb_by: List[List[int]]
     rsend: List[int]
     rrecv: List[int]
+    _sel_t: dict = field(default_factory=dict)
+
+    def sel_index(self, dev) -> torch.Tensor:
+        """`sel` as an index tensor on `dev`, made once per device."""
+        t = self._sel_t.get(dev)
+        if t is None:
+            t = self._sel_t[dev] = torch.tensor(self.sel, dtype=torch.int64, device=dev)
+        return t
 
 
 @functools.lru_cache(maxsize=256)
@@ -362,12 +370,17 @@ def _repair_columns(enc, local, plan: RepairPlan, rank, world, group, crcs, time
     # 1. forward exchange: to rank r != rank, my shipped shards' columns [c_r, c_r + L_r)
     if world > 1:
         send = local.new_empty(sum(lay.fsend))
-        src = local if lay.sel == list(range(n_own)) else local[:, lay.sel]
+        every = lay.sel == list(range(n_own))
+        idx = None if every else lay.sel_index(dev)
         n_me, o = len(lay.sel), 0
         for r in range(world):
             if lay.fsend[r]:
                 c, L = cols[r]
-                send[o:o + lay.fsend[r]].view(nb, n_me, L).copy_(src[:, :, c:c + L])
+                dst = send[o:o + lay.fsend[r]].view(nb, n_me, L)
+                if every:
+                    dst.copy_(local[:, :, c:c + L])
+                else:  # the shipped shards' columns gathered straight into the send block
+                    torch.index_select(local[:, :, c:c + L], 1, idx, out=dst)
             o += lay.fsend[r]
         recv = local.new_empty(sum(lay.frecv))
         _a2a(recv, send, lay.frecv, lay.fsend, world, group)
