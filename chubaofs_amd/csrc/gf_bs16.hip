@@ -8,12 +8,25 @@
 // tile's top, where the other wave of the SIMD covers their latency.  EC16P20L2's fused encode,
 // 64 x 262,144: 131.9 us against 148.6 us for the 16x16-dyadic v_perm kernel (profiles/r04/
 // bs_probe.txt); it issues ~40 % fewer VALU instructions at 2 instead of 4 waves per SIMD.
+// The network takes its inputs in the paired basis (gf_bitslice.hpp bs_pair_basis): each dyadic
+// row pair of the 20 global rows then shares the half over the odd columns, 3262 instead of 3904
+// XOR ops per 32-byte column for the 22 rows.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <mutex>
 
+#if !defined(CFSEC_BS_NET_G)
 #include "bs_net_ec16p20l2.hpp"
+#elif CFSEC_BS_NET_G == 2  // A/B of row-group CSE variants (tools/gen_bs_net.py --group=G)
+#include "bs_net_ec16p20l2_g2.hpp"
+#elif CFSEC_BS_NET_G == 4
+#include "bs_net_ec16p20l2_g4.hpp"
+#elif CFSEC_BS_NET_G == 5
+#include "bs_net_ec16p20l2_g5.hpp"
+#elif CFSEC_BS_NET_G == 10
+#include "bs_net_ec16p20l2_g10.hpp"
+#endif
 #include "gf_bitslice.hpp"
 #include "gf256.hpp"
 #include "gf_launch.hpp"
@@ -81,6 +94,7 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
     __builtin_amdgcn_s_waitcnt(kBsWaitLgkm0);
 #pragma unroll
     for (int i = 0; i < K; ++i) bs_transpose8(&x[8 * i]);
+    if constexpr (Net::Paired) bs_pair_basis<K>(x);
     __builtin_amdgcn_sched_barrier(0);
     prefetch(t + nw < ntiles ? t + nw : t);  // branch-free: nothing sinks below it (the last re-reads)
     __builtin_amdgcn_sched_barrier(0);
@@ -196,6 +210,7 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
 #pragma unroll
     for (int i = 0; i < kBsK; ++i)
       if (CFSEC_BS_SKIPZ == 0 || a.src[i] < kBsK) bs_transpose8(&x[8 * i]);  // a missing slot's zeros need none
+    if constexpr (BsEc16p20l2::Paired) bs_pair_basis<kBsK>(x);
     if constexpr (ND > 0) {
       // 2. syndromes of the stand-ins over the present data (missing slots are zero planes), in
       // bytes: the row's planes transposed back and XOR-ed into the stored copy
@@ -228,14 +243,24 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
         bs_transpose8(d);
 #pragma unroll
         for (int i = 0; i < kBsK; ++i) {
+          // the slot held zero planes; in the paired basis the even slot of its pair holds the
+          // pair's sum, which takes d too (both slots of a pair missing: d_even ^ d_odd there)
+          const int e = BsEc16p20l2::Paired ? (i & ~1) : i;  // folds after the unroll
           if constexpr (CFSEC_BS_INS == 1) {
-            if (i == r.slot[j])  // uniform: one slot's 8 moves
+            if (i == r.slot[j]) {  // uniform: one slot's moves
 #pragma unroll
-              for (int w = 0; w < 8; ++w) x[8 * i + w] = d[w];
+              for (int w = 0; w < 8; ++w) x[8 * e + w] ^= d[w];
+              if (e != i)
+#pragma unroll
+                for (int w = 0; w < 8; ++w) x[8 * i + w] = d[w];
+            }
           } else {
             const uint32_t m = i == r.slot[j] ? ~0u : 0u;
 #pragma unroll
-            for (int w = 0; w < 8; ++w) x[8 * i + w] ^= d[w] & m;
+            for (int w = 0; w < 8; ++w) x[8 * e + w] ^= d[w] & m;
+            if (e != i)
+#pragma unroll
+              for (int w = 0; w < 8; ++w) x[8 * i + w] ^= d[w] & m;
           }
         }
       }

@@ -50,6 +50,13 @@ __device__ __forceinline__ void transpose8(uint32_t* w) {
   for (int i = 0; i < 4; ++i) swapmove(w[i], w[i + 4], 4, 0x0F0F0F0Fu);
 }
 
+// the network header's input basis (tools/gen_bs_net.py --paired): even rows' planes hold the pair's XOR
+__device__ __forceinline__ void pair_basis(uint32_t* x) {
+  if constexpr (cfsec::dev::kBsEc16p20l2Paired)
+    for (int c = 0; c < K; c += 2)
+      for (int j = 0; j < 8; ++j) x[8 * c + j] ^= x[8 * (c + 1) + j];
+}
+
 __device__ __forceinline__ u32x4 ld16nt(const uint8_t* p) {
   return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
 }
@@ -71,6 +78,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
   }
 #pragma unroll
   for (int c = 0; c < K; ++c) transpose8(&x[8 * c]);
+  pair_basis(x);
   cfsec::dev::bs_net_ec16p20l2(x, [&](int r, uint32_t (&o)[8]) {
     transpose8(o);
     uint8_t* p = row0 + (size_t)(K + r) * S + off;
@@ -128,6 +136,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     uint8_t* row0 = base + (size_t)stripe * ROWS * S;
 #pragma unroll
     for (int c = 0; c < K; ++c) transpose8(&x[8 * c]);
+    pair_basis(x);
     cfsec::dev::bs_net_ec16p20l2(x, [&](int r, uint32_t (&o)[8]) {
       transpose8(o);
       uint8_t* p = row0 + (size_t)(K + r) * S + off;
@@ -190,6 +199,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     for (int c = 0; c < kHalfRows; ++c) transpose8(&x[8 * c]);
 #pragma unroll
     for (int c = kHalfRows; c < K; ++c) transpose8(&x[8 * c]);
+    pair_basis(x);
     __builtin_amdgcn_sched_barrier(0);
     prefetch(t + nw < ntiles ? t + nw : t);  // branch-free (the last tile re-reads itself): no code sinks past it
     __builtin_amdgcn_sched_barrier(0);

@@ -140,6 +140,9 @@ __device__ __forceinline__ void solve(const RepairArgs& a, uint32_t (&x)[128], u
       const uint32_t m = i == a.slot[j] ? ~0u : 0u;
 #pragma unroll
       for (int w = 0; w < 8; ++w) x[8 * i + w] ^= d[j][w] & m;
+      if (cfsec::dev::kBsEc16p20l2Paired && !(i & 1))  // paired basis: an odd slot's d joins its pair's sum too
+#pragma unroll
+        for (int w = 0; w < 8; ++w) x[8 * i + w] ^= d[j][w] & (i + 1 < 16 && a.slot[j] == i + 1 ? ~0u : 0u);
     }
   }
 }
@@ -179,6 +182,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < K; ++i) transpose8(&x[8 * i]);
+    if constexpr (cfsec::dev::kBsEc16p20l2Paired)  // the network header's paired basis
+      for (int c = 0; c < K; c += 2)
+        for (int j = 0; j < 8; ++j) x[8 * c + j] ^= x[8 * (c + 1) + j];
     // 1-3: syndromes and the missing data rows
     uint8_t* mrow[4];
     if constexpr (ND > 0) {
@@ -247,6 +253,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     x[8 * c + 4] = q.x; x[8 * c + 5] = q.y; x[8 * c + 6] = q.z; x[8 * c + 7] = q.w;
     transpose8(&x[8 * c]);
   }
+  if constexpr (cfsec::dev::kBsEc16p20l2Paired)
+    for (int c = 0; c < K; c += 2)
+      for (int j = 0; j < 8; ++j) x[8 * c + j] ^= x[8 * (c + 1) + j];
   cfsec::dev::bs_net_ec16p20l2(x, [&](int r, uint32_t (&o)[8]) {
     transpose8(o);
     uint8_t* p = row0 + (size_t)(K + r) * S + off;

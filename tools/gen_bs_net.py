@@ -15,7 +15,7 @@ the inverse of its top k rows, reedsolomon.go:220-244) and of the CubeFS local r
 checks its engine's coefficients against these constants before it takes the network
 (gf_bs16.hip), and the probes tools/bs_probe.hip / bs_repair_probe.hip use it too.
 
-  python3 tools/gen_bs_net.py ec16p20l2 > chubaofs_amd/csrc/bs_net_ec16p20l2.hpp
+  python3 tools/gen_bs_net.py ec16p20l2 --paired > chubaofs_amd/csrc/bs_net_ec16p20l2.hpp
   python3 tools/gen_bs_net.py ec15p12 | ec12p9   (measured, not shipped: profiles/r04/bsk_ab.txt)
 """
 import sys
@@ -122,6 +122,185 @@ def row_network(row):
     return n_in, temps, outs
 
 
+def _paar(B, allowed=None, limit=None):
+    """Greedy Paar on B (outputs x columns, 0/1), appending one column per chosen pair; allowed(B,
+    col) may veto a pair, limit caps the pairs taken.  Returns the new pairs."""
+    temps = []
+    while limit is None or len(temps) < limit:
+        C = B.T @ B
+        np.fill_diagonal(C, 0)
+        picked = None
+        while True:
+            i, j = np.unravel_index(np.argmax(C), C.shape)
+            if C[i, j] < 2:
+                break
+            col = B[:, i] & B[:, j]
+            if allowed is None or allowed(col):
+                picked = (int(i), int(j), col)
+                break
+            C[i, j] = C[j, i] = 0
+        if picked is None:
+            break
+        i, j, col = picked
+        B[:, i] -= col
+        B[:, j] -= col
+        B = np.concatenate([B, col[:, None]], axis=1)
+        temps.append((i, j))
+    return B, temps
+
+
+def group_network(rows, shared=None):
+    """Paar's greedy CSE over the 8 * len(rows) output planes of a group of rows, with pairs shared
+    across the group's rows too (fewer XORs, more temporaries live across the group).  shared caps
+    the pairs used by more than one row (registers live across a row boundary); past it each row
+    continues with its own pairs, which may use the shared ones."""
+    B = np.concatenate([np.concatenate([bitmat(c) for c in row], axis=1) for row in rows], axis=0)
+    n_in = B.shape[1]
+    nr = len(rows)
+    if shared is None:
+        B, temps = _paar(B)
+    else:
+        spans = lambda col: len({o // 8 for o in np.nonzero(col)[0]}) > 1
+        count = [0]
+
+        def allowed(col):
+            if spans(col):
+                if count[0] >= shared:
+                    return False
+                count[0] += 1
+            return True
+        B, temps = _paar(B, allowed)
+        # the pairs a row found only among its own outputs after the cap are still row-private
+    outs = [[int(s) for s in np.nonzero(B[o])[0]] for o in range(B.shape[0])]
+    return n_in, temps, outs
+
+
+def xor_tree(terms):
+    """A balanced tree of 3-input XORs over the terms: (expression, VALU ops)."""
+    if not terms:
+        return "0u", 0
+    ops = 0
+    while len(terms) > 1:
+        nxt = []
+        for i in range(0, len(terms), 3):
+            g = terms[i:i + 3]
+            if len(g) == 3:
+                nxt.append(f"bs_x3({g[0]}, {g[1]}, {g[2]})")
+            elif len(g) == 2:
+                nxt.append(f"({g[0]} ^ {g[1]})")
+            else:
+                nxt.append(g[0])
+            ops += len(g) > 1
+        terms = nxt
+    return terms[0], ops
+
+
+def emit_group(name, gi, r0, rows, nx, lines):
+    """Rows r0 .. r0 + len(rows) - 1 as one function with the pairs shared across them; a row
+    whose index is >= NR is dropped at compile time (its private temporaries die as dead code)."""
+    n_in, temps, outs = group_network(rows, SHARED)
+    tname = lambda s_: f"x[{s_}]" if s_ < n_in else f"t{s_ - n_in}"
+    done = set()
+    body = []
+
+    def need(s_):
+        if s_ < n_in or s_ in done:
+            return
+        a_, b_ = temps[s_ - n_in]
+        need(a_)
+        need(b_)
+        done.add(s_)
+        body.append(f"  const uint32_t {tname(s_)} = {tname(a_)} ^ {tname(b_)};")
+
+    ops = len(temps)
+    for q in range(len(rows)):
+        r = r0 + q
+        body.append(f"  uint32_t o{q}[8];")
+        for o in range(8):
+            sig = outs[8 * q + o]
+            for s_ in sig:
+                need(s_)
+            expr, n = xor_tree([tname(s_) for s_ in sig])
+            ops += n
+            body.append(f"  o{q}[{o}] = {expr};")
+        body.append(f"  if constexpr ({r} < NR) {{")
+        body.append(f"    emit({r}, o{q});")
+        if BARRIER:
+            body.append("    __builtin_amdgcn_sched_barrier(0);")
+        body.append("  }")
+    lines.append(f"// rows {r0}..{r0 + len(rows) - 1}: {len(temps)} shared pairs, {ops} VALU ops per 32-byte column")
+    lines.append("template <int NR, class Emit>")
+    lines.append(f"__device__ __forceinline__ void bs_grp_{name}_{gi}(const uint32_t (&x)[{nx}], Emit&& emit) {{")
+    lines += body
+    lines.append("}")
+    return ops
+
+
+def paired_row(row):
+    """A row's coefficients in the paired basis: inputs (u_p = x_2p ^ x_2p+1, x_2p+1), so
+    c x_2p + d x_2p+1 = c u_p + (c ^ d) x_2p+1."""
+    out = []
+    for p in range(0, len(row), 2):
+        out += [row[p], row[p] ^ row[p + 1]]
+    return out
+
+
+def half_network(coefs, parity, prefix, body, ops_out, extra=None):
+    """sum_p coefs[p] * plane set p, the plane set p being x[8 (2p + parity) + j]; Paar per output
+    block; extra[j] (an expression) joins output j's XOR tree.  Appends the code to body and returns
+    the 8 output expressions."""
+    n_in, temps, outs = row_network(list(coefs))
+    xi = lambda s_: f"x[{8 * (2 * (s_ // 8) + parity) + s_ % 8}]"
+    tname = lambda s_: xi(s_) if s_ < n_in else f"{prefix}{s_ - n_in}"
+    done = set()
+
+    def need(s_):
+        if s_ < n_in or s_ in done:
+            return
+        a_, b_ = temps[s_ - n_in]
+        need(a_)
+        need(b_)
+        done.add(s_)
+        body.append(f"  const uint32_t {tname(s_)} = {tname(a_)} ^ {tname(b_)};")
+
+    exprs = []
+    ops = len(temps)
+    for o, sig in enumerate(outs):
+        for s_ in sig:
+            need(s_)
+        terms = [tname(s_) for s_ in sig] + ([extra[o]] if extra else [])
+        e, n = xor_tree(terms)
+        ops += n
+        exprs.append(e)
+    ops_out.append(ops)
+    return exprs
+
+
+def emit_pair(name, q, rows, nx, lines):
+    """Rows 2q and 2q + 1 of a dyadic pair (row 2q+1 = row 2q with columns c and c^1 swapped) in
+    the paired basis: out_2q = A(u) ^ B(x_odd), out_2q+1 = A'(u) ^ B(x_odd) with B shared."""
+    r = 2 * q
+    a, b = rows[r], rows[r + 1]
+    assert all(b[c] == a[c ^ 1] for c in range(len(a))), "not a dyadic row pair"
+    body = []
+    ops = []
+    bexp = half_network([a[2 * p] ^ a[2 * p + 1] for p in range(len(a) // 2)], 1, "tb", body, ops)
+    body.append("  uint32_t b[8];")
+    body += [f"  b[{j}] = {e};" for j, e in enumerate(bexp)]
+    bref = [f"b[{j}]" for j in range(8)]
+    e0 = half_network([a[2 * p] for p in range(len(a) // 2)], 0, "ta", body, ops, bref)
+    body += [f"  o0[{j}] = {e};" for j, e in enumerate(e0)]
+    e1 = half_network([a[2 * p + 1] for p in range(len(a) // 2)], 0, "tc", body, ops, bref)
+    body += [f"  o1[{j}] = {e};" for j, e in enumerate(e1)]
+    total = sum(ops)
+    lines.append(f"// rows {r}, {r + 1} (a dyadic pair): {total} VALU ops per 32-byte column")
+    lines.append("template <>")
+    lines.append(f"__device__ __forceinline__ void bs_pair_{name}<{q}>(const uint32_t (&x)[{nx}], uint32_t (&o0)[8], uint32_t (&o1)[8]) {{")
+    lines += body
+    lines.append("}")
+    return total
+
+
 def emit_row(name, r, row, lines):
     """Row r's network as a specialization bs_row_<name><r>(x, o)."""
     n_in, temps, outs = row_network(row)
@@ -172,6 +351,9 @@ def emit_row(name, r, row, lines):
 
 
 BARRIER = "--no-barrier" not in sys.argv
+GROUP = next((int(a.split("=")[1]) for a in sys.argv if a.startswith("--group=")), 1)
+PAIRED = "--paired" in sys.argv
+SHARED = next((int(a.split("=")[1]) for a in sys.argv if a.startswith("--shared=")), None)
 
 CODES = {
     # name: (title, rows, note on NR)
@@ -190,14 +372,37 @@ def main():
     nx = 8 * k
     lines = []
     total = 0
-    for r, row in enumerate(rows):
-        total += emit_row(code, r, row, lines)
+    npairs = 0
+    if PAIRED:
+        # rows in the paired basis; the leading dyadic row pairs share their odd-column half
+        prow = [paired_row(row) for row in rows]
+        while 2 * npairs + 1 < m and all(rows[2 * npairs + 1][c] == rows[2 * npairs][c ^ 1] for c in range(k)):
+            npairs += 1
+        for r, row in enumerate(prow):
+            emit_row(code, r, row, lines)
+        plines = []
+        for q in range(npairs):
+            total += emit_pair(code, q, rows, nx, plines)
+        rest = 0
+        for r in range(2 * npairs, m):
+            n_in, temps, outs = row_network(prow[r])
+            rest += len(temps) + sum(xor_tree(["a"] * len(sg))[1] for sg in outs)
+        total += rest
+    else:
+        for r, row in enumerate(rows):
+            total += emit_row(code, r, row, lines)
     Name = "Bs" + code[0].upper() + code[1:]
     out = sys.stdout
     out.write(f"// bs_net_{code}.hpp -- GENERATED by tools/gen_bs_net.py {code}; do not edit.\n")
     out.write(f"//\n// {title} as a\n")
     out.write(f"// bit-sliced XOR network: {total} VALU ops per 32-byte column for all {m} rows.\n")
-    out.write("// x[8c + j]: bit plane j of data row c; o: the output row's 8 planes.\n")
+    if PAIRED:
+        out.write(f"// Paired basis (k{Name}Paired): x[8c + j] is bit plane j of data row c for odd c and of\n"
+                  "// (row c ^ row c + 1) for even c -- the caller XORs each odd column's planes into the even\n"
+                  f"// one's after the transposes.  Rows 0..{2 * npairs - 1} come as dyadic pairs sharing the odd-column half\n"
+                  "// (bs_pair_*); every row also as a single network in that basis (bs_row_*).\n")
+    else:
+        out.write("// x[8c + j]: bit plane j of data row c; o: the output row's 8 planes.\n")
     out.write("#pragma once\n#include <cstdint>\n\nnamespace cfsec {\nnamespace dev {\n\n")
     out.write(f"constexpr uint8_t k{Name}Rows[{m}][{k}] = {{\n")
     for row in rows:
@@ -206,16 +411,46 @@ def main():
     out.write("#ifndef CFSEC_BS_X3\n#define CFSEC_BS_X3\n")
     out.write("__device__ __forceinline__ uint32_t bs_x3(uint32_t a, uint32_t b, uint32_t c) {\n"
               "  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);\n}\n#endif\n\n")
+    out.write(f"constexpr bool k{Name}Paired = {'true' if PAIRED else 'false'};\n\n")
     out.write(f"template <int R>\n__device__ __forceinline__ void bs_row_{code}(const uint32_t (&x)[{nx}], uint32_t (&o)[8]);\n\n")
     out.write("\n".join(lines) + "\n\n")
-    out.write(f"// rows 0 .. NR-1 in order ({nr_note}); emit(r, o) consumes row r's planes\n")
-    out.write(f"template <int NR = {m}, class Emit>\n__device__ __forceinline__ void bs_net_{code}(const uint32_t (&x)[{nx}], Emit&& emit) {{\n")
-    for r in range(m):
-        out.write(f"  if constexpr ({r} < NR) {{\n    uint32_t o[8];\n    bs_row_{code}<{r}>(x, o);\n    emit({r}, o);\n")
-        if BARRIER:
-            out.write("    __builtin_amdgcn_sched_barrier(0);\n")
-        out.write("  }\n")
-    out.write("}\n\n")
+    if PAIRED:
+        out.write(f"template <int Q>\n__device__ __forceinline__ void bs_pair_{code}(const uint32_t (&x)[{nx}], uint32_t (&o0)[8], uint32_t (&o1)[8]);\n\n")
+        out.write("\n".join(plines) + "\n\n")
+        out.write(f"// rows 0 .. NR-1 in order ({nr_note}); emit(r, o) consumes row r's planes\n")
+        out.write(f"template <int NR = {m}, class Emit>\n__device__ __forceinline__ void bs_net_{code}(const uint32_t (&x)[{nx}], Emit&& emit) {{\n")
+        bar = "    __builtin_amdgcn_sched_barrier(0);\n" if BARRIER else ""
+        for q in range(npairs):
+            out.write(f"  if constexpr ({2 * q} < NR) {{\n    uint32_t o0[8], o1[8];\n    bs_pair_{code}<{q}>(x, o0, o1);\n"
+                      f"    emit({2 * q}, o0);\n{bar}    if constexpr ({2 * q + 1} < NR) emit({2 * q + 1}, o1);\n{bar}  }}\n")
+        for r in range(2 * npairs, m):
+            out.write(f"  if constexpr ({r} < NR) {{\n    uint32_t o[8];\n    bs_row_{code}<{r}>(x, o);\n    emit({r}, o);\n{bar}  }}\n")
+        out.write("}\n\n")
+    if PAIRED:
+        pass
+    elif GROUP > 1:
+        glines = []
+        gtotal = 0
+        groups = [(r0, rows[r0:r0 + GROUP]) for r0 in range(0, m, GROUP)]
+        for gi, (r0, grows) in enumerate(groups):
+            gtotal += emit_group(code, gi, r0, grows, nx, glines)
+        out.write(f"// the full network with pairs shared inside groups of {GROUP} rows: {gtotal} VALU ops per\n"
+                  f"// 32-byte column (rows alone: {total})\n")
+        out.write("\n".join(glines) + "\n\n")
+        out.write(f"// rows 0 .. NR-1 in order ({nr_note}); emit(r, o) consumes row r's planes\n")
+        out.write(f"template <int NR = {m}, class Emit>\n__device__ __forceinline__ void bs_net_{code}(const uint32_t (&x)[{nx}], Emit&& emit) {{\n")
+        for gi, (r0, grows) in enumerate(groups):
+            out.write(f"  if constexpr ({r0} < NR) bs_grp_{code}_{gi}<NR>(x, emit);\n")
+        out.write("}\n\n")
+    else:
+        out.write(f"// rows 0 .. NR-1 in order ({nr_note}); emit(r, o) consumes row r's planes\n")
+        out.write(f"template <int NR = {m}, class Emit>\n__device__ __forceinline__ void bs_net_{code}(const uint32_t (&x)[{nx}], Emit&& emit) {{\n")
+        for r in range(m):
+            out.write(f"  if constexpr ({r} < NR) {{\n    uint32_t o[8];\n    bs_row_{code}<{r}>(x, o);\n    emit({r}, o);\n")
+            if BARRIER:
+                out.write("    __builtin_amdgcn_sched_barrier(0);\n")
+            out.write("  }\n")
+        out.write("}\n\n")
     out.write("// row r chosen at run time (uniform)\n")
     out.write(f"__device__ __forceinline__ void bs_row_{code}_rt(int r, const uint32_t (&x)[{nx}], uint32_t (&o)[8]) {{\n  switch (r) {{\n")
     for r in range(m):
@@ -223,6 +458,7 @@ def main():
     out.write("    default: for (int j = 0; j < 8; ++j) o[j] = 0u;\n  }\n}\n\n")
     out.write(f"// the network as a type for the K-input kernels (gf_bs16.hip)\n")
     out.write(f"struct {Name} {{\n  static constexpr int K = {k}, M = {m};\n")
+    out.write(f"  static constexpr bool Paired = k{Name}Paired;  // inputs in the paired basis (see the top)\n")
     out.write(f"  static const uint8_t* rows() {{ return &k{Name}Rows[0][0]; }}\n")
     out.write(f"  template <int NR, class Emit>\n  __device__ static __forceinline__ void net(const uint32_t (&x)[{nx}], Emit&& emit) {{\n")
     out.write(f"    bs_net_{code}<NR>(x, static_cast<Emit&&>(emit));\n  }}\n}};\n\n")
