@@ -16,17 +16,7 @@
 #include <algorithm>
 #include <mutex>
 
-#if !defined(CFSEC_BS_NET_G)
 #include "bs_net_ec16p20l2.hpp"
-#elif CFSEC_BS_NET_G == 2  // A/B of row-group CSE variants (tools/gen_bs_net.py --group=G)
-#include "bs_net_ec16p20l2_g2.hpp"
-#elif CFSEC_BS_NET_G == 4
-#include "bs_net_ec16p20l2_g4.hpp"
-#elif CFSEC_BS_NET_G == 5
-#include "bs_net_ec16p20l2_g5.hpp"
-#elif CFSEC_BS_NET_G == 10
-#include "bs_net_ec16p20l2_g10.hpp"
-#endif
 #include "gf_bitslice.hpp"
 #include "gf256.hpp"
 #include "gf_launch.hpp"
