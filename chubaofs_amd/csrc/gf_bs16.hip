@@ -101,7 +101,7 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
 //      parities' syndromes, = A d with A the nd x nd block of the parity matrix at those rows and
 //      the missing columns;
 //   3. d = A^-1 s in byte form (v_perm products, tables from the host), stored, transposed and
-//      masked into their (zero) slots -- no register indexing;
+//      written into their (zero) slots and the paired basis' pair sums -- no register indexing;
 //   4. the full network: each parity (and extra) row stored (pstore), compared with its stored copy
 //      through a 3-deep LDS ring filled by global_load_lds 2 compared rows ahead (pcmp; a mismatch
 //      sets the stripe's flag), or skipped (the stand-ins, consistent by construction).
