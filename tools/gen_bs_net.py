@@ -15,7 +15,7 @@ the inverse of its top k rows, reedsolomon.go:220-244) and of the CubeFS local r
 checks its engine's coefficients against these constants before it takes the network
 (gf_bs16.hip), and the probes tools/bs_probe.hip / bs_repair_probe.hip use it too.
 
-  python3 tools/gen_bs_net.py ec16p20l2 --paired > chubaofs_amd/csrc/bs_net_ec16p20l2.hpp
+  python3 tools/gen_bs_net.py ec16p20l2 --paired --joint > chubaofs_amd/csrc/bs_net_ec16p20l2.hpp
   python3 tools/gen_bs_net.py ec15p12 | ec12p9   (measured, not shipped: profiles/r04/bsk_ab.txt)
 """
 import sys
@@ -248,8 +248,16 @@ def paired_row(row):
 def half_network(coefs, parity, prefix, body, ops_out, extra=None):
     """sum_p coefs[p] * plane set p, the plane set p being x[8 (2p + parity) + j]; Paar per output
     block; extra[j] (an expression) joins output j's XOR tree.  Appends the code to body and returns
-    the 8 output expressions."""
-    n_in, temps, outs = row_network(list(coefs))
+    the 8 output expressions.  coefs may also be a list of coefficient lists: one Paar over all
+    their outputs (pairs shared between them), 8 expressions per list, concatenated."""
+    if coefs and isinstance(coefs[0], (list, tuple)):
+        B = np.concatenate([np.concatenate([bitmat(c) for c in cl], axis=1) for cl in coefs], axis=0)
+        n_in = B.shape[1]
+        B, temps = _paar(B)
+        outs = [[int(s) for s in np.nonzero(B[o])[0]] for o in range(B.shape[0])]
+        extra = (extra or []) * len(coefs) if extra else None
+    else:
+        n_in, temps, outs = row_network(list(coefs))
     xi = lambda s_: f"x[{8 * (2 * (s_ // 8) + parity) + s_ % 8}]"
     tname = lambda s_: xi(s_) if s_ < n_in else f"{prefix}{s_ - n_in}"
     done = set()
@@ -288,10 +296,16 @@ def emit_pair(name, q, rows, nx, lines):
     body.append("  uint32_t b[8];")
     body += [f"  b[{j}] = {e};" for j, e in enumerate(bexp)]
     bref = [f"b[{j}]" for j in range(8)]
-    e0 = half_network([a[2 * p] for p in range(len(a) // 2)], 0, "ta", body, ops, bref)
-    body += [f"  o0[{j}] = {e};" for j, e in enumerate(e0)]
-    e1 = half_network([a[2 * p + 1] for p in range(len(a) // 2)], 0, "tc", body, ops, bref)
-    body += [f"  o1[{j}] = {e};" for j, e in enumerate(e1)]
+    if JOINT:  # A and A' from one Paar: their pairs shared too
+        e01 = half_network([[a[2 * p] for p in range(len(a) // 2)], [a[2 * p + 1] for p in range(len(a) // 2)]],
+                           0, "ta", body, ops, bref)
+        body += [f"  o0[{j}] = {e};" for j, e in enumerate(e01[:8])]
+        body += [f"  o1[{j}] = {e};" for j, e in enumerate(e01[8:])]
+    else:
+        e0 = half_network([a[2 * p] for p in range(len(a) // 2)], 0, "ta", body, ops, bref)
+        body += [f"  o0[{j}] = {e};" for j, e in enumerate(e0)]
+        e1 = half_network([a[2 * p + 1] for p in range(len(a) // 2)], 0, "tc", body, ops, bref)
+        body += [f"  o1[{j}] = {e};" for j, e in enumerate(e1)]
     total = sum(ops)
     lines.append(f"// rows {r}, {r + 1} (a dyadic pair): {total} VALU ops per 32-byte column")
     lines.append("template <>")
@@ -353,6 +367,7 @@ def emit_row(name, r, row, lines):
 BARRIER = "--no-barrier" not in sys.argv
 GROUP = next((int(a.split("=")[1]) for a in sys.argv if a.startswith("--group=")), 1)
 PAIRED = "--paired" in sys.argv
+JOINT = "--joint" in sys.argv
 SHARED = next((int(a.split("=")[1]) for a in sys.argv if a.startswith("--shared=")), None)
 
 CODES = {
@@ -384,9 +399,12 @@ def main():
         for q in range(npairs):
             total += emit_pair(code, q, rows, nx, plines)
         rest = 0
-        for r in range(2 * npairs, m):
-            n_in, temps, outs = row_network(prow[r])
-            rest += len(temps) + sum(xor_tree(["a"] * len(sg))[1] for sg in outs)
+        if JOINT and m - 2 * npairs > 1:  # the rows after the pairs as one group (pairs shared)
+            rest = emit_group(code, 0, 2 * npairs, prow[2 * npairs:], nx, plines)
+        else:
+            for r in range(2 * npairs, m):
+                n_in, temps, outs = row_network(prow[r])
+                rest += len(temps) + sum(xor_tree(["a"] * len(sg))[1] for sg in outs)
         total += rest
     else:
         for r, row in enumerate(rows):
@@ -423,8 +441,11 @@ def main():
         for q in range(npairs):
             out.write(f"  if constexpr ({2 * q} < NR) {{\n    uint32_t o0[8], o1[8];\n    bs_pair_{code}<{q}>(x, o0, o1);\n"
                       f"    emit({2 * q}, o0);\n{bar}    if constexpr ({2 * q + 1} < NR) emit({2 * q + 1}, o1);\n{bar}  }}\n")
-        for r in range(2 * npairs, m):
-            out.write(f"  if constexpr ({r} < NR) {{\n    uint32_t o[8];\n    bs_row_{code}<{r}>(x, o);\n    emit({r}, o);\n{bar}  }}\n")
+        if JOINT and m - 2 * npairs > 1:
+            out.write(f"  if constexpr ({2 * npairs} < NR) bs_grp_{code}_0<NR>(x, emit);\n")
+        else:
+            for r in range(2 * npairs, m):
+                out.write(f"  if constexpr ({r} < NR) {{\n    uint32_t o[8];\n    bs_row_{code}<{r}>(x, o);\n    emit({r}, o);\n{bar}  }}\n")
         out.write("}\n\n")
     if PAIRED:
         pass
