@@ -826,13 +826,16 @@ def test_ec16p20l2_tasklet_bitsliced_repair(S):
     [bids, 38, S] buffer, pairs of bids per erasure pattern so every group is one affine run; S =
     264,240 leaves a 48-byte row tail to the dyadic kernel): nothing missing but parities ({16, 17}),
     one and two missing data rows ({3, 20}, {0, 1, 16, 17}), the same with a corrupted compared parity
-    and a corrupted data row (Verify must fail), and three missing data rows (the dyadic kernel) --
-    statuses and every shard against the reference loop restated by the ec oracle."""
+    and a corrupted data row (Verify must fail), and three missing data rows (the dyadic kernel);
+    the paired basis' slot cases -- one even slot ({6, 25}), even + odd in different pairs ({4, 11}),
+    two even ({8, 14}), two odd ({7, 13}) -- statuses and every shard against the reference loop
+    restated by the ec oracle."""
     mode = cm.EC16P20L2
     t = cm.GetTactic(mode)
     n = t.N + t.M + t.L
     enc = ec_new(mode)
-    patterns = [[16, 17], [3, 20], [0, 1, 16, 17], [0, 1, 16, 17], [5, 30], [0, 1, 2, 16]]
+    patterns = [[16, 17], [3, 20], [0, 1, 16, 17], [0, 1, 16, 17], [5, 30], [0, 1, 2, 16],
+                [6, 25], [4, 11], [8, 14], [7, 13]]
     nb = 2 * len(patterns)
     buf = torch.empty((nb, n, S), dtype=torch.uint8, device="cuda")
     assert buf.data_ptr() % 16 == 0
@@ -849,6 +852,8 @@ def test_ec16p20l2_tasklet_bitsliced_repair(S):
             work[j][rnd.randrange(S)] ^= 1 + rnd.randrange(255)
         if b == 9:  # a local parity corrupted
             work[37][rnd.randrange(S)] ^= 0x11
+        if b == 17:  # the present partner of a missing even slot (9 beside 8) corrupted
+            work[9][rnd.randrange(S)] ^= 0x5A
         want.append(sequential(enc, [w.copy() for w in work], bad))
         buf[b] = torch.from_numpy(np.stack(work))
         bads.append(bad)
