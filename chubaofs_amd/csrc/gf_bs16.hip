@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstddef>
 #include <mutex>
 
 #include "bs_net_ec16p20l2.hpp"
@@ -38,7 +39,27 @@ constexpr int kBsK = 16, kBsPrefetch = 8, kBsWaves = 8;
 #ifndef CFSEC_BS_REP_LDNT
 #define CFSEC_BS_REP_LDNT 1
 #endif
+// row pointers (and the repair's row masks) re-read where used: the repair 1-2 % faster, the encode
+// no faster (profiles/r04/bs_reload_ab.txt), A/B
+#ifndef CFSEC_BS_REP_RELOAD
+#define CFSEC_BS_REP_RELOAD 1
+#endif
+#ifndef CFSEC_BS_ENC_RELOAD
+#define CFSEC_BS_ENC_RELOAD 0
+#endif
 constexpr int kBsEncGlds = CFSEC_BS_ENC_GLDS, kBsRepGlds = CFSEC_BS_REP_GLDS;
+
+// Row pointer j of the kernels' GfArgs (their first argument, at offset 0 of the argument segment)
+// by a scalar load whose offset the compiler cannot see through: the kernels name up to 40 rows,
+// and held across the tile loop their pointers (with the per-row conditions) outgrow the SGPRs --
+// the spilled ones come back through v_readlane, ~240 per tile in the repair kernel.  Re-read
+// where used, they cost a scalar-cache load each.
+__device__ __forceinline__ const uint8_t* bs_kernarg_ptr(uint32_t j) {
+  typedef const __attribute__((address_space(4))) uint64_t ku64;
+  uint32_t w = __builtin_amdgcn_readfirstlane((uint32_t)(offsetof(dev::GfArgs, ptr) / 8) + j);
+  asm volatile("" : "+s"(w));
+  return reinterpret_cast<const uint8_t*>(((ku64*)__builtin_amdgcn_kernarg_segment_ptr())[w]);
+}
 constexpr bool kBsEncLdNt = CFSEC_BS_ENC_LDNT, kBsRepLdNt = CFSEC_BS_REP_LDNT;
 
 // Encode: Net's K inputs -> its first M rows (K <= 16: 8 K input planes in registers)
@@ -55,11 +76,16 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
   uint8_t* pre = lds[wave];
   const uint32_t nw = gridDim.x * kBsWaves;
   // row i of stripe s (inputs 0..K-1, then outputs), at the lane's first byte of column tile c
+  // row pointer j of the argument block, re-read where used (bs_kernarg_ptr)
+  const auto ptr_at = [&](uint32_t j) -> const uint8_t* {
+    if constexpr (CFSEC_BS_ENC_RELOAD) return bs_kernarg_ptr(j);
+    else return a.ptr[j];
+  };
   const auto row = [&](uint32_t s, int i, uint32_t c) -> uint8_t* {
     const uint8_t* base;
-    if (i < K) base = a.sstride ? a.ptr[i] + (int64_t)s * a.sstride : a.ptr[(size_t)s * K + i];
-    else base = a.sstride ? a.ptr[K + (i - K)] + (int64_t)s * a.sstride
-                          : a.ptr[(size_t)a.tab * K + (size_t)s * M + (i - K)];
+    if (i < K) base = a.sstride ? ptr_at(i) + (int64_t)s * a.sstride : ptr_at(s * K + i);
+    else base = a.sstride ? ptr_at(K + (i - K)) + (int64_t)s * a.sstride
+                          : ptr_at(a.tab * K + s * M + (i - K));
     return const_cast<uint8_t*>(base) + (size_t)c * kBsWaveBytes + lane * 16;
   };
   const auto prefetch = [&](uint32_t t) {
@@ -164,11 +190,18 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
   if (blockIdx.x == 0)  // the checksum words the pass after this one accumulates into
     for (uint32_t i = threadIdx.x; i < a.nzw; i += blockDim.x) a.zw[i] = 0u;
   // affine batches only (the launcher checks): row i of stripe s at ptr[i] + s * sstride
+  const auto row_ptr = [&](int i) -> const uint8_t* {
+    if constexpr (CFSEC_BS_REP_RELOAD) {
+      return bs_kernarg_ptr(i);
+    } else {
+      return a.ptr[i];
+    }
+  };
   const auto input = [&](uint32_t s, int i, uint32_t c) -> const uint8_t* {
-    return a.ptr[i] + (int64_t)s * a.sstride + (size_t)c * kBsWaveBytes + lane * 16;
+    return row_ptr(i) + (int64_t)s * a.sstride + (size_t)c * kBsWaveBytes + lane * 16;
   };
   const auto output = [&](uint32_t s, int o, uint32_t c) -> uint8_t* {
-    return const_cast<uint8_t*>(a.ptr[kBsK + o]) + (int64_t)s * a.sstride + (size_t)c * kBsWaveBytes + lane * 16;
+    return const_cast<uint8_t*>(row_ptr(kBsK + o)) + (int64_t)s * a.sstride + (size_t)c * kBsWaveBytes + lane * 16;
   };
   const auto slot_ptr = [&](uint32_t s, int i, uint32_t c) -> const uint8_t* {  // data row i, or zeros
     const int src = a.src[i];
@@ -197,9 +230,15 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
     for (int i = 0; i < kRepPrefetch; ++i) bs_lds_row(pre + i * kBsWaveBytes, lane, &x[8 * i]);
     __builtin_amdgcn_s_waitcnt(kBsWaitLgkm0);
     __builtin_amdgcn_sched_barrier(0);
+    // which slots are present, one bit each, re-read per tile (opaque) like the row masks
+    uint32_t present = 0;
+#pragma unroll
+    for (int i = 0; i < kBsK; ++i) present |= (a.src[i] < kBsK ? 1u : 0u) << i;
+    present = __builtin_amdgcn_readfirstlane(present);
+    if constexpr (CFSEC_BS_REP_RELOAD) asm volatile("" : "+s"(present));
 #pragma unroll
     for (int i = 0; i < kBsK; ++i)
-      if (CFSEC_BS_SKIPZ == 0 || a.src[i] < kBsK) bs_transpose8(&x[8 * i]);  // a missing slot's zeros need none
+      if (CFSEC_BS_SKIPZ == 0 || (present >> i & 1)) bs_transpose8(&x[8 * i]);  // a missing slot's zeros need none
     if constexpr (BsEc16p20l2::Paired) bs_pair_basis<kBsK>(x);
     if constexpr (ND > 0) {
       // 2. syndromes of the stand-ins over the present data (missing slots are zero planes), in
@@ -212,9 +251,12 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
 #pragma unroll
         for (int w = 0; w < 8; ++w) y[q][w] ^= o[w];
       }
-      // 3. d = A^-1 s, stored, into its slot
+      // 3. d = A^-1 s, stored, into its slot (the slot bytes re-read per tile, as the row masks)
+      uint32_t slots = (uint32_t)r.slot[0] | (uint32_t)r.slot[1] << 8 | (uint32_t)r.slot[2] << 16 | (uint32_t)r.slot[3] << 24;
+      if constexpr (CFSEC_BS_REP_RELOAD) asm volatile("" : "+s"(slots));
 #pragma unroll
       for (int j = 0; j < ND; ++j) {
+        const uint32_t slot_j = slots >> (8 * j) & 0xFFu;
         uint32_t d[8];
 #pragma unroll
         for (int w = 0; w < 8; ++w) d[w] = 0u;
@@ -237,7 +279,7 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
           // pair's sum, which takes d too (both slots of a pair missing: d_even ^ d_odd there)
           const int e = BsEc16p20l2::Paired ? (i & ~1) : i;  // folds after the unroll
           if constexpr (CFSEC_BS_INS == 1) {
-            if (i == r.slot[j]) {  // uniform: one slot's moves
+            if (i == slot_j) {  // uniform: one slot's moves
 #pragma unroll
               for (int w = 0; w < 8; ++w) x[8 * e + w] ^= d[w];
               if (e != i)
@@ -245,7 +287,7 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
                 for (int w = 0; w < 8; ++w) x[8 * i + w] = d[w];
             }
           } else {
-            const uint32_t m = i == r.slot[j] ? ~0u : 0u;
+            const uint32_t m = i == slot_j ? ~0u : 0u;
 #pragma unroll
             for (int w = 0; w < 8; ++w) x[8 * e + w] ^= d[w] & m;
             if (e != i)
@@ -271,11 +313,15 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
     prefetch(t + nw < ntiles ? t + nw : t);
     __builtin_amdgcn_sched_barrier(0);
     uint32_t diff = 0;
+    // the row masks re-read per tile (opaque): hoisted, their 44 per-row conditions outlive the
+    // SGPRs as 64-bit lane masks and come back through v_readlane
+    uint32_t pst = a.pstore, pcm = a.pcmp;
+    if constexpr (CFSEC_BS_REP_RELOAD) asm volatile("" : "+s"(pst), "+s"(pcm));
     bs_net_ec16p20l2<M>(x, [&](int p, uint32_t (&o)[8]) {
-      if (a.pstore >> p & 1) {
+      if (pst >> p & 1) {
         bs_transpose8(o);
         bs_st_rebuilt(output(s, ND + p, c), o);
-      } else if (a.pcmp >> p & 1) {
+      } else if (pcm >> p & 1) {
         // this row's copy; the next compared row's may still fly (anything issued between them is
         // waited for too: retirement is in order)
         if (q_issue - q_read > 1) __builtin_amdgcn_s_waitcnt(bs_waitcnt_vm(2));
