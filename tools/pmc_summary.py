@@ -12,7 +12,7 @@ agg = defaultdict(lambda: defaultdict(list))
 for r in rows:
     agg[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, ctrs in agg.items():
-    short = k.split("(")[0].replace("void ", "")[-70:]
+    short = k.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")[-70:]
     print(short)
     for c, v in sorted(ctrs.items()):
         print(f"    {c:28s} n={len(v):5d} mean={sum(v) / len(v):.4g}")
