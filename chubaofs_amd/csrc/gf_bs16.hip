@@ -178,6 +178,7 @@ __device__ __forceinline__ void bs_mul_acc8(uint32_t* acc, const uint32_t* s0, c
 }
 
 template <int M, int ND>
+// (GfArgs must stay the first parameter: bs_kernarg_ptr reads its ptr[] at offset 0 of the arguments)
 __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2, 2))) void gf_bs16_repair_kernel(
     const dev::GfArgs a, const BsRepairArgs r, uint32_t tiles_per_stripe, uint32_t ntiles) {
   using namespace dev;
