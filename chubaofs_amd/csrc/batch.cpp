@@ -87,12 +87,29 @@ hipError_t launch_group(const Group& g, uint32_t* dflags, hipStream_t s) {
     }
     return true;
   };
-  size_t t0 = 0;
-  while (t0 < nt) {
+  // Runs shorter than kMinRun stripes (separately allocated shards: blobnode's per-vuid buffers)
+  // are not launched one by one -- a launch per stripe leaves most of the GPU idle (C5's tasklet
+  // with every shard at its own address: 64 launches of 16 workgroups, 1.9 ms) -- but gathered into
+  // pointer-table runs, which the launchers split into as many stripes per launch as their argument
+  // block holds.
+  constexpr size_t kMinRun = 4;
+  const auto run_end = [&](size_t t0) {
     size_t t1 = t0 + 1;
     if (t1 < nt) {
       const int64_t d = addr(g.in[t1 * k]) - addr(g.in[t0 * k]);
       while (t1 < nt && d != 0 && stride_ok(t1 - 1, d)) ++t1;
+    }
+    return t1;
+  };
+  size_t t0 = 0;
+  while (t0 < nt) {
+    size_t t1 = run_end(t0);
+    if (t1 - t0 < kMinRun) {  // extend over the following short runs
+      while (t1 < nt) {
+        const size_t t2 = run_end(t1);
+        if (t2 - t1 >= kMinRun) break;
+        t1 = t2;
+      }
     }
     const hipError_t e = launch_group_run(g, t0, t1, dflags, s);
     if (e != hipSuccess) return e;

@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <cstddef>
+#include <cstring>
 #include <mutex>
 
 #include "bs_net_ec16p20l2.hpp"
@@ -140,7 +141,25 @@ struct BsRepairArgs {
   dev::u32x4 t01[16];   // A^-1 product tables, entry j * 4 + q (gf_device.hpp coef_tables layout)
   uint32_t t2[16];
   const uint8_t* zero;  // kBsWaveBytes of zeros
+  const uint8_t* base;  // TAB: row (s, i) at base + the 32-bit offset s * (16 + ND + M) + i of the table
 };
+
+// TAB launches keep their row offsets where a repair launch does not read its GfArgs: from coef to
+// the end of ptr (coef, slen, padding, ptr: the struct's last fields, in that order)
+constexpr size_t kBsTabOff = offsetof(dev::GfArgs, coef);
+static_assert(offsetof(dev::GfArgs, slen) > kBsTabOff && offsetof(dev::GfArgs, ptr) > offsetof(dev::GfArgs, slen) &&
+                  offsetof(dev::GfArgs, ptr) + sizeof(dev::GfArgs::ptr) + 16 > sizeof(dev::GfArgs) && kBsTabOff % 4 == 0,
+              "GfArgs: coef, slen, ptr last");
+static_assert(sizeof(dev::GfArgs) + sizeof(BsRepairArgs) + 8 <= 4096, "repair kernel arguments within 4 KiB");
+constexpr int kBsTabWords = (int)((offsetof(dev::GfArgs, ptr) + sizeof(dev::GfArgs::ptr) - kBsTabOff) / 4);
+
+// word j of the kernel arguments' table area, by an opaque scalar load (as bs_kernarg_ptr)
+__device__ __forceinline__ uint32_t bs_kernarg_u32(uint32_t j) {
+  typedef const __attribute__((address_space(4))) uint32_t ku32;
+  uint32_t w = __builtin_amdgcn_readfirstlane((uint32_t)(kBsTabOff / 4) + j);
+  asm volatile("" : "+s"(w));
+  return ((ku32*)__builtin_amdgcn_kernarg_segment_ptr())[w];
+}
 
 #ifndef CFSEC_BS_PF
 #define CFSEC_BS_PF 7  // slots prefetched into LDS per wave (A/B)
@@ -177,8 +196,9 @@ __device__ __forceinline__ void bs_mul_acc8(uint32_t* acc, const uint32_t* s0, c
              __builtin_amdgcn_perm(0u, t2, s2[w]);
 }
 
-template <int M, int ND>
-// (GfArgs must stay the first parameter: bs_kernarg_ptr reads its ptr[] at offset 0 of the arguments)
+// (GfArgs must stay the first parameter: bs_kernarg_ptr / bs_kernarg_u32 read it at offset 0 of
+// the arguments)
+template <int M, int ND, bool TAB>
 __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2, 2))) void gf_bs16_repair_kernel(
     const dev::GfArgs a, const BsRepairArgs r, uint32_t tiles_per_stripe, uint32_t ntiles) {
   using namespace dev;
@@ -190,19 +210,21 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
   const uint32_t nw = gridDim.x * kBsWaves;
   if (blockIdx.x == 0)  // the checksum words the pass after this one accumulates into
     for (uint32_t i = threadIdx.x; i < a.nzw; i += blockDim.x) a.zw[i] = 0u;
-  // affine batches only (the launcher checks): row i of stripe s at ptr[i] + s * sstride
-  const auto row_ptr = [&](int i) -> const uint8_t* {
-    if constexpr (CFSEC_BS_REP_RELOAD) {
-      return bs_kernarg_ptr(i);
+  // affine batches: row i of stripe s at ptr[i] + s * sstride; TAB: at base + its table offset
+  const auto row_ptr = [&](uint32_t s, int i) -> const uint8_t* {
+    if constexpr (TAB) {
+      return r.base + bs_kernarg_u32(s * (uint32_t)(kBsK + ND + M) + (uint32_t)i);
+    } else if constexpr (CFSEC_BS_REP_RELOAD) {
+      return bs_kernarg_ptr(i) + (int64_t)s * a.sstride;
     } else {
-      return a.ptr[i];
+      return a.ptr[i] + (int64_t)s * a.sstride;
     }
   };
   const auto input = [&](uint32_t s, int i, uint32_t c) -> const uint8_t* {
-    return row_ptr(i) + (int64_t)s * a.sstride + (size_t)c * kBsWaveBytes + lane * 16;
+    return row_ptr(s, i) + (size_t)c * kBsWaveBytes + lane * 16;
   };
   const auto output = [&](uint32_t s, int o, uint32_t c) -> uint8_t* {
-    return const_cast<uint8_t*>(row_ptr(kBsK + o)) + (int64_t)s * a.sstride + (size_t)c * kBsWaveBytes + lane * 16;
+    return const_cast<uint8_t*>(row_ptr(s, kBsK + o)) + (size_t)c * kBsWaveBytes + lane * 16;
   };
   const auto slot_ptr = [&](uint32_t s, int i, uint32_t c) -> const uint8_t* {  // data row i, or zeros
     const int src = a.src[i];
@@ -431,16 +453,26 @@ void coef_tables_host(uint8_t c, dev::u32x4& t01, uint32_t& t2) {  // gf_device.
   t2 = tt2;
 }
 
-template <int M>
+template <int M, bool TAB>
 hipError_t launch_rep_m(int nd, const dev::GfArgs& a, const BsRepairArgs& r, unsigned grid, uint32_t tps,
                         uint32_t nt, hipStream_t st) {
   switch (nd) {
-    case 0: hipLaunchKernelGGL((gf_bs16_repair_kernel<M, 0>), dim3(grid), dim3(64 * kBsWaves), 0, st, a, r, tps, nt); break;
-    case 1: hipLaunchKernelGGL((gf_bs16_repair_kernel<M, 1>), dim3(grid), dim3(64 * kBsWaves), 0, st, a, r, tps, nt); break;
-    case 2: hipLaunchKernelGGL((gf_bs16_repair_kernel<M, 2>), dim3(grid), dim3(64 * kBsWaves), 0, st, a, r, tps, nt); break;
+    case 0: hipLaunchKernelGGL((gf_bs16_repair_kernel<M, 0, TAB>), dim3(grid), dim3(64 * kBsWaves), 0, st, a, r, tps, nt); break;
+    case 1: hipLaunchKernelGGL((gf_bs16_repair_kernel<M, 1, TAB>), dim3(grid), dim3(64 * kBsWaves), 0, st, a, r, tps, nt); break;
+    case 2: hipLaunchKernelGGL((gf_bs16_repair_kernel<M, 2, TAB>), dim3(grid), dim3(64 * kBsWaves), 0, st, a, r, tps, nt); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
+}
+
+bool rep_args(int nd, const uint8_t* missing, const uint8_t* prow, const uint8_t* ainv, BsRepairArgs& r) {
+  for (int q = 0; q < nd; ++q) {
+    r.slot[q] = missing[q];
+    r.prow[q] = prow[q];
+    for (int j = 0; j < nd; ++j) coef_tables_host(ainv[j * 4 + q], r.t01[j * 4 + q], r.t2[j * 4 + q]);
+  }
+  r.zero = zero_tile();
+  return r.zero != nullptr;
 }
 }  // namespace
 
@@ -452,16 +484,55 @@ hipError_t launch_bs16_repair(int nd, int ne, const uint8_t* missing, const uint
       (len % dev::kBsWaveBytes) || (a.pcmp && !a.flags))
     return hipErrorInvalidValue;
   BsRepairArgs r{};
-  for (int q = 0; q < nd; ++q) {
-    r.slot[q] = missing[q];
-    r.prow[q] = prow[q];
-    for (int j = 0; j < nd; ++j) coef_tables_host(ainv[j * 4 + q], r.t01[j * 4 + q], r.t2[j * 4 + q]);
-  }
-  r.zero = zero_tile();
-  if (!r.zero) return hipErrorOutOfMemory;
+  if (!rep_args(nd, missing, prow, ainv, r)) return hipErrorOutOfMemory;
   const unsigned grid = (unsigned)std::min<uint64_t>((uint64_t)cu_count(), (ntiles + kBsWaves - 1) / kBsWaves);
-  return ne == 2 ? launch_rep_m<22>(nd, a, r, grid, tps, (uint32_t)ntiles, st)
-                 : launch_rep_m<20>(nd, a, r, grid, tps, (uint32_t)ntiles, st);
+  return ne == 2 ? launch_rep_m<22, false>(nd, a, r, grid, tps, (uint32_t)ntiles, st)
+                 : launch_rep_m<20, false>(nd, a, r, grid, tps, (uint32_t)ntiles, st);
+}
+
+int bs_tab_stripes(int mo) { return kBsTabWords / (kBsK + mo); }
+
+hipError_t launch_bs16_repair_tab(int nd, int ne, const uint8_t* missing, const uint8_t* prow, const uint8_t* ainv,
+                                  const dev::GfArgs& a, const uint8_t* const* rows, unsigned ns, uint64_t len,
+                                  hipStream_t st, bool* ok) {
+  const int mo = nd + 20 + ne, per = bs_tab_stripes(mo);
+  const uint32_t tps = (uint32_t)(len / dev::kBsWaveBytes);
+  *ok = false;
+  if (nd < 0 || nd > kBsRepairMaxNd || (ne != 0 && ne != 2) || tps == 0 || (len % dev::kBsWaveBytes) ||
+      (a.pcmp && !a.flags) || !rows || ns == 0)
+    return hipErrorInvalidValue;
+  const size_t nrows = (size_t)ns * (kBsK + mo);
+  uintptr_t lo = ~(uintptr_t)0, hi = 0;
+  for (size_t i = 0; i < nrows; ++i) {
+    lo = std::min(lo, (uintptr_t)rows[i]);
+    hi = std::max(hi, (uintptr_t)rows[i]);
+  }
+  if (hi - lo > 0xFFFFFFFFull) return hipSuccess;  // not ok: the caller keeps its route
+  *ok = true;
+  BsRepairArgs r{};
+  if (!rep_args(nd, missing, prow, ainv, r)) return hipErrorOutOfMemory;
+  r.base = reinterpret_cast<const uint8_t*>(lo);
+  static thread_local dev::GfArgs t;
+  std::memcpy(&t, &a, sizeof(dev::GfArgs));
+  t.sstride = 0;
+  t.tab = 1;
+  for (unsigned s0 = 0; s0 < ns; s0 += (unsigned)per) {
+    const unsigned n = std::min<unsigned>((unsigned)per, ns - s0);
+    uint32_t off[kBsTabWords];
+    for (size_t i = 0; i < (size_t)n * (kBsK + mo); ++i)
+      off[i] = (uint32_t)((uintptr_t)rows[(size_t)s0 * (kBsK + mo) + i] - lo);
+    std::memcpy(reinterpret_cast<uint8_t*>(&t) + kBsTabOff, off, (size_t)n * (kBsK + mo) * 4);
+    t.flags = a.flags ? a.flags + s0 : nullptr;
+    t.nstripes = n;
+    const uint64_t ntiles = (uint64_t)tps * n;
+    const unsigned grid = (unsigned)std::min<uint64_t>((uint64_t)cu_count(), (ntiles + kBsWaves - 1) / kBsWaves);
+    const hipError_t e = ne == 2 ? launch_rep_m<22, true>(nd, t, r, grid, tps, (uint32_t)ntiles, st)
+                                 : launch_rep_m<20, true>(nd, t, r, grid, tps, (uint32_t)ntiles, st);
+    if (e != hipSuccess) return e;
+    t.zw = nullptr;  // the first launch zeroed them
+    t.nzw = 0;
+  }
+  return hipSuccess;
 }
 
 }  // namespace cfsec

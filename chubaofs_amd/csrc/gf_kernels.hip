@@ -129,6 +129,12 @@ static const bool kBs16 = [] {
   const char* v = std::getenv("CFSEC_BS16");
   return !(v && v[0] == '0');
 }();
+// ... and its pointer-table form for repairs of stripes at unrelated addresses; CFSEC_BS_TAB=0
+// leaves those to the dyadic kernel (A/B)
+static const bool kBsTab = [] {
+  const char* v = std::getenv("CFSEC_BS_TAB");
+  return !(v && v[0] == '0');
+}();
 static bool aligned16(const dev::GfArgs& a, int nptr) {
   if (a.sstride & 15) return false;
   for (int i = 0; i < nptr; ++i)
@@ -412,6 +418,39 @@ hipError_t launch_dy16_repair(const Dy16RepairJob& job, hipStream_t stream) {
   a.nzw = job.nzero;
   std::memcpy(a.src, job.src, 16);
   std::memcpy(a.coef, job.coef, (size_t)(20 + ne + nd) * 16);
+  // Stripes at unrelated addresses (every shard its own buffer, as blobnode assembles a bid): the
+  // bit-sliced repair over a table of 32-bit row offsets, ~20 stripes per launch, for the whole
+  // 2 KiB column runs; the dyadic kernel below then covers only the rows' tails.
+  uint64_t tab_full = 0;
+  if (!sstride && job.nstripes > 1 && job.syn && kBs16 && nd <= kBsRepairMaxNd && !job.lens && kBsTab &&
+      bs_matches(job.coef, 20 + ne, 16) && job.len >= kBs16Tile) {
+    static thread_local std::vector<const uint8_t*> rows;
+    rows.resize((size_t)job.nstripes * (16 + mo));
+    bool al = true;
+    for (int s = 0; s < job.nstripes; ++s) {
+      for (int c = 0; c < 16; ++c) rows[(size_t)s * (16 + mo) + c] = job.in[(size_t)s * 16 + c];
+      for (int r = 0; r < mo; ++r) rows[(size_t)s * (16 + mo) + 16 + r] = job.out[(size_t)s * mo + r];
+    }
+    for (const uint8_t* p : rows) al = al && !(reinterpret_cast<uintptr_t>(p) & 15);
+    if (al) {
+      uint8_t missing[4] = {};
+      for (int i = 0; i < 16; ++i)
+        if (job.src[i] >= 16) missing[job.src[i] - 16] = (uint8_t)i;
+      dev::GfArgs t = a;
+      t.flags = job.flags;
+      bool ok = false;
+      const uint64_t full = job.len / kBs16Tile * kBs16Tile;
+      const hipError_t e = launch_bs16_repair_tab(nd, ne, missing, job.prow, job.ainv, t, rows.data(),
+                                                  (unsigned)job.nstripes, full, stream, &ok);
+      if (e != hipSuccess) return e;
+      if (ok) {
+        tab_full = full;
+        a.zw = nullptr;  // the first launch zeroed them
+        a.nzw = 0;
+        if (full == job.len) return hipSuccess;
+      }
+    }
+  }
   for (int s0 = 0; s0 < job.nstripes; s0 += per) {
     const int ns = std::min(per, job.nstripes - s0);
     const int tab = sstride ? 1 : ns;
@@ -435,7 +474,7 @@ hipError_t launch_dy16_repair(const Dy16RepairJob& job, hipStream_t stream) {
     }
     // the syndrome form of the bit-sliced network (gf_bs16.hip) for the whole 2 KiB column runs of
     // 16-byte aligned rows, the dyadic repair kernel for the rest of each row
-    const uint64_t full = job.syn && kBs16 && nd <= kBsRepairMaxNd && tab == 1 && !job.lens &&
+    const uint64_t full = job.syn && kBs16 && nd <= kBsRepairMaxNd && tab == 1 && !tab_full && !job.lens &&
                                   bs_matches(job.coef, 20 + ne, 16) && aligned16(a, tab * (16 + mo))
                               ? llen / kBs16Tile * kBs16Tile
                               : 0;
@@ -446,13 +485,14 @@ hipError_t launch_dy16_repair(const Dy16RepairJob& job, hipStream_t stream) {
       const hipError_t e = launch_bs16_repair(nd, ne, missing, job.prow, job.ainv, a, (unsigned)ns, full, stream);
       if (e != hipSuccess) return e;
     }
-    if (full < llen) {
+    const uint64_t done = full ? full : tab_full;  // columns the bit-sliced kernel covered
+    if (done < llen) {
       const dev::GfArgs* ta = &a;
       static thread_local dev::GfArgs tail;
-      if (full) {
+      if (done) {
         std::memcpy(&tail, &a, sizeof(dev::GfArgs));
-        for (int i = 0; i < tab * (16 + mo); ++i) tail.ptr[i] = a.ptr[i] + full;
-        tail.len = llen - full;
+        for (int i = 0; i < tab * (16 + mo); ++i) tail.ptr[i] = a.ptr[i] + done;
+        tail.len = llen - done;
         ta = &tail;
       }
       const hipError_t e = launch_dy16_repair_args(nd, ne, *ta, (unsigned)ns, stream);

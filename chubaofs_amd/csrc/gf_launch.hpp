@@ -110,6 +110,15 @@ hipError_t launch_bs(int k, int m, const dev::GfArgs& a, unsigned ns, uint64_t l
 constexpr int kBsRepairMaxNd = 2;
 hipError_t launch_bs16_repair(int nd, int ne, const uint8_t* missing, const uint8_t* prow, const uint8_t* ainv,
                               const dev::GfArgs& a, unsigned ns, uint64_t len, hipStream_t st);
+// The same for stripes at unrelated addresses (every shard its own buffer): rows[s * (16 + mo) + i]
+// (the 16 inputs, then the mo = nd + 20 + ne outputs of stripe s) for ns stripes, every pointer
+// 16-byte aligned; a's other fields (flags, zw, pstore / pcmp, src) as for launch_bs16_repair.  The
+// rows go into the launch as 32-bit offsets from the lowest address, kBsTabStripes(mo) stripes per
+// launch; false in *ok when the rows span 4 GiB or more (the caller keeps its route).
+int bs_tab_stripes(int mo);
+hipError_t launch_bs16_repair_tab(int nd, int ne, const uint8_t* missing, const uint8_t* prow, const uint8_t* ainv,
+                                  const dev::GfArgs& a, const uint8_t* const* rows, unsigned ns, uint64_t len,
+                                  hipStream_t st, bool* ok);
 
 // repair_dy16 on a GfArgs block (gf_dy16.hip); launch_dy16_repair (gf_kernels.hip) fills it.
 hipError_t launch_dy16_repair_args(int nd, int ne, const dev::GfArgs& a, unsigned ns, hipStream_t st);

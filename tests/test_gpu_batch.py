@@ -820,6 +820,56 @@ def test_async_over_32_inputs_not_supported():
     assert st == [0]
 
 
+@pytest.mark.parametrize("S", [4096, 6144 + 48])
+def test_ec16p20l2_scattered_tasklet_bitsliced_repair(S):
+    """C5-shaped repairs whose shards each sit at their own address (blobnode assembles a bid from
+    per-vuid buffers, work_shard_recover.go:711-716): the bit-sliced repair over a table of row
+    offsets (~20 bids per launch: the 24 bids of C5's pattern take 2), the dyadic kernel for the 48-byte row
+    tails and for three missing data rows -- statuses and every shard against the ec oracle's
+    repair loop, with corrupted compared parities, data and local rows."""
+    mode = cm.EC16P20L2
+    t = cm.GetTactic(mode)
+    n = t.N + t.M + t.L
+    enc = ec_new(mode)
+    patterns = [[16, 17], [3, 20], [0, 1, 16, 17], [6, 25], [4, 11], [8, 14], [7, 13], [0, 1, 2, 16]]
+    nb = 44
+    rnd = random.Random(S + 1)
+    slot = S + 512
+    pool = torch.zeros(nb * n * slot + 4096, dtype=torch.uint8, device="cuda")
+    perm = list(range(nb * n))
+    rnd.shuffle(perm)
+    views, bads, want = [], [], []
+    for b in range(nb):
+        good = ec_full_codeword(enc, t, S, 500 + b)
+        bad = [0, 1, 16, 17] if b < 24 else patterns[b % len(patterns)]  # 24 of C5's pattern: 2 launches
+        work = [g.copy() for g in good]
+        for i in bad:
+            work[i][:] = 0
+        if b % 11 == 5:  # a compared global parity corrupted
+            j = next(x for x in range(16, 36) if x not in bad)
+            work[j][rnd.randrange(S)] ^= 0x3C
+        if b % 11 == 7:  # a present data row corrupted
+            j = next(x for x in range(16) if x not in bad)
+            work[j][rnd.randrange(S)] ^= 0x81
+        if b % 13 == 9:  # a local parity corrupted
+            work[37][rnd.randrange(S)] ^= 0x11
+        want.append(sequential(enc, [w.copy() for w in work], bad))
+        row = []
+        for i in range(n):
+            o = perm[b * n + i] * slot + 16 * rnd.randrange(16)
+            v = pool[o:o + S]
+            v.copy_(torch.from_numpy(work[i]))
+            row.append(v)
+        views.append(row)
+        bads.append(bad)
+    status = enc.ReconstructBatch(views, bads)
+    assert status == [w[0] for w in want], (status, [w[0] for w in want])
+    assert {w[0] for w in want} == {0, _lib.ErrVerify.status}
+    for b in range(nb):
+        for i in range(n):
+            assert np.array_equal(views[b][i].cpu().numpy(), want[b][1][i]), (S, b, bads[b], i)
+
+
 @pytest.mark.parametrize("S", [4096, 262144 + 2048 + 48])
 def test_ec16p20l2_tasklet_bitsliced_repair(S):
     """C5-shaped repairs through the bit-sliced repair kernel (gf_bs16.hip: aligned rows of one
