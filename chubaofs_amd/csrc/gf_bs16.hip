@@ -142,6 +142,7 @@ struct BsRepairArgs {
   uint32_t t2[16];
   const uint8_t* zero;  // kBsWaveBytes of zeros
   const uint8_t* base;  // TAB: row (s, i) at base + the 32-bit offset s * (16 + ND + M) + i of the table
+  const uint32_t* dtab; // TAB 2: that table in device memory (TAB 1: in the argument block)
 };
 
 // TAB launches keep their row offsets where a repair launch does not read its GfArgs: from coef to
@@ -198,7 +199,7 @@ __device__ __forceinline__ void bs_mul_acc8(uint32_t* acc, const uint32_t* s0, c
 
 // (GfArgs must stay the first parameter: bs_kernarg_ptr / bs_kernarg_u32 read it at offset 0 of
 // the arguments)
-template <int M, int ND, bool TAB>
+template <int M, int ND, int TAB>
 __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2, 2))) void gf_bs16_repair_kernel(
     const dev::GfArgs a, const BsRepairArgs r, uint32_t tiles_per_stripe, uint32_t ntiles) {
   using namespace dev;
@@ -212,7 +213,12 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
     for (uint32_t i = threadIdx.x; i < a.nzw; i += blockDim.x) a.zw[i] = 0u;
   // affine batches: row i of stripe s at ptr[i] + s * sstride; TAB: at base + its table offset
   const auto row_ptr = [&](uint32_t s, int i) -> const uint8_t* {
-    if constexpr (TAB) {
+    if constexpr (TAB == 2) {
+      typedef const __attribute__((address_space(4))) uint32_t cu32;
+      uint32_t w = __builtin_amdgcn_readfirstlane(s * (uint32_t)(kBsK + ND + M) + (uint32_t)i);
+      asm volatile("" : "+s"(w));
+      return r.base + ((cu32*)r.dtab)[w];  // a scalar load: the table is read-only for the launch
+    } else if constexpr (TAB == 1) {
       return r.base + bs_kernarg_u32(s * (uint32_t)(kBsK + ND + M) + (uint32_t)i);
     } else if constexpr (CFSEC_BS_REP_RELOAD) {
       return bs_kernarg_ptr(i) + (int64_t)s * a.sstride;
@@ -453,7 +459,7 @@ void coef_tables_host(uint8_t c, dev::u32x4& t01, uint32_t& t2) {  // gf_device.
   t2 = tt2;
 }
 
-template <int M, bool TAB>
+template <int M, int TAB>
 hipError_t launch_rep_m(int nd, const dev::GfArgs& a, const BsRepairArgs& r, unsigned grid, uint32_t tps,
                         uint32_t nt, hipStream_t st) {
   switch (nd) {
@@ -486,11 +492,55 @@ hipError_t launch_bs16_repair(int nd, int ne, const uint8_t* missing, const uint
   BsRepairArgs r{};
   if (!rep_args(nd, missing, prow, ainv, r)) return hipErrorOutOfMemory;
   const unsigned grid = (unsigned)std::min<uint64_t>((uint64_t)cu_count(), (ntiles + kBsWaves - 1) / kBsWaves);
-  return ne == 2 ? launch_rep_m<22, false>(nd, a, r, grid, tps, (uint32_t)ntiles, st)
-                 : launch_rep_m<20, false>(nd, a, r, grid, tps, (uint32_t)ntiles, st);
+  return ne == 2 ? launch_rep_m<22, 0>(nd, a, r, grid, tps, (uint32_t)ntiles, st)
+                 : launch_rep_m<20, 0>(nd, a, r, grid, tps, (uint32_t)ntiles, st);
 }
 
 int bs_tab_stripes(int mo) { return kBsTabWords / (kBsK + mo); }
+
+// The row-offset table in device memory (TAB 2: any number of stripes in one launch), one per
+// device: a pinned staging copy and its device twin, reused once the previous launch that read them
+// has completed (an event), grown on demand.  CFSEC_BS_DTAB=0 keeps the argument-block table (A/B).
+#ifndef CFSEC_BS_DTAB
+#define CFSEC_BS_DTAB 1
+#endif
+struct BsDevTable {
+  std::mutex mu;
+  uint32_t* host = nullptr;
+  uint32_t* dev = nullptr;
+  size_t cap = 0;
+  hipEvent_t done = nullptr;
+  bool pending = false;
+};
+
+BsDevTable* dev_table() {
+  static BsDevTable t[64];
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= 64) return nullptr;
+  return &t[d];
+}
+
+// under t.mu: room for n words, the previous user's reads done
+bool dev_table_reserve(BsDevTable& t, size_t n) {
+  if (t.pending && hipEventSynchronize(t.done) != hipSuccess) return false;
+  t.pending = false;
+  if (!t.done && hipEventCreateWithFlags(&t.done, hipEventDisableTiming) != hipSuccess) return false;
+  if (n <= t.cap) return true;
+  if (t.host) (void)hipHostFree(t.host);
+  if (t.dev) (void)hipFree(t.dev);
+  t.host = nullptr;
+  t.dev = nullptr;
+  t.cap = 0;
+  const size_t cap = std::max<size_t>(n, 4096);
+  if (hipHostMalloc(reinterpret_cast<void**>(&t.host), cap * 4, hipHostMallocDefault) != hipSuccess) return false;
+  if (hipMalloc(reinterpret_cast<void**>(&t.dev), cap * 4) != hipSuccess) {
+    (void)hipHostFree(t.host);
+    t.host = nullptr;
+    return false;
+  }
+  t.cap = cap;
+  return true;
+}
 
 hipError_t launch_bs16_repair_tab(int nd, int ne, const uint8_t* missing, const uint8_t* prow, const uint8_t* ainv,
                                   const dev::GfArgs& a, const uint8_t* const* rows, unsigned ns, uint64_t len,
@@ -516,6 +566,26 @@ hipError_t launch_bs16_repair_tab(int nd, int ne, const uint8_t* missing, const 
   std::memcpy(&t, &a, sizeof(dev::GfArgs));
   t.sstride = 0;
   t.tab = 1;
+  if (BsDevTable* dt = CFSEC_BS_DTAB && ns > (unsigned)per ? dev_table() : nullptr) {
+    std::lock_guard<std::mutex> lk(dt->mu);
+    if (dev_table_reserve(*dt, nrows)) {
+      for (size_t i = 0; i < nrows; ++i) dt->host[i] = (uint32_t)((uintptr_t)rows[i] - lo);
+      hipError_t e = hipMemcpyAsync(dt->dev, dt->host, nrows * 4, hipMemcpyHostToDevice, st);
+      if (e != hipSuccess) return e;
+      r.dtab = dt->dev;
+      t.nstripes = ns;
+      const uint64_t ntiles = (uint64_t)tps * ns;
+      if (ntiles > 0xFFFFFFFFull) return hipErrorInvalidValue;
+      const unsigned grid = (unsigned)std::min<uint64_t>((uint64_t)cu_count(), (ntiles + kBsWaves - 1) / kBsWaves);
+      e = ne == 2 ? launch_rep_m<22, 2>(nd, t, r, grid, tps, (uint32_t)ntiles, st)
+                  : launch_rep_m<20, 2>(nd, t, r, grid, tps, (uint32_t)ntiles, st);
+      if (e != hipSuccess) return e;
+      e = hipEventRecord(dt->done, st);
+      if (e != hipSuccess) return e;
+      dt->pending = true;
+      return hipSuccess;
+    }
+  }
   for (unsigned s0 = 0; s0 < ns; s0 += (unsigned)per) {
     const unsigned n = std::min<unsigned>((unsigned)per, ns - s0);
     uint32_t off[kBsTabWords];
@@ -526,8 +596,8 @@ hipError_t launch_bs16_repair_tab(int nd, int ne, const uint8_t* missing, const 
     t.nstripes = n;
     const uint64_t ntiles = (uint64_t)tps * n;
     const unsigned grid = (unsigned)std::min<uint64_t>((uint64_t)cu_count(), (ntiles + kBsWaves - 1) / kBsWaves);
-    const hipError_t e = ne == 2 ? launch_rep_m<22, true>(nd, t, r, grid, tps, (uint32_t)ntiles, st)
-                                 : launch_rep_m<20, true>(nd, t, r, grid, tps, (uint32_t)ntiles, st);
+    const hipError_t e = ne == 2 ? launch_rep_m<22, 1>(nd, t, r, grid, tps, (uint32_t)ntiles, st)
+                                 : launch_rep_m<20, 1>(nd, t, r, grid, tps, (uint32_t)ntiles, st);
     if (e != hipSuccess) return e;
     t.zw = nullptr;  // the first launch zeroed them
     t.nzw = 0;
