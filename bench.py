@@ -1225,12 +1225,49 @@ def other_configs(args, torch, dev, stream, cpu):
         for i in range(tot5):
             want = zlib.crc32(g5h[bid, i].tobytes()) & 0xFFFFFFFF if i in er5 else 0
             assert int(w5[bid, i]) == want, f"C5 checksum of bid {bid} shard {i}"
+    # blobnode's own layout: every shard of the tasklet at its own address (a bid assembled from
+    # per-vuid ShardsBuf buffers, work_shard_recover.go:711-716) -- the same rows copied into shuffled
+    # slots of a pool, so no two rows share a stride
+    rnd5 = np.random.default_rng(5)
+    slot5 = p5 + 4096
+    pool5 = torch.empty((NBATCH, nb5 * tot5 * slot5 + 4096), dtype=torch.uint8, device=dev)
+    sc5, scv5 = [], []
+    for b in range(NBATCH):
+        perm = rnd5.permutation(nb5 * tot5)
+        rows = [[None] * tot5 for _ in range(nb5)]
+        for bid in range(nb5):
+            for i in range(tot5):
+                o = int(perm[bid * tot5 + i]) * slot5 + 256 * int(rnd5.integers(16))
+                rows[bid][i] = pool5[b, o:o + S5]
+                rows[bid][i].copy_(gold5[b, bid, i])
+        scv5.append(rows)
+        sc5.append(BatchMarshal(rows, tot5))
+
+    def rep5s(i):
+        bm = sc5[i % NBATCH]
+        _lib.check(e5._L.cfsec_ec_reconstruct_batch_async(e5._h, bm.arr, tot5, nb5, bad5, off5, 1, st5,
+                                                          fl5.data_ptr(), None, stream.cuda_stream))
+
+    def zero5s():
+        for rows in scv5:
+            for bid in range(nb5):
+                for i in er5:
+                    rows[bid][i].zero_()
+
+    def check5s():
+        for b in range(NBATCH):
+            got = torch.stack([torch.stack([scv5[b][bid][i] for i in er5]) for bid in range(nb5)])
+            assert torch.equal(got, gold5[b, :, er5]), "C5 scattered: rebuilt rows differ from the golden"
+
+    rsc = gated_calls(torch, stream, rep5s, NBATCH, secs, zero5s, check5s, sync_call=False)
+    assert list(st5) == [0] * nb5 and not bool(fl5.any().item()), "C5: Verify failed (scattered run)"
+    del sc5, scv5, pool5
     # per bid, one pass: reads 16 inputs + the 16 other global parities and the 2 local parities
     # it checks, writes 2 data + 2 parity rows (the local Verify rides in the global pass: the
     # separate AZ-local pass would re-read 2 x 19 shards)
     alg5 = (16 + 16 + 2 + 4) * S5
     c5 = {"workload": (f"EC16P20L2 repair tasklet on one GPU: {nb5} bids x S={S5}, erased {{0,1,16,17}}, "
-                       "Reconstruct + Verify per bid in one cfsec_ec_reconstruct_batch: one fused pass per bid (16x16-dyadic "
+                       "Reconstruct + Verify per bid in one cfsec_ec_reconstruct_batch: one fused pass per bid (bit-sliced "
                        "repair kernel; global and local parities checked in it)"),
           "data_GBps": round(N5 * S5 * nb5 * rs["calls_per_s"] / 1e9, 1),
           "roofline_frac": round(alg5 * nb5 * rs["calls_per_s"] / 1e9 / HBM_PEAK_GBPS, 4),
@@ -1238,6 +1275,11 @@ def other_configs(args, torch, dev, stream, cpu):
           "kernel_ms": round(ra["kernel_ms_per_call"], 4),
           "kernel_roofline_frac": frac(alg5 * nb5, ra["kernel_ms_per_call"]),
           "with_crc_kernel_ms": round(rc["kernel_ms_per_call"], 4),
+          "scattered_kernel_ms": round(rsc["kernel_ms_per_call"], 4),
+          "scattered_kernel_roofline_frac": frac(alg5 * nb5, rsc["kernel_ms_per_call"]),
+          "scattered_note": ("the same tasklet with every shard at its own address (blobnode's per-vuid buffers): "
+                             "cfsec_ec_reconstruct_batch_async device time per call, rebuilt rows checked against the "
+                             "golden"),
           "with_crc_over_kernel": round(rc["kernel_ms_per_call"] / ra["kernel_ms_per_call"], 3),
           "with_crc_note": ("cfsec_ec_reconstruct_batch_async with the rebuilt shards' checksums (256 words per "
                             "call, checked against zlib on the golden rows): device time per call, and its ratio "
