@@ -63,10 +63,18 @@ __device__ __forceinline__ const uint8_t* bs_kernarg_ptr(uint32_t j) {
 }
 constexpr bool kBsEncLdNt = CFSEC_BS_ENC_LDNT, kBsRepLdNt = CFSEC_BS_REP_LDNT;
 
+// A row-offset table in device memory (TAB 2 launches): row i of stripe s at base + dtab[s * (K +
+// M) + i] -- stripes whose shards each sit at their own address, any number per launch
+struct BsTabArgs {
+  const uint8_t* base;
+  const uint32_t* dtab;
+};
+
 // Encode: Net's K inputs -> its first M rows (K <= 16: 8 K input planes in registers)
-template <class Net, int M>
+// (GfArgs must stay the first parameter: bs_kernarg_ptr reads it at offset 0 of the arguments)
+template <class Net, int M, int TAB>
 __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2, 2))) void gf_bs_kernel(
-    const dev::GfArgs a, uint32_t tiles_per_stripe, uint32_t ntiles) {
+    const dev::GfArgs a, const BsTabArgs tb, uint32_t tiles_per_stripe, uint32_t ntiles) {
   using namespace dev;
   constexpr int K = Net::K, PF = K < kBsPrefetch ? K : kBsPrefetch;
   constexpr int NW = 2 * (K - PF) + 2 * M;  // vector memory ops a tile issues after its prefetch
@@ -84,9 +92,16 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
   };
   const auto row = [&](uint32_t s, int i, uint32_t c) -> uint8_t* {
     const uint8_t* base;
-    if (i < K) base = a.sstride ? ptr_at(i) + (int64_t)s * a.sstride : ptr_at(s * K + i);
-    else base = a.sstride ? ptr_at(K + (i - K)) + (int64_t)s * a.sstride
-                          : ptr_at(a.tab * K + s * M + (i - K));
+    if constexpr (TAB == 2) {
+      typedef const __attribute__((address_space(4))) uint32_t cu32;
+      uint32_t w = __builtin_amdgcn_readfirstlane(s * (uint32_t)(K + M) + (uint32_t)i);
+      asm volatile("" : "+s"(w));
+      base = tb.base + ((cu32*)tb.dtab)[w];  // a scalar load: the table is read-only for the launch
+    } else if (i < K) {
+      base = a.sstride ? ptr_at(i) + (int64_t)s * a.sstride : ptr_at(s * K + i);
+    } else {
+      base = a.sstride ? ptr_at(K + (i - K)) + (int64_t)s * a.sstride : ptr_at(a.tab * K + s * M + (i - K));
+    }
     return const_cast<uint8_t*>(base) + (size_t)c * kBsWaveBytes + lane * 16;
   };
   const auto prefetch = [&](uint32_t t) {
@@ -390,9 +405,10 @@ bool rows_match(const uint8_t* coef, int m) {
   return true;
 }
 
-template <class Net, int M>
-hipError_t launch_net(const dev::GfArgs& a, unsigned grid, uint32_t tps, uint32_t nt, hipStream_t st) {
-  hipLaunchKernelGGL((gf_bs_kernel<Net, M>), dim3(grid), dim3(64 * kBsWaves), 0, st, a, tps, nt);
+template <class Net, int M, int TAB = 0>
+hipError_t launch_net(const dev::GfArgs& a, unsigned grid, uint32_t tps, uint32_t nt, hipStream_t st,
+                      BsTabArgs tb = {nullptr, nullptr}) {
+  hipLaunchKernelGGL((gf_bs_kernel<Net, M, TAB>), dim3(grid), dim3(64 * kBsWaves), 0, st, a, tb, tps, nt);
   return hipGetLastError();
 }
 }  // namespace
@@ -602,6 +618,46 @@ hipError_t launch_bs16_repair_tab(int nd, int ne, const uint8_t* missing, const 
     t.zw = nullptr;  // the first launch zeroed them
     t.nzw = 0;
   }
+  return hipSuccess;
+}
+
+
+hipError_t launch_bs_tab(int k, int m, const dev::GfArgs& a, const uint8_t* const* rows, unsigned ns, uint64_t len,
+                         hipStream_t st, bool* ok) {
+  *ok = false;
+  const uint32_t tps = (uint32_t)(len / dev::kBsWaveBytes);
+  const uint64_t ntiles = (uint64_t)tps * ns;
+  if (k != 16 || (m != 20 && m != 22) || tps == 0 || ntiles > 0xFFFFFFFFull || (len % dev::kBsWaveBytes) || !rows ||
+      ns == 0)
+    return hipErrorInvalidValue;
+  const size_t nrows = (size_t)ns * (k + m);
+  uintptr_t lo = ~(uintptr_t)0, hi = 0;
+  for (size_t i = 0; i < nrows; ++i) {
+    lo = std::min(lo, (uintptr_t)rows[i]);
+    hi = std::max(hi, (uintptr_t)rows[i]);
+  }
+  if (hi - lo > 0xFFFFFFFFull) return hipSuccess;  // not ok: the caller keeps its route
+  BsDevTable* dt = dev_table();
+  if (!dt) return hipSuccess;
+  std::lock_guard<std::mutex> lk(dt->mu);
+  if (!dev_table_reserve(*dt, nrows)) return hipSuccess;
+  for (size_t i = 0; i < nrows; ++i) dt->host[i] = (uint32_t)((uintptr_t)rows[i] - lo);
+  hipError_t e = hipMemcpyAsync(dt->dev, dt->host, nrows * 4, hipMemcpyHostToDevice, st);
+  if (e != hipSuccess) return e;
+  *ok = true;
+  static thread_local dev::GfArgs t;
+  std::memcpy(&t, &a, sizeof(dev::GfArgs));
+  t.sstride = 0;
+  t.tab = 1;
+  t.nstripes = ns;
+  const BsTabArgs tb{reinterpret_cast<const uint8_t*>(lo), dt->dev};
+  const unsigned grid = (unsigned)std::min<uint64_t>((uint64_t)cu_count(), (ntiles + kBsWaves - 1) / kBsWaves);
+  e = m == 22 ? launch_net<dev::BsEc16p20l2, 22, 2>(t, grid, tps, (uint32_t)ntiles, st, tb)
+              : launch_net<dev::BsEc16p20l2, 20, 2>(t, grid, tps, (uint32_t)ntiles, st, tb);
+  if (e != hipSuccess) return e;
+  e = hipEventRecord(dt->done, st);
+  if (e != hipSuccess) return e;
+  dt->pending = true;
   return hipSuccess;
 }
 

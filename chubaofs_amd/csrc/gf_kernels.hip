@@ -211,6 +211,32 @@ hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
       stripes_per_launch = (int)std::min<size_t>(stripes_per_launch, std::max<size_t>(1, 0x7fffffffu / tiles));
       if (fixed) stripes_per_launch = std::min(stripes_per_launch, 65535);  // grid.y = stripes
       if (tiles > 0x7fffffffu) return hipErrorInvalidValue;
+      // stripes at unrelated addresses (more than one argument block holds) of the bit-sliced
+      // encode shapes: one launch through a device table of row offsets for the whole 2 KiB column
+      // runs (launch_bs_tab); the chunks below then code only the rows' tails
+      uint64_t tab_full = 0;
+      if (!sstride && mode == MatVecMode::kStore && !job.lens && kBs16 && kBsTab && c0 == 0 && r0 == 0 &&
+          kc == job.k && mc == job.m && job.nstripes > stripes_per_launch && job.len >= kBs16Tile &&
+          bs_matches(job.coef, mc, kc)) {
+        static thread_local std::vector<const uint8_t*> rows;
+        rows.resize((size_t)job.nstripes * per_stripe);
+        bool al = true;
+        for (int s = 0; s < job.nstripes; ++s) {
+          for (int c = 0; c < kc; ++c) rows[(size_t)s * per_stripe + c] = job.in[(size_t)s * job.k + c];
+          for (int r = 0; r < mc; ++r) rows[(size_t)s * per_stripe + kc + r] = job.out[(size_t)s * job.m + r];
+        }
+        for (const uint8_t* p : rows) al = al && !(reinterpret_cast<uintptr_t>(p) & 15);
+        if (al) {
+          a.flags = nullptr;
+          a.pstore = a.pcmp = 0;
+          bool ok = false;
+          const uint64_t full = job.len / kBs16Tile * kBs16Tile;
+          const hipError_t e = launch_bs_tab(kc, mc, a, rows.data(), (unsigned)job.nstripes, full, stream, &ok);
+          if (e != hipSuccess) return e;
+          if (ok) tab_full = full;
+          if (ok && full == job.len) continue;
+        }
+      }
       for (int s0 = 0; s0 < job.nstripes; s0 += stripes_per_launch) {
         const int ns = std::min(stripes_per_launch, job.nstripes - s0);
         const int tab = sstride ? 1 : ns;  // stripes held in the pointer table
@@ -247,8 +273,8 @@ hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
         // encodes of the bit-sliced shapes (gf_bs16.hip: EC16P20, EC16P20L2's fused encode) with 16-byte
         // aligned rows: the whole 2 KiB column runs through the network, the rest of each row through
         // the kernel chosen below
-        const uint64_t full = mode == MatVecMode::kStore && !job.lens && kBs16 && c0 == 0 && r0 == 0 && kc == job.k &&
-                                      mc == job.m && bs_ok(a, kc, mc, tab)
+        const uint64_t full = mode == MatVecMode::kStore && !tab_full && !job.lens && kBs16 && c0 == 0 && r0 == 0 &&
+                                      kc == job.k && mc == job.m && bs_ok(a, kc, mc, tab)
                                   ? llen / kBs16Tile * kBs16Tile
                                   : 0;
         // Verify of the same shapes: the bit-sliced repair kernel with nothing missing, every row compared
@@ -266,12 +292,12 @@ hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
           e = launch_bs16_repair(0, mc - 20, nullptr, nullptr, nullptr, a, (unsigned)ns, vfull, stream);
           if (e != hipSuccess) return e;
         }
-        if (full || vfull) {
+        if (full || vfull || tab_full) {
           if (full) {
             e = launch_bs(kc, mc, a, (unsigned)ns, full, stream);
             if (e != hipSuccess) return e;
           }
-          const uint64_t done = full ? full : vfull;
+          const uint64_t done = full ? full : vfull ? vfull : tab_full;
           if (done == llen) continue;
           for (int i = 0; i < tab * (kc + mc); ++i) a.ptr[i] += done;
           llen -= done;

@@ -116,6 +116,11 @@ hipError_t launch_bs16_repair(int nd, int ne, const uint8_t* missing, const uint
 // rows go into the launch as 32-bit offsets from the lowest address, kBsTabStripes(mo) stripes per
 // launch; false in *ok when the rows span 4 GiB or more (the caller keeps its route).
 int bs_tab_stripes(int mo);
+// launch_bs for stripes at unrelated addresses: rows[s * (k + m) + i] (inputs, then outputs), any
+// number of stripes in one launch through a device copy of their 32-bit offsets; *ok false when the
+// rows span 4 GiB or more or the table cannot be had (the caller keeps its route)
+hipError_t launch_bs_tab(int k, int m, const dev::GfArgs& a, const uint8_t* const* rows, unsigned ns, uint64_t len,
+                         hipStream_t st, bool* ok);
 hipError_t launch_bs16_repair_tab(int nd, int ne, const uint8_t* missing, const uint8_t* prow, const uint8_t* ainv,
                                   const dev::GfArgs& a, const uint8_t* const* rows, unsigned ns, uint64_t len,
                                   hipStream_t st, bool* ok);

@@ -821,6 +821,42 @@ def test_async_over_32_inputs_not_supported():
 
 
 @pytest.mark.parametrize("S", [4096, 6144 + 48])
+def test_ec16p20l2_scattered_encode_batch_bitsliced(S):
+    """An encode batch of the 16 + 20 code whose shards each sit at their own address, more stripes
+    than one argument block holds: the bit-sliced encode through a device table of row offsets (one
+    launch), the rows' 48-byte tails on the pointer-table chunks -- every parity (and local) row
+    against the ec oracle's Encode (lrcencoder.go / encoder.go over KRS)."""
+    mode = cm.EC16P20L2
+    t = cm.GetTactic(mode)
+    n = t.N + t.M + t.L
+    enc = ec_new(mode)
+    nb = 24
+    rnd = random.Random(S + 7)
+    slot = S + 512
+    pool = torch.full((nb * n * slot + 4096,), 0xA5, dtype=torch.uint8, device="cuda")
+    perm = list(range(nb * n))
+    rnd.shuffle(perm)
+    views, want = [], []
+    for b in range(nb):
+        data = [gen_mock_bytes(900 + 31 * b + i, S) for i in range(t.N)]
+        ref = [Slice.of(d) for d in data] + [Slice.of(np.zeros(S, np.uint8)) for _ in range(t.M + t.L)]
+        assert ECOracle.from_tactic(t).encode(ref) == 0
+        want.append([r.view().copy() for r in ref])
+        row = []
+        for i in range(n):
+            o = perm[b * n + i] * slot + 16 * rnd.randrange(16)
+            v = pool[o:o + S]
+            if i < t.N:
+                v.copy_(torch.from_numpy(data[i]))
+            row.append(v)
+        views.append(row)
+    assert enc.EncodeBatch(views) == [0] * nb
+    for b in range(nb):
+        for i in range(n):
+            assert np.array_equal(views[b][i].cpu().numpy(), want[b][i]), (mode, S, b, i)
+
+
+@pytest.mark.parametrize("S", [4096, 6144 + 48])
 def test_ec16p20l2_scattered_tasklet_bitsliced_repair(S):
     """C5-shaped repairs whose shards each sit at their own address (blobnode assembles a bid from
     per-vuid buffers, work_shard_recover.go:711-716): the bit-sliced repair over a table of row
