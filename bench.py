@@ -232,13 +232,23 @@ def cpu_saturated(S, prow, drows, seconds, callers):
 
 
 # ----------------------------------------------------------------- GPU
-def leg(fn):
+GATE_FAILURES = []  # secondary legs whose gate (or anything else) failed: top level of the line + exit status
+
+
+def leg(name, fn):
+    """A secondary leg: its exception is recorded in its field AND in the line's top-level
+    `gate_failures`, and makes the run exit non-zero (after the line is printed: the headline stays)."""
     try:
         return fn()
     except Exception as e:  # noqa: BLE001 -- reported in the JSON line, with the traceback on stderr
         import traceback
         traceback.print_exc()
-        return {"error": f"{type(e).__name__}: {e}"}
+        msg = f"{type(e).__name__}: {e}"
+        GATE_FAILURES.append({"leg": name, "error": msg})
+        return {"error": msg}
+
+
+EXIT_GATE_FAILED = 3
 
 
 def main():
@@ -444,10 +454,10 @@ def main():
         # the secondary legs run after the headline is measured and gated: an exception in one (every
         # rank runs the same code on the same shapes, so it raises on all of them) is recorded in its
         # field instead of costing the job its headline line
-        extra["C5_multi_gpu_repair"] = leg(lambda: multi_gpu_repair(args, torch, dev, rank, world))
-        extra["segment_reconstruct_data"] = leg(lambda: segment_latency(args, torch, dev, cpu=cpu_here))
-        extra["configs"] = leg(lambda: other_configs(args, torch, dev, stream, cpu=cpu_here))
-        extra["host_path"] = leg(lambda: host_path(args, torch, dev, world))
+        extra["C5_multi_gpu_repair"] = leg("C5_multi_gpu_repair", lambda: multi_gpu_repair(args, torch, dev, rank, world))
+        extra["segment_reconstruct_data"] = leg("segment_reconstruct_data", lambda: segment_latency(args, torch, dev, cpu=cpu_here))
+        extra["configs"] = leg("configs", lambda: other_configs(args, torch, dev, stream, cpu=cpu_here))
+        extra["host_path"] = leg("host_path", lambda: host_path(args, torch, dev, world))
 
     if rank != 0:
         if world > 1:
@@ -500,12 +510,17 @@ def main():
         "strong_scaling": strong,
         "cpu_baseline": cpu,
     }
+    out["gate_failures"] = GATE_FAILURES  # [] when every secondary leg's gate held
     out.update(extra)
     if "device_copy_GBps" in extra:
         out["roofline"]["frac_of_measured_copy"] = round(achieved / extra["device_copy_GBps"], 4)
     print(json.dumps(out), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
+    if GATE_FAILURES:
+        print(f"bench: {len(GATE_FAILURES)} secondary gate(s) failed: "
+              + "; ".join(f"{g['leg']}: {g['error']}" for g in GATE_FAILURES), file=sys.stderr, flush=True)
+        sys.exit(EXIT_GATE_FAILED)
 
 
 def secondary(args, torch, enc, batch, ptrs, stream, S, nst, pitch, dev, launch_bytes, data_bytes):

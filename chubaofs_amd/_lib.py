@@ -80,6 +80,7 @@ SIGNATURES = {
     "cfsec_last_error": ([], ctypes.c_char_p),
     "cfsec_status_name": ([_I], ctypes.c_char_p),
     "cfsec_device_count": ([], _I),
+    "cfsec_set_sync_poll": ([_I], _I),
     "cfsec_rs_new": ([_I, _I, _I, _P(_V)], _I),
     "cfsec_rs_free": ([_V], None),
     "cfsec_rs_data_shards": ([_V], _I),

@@ -206,6 +206,8 @@ int cfsec_device_count(void) {
   return n;
 }
 
+int cfsec_set_sync_poll(int on) { return cfsec::sync_poll_mode().exchange(on ? 1 : 0); }
+
 // ---------------- reedsolomon.Encoder ----------------
 
 int cfsec_rs_new(int data_shards, int parity_shards, int device, cfsec_rs** out) {

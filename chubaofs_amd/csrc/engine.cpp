@@ -1,5 +1,7 @@
 // engine.cpp -- RSEngine / ECEncoder / LrcEncoder host logic (see engine.hpp).
+#include <atomic>
 #include <chrono>
+#include <thread>
 
 #include "engine.hpp"
 
@@ -199,7 +201,8 @@ Status DeviceContext::acquire(size_t bytes, size_t nflags, Workspace** out, size
     ws->nflags = 0;
     st = hip_status(hipMalloc(reinterpret_cast<void**>(&ws->dflags), nf * 4), "hipMalloc(flags)");
     if (st == CFSEC_OK)
-      st = hip_status(hipHostMalloc(reinterpret_cast<void**>(&ws->hflags), nf * 4, hipHostMallocDefault),
+      st = hip_status(hipHostMalloc(reinterpret_cast<void**>(&ws->hflags), nf * 4,
+                                    hipHostMallocMapped | hipHostMallocCoherent),
                       "hipHostMalloc(flags)");
     if (st == CFSEC_OK)
       st = hip_status(hipHostGetDevicePointer(reinterpret_cast<void**>(&ws->hflags_dev), ws->hflags, 0),
@@ -229,7 +232,7 @@ Status DeviceContext::acquire(size_t bytes, size_t nflags, Workspace** out, size
     ws->ncrc = 0;
     st = hip_status(hipMalloc(reinterpret_cast<void**>(&ws->dcrc), nc * 4), "hipMalloc(crc words)");
     if (st == CFSEC_OK)
-      st = hip_status(hipHostMalloc(reinterpret_cast<void**>(&ws->hcrc), nc * 4, hipHostMallocDefault),
+      st = hip_status(hipHostMalloc(reinterpret_cast<void**>(&ws->hcrc), nc * 4, hipHostMallocCoherent),
                       "hipHostMalloc(crc words)");
     if (st == CFSEC_OK) ws->ncrc = nc;
   }
@@ -256,13 +259,18 @@ void DeviceContext::release(Workspace* ws) {
   free_.push_back(ws);
 }
 
-Status DeviceContext::finish(Workspace* ws, hipStream_t stream) {
-  static const bool kPoll = [] {  // CFSEC_SYNC_POLL=0: hipStreamSynchronize always (A/B)
+// CFSEC_SYNC_POLL=0 (or cfsec_set_sync_poll(0)): hipStreamSynchronize always (A/B, tests)
+std::atomic<int>& sync_poll_mode() {
+  static std::atomic<int> mode{[] {
     const char* v = std::getenv("CFSEC_SYNC_POLL");
-    return !(v && v[0] == '0');
-  }();
+    return (v && v[0] == '0') ? 0 : 1;
+  }()};
+  return mode;
+}
+
+Status DeviceContext::finish(Workspace* ws, hipStream_t stream) {
   const auto blocking = [&] { return hip_status(hipStreamSynchronize(stream), "hipStreamSynchronize"); };
-  if (!kPoll) return blocking();
+  if (!sync_poll_mode().load(std::memory_order_relaxed)) return blocking();
   if (!ws->hmark) {
     void* h = nullptr;
     if (hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
@@ -285,13 +293,20 @@ Status DeviceContext::finish(Workspace* ws, hipStream_t stream) {
     (void)hipGetLastError();
     return blocking();
   }
+  // The marker is written after the call's kernels and copies on this stream; the words the caller
+  // reads next (hflags, hcrc) are coherent host memory, so they are visible once the marker is.
+  // Busy-polling for the first kSpinBusyUs (a call's own latency), yielding the core after that.
   const auto t0 = std::chrono::steady_clock::now();
+  bool busy = true;
   for (uint32_t spin = 0;; ++spin) {
     if (__atomic_load_n(ws->hmark, __ATOMIC_ACQUIRE) == seq) return CFSEC_OK;
-    __builtin_ia32_pause();
-    if ((spin & 1023u) == 1023u &&
-        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() > kSpinLimitUs)
-      return blocking();
+    if (busy) __builtin_ia32_pause();
+    else std::this_thread::yield();
+    if ((spin & 255u) == 255u) {
+      const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+      if (us > kSpinLimitUs) return blocking();
+      busy = us < kSpinBusyUs;
+    }
   }
 }
 

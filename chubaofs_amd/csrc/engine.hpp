@@ -5,6 +5,7 @@
 //   ECEncoder  restates ec.Encoder (blobstore/common/ec/encoder.go) and
 //   LrcEncoder the LRC variant (blobstore/common/ec/lrcencoder.go).
 #pragma once
+#include <atomic>
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -23,6 +24,10 @@
 #include "kernels.hpp"
 
 namespace cfsec {
+
+// synchronous calls poll a marker word (1) or hipStreamSynchronize (0): cfsec_set_sync_poll
+std::atomic<int>& sync_poll_mode();
+
 
 using Status = int;  // cfsec_status
 
@@ -98,6 +103,7 @@ class DeviceContext {
   // long host batch, a fault: the runtime then reports the error).
   Status finish(Workspace* ws, hipStream_t stream);
   static constexpr double kSpinLimitUs = 20000.0;
+  static constexpr double kSpinBusyUs = 200.0;
   // Order ws->stream after the work already queued on the legacy default stream (and, by that
   // stream's semantics, on every blocking stream of the device): a device-memory call made
   // without a caller stream must not read its input before the kernel that produced it ran.

@@ -50,6 +50,20 @@ constexpr int kBsK = 16, kBsPrefetch = 8, kBsWaves = 8;
 #endif
 constexpr int kBsEncGlds = CFSEC_BS_ENC_GLDS, kBsRepGlds = CFSEC_BS_REP_GLDS;
 
+// Both kernels end their tile loop with an LDS-DMA re-prefetch in flight (branch-free: the last
+// tile re-reads itself).  s_endpgm does not wait for it, and once every wave of the workgroup has
+// ended its 160 KiB of LDS goes to the next workgroup placed on the CU -- possibly another launch's,
+// whose freshly prefetched slots the late DMA then overwrites.  Round 4's false ErrVerify (two
+// processes, or two streams, repairing at once; profiles/r05/stale_dma_probe.txt) was this.  So
+// every wave drains its vector memory operations before it ends.  CFSEC_BS_DRAIN=0: the round-4
+// form (A/B and the reproduction only).
+#ifndef CFSEC_BS_DRAIN
+#define CFSEC_BS_DRAIN 1
+#endif
+__device__ __forceinline__ void bs_drain_exit() {
+  if constexpr (CFSEC_BS_DRAIN) __builtin_amdgcn_s_waitcnt(dev::bs_waitcnt_vm(0));
+}
+
 // Row pointer j of the kernels' GfArgs (their first argument, at offset 0 of the argument segment)
 // by a scalar load whose offset the compiler cannot see through: the kernels name up to 40 rows,
 // and held across the tile loop their pointers (with the per-row conditions) outgrow the SGPRs --
@@ -135,6 +149,9 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
       bs_st_row(row(s, K + r, c), o);
     });
   }
+  // the last tile's re-prefetch is still in flight: the wave's LDS must not be handed to the next
+  // workgroup on this CU (another launch's) while a DMA can still land in it (bs_drain_exit)
+  bs_drain_exit();
 }
 
 // Reconstruct + Verify of the 16 + 20 code (C5's repair pass) in the same form, the syndrome way:
@@ -191,6 +208,11 @@ __device__ __forceinline__ uint32_t bs_kernarg_u32(uint32_t j) {
 #endif
 #ifndef CFSEC_BS_INS
 #define CFSEC_BS_INS 1  // a solved row into its slot: 0 masked XOR over every slot, 1 uniform branch (A/B)
+#endif
+#ifndef CFSEC_BS_DEBUG_FLAGS
+// 1: a failed compare writes 0x80000000 | row << 24 | column tile (the stripe's first mismatching
+// compared row of the lane that wrote last) instead of 1 into the stripe's flag word (diagnosis)
+#define CFSEC_BS_DEBUG_FLAGS 0
 #endif
 constexpr int kRepPrefetch = CFSEC_BS_PF, kRepRing = CFSEC_BS_RING;
 static_assert(kRepRing >= 3 || kRepRing == 2, "ring of 2 or more rows");
@@ -356,7 +378,8 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
     __builtin_amdgcn_sched_barrier(0);
     prefetch(t + nw < ntiles ? t + nw : t);
     __builtin_amdgcn_sched_barrier(0);
-    uint32_t diff = 0;
+    uint32_t diff = 0, first_bad = 0;
+    (void)first_bad;
     // the row masks re-read per tile (opaque): hoisted, their 44 per-row conditions outlive the
     // SGPRs as 64-bit lane masks and come back through v_readlane
     uint32_t pst = a.pstore, pcm = a.pcmp;
@@ -376,12 +399,20 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
         ++q_read;
         issue_ring();
         bs_transpose8(v);
+        uint32_t dd = 0;
 #pragma unroll
-        for (int w = 0; w < 8; ++w) diff |= v[w] ^ o[w];
+        for (int w = 0; w < 8; ++w) dd |= v[w] ^ o[w];
+        if constexpr (CFSEC_BS_DEBUG_FLAGS)
+          if (dd && !first_bad) first_bad = 0x80000000u | (uint32_t)p << 24 | (c & 0xFFFFFFu);
+        diff |= dd;
       }
     });
-    if (diff) set_flag(a.flags, s);
+    if (diff) {
+      if constexpr (CFSEC_BS_DEBUG_FLAGS) __hip_atomic_store(a.flags + s, first_bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      else set_flag(a.flags, s);
+    }
   }
+  bs_drain_exit();
 }
 
 int cu_count() {
@@ -514,48 +545,66 @@ hipError_t launch_bs16_repair(int nd, int ne, const uint8_t* missing, const uint
 
 int bs_tab_stripes(int mo) { return kBsTabWords / (kBsK + mo); }
 
-// The row-offset table in device memory (TAB 2: any number of stripes in one launch), one per
-// device: a pinned staging copy and its device twin, reused once the previous launch that read them
-// has completed (an event), grown on demand.  CFSEC_BS_DTAB=0 keeps the argument-block table (A/B).
+// The row-offset tables in device memory (TAB 2: any number of stripes in one launch): a small ring
+// per device, each slot a pinned staging copy and its device twin, free again once the launch that
+// read it has completed (its event, polled -- a launch never blocks the host on another caller's
+// work); with every slot still in flight the caller takes the argument-block route (TAB 1 launches,
+// or the encode's pointer-table chunks).  CFSEC_BS_DTAB=0 keeps the argument-block table (A/B).
 #ifndef CFSEC_BS_DTAB
 #define CFSEC_BS_DTAB 1
 #endif
+constexpr int kBsDevTables = 8;
+constexpr size_t kBsDevTableMin = 64 * 1024;  // words per slot: growth (a hipFree) stays rare
 struct BsDevTable {
-  std::mutex mu;
   uint32_t* host = nullptr;
   uint32_t* dev = nullptr;
   size_t cap = 0;
   hipEvent_t done = nullptr;
   bool pending = false;
 };
+struct BsDevTables {
+  std::mutex mu;
+  BsDevTable slot[kBsDevTables];
+};
 
-BsDevTable* dev_table() {
-  static BsDevTable t[64];
+BsDevTables* dev_tables() {
+  static BsDevTables t[64];
   int d = 0;
   if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= 64) return nullptr;
   return &t[d];
 }
 
-// under t.mu: room for n words, the previous user's reads done
-bool dev_table_reserve(BsDevTable& t, size_t n) {
-  if (t.pending && hipEventSynchronize(t.done) != hipSuccess) return false;
-  t.pending = false;
-  if (!t.done && hipEventCreateWithFlags(&t.done, hipEventDisableTiming) != hipSuccess) return false;
-  if (n <= t.cap) return true;
-  if (t.host) (void)hipHostFree(t.host);
-  if (t.dev) (void)hipFree(t.dev);
-  t.host = nullptr;
-  t.dev = nullptr;
-  t.cap = 0;
-  const size_t cap = std::max<size_t>(n, 4096);
-  if (hipHostMalloc(reinterpret_cast<void**>(&t.host), cap * 4, hipHostMallocDefault) != hipSuccess) return false;
-  if (hipMalloc(reinterpret_cast<void**>(&t.dev), cap * 4) != hipSuccess) {
-    (void)hipHostFree(t.host);
-    t.host = nullptr;
-    return false;
+// A free slot with room for n words (under the ring's mutex), or nullptr: every slot still read by
+// a launch in flight, or no memory
+BsDevTable* dev_table_reserve(BsDevTables& r, size_t n) {
+  BsDevTable* t = nullptr;
+  for (BsDevTable& c : r.slot) {
+    if (c.pending) {
+      const hipError_t q = hipEventQuery(c.done);
+      if (q == hipErrorNotReady) continue;
+      if (q != hipSuccess) return nullptr;
+      c.pending = false;
+    }
+    if (!t || (t->cap < n && c.cap >= n)) t = &c;  // prefer a slot that needs no growth
+    if (t->cap >= n) break;
   }
-  t.cap = cap;
-  return true;
+  if (!t) return nullptr;
+  if (!t->done && hipEventCreateWithFlags(&t->done, hipEventDisableTiming) != hipSuccess) return nullptr;
+  if (n <= t->cap) return t;
+  if (t->host) (void)hipHostFree(t->host);
+  if (t->dev) (void)hipFree(t->dev);
+  t->host = nullptr;
+  t->dev = nullptr;
+  t->cap = 0;
+  const size_t cap = std::max<size_t>(n, kBsDevTableMin);
+  if (hipHostMalloc(reinterpret_cast<void**>(&t->host), cap * 4, hipHostMallocDefault) != hipSuccess) return nullptr;
+  if (hipMalloc(reinterpret_cast<void**>(&t->dev), cap * 4) != hipSuccess) {
+    (void)hipHostFree(t->host);
+    t->host = nullptr;
+    return nullptr;
+  }
+  t->cap = cap;
+  return t;
 }
 
 hipError_t launch_bs16_repair_tab(int nd, int ne, const uint8_t* missing, const uint8_t* prow, const uint8_t* ainv,
@@ -582,9 +631,9 @@ hipError_t launch_bs16_repair_tab(int nd, int ne, const uint8_t* missing, const 
   std::memcpy(&t, &a, sizeof(dev::GfArgs));
   t.sstride = 0;
   t.tab = 1;
-  if (BsDevTable* dt = CFSEC_BS_DTAB && ns > (unsigned)per ? dev_table() : nullptr) {
-    std::lock_guard<std::mutex> lk(dt->mu);
-    if (dev_table_reserve(*dt, nrows)) {
+  if (BsDevTables* ring = CFSEC_BS_DTAB && ns > (unsigned)per ? dev_tables() : nullptr) {
+    std::lock_guard<std::mutex> lk(ring->mu);
+    if (BsDevTable* dt = dev_table_reserve(*ring, nrows)) {
       for (size_t i = 0; i < nrows; ++i) dt->host[i] = (uint32_t)((uintptr_t)rows[i] - lo);
       hipError_t e = hipMemcpyAsync(dt->dev, dt->host, nrows * 4, hipMemcpyHostToDevice, st);
       if (e != hipSuccess) return e;
@@ -637,10 +686,11 @@ hipError_t launch_bs_tab(int k, int m, const dev::GfArgs& a, const uint8_t* cons
     hi = std::max(hi, (uintptr_t)rows[i]);
   }
   if (hi - lo > 0xFFFFFFFFull) return hipSuccess;  // not ok: the caller keeps its route
-  BsDevTable* dt = dev_table();
-  if (!dt) return hipSuccess;
-  std::lock_guard<std::mutex> lk(dt->mu);
-  if (!dev_table_reserve(*dt, nrows)) return hipSuccess;
+  BsDevTables* ring = dev_tables();
+  if (!ring) return hipSuccess;
+  std::lock_guard<std::mutex> lk(ring->mu);
+  BsDevTable* dt = dev_table_reserve(*ring, nrows);
+  if (!dt) return hipSuccess;  // not ok: every table in flight, the caller keeps its route
   for (size_t i = 0; i < nrows; ++i) dt->host[i] = (uint32_t)((uintptr_t)rows[i] - lo);
   hipError_t e = hipMemcpyAsync(dt->dev, dt->host, nrows * 4, hipMemcpyHostToDevice, st);
   if (e != hipSuccess) return e;

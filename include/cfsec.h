@@ -95,6 +95,10 @@ const char* cfsec_last_error(void);
 const char* cfsec_status_name(int status);
 /* Number of visible HIP devices (0 if none; never an error). */
 int cfsec_device_count(void);
+/* How synchronous calls wait for their stream (no reference counterpart: a tuning knob):
+ * 1 = poll a pinned marker word the stream writes after the call's work (default), 0 =
+ * hipStreamSynchronize.  Process-wide; returns the previous mode.  Env: CFSEC_SYNC_POLL=0. */
+int cfsec_set_sync_poll(int on);
 
 /* ---------------- reedsolomon.Encoder seam ---------------- */
 /* reedsolomon.New(dataShards, parityShards) -- KRS/reedsolomon.go:413-581.  The engine binds
