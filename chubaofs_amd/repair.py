@@ -410,7 +410,10 @@ def _repair_columns(enc, local, plan: RepairPlan, rank, world, group, crcs, time
     _max_reduce(flags, world, group)
     # 4. return exchange: the rebuilt rows' columns to their owners, [nb, n_rebuilt(owner), L_me]
     out_idx, rsend, rrecv = lay.out_idx, lay.rsend, lay.rrecv
-    if world > 1 and (sum(rsend) or sum(rrecv)):
+    # entered by every rank or by none (a collective): the condition depends on the plan and S only --
+    # a rank with no columns (S < world * 256) or no rebuilt rows of its own still joins with empty
+    # blocks (round 5: at world 8 such a rank skipped it and the others hung)
+    if world > 1 and plan.rebuilt and S:
         send = local.new_empty(sum(rsend))
         o = 0
         for o_ in range(world):

@@ -130,6 +130,18 @@ CASES = {
     "EC12P4": dict(mode=cm.EC12P4, nb=4, S=1111, bad=[0, 1, 2, 3], corrupt=[(1, 13, 3)]),
     "EC12P4_toofew": dict(mode=cm.EC12P4, nb=3, S=999, bad=[[0, 1, 2, 3, 4], [0], []], corrupt=[(1, 15, 0)]),
 }
+# BASELINE configs[4] at world 8 (38 shards over 8 ranks: 5,5,5,5,5,5,4,4): C5's bad set over a
+# 64-bid tasklet at a small S (8 ranks' 256-B column slices, the last one ragged), and C5's own
+# S = 262,144 (32 KiB columns per rank) over fewer bids; corrupted data / global / local survivors;
+# EC16P20L2_local's S = 3000 leaves ranks 6 and 7 without columns (the hang round 5 found: such a
+# rank skipped the return exchange)
+CASES_W8 = {
+    "C5_64bids": dict(mode=cm.EC16P20L2, nb=64, S=8 * 512 + 37, bad=[0, 1, 16, 17],
+                      corrupt=[(3, 5, 100), (17, 20, 4000), (40, 36, 7), (63, 37, 4132)]),
+    "C5_S262144": dict(mode=cm.EC16P20L2, nb=6, S=262144, bad=[0, 1, 16, 17],
+                       corrupt=[(1, 2, 32768 * 3 + 5), (4, 30, 262143)]),
+    "EC16P20L2_local": CASES["EC16P20L2_local"],
+}
 
 
 def _cpu_worker(rank, world, port, case, strategy):
@@ -138,7 +150,7 @@ def _cpu_worker(rank, world, port, case, strategy):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         torch.set_num_threads(1)
-        c = CASES[case]
+        c = CASES[case] if case in CASES else CASES_W8[case]
         full, per = make_tasklet(c["mode"], c["nb"], c["S"], 11, c["bad"], c["corrupt"])
         want_st, want_rows, want_crc = oracle_repair(c["mode"], full, per)
         n = full.shape[1]
@@ -161,6 +173,22 @@ def test_repair_oracle_decoder_gloo(world, strategy, case):
     oracle's whole-bid repair: statuses (ErrVerify on corrupted survivors, ErrTooFewShards), rebuilt
     rows, untouched present rows, and the rebuilt rows' ChecksumIEEE combined from column slices."""
     mp.spawn(_cpu_worker, args=(world, free_port(), case, strategy), nprocs=world, join=True)
+
+
+@pytest.mark.parametrize("strategy", ["columns", "allgather"])
+@pytest.mark.parametrize("case", sorted(CASES_W8))
+def test_repair_oracle_decoder_gloo_world8(case, strategy):
+    """World 8, the node BASELINE configs[4] names: the 8-way owner map, the column split (32 KiB per
+    rank at S = 262,144), both exchanges and the reductions around the oracle decoder equal the
+    oracle's whole-bid repair, with corrupted survivors (ErrVerify) and bad local parities."""
+    c = CASES_W8[case]
+    n = cm.GetTactic(c["mode"]).N + cm.GetTactic(c["mode"]).M + cm.GetTactic(c["mode"]).L
+    assert [len(repair.owned(r, n, 8)) for r in range(8)] == [5, 5, 5, 5, 5, 5, 4, 4]
+    if c["S"] == 262144:
+        assert [L for _, L in repair.column_split(c["S"], 8)] == [32768] * 8
+    if c["S"] < 8 * 512:  # ranks 6 and 7 hold no columns: they still join both exchanges (empty blocks)
+        assert [L for _, L in repair.column_split(c["S"], 8)][-2:] == [0, 0]
+    mp.spawn(_cpu_worker, args=(8, free_port(), case, strategy), nprocs=8, join=True)
 
 
 def test_repair_oracle_decoder_world1():
@@ -293,7 +321,7 @@ def _gpu_worker(rank, world, port, case, strategy):
             mode, nb, S, bad, corrupt = cm.EC16P20L2, 64, 262144, [0, 1, 16, 17], [(7, 30, 12345), (40, 37, 262143),
                                                                                  (41, 2, 0)]
         else:
-            c = CASES[case]
+            c = CASES[case] if case in CASES else CASES_W8[case]
             mode, nb, S, bad, corrupt = c["mode"], c["nb"], c["S"], c["bad"], c["corrupt"]
         full, per = make_tasklet(mode, nb, S, 17, bad, corrupt)
         want = oracle_repair(mode, full, per)
@@ -317,3 +345,11 @@ def test_repair_gpu_multi_rank_shared_device(world, strategy, case):
     if case == "C5" and strategy == "allgather" and world == 3:
         pytest.skip("covered by world 2; keeps the box's host memory use small")
     mp.spawn(_gpu_worker, args=(world, free_port(), case, strategy), nprocs=world, join=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["EC16P20L2", "C5_64bids"])
+def test_repair_gpu_world8_shared_device(case):
+    """World 8 with the HIP decoder, all eight ranks on the box's one GPU (gloo transport): the
+    8-way owner map and column split with the real per-rank decode, against the oracle's repair."""
+    mp.spawn(_gpu_worker, args=(8, free_port(), case, "columns"), nprocs=8, join=True)
