@@ -1227,12 +1227,20 @@ def other_configs(args, torch, dev, stream, cpu):
                                                           stream.cuda_stream))
 
     zero5 = lambda: b5[:, :, er5, :].zero_()
+
+    def check5_status(what):
+        """every bid's planning status OK and no Verify flag set -- else which bids, with the raw flag
+        words (a CFSEC_BS_DEBUG_FLAGS=1 library writes 0x80000000 | compared row << 24 | column tile)"""
+        fl = fl5.cpu().numpy().view(np.uint32)
+        bad_st = {b: int(v) for b, v in enumerate(st5) if v}
+        bad_fl = {b: hex(int(v)) for b, v in enumerate(fl) if v}
+        assert not bad_st and not bad_fl, f"C5: Verify failed ({what}): status {bad_st} flags {bad_fl}"
     rs = gated_calls(torch, stream, rep5, NBATCH, secs, zero5, check5, sync_call=True)
     assert list(st5) == [0] * nb5
     ra = gated_calls(torch, stream, rep5a, NBATCH, secs, zero5, check5, sync_call=False)
-    assert list(st5) == [0] * nb5 and not bool(fl5.any().item()), "C5: Verify failed"
+    check5_status("async run")
     rc = gated_calls(torch, stream, rep5c, NBATCH, secs, zero5, check5, sync_call=False)
-    assert list(st5) == [0] * nb5 and not bool(fl5.any().item()), "C5: Verify failed (crc run)"
+    check5_status("crc run")
     # the words against zlib on the golden rebuilt rows (every bid of batch 0), 0 for the others
     w5 = cw5[0].cpu().numpy().view(np.uint32).reshape(nb5, tot5)
     g5h = gold5[0].cpu().numpy()
@@ -1275,7 +1283,7 @@ def other_configs(args, torch, dev, stream, cpu):
             assert torch.equal(got, gold5[b, :, er5]), "C5 scattered: rebuilt rows differ from the golden"
 
     rsc = gated_calls(torch, stream, rep5s, NBATCH, secs, zero5s, check5s, sync_call=False)
-    assert list(st5) == [0] * nb5 and not bool(fl5.any().item()), "C5: Verify failed (scattered run)"
+    check5_status("scattered run")
     del sc5, scv5, pool5
     # per bid, one pass: reads 16 inputs + the 16 other global parities and the 2 local parities
     # it checks, writes 2 data + 2 parity rows (the local Verify rides in the global pass: the

@@ -163,6 +163,8 @@ def lib():
             pass
         L = ctypes.CDLL(LIB_PATH)
         for name, (args, res) in SIGNATURES.items():
+            if os.environ.get("CFSEC_LIB_PATH") and not hasattr(L, name):
+                continue  # an older probe build (A/B of an earlier round's library): newer entry points absent
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = res

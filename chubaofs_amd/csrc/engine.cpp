@@ -797,14 +797,25 @@ Status RSEngine::split(uint8_t* data, size_t len, size_t cap, cfsec_shard* out, 
   }
   const size_t full = std::min<size_t>(eff / per, tot);
   const size_t npad = tot - full;
-  if (pad_needed) *pad_needed = npad * per;
-  if (npad > 0 && (!pad || pad_len < npad * per)) return CFSEC_ERR_INVALID_ARG;
+  // the padding shards as AllocAligned(npad, per) lays them out (KRS/unsafe.go:17-41): a 64-byte
+  // aligned start, each shard at a 64-byte rounded stride with that stride as its capacity
+  const size_t each = (per + 63) / 64 * 64;
+  if (pad_needed) *pad_needed = npad ? npad * each + 63 : 0;
+  if (npad > 0 && (!pad || pad_len < npad * each + 63)) return CFSEC_ERR_INVALID_ARG;
+  uint8_t* base = pad;
   if (npad > 0) {
-    std::memset(pad, 0, npad * per);
-    if (len > per * full) std::memcpy(pad, data + per * full, len - per * full);
+    base = pad + ((64 - (reinterpret_cast<uintptr_t>(pad) & 63)) & 63);
+    std::memset(base, 0, npad * each);
+    // the partial data after the full shards, copied shard by shard (copy(padding[i], copyFrom))
+    size_t from = per * full;
+    for (size_t j = 0; j < npad && from < len; ++j) {
+      const size_t c = std::min(per, len - from);
+      std::memcpy(base + j * each, data + from, c);
+      from += c;
+    }
   }
   for (size_t i = 0; i < full; ++i) out[i] = cfsec_shard{data + i * per, per, per};
-  for (size_t j = 0; j < npad; ++j) out[full + j] = cfsec_shard{pad + j * per, per, per};
+  for (size_t j = 0; j < npad; ++j) out[full + j] = cfsec_shard{base + j * each, per, each};
   return CFSEC_OK;
 }
 

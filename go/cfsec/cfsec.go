@@ -33,6 +33,7 @@ import (
 	"fmt"
 	"io"
 	"runtime"
+	"sync/atomic"
 	"unsafe"
 
 	"github.com/klauspost/reedsolomon"
@@ -62,10 +63,22 @@ func stripeOf(shards [][]byte) (base *C.uint8_t, size, stride int, ok bool) {
 		}
 	}
 	if _, one := regionOf(p0, (len(shards)-1)*stride+size); !one {
+		// an equal-stride stripe outside every registered allocation (an ec.Buffer nobody passed
+		// to RegisterBuffer): it still works, through callVec -- on Go < 1.21 that stages every
+		// shard through C memory, two host copies per call.  Counted, so an integration that
+		// forgot RegisterBuffer sees it (UnregisteredStripes).
+		atomic.AddUint64(&unregisteredStripes, 1)
 		return nil, 0, 0, false
 	}
 	return (*C.uint8_t)(unsafe.Pointer(&shards[0][0])), size, stride, true
 }
+
+var unregisteredStripes uint64
+
+// UnregisteredStripes is the number of calls so far whose shards formed one equal-stride stripe
+// (ec.Buffer's layout) that lay in no RegisterBuffer / HostAlloc region, so it missed the single-
+// pointer zero-copy path.  Nonzero means some ec.Buffer allocation should be registered.
+func UnregisteredStripes() uint64 { return atomic.LoadUint64(&unregisteredStripes) }
 
 // stripeOfMissing is stripeOf for a Reconstruct input: a missing shard (len 0) counts when its
 // capacity holds the shard at its place in the stripe; missing lists those indices.
@@ -126,7 +139,6 @@ type Engine struct {
 	h            *C.cfsec_rs
 	dataShards   int
 	parityShards int
-	cpu          reedsolomon.Encoder // Split / Join only (host bookkeeping)
 }
 
 var _ reedsolomon.Encoder = (*Engine)(nil)
@@ -172,12 +184,7 @@ func New(dataShards, parityShards int) (*Engine, error) {
 	if err := toError(C.cfsec_rs_new(C.int(dataShards), C.int(parityShards), -1, &h)); err != nil {
 		return nil, err
 	}
-	cpu, err := reedsolomon.New(dataShards, parityShards)
-	if err != nil {
-		C.cfsec_rs_free(h)
-		return nil, err
-	}
-	e := &Engine{h: h, dataShards: dataShards, parityShards: parityShards, cpu: cpu}
+	e := &Engine{h: h, dataShards: dataShards, parityShards: parityShards}
 	runtime.SetFinalizer(e, func(e *Engine) { C.cfsec_rs_free(e.h) })
 	return e, nil
 }
@@ -319,13 +326,108 @@ func (e *Engine) Reconstruct(shards [][]byte) error { return e.reconstruct(shard
 
 func (e *Engine) ReconstructData(shards [][]byte) error { return e.reconstruct(shards, true) }
 
-// Split and Join are host bookkeeping with no coding in them, so they are klauspost's own
-// (KRS/reedsolomon.go:1574-1632, 1646-1684) on a CPU engine of the same shape: the shard views,
-// the AllocAligned padding and the io.Writer's write pattern are the reference's by construction.
-func (e *Engine) Split(data []byte) ([][]byte, error) { return e.cpu.Split(data) }
+// Split is the engine's cfsec_rs_split (KRS/reedsolomon.go:1574-1632, the restatement tests/
+// test_capi.py pins): the data shards are views data[off:off+per:off+per] of data itself, the
+// padding shards views of one Go buffer the engine lays out as AllocAligned does (64-byte aligned,
+// stride and capacity per rounded up to 64).  The engine returns addresses; they are turned back
+// into offsets of the two Go buffers here, so no Go pointer outlives the call on the C side.
+func (e *Engine) Split(data []byte) ([][]byte, error) {
+	tot := e.dataShards + e.parityShards
+	arr := (*C.cfsec_shard)(C.malloc(C.size_t(tot) * C.size_t(unsafe.Sizeof(C.cfsec_shard{}))))
+	defer C.free(unsafe.Pointer(arr))
+	out := unsafe.Slice(arr, tot)
+	var dp *C.uint8_t
+	full := data[:cap(data)]
+	if len(full) > 0 {
+		dp = (*C.uint8_t)(unsafe.Pointer(&full[0]))
+	}
+	var need C.size_t
+	st := C.cfsec_rs_split(e.h, dp, C.size_t(len(data)), C.size_t(cap(data)), arr, nil, 0, &need)
+	var pad []byte
+	if st == C.CFSEC_ERR_INVALID_ARG && need > 0 {
+		pad = make([]byte, int(need))
+		st = C.cfsec_rs_split(e.h, dp, C.size_t(len(data)), C.size_t(cap(data)), arr,
+			(*C.uint8_t)(unsafe.Pointer(&pad[0])), need, &need)
+	}
+	if err := toError(st); err != nil {
+		return nil, err
+	}
+	view := func(buf []byte, el C.cfsec_shard) ([]byte, bool) {
+		if len(buf) == 0 {
+			return nil, false
+		}
+		off := int(uintptr(unsafe.Pointer(el.data)) - uintptr(unsafe.Pointer(&buf[0])))
+		if off < 0 || off+int(el.cap) > len(buf) {
+			return nil, false
+		}
+		return buf[off : off+int(el.len) : off+int(el.cap)], true
+	}
+	dst := make([][]byte, tot)
+	for i, el := range out {
+		v, ok := view(full, el)
+		if !ok {
+			if v, ok = view(pad, el); !ok {
+				return nil, fmt.Errorf("%w: split returned a shard outside its buffers", errInvalidArg)
+			}
+		}
+		dst[i] = v
+	}
+	return dst, nil
+}
 
+// Join is the engine's cfsec_rs_join (KRS/reedsolomon.go:1646-1684): the same argument checks and
+// errors (ErrTooFewShards, ErrReconstructRequired for a nil data shard, ErrShortData), the first
+// outSize bytes of the data shards gathered by the engine, then written to dst shard by shard as the
+// reference writes them (a Write per data shard, the last one cut at outSize).
 func (e *Engine) Join(dst io.Writer, shards [][]byte, outSize int) error {
-	return e.cpu.Join(dst, shards, outSize)
+	k := len(shards)
+	if k > e.dataShards {
+		k = e.dataShards
+	}
+	data := shards[:k]
+	// the engine reads at most outSize bytes of the data shards: those bytes cross in C memory (Go
+	// 1.17 forbids Go pointers inside a C array), each shard's true length beside them
+	arr := (*C.cfsec_shard)(C.malloc(C.size_t(k+1) * C.size_t(unsafe.Sizeof(C.cfsec_shard{}))))
+	defer C.free(unsafe.Pointer(arr))
+	els := unsafe.Slice(arr, k+1)
+	stage := C.malloc(C.size_t(outSize + 1))
+	defer C.free(stage)
+	mem := unsafe.Slice((*byte)(stage), outSize+1)
+	used := 0
+	for i, s := range data {
+		els[i] = C.cfsec_shard{data: nil, len: C.size_t(len(s)), cap: C.size_t(len(s))}
+		if s == nil {
+			continue // a nil data shard: ErrReconstructRequired
+		}
+		n := len(s)
+		if n > outSize-used {
+			n = outSize - used
+		}
+		copy(mem[used:used+n], s[:n])
+		// non-nil: a non-NULL address even for an empty shard (never read beyond its n bytes)
+		els[i].data = (*C.uint8_t)(unsafe.Add(stage, used))
+		used += n
+	}
+	out := make([]byte, outSize+1)
+	if err := toError(C.cfsec_rs_join(e.h, (*C.uint8_t)(unsafe.Pointer(&out[0])), C.size_t(outSize), arr,
+		C.int(len(shards)), C.size_t(outSize))); err != nil {
+		return err
+	}
+	write := outSize
+	pos := 0
+	for _, s := range data {
+		if write < len(s) {
+			_, err := dst.Write(out[pos : pos+write])
+			return err
+		}
+		n, err := dst.Write(out[pos : pos+len(s)])
+		if err != nil {
+			return err
+		}
+		write -= n
+		pos += n
+	}
+	return nil
 }
 
 func (e *Engine) EncodeIdx(dataShard []byte, idx int, parity [][]byte) error {

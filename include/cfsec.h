@@ -123,7 +123,9 @@ int cfsec_rs_reconstruct(cfsec_rs* h, cfsec_shard* shards, int n, int mem, void*
 int cfsec_rs_reconstruct_data(cfsec_rs* h, cfsec_shard* shards, int n, int mem, void* stream);
 /* Split -- KRS/reedsolomon.go:1574-1632 (host memory).  data has len/cap; the engine fills
  * out[0..total) with views into data and, when cap is short, into pad (caller-owned, at least
- * *pad_needed bytes; call once with pad == NULL to learn pad_needed). */
+ * *pad_needed bytes; call once with pad == NULL to learn pad_needed), laid out as the reference's
+ * AllocAligned (KRS/unsafe.go:17-41): from the first 64-byte aligned address of pad, shard j at
+ * j * roundup(per, 64), len per, cap roundup(per, 64). */
 int cfsec_rs_split(cfsec_rs* h, uint8_t* data, size_t len, size_t cap, cfsec_shard* out,
                    uint8_t* pad, size_t pad_len, size_t* pad_needed);
 /* Join -- KRS/reedsolomon.go:1646-1684 (host memory): copies out_size bytes into dst. */

@@ -103,6 +103,47 @@ def py_split(k, total, data, length):
     return out
 
 
+@pytest.mark.parametrize("k,m,length,cap", [(6, 6, 11, 11), (12, 4, 1000, 1003), (4, 2, 130, 140), (3, 3, 1, 1),
+                                           (12, 4, 4096, 8192)])
+def test_split_views_caps_and_padding_layout(k, m, length, cap):
+    """cfsec_rs_split's shard headers as the reference builds them: data shards data[:per:per], padding
+    shards from AllocAligned(npad, per) (KRS/unsafe.go:17-41) -- a 64-byte aligned start, a stride and
+    capacity of per rounded up to 64 -- with the partial tail copied shard by shard; pad_needed covers
+    the alignment slack."""
+    import ctypes
+    from chubaofs_amd import reedsolomon
+    e = reedsolomon.New(k, m)
+    tot = k + m
+    data = np.random.default_rng(length + cap).integers(0, 256, cap, dtype=np.uint8)
+    ref = data.copy()
+    out = (_lib.Shard * tot)()
+    need = ctypes.c_size_t(0)
+    L = e._L
+    st = L.cfsec_rs_split(e._h, data.ctypes.data, length, cap, out, None, 0, ctypes.byref(need))
+    per = (length + k - 1) // k
+    each = (per + 63) // 64 * 64
+    full = min(min(cap, per * tot) // per, tot) if cap > length else min(length // per, tot)
+    npad = tot - full
+    if npad == 0:
+        assert st == 0 and need.value == 0
+    else:
+        assert st == _lib.ErrInvalidArg.status and need.value == npad * each + 63
+        for shift in range(3):  # any start: the engine aligns inside the buffer
+            raw = np.zeros(need.value + 64, np.uint8)
+            pad_ptr = raw.ctypes.data + shift
+            st = L.cfsec_rs_split(e._h, data.ctypes.data, length, cap, out, pad_ptr, need.value, ctypes.byref(need))
+            assert st == 0
+            base = out[full].data
+            assert base % 64 == 0 and 0 <= base - pad_ptr < 64
+            for j in range(npad):
+                assert out[full + j].data == base + j * each and out[full + j].len == per
+                assert out[full + j].cap == each
+    for i in range(full):
+        assert out[i].data == data.ctypes.data + i * per and out[i].len == per and out[i].cap == per
+    got = [bytes(ctypes.string_at(out[i].data, per)) for i in range(tot)]
+    assert got == py_split(k, tot, ref, length)
+
+
 @pytest.mark.parametrize("k,m", [(6, 6), (12, 4), (15, 12), (1, 1)])
 @pytest.mark.parametrize("length,cap", [(1, 1), (11, 11), (11, 1024), (1000, 1000), (1000, 1003), (4096, 8192)])
 def test_split_join(k, m, length, cap):
