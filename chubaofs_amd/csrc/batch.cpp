@@ -63,6 +63,12 @@ struct Group {
   uint32_t* direct = nullptr;      // or: task i's Verify word is direct[i] (consecutive items' words)
   uint32_t* zero_words = nullptr;  // dy16: the call's checksum words, zeroed by the group's first launch
   uint32_t nzero = 0;
+  // dy16: the stored rows' checksums in the repair pass (dy16_crc_group): task i's checksummed row k
+  // into crc_words[i * crc_stride + crc_slot[k]]; crc_done[i] = 1 once a launch accumulated them
+  uint32_t* crc_words = nullptr;
+  uint32_t crc_stride = 0;
+  uint8_t crc_slot[4] = {};
+  std::vector<char>* crc_done = nullptr;
 };
 
 hipError_t launch_group_run(const Group& g, size_t t0, size_t t1, uint32_t* dflags, hipStream_t s);
@@ -145,6 +151,12 @@ hipError_t launch_group_run(const Group& g, size_t t0, size_t t1, uint32_t* dfla
     if (t0 == 0) {
       job.zero_words = g.zero_words;
       job.nzero = g.nzero;
+    }
+    if (g.crc_words && g.crc_done) {
+      job.crc_words = g.crc_words + t0 * g.crc_stride;
+      job.crc_stride = g.crc_stride;
+      std::memcpy(job.crc_slot, g.crc_slot, 4);
+      job.crc_done = g.crc_done->data() + t0;
     }
     return launch_dy16_repair(job, s);
   }
@@ -234,6 +246,55 @@ bool fused_crc_group(const Group& g, uint32_t* dcrc, size_t nwords, const std::m
                    "launch_matvec_crc(batch)");
   if (std::getenv("CFSEC_TRACE_BATCH"))  // which groups fused, for tests
     std::fprintf(stderr,"cfsec batch: fused crc group k=%d m=%d tasks=%zu len=%llu\n", k, m, nt, (unsigned long long)len);
+  return true;
+}
+
+// A dy16 (16 + 20 code) repair group whose stored rows -- the rebuilt data rows and the rebuilt parity
+// rows, at most 4 per bid (C5's {0, 1, 16, 17}) -- are checksummed by the bit-sliced repair pass
+// itself (gf_bs16.hip CRC launches) instead of a second pass over the rebuilt rows: every task one
+// checksummed task of its bid (crc == 1, no index remap), one length (a multiple of the kernel's
+// 2 KiB tile), the words at one stride.  Sets the group's crc_* fields; the launches report which
+// tasks they covered (crc_done), the rest keep the separate pass.  The words must be zeroed before.
+bool dy16_crc_group(Group& g, uint32_t* dcrc, size_t nwords, const std::map<int, int>& tasks_per_owner,
+                    std::vector<char>* done) {
+  // Off unless CFSEC_BS_REPAIR_CRC=1 (read per call): measured slower than the separate pass on
+  // C5's tasklet (profiles/r05/c5_repair_crc.txt: 178-183 vs 154-156 us per call) -- the repair
+  // kernel sits at 253 of 256 VGPRs at 2 waves per SIMD, so the Horner registers and lookups spill
+  // or serialise, and the block tile order it needs costs 8 % by itself
+  const char* on = std::getenv("CFSEC_BS_REPAIR_CRC");
+  if (!on || on[0] != '1') return false;
+  const Dy16Plan* d = g.plan->dy16.get();
+  const size_t nt = g.tasks.size();
+  if (!d || !d->syn || d->nd > kBsRepairMaxMissing || nt == 0 || !dcrc) return false;
+  const uint64_t len = g.lens[0];
+  if (len == 0 || len % kBsRepairTileBytes) return false;
+  // checksummed rows in the kernel's order: the missing data rows, then the stored parity rows
+  std::vector<int> rows;
+  for (int j = 0; j < d->nd; ++j) rows.push_back(d->rows[j]);
+  for (int p = 0; p < 22; ++p)
+    if (d->pstore >> p & 1u) rows.push_back(d->rows[d->nd + p]);
+  if (rows.empty() || rows.size() > 4) return false;
+  std::vector<int> stored(g.plan->out.begin(), g.plan->out.begin() + g.plan->nstore);
+  std::vector<int> sorted_rows = rows;
+  std::sort(stored.begin(), stored.end());
+  std::sort(sorted_rows.begin(), sorted_rows.end());
+  if (stored != sorted_rows) return false;  // the separate pass would checksum other rows
+  int64_t cs = 0;
+  for (size_t i = 0; i < nt; ++i) {
+    const StripeTask* t = g.tasks[i];
+    if (t->crc != 1 || t->crc_map || g.lens[i] != len || tasks_per_owner.at(t->owner) != 1) return false;
+    if (i == 1) cs = t->crc_word - g.tasks[0]->crc_word;
+    if (i >= 1 && t->crc_word - g.tasks[i - 1]->crc_word != cs) return false;
+  }
+  const int maxrow = *std::max_element(rows.begin(), rows.end());
+  if (nt == 1) cs = maxrow + 1;
+  const int64_t w0 = g.tasks[0]->crc_word;
+  if (cs <= maxrow || maxrow > 255 || w0 < 0 || (size_t)(w0 + cs * (int64_t)nt) > nwords) return false;
+  g.crc_words = dcrc + w0;
+  g.crc_stride = (uint32_t)cs;
+  for (size_t k = 0; k < rows.size(); ++k) g.crc_slot[k] = (uint8_t)rows[k];
+  done->assign(nt, 0);
+  g.crc_done = done;
   return true;
 }
 
@@ -862,23 +923,40 @@ Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceCont
       };
       std::vector<Group> groups = make_groups(dph, &next_flag, dptr);
       route(groups);
+      // dy16 groups that checksum their rebuilt rows in the repair pass itself
+      std::vector<std::vector<char>> crc_done(groups.size());
+      bool any_crc_fused = false;
+      if (sums)
+        for (size_t gi = 0; gi < groups.size(); ++gi)
+          any_crc_fused |= dy16_crc_group(groups[gi], dcrc, crc->n, tasks_per_owner, &crc_done[gi]);
       if (zero_first) {  // make_groups keeps first-appearance order: groups[0] holds direct.front()
-        if (!groups.empty() && groups[0].plan->dy16) {
+        if (!groups.empty() && groups[0].plan->dy16 && !any_crc_fused) {
           groups[0].zero_words = dcrc;
           groups[0].nzero = (uint32_t)crc->n;
-        } else {
+        } else {  // (the repair pass's checksum atomics must find the words zeroed already)
           st = hip_status(hipMemsetAsync(dcrc, 0, crc->n * 4, lane[0]), "hipMemsetAsync(crc)");
         }
         zero_first = false;
       }
       std::set<const StripeTask*> fused;  // tasks whose checksums a fused product + CRC launch took
-      for (const Group& gr : groups) {
+      for (size_t gi = 0; gi < groups.size(); ++gi) {
+        const Group& gr = groups[gi];
         if (st != CFSEC_OK) break;
         if (sums && fused_crc_group(gr, dcrc, crc->n, tasks_per_owner, lane[0], &st)) {
           fused.insert(gr.tasks.begin(), gr.tasks.end());
           continue;
         }
         st = hip_status(launch_group(gr, ws->bflags, lane[0]), "launch_matvec(batch)");
+        if (gr.crc_done) {
+          int nf = 0;
+          for (size_t i = 0; i < gr.tasks.size(); ++i)
+            if ((*gr.crc_done)[i]) {
+              fused.insert(gr.tasks[i]);
+              ++nf;
+            }
+          if (std::getenv("CFSEC_TRACE_BATCH"))
+            std::fprintf(stderr, "cfsec batch: repair-pass crc group tasks=%zu fused=%d\n", gr.tasks.size(), nf);
+        }
       }
       record(groups);
       if (st == CFSEC_OK) {

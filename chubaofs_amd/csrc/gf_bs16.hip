@@ -16,7 +16,9 @@
 #include <algorithm>
 #include <cstddef>
 #include <cstring>
+#include <map>
 #include <mutex>
+#include <vector>
 
 #include "bs_net_ec16p20l2.hpp"
 #include "gf_bitslice.hpp"
@@ -175,6 +177,13 @@ struct BsRepairArgs {
   const uint8_t* zero;  // kBsWaveBytes of zeros
   const uint8_t* base;  // TAB: row (s, i) at base + the 32-bit offset s * (16 + ND + M) + i of the table
   const uint32_t* dtab; // TAB 2: that table in device memory (TAB 1: in the argument block)
+  // CRC launches (the rebuilt shards' crc32.ChecksumIEEE in the same pass): checksummed row k of
+  // stripe s XOR-accumulates into crcw[s * crc_stride + crc_slot[k]] (zeroed before the launch)
+  uint32_t* crcw;
+  const uint32_t* ctab;  // kBsCrcTabs 5-bit tables (bs_crc_tables)
+  const uint32_t* cpow;  // tiles_per_stripe words: x^(8 * 2048 * j) mod P
+  uint32_t crc_stride, crc_ones;  // crc_ones: shift(~0, S) ^ ~0, folded in by each row's first segment
+  uint8_t crc_slot[4];
 };
 
 // TAB launches keep their row offsets where a repair launch does not read its GfArgs: from coef to
@@ -214,8 +223,89 @@ __device__ __forceinline__ uint32_t bs_kernarg_u32(uint32_t j) {
 // compared row of the lane that wrote last) instead of 1 into the stripe's flag word (diagnosis)
 #define CFSEC_BS_DEBUG_FLAGS 0
 #endif
+#ifndef CFSEC_BS_BLOCKED
+#define CFSEC_BS_BLOCKED 0  // 1: every repair launch maps each wave to a block of consecutive tiles (A/B)
+#endif
 constexpr int kRepPrefetch = CFSEC_BS_PF, kRepRing = CFSEC_BS_RING;
 static_assert(kRepRing >= 3 || kRepRing == 2, "ring of 2 or more rows");
+
+// ---- the rebuilt shards' checksums inside the repair pass (CRC launches) ----
+// crc32.ChecksumIEEE(M) = f(0, M) ^ shift(~0, |M|) ^ ~0 (gf_crc.hpp's algebra, reflected: bit 31 =
+// x^0).  A CRC launch gives each wave one block of consecutive column tiles (one stripe, or two when
+// the block crosses a stripe end) instead of every nw-th tile, so each lane keeps a Horner register
+// per checksummed row over its tiles: R <- shift(R, 2048) ^ shift(f(0, a), 1024) ^ f(0, b), with a,
+// b its two 16-byte pieces (bytes 16 l and 1024 + 16 l of the tile) -- 63 lookups in 5-bit tables
+// per row and tile.  At a segment's end the 64 lanes' registers fold in a 6-level tree over lane
+// pairs (shift by 16 * 2^k bytes, 7 lookups a level), one multiply moves the sum from the segment's
+// last tile to the row's end, and lane 0 XORs it into the row's word.  At most kBsCrcRows rows per
+// stripe (C5: 2 data + 2 parity rows); the launch needs 16 KiB of LDS for the tables, so its waves
+// prefetch one slot fewer.
+constexpr int kBsCrcRows = 4;
+static_assert(kBsRepairTileBytes == dev::kBsWaveBytes && kBsRepairMaxMissing == kBsRepairMaxNd, "kernels.hpp mirrors");
+constexpr int kBsCrcTabA = 0, kBsCrcTabB = 28, kBsCrcTabR = 56, kBsCrcTabTree = 63, kBsCrcTabs = 105;
+constexpr int kBsCrcLdsBytes = kBsCrcTabs * 32 * 4;
+constexpr int kRepPrefetchCrc = CFSEC_BS_PF - 1;
+constexpr uint32_t kBsCrcPoly = 0xEDB88320u;
+
+// XOR of the 7 lookups of word v's 5-bit fields (bits 0, 5, ..., 25 and 30) in tables tb[f * 32]
+// (gf_crc.hpp five_word: the masked copies make each extract the byte offset 4 * field)
+__device__ __forceinline__ uint32_t bs_five7(const uint32_t* tb, uint32_t v) {
+  uint32_t e = v & 0xC1F07C00u, o = v & 0x3E0F83E0u;
+  asm volatile("" : "+v"(e), "+v"(o));
+  const uint32_t off[7] = {(v << 2) & 0x7Cu,           __builtin_amdgcn_ubfe(o, 3, 7),  __builtin_amdgcn_ubfe(e, 8, 7),
+                           __builtin_amdgcn_ubfe(o, 13, 7), __builtin_amdgcn_ubfe(e, 18, 7), __builtin_amdgcn_ubfe(o, 23, 7),
+                           __builtin_amdgcn_ubfe(e, 28, 4)};
+  uint32_t t[7];
+#pragma unroll
+  for (int f = 0; f < 7; ++f)
+    t[f] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(tb + f * 32) + off[f]);
+  return dev::bs_x3(dev::bs_x3(t[0], t[1], t[2]), dev::bs_x3(t[3], t[4], t[5]), t[6]);
+}
+
+// a lane's contribution of one 32-byte row tile o (bytes, as stored): shift(f(0, a), 1024) ^ f(0, b)
+__device__ __forceinline__ uint32_t bs_crc_tile(const uint32_t* ct, const uint32_t* o) {
+  const uint32_t* ta = ct + kBsCrcTabA * 32;
+  const uint32_t* tb = ct + kBsCrcTabB * 32;
+  return dev::bs_x3(dev::bs_x3(bs_five7(ta, o[0]), bs_five7(ta + 224, o[1]), bs_five7(ta + 448, o[2])),
+                    dev::bs_x3(bs_five7(ta + 672, o[3]), bs_five7(tb, o[4]), bs_five7(tb + 224, o[5])),
+                    bs_five7(tb + 448, o[6]) ^ bs_five7(tb + 672, o[7]));
+}
+
+// bs_crc_tile word by word (7 lookups in flight at a time): inside the network, where the registers
+// are spent
+__device__ __forceinline__ uint32_t bs_crc_tile_seq(const uint32_t* ct, const uint32_t* o) {
+  uint32_t u = 0;
+#pragma unroll
+  for (int w = 0; w < 8; ++w) {
+    u ^= bs_five7(ct + (w < 4 ? kBsCrcTabA + 7 * w : kBsCrcTabB + 7 * (w - 4)) * 32, o[w]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  return u;
+}
+
+// a * b mod P (reflected)
+__device__ __forceinline__ uint32_t bs_mulmod(uint32_t a, uint32_t b) {
+  uint32_t p = 0;
+#pragma unroll
+  for (int i = 31; i >= 0; --i) {
+    p ^= (a >> i & 1u) ? b : 0u;
+    b = (b >> 1) ^ ((b & 1u) ? kBsCrcPoly : 0u);
+  }
+  return p;
+}
+
+// the 64 lanes' registers (lane l's bytes before lane l + 1's, 16-byte units) folded into one word,
+// in every lane: level k combines lane groups of 2^k, the lower group shifted by 16 * 2^k bytes
+__device__ __forceinline__ uint32_t bs_crc_lanes(const uint32_t* ct, uint32_t v, uint32_t lane) {
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const uint32_t other = (uint32_t)__shfl_xor((int)v, 1 << k, 64);
+    const bool upper = lane >> k & 1u;
+    const uint32_t lo = upper ? other : v, hi = upper ? v : other;
+    v = bs_five7(ct + (kBsCrcTabTree + 7 * k) * 32, lo) ^ hi;
+  }
+  return v;
+}
 
 __device__ __forceinline__ void bs_st_rebuilt(uint8_t* p, const uint32_t* o) {
   if constexpr (CFSEC_BS_REP_ST) {
@@ -236,16 +326,25 @@ __device__ __forceinline__ void bs_mul_acc8(uint32_t* acc, const uint32_t* s0, c
 
 // (GfArgs must stay the first parameter: bs_kernarg_ptr / bs_kernarg_u32 read it at offset 0 of
 // the arguments)
-template <int M, int ND, int TAB>
+template <int M, int ND, int TAB, bool CRC = false>
 __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2, 2))) void gf_bs16_repair_kernel(
     const dev::GfArgs a, const BsRepairArgs r, uint32_t tiles_per_stripe, uint32_t ntiles) {
   using namespace dev;
   constexpr int MO = ND + M;  // output rows per stripe: missing data rows, 20 parity rows, extras
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kBsWaves][(kRepPrefetch + kRepRing) * kBsWaveBytes];
+  constexpr int PF = CRC ? kRepPrefetchCrc : kRepPrefetch;
+  constexpr int kWaveLds = (PF + kRepRing) * kBsWaveBytes;
+  // one LDS array (a second __shared__ object can cost a vmcnt(0) before the first ds_read)
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kBsWaves * kWaveLds + (CRC ? kBsCrcLdsBytes : 0)];
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  uint8_t* pre = lds[wave];
-  uint8_t* ring = lds[wave] + kRepPrefetch * kBsWaveBytes;
+  uint8_t* pre = lds + wave * kWaveLds;
+  uint8_t* ring = pre + PF * kBsWaveBytes;
+  const uint32_t* ct = reinterpret_cast<const uint32_t*>(lds + kBsWaves * kWaveLds);
   const uint32_t nw = gridDim.x * kBsWaves;
+  if constexpr (CRC) {  // the checksum tables, once per workgroup (before any wave may leave)
+    for (uint32_t i = threadIdx.x; i < kBsCrcTabs * 8; i += blockDim.x)
+      reinterpret_cast<u32x4*>(lds + kBsWaves * kWaveLds)[i] = reinterpret_cast<const u32x4*>(r.ctab)[i];
+    __syncthreads();
+  }
   if (blockIdx.x == 0)  // the checksum words the pass after this one accumulates into
     for (uint32_t i = threadIdx.x; i < a.nzw; i += blockDim.x) a.zw[i] = 0u;
   // affine batches: row i of stripe s at ptr[i] + s * sstride; TAB: at base + its table offset
@@ -276,24 +375,38 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
   const auto prefetch = [&](uint32_t t) {
     const uint32_t s = t / tiles_per_stripe, c = t % tiles_per_stripe;
 #pragma unroll
-    for (int i = 0; i < kRepPrefetch; ++i) bs_glds_row<kBsRepGlds>(slot_ptr(s, i, c), pre + i * kBsWaveBytes);
+    for (int i = 0; i < PF; ++i) bs_glds_row<kBsRepGlds>(slot_ptr(s, i, c), pre + i * kBsWaveBytes);
   };
-  uint32_t t = blockIdx.x * kBsWaves + wave;
-  if (t >= ntiles) return;
+  // tiles: every nw-th (t0 = the wave's index), or for CRC launches one block of consecutive tiles
+  constexpr bool kBlocked = CRC || CFSEC_BS_BLOCKED;
+  const uint32_t wid = blockIdx.x * kBsWaves + wave;
+  const uint32_t per_wave = kBlocked ? (ntiles + nw - 1) / nw : 0;
+  uint32_t t = kBlocked ? wid * per_wave : wid;
+  const uint32_t t_end = kBlocked ? min(t + per_wave, ntiles) : ntiles, t_step = kBlocked ? 1u : nw;
+  if (t >= t_end) return;
   prefetch(t);
   __builtin_amdgcn_s_waitcnt(bs_waitcnt_vm(0));
-  for (; t < ntiles; t += nw) {
+  // CRC: each checksummed row's Horner register (lane-wise), the rows' count, the segment's first tile
+  uint32_t R[kBsCrcRows] = {};
+  uint32_t ncrc = 0, seg_c0 = t % tiles_per_stripe;
+  if constexpr (CRC) {
+    ncrc = (uint32_t)ND + (uint32_t)__builtin_popcount(a.pstore);
+    ncrc = __builtin_amdgcn_readfirstlane(ncrc);
+  }
+  (void)ncrc;
+  (void)seg_c0;
+  for (; t < t_end; t += t_step) {
     const uint32_t s = t / tiles_per_stripe, c = t % tiles_per_stripe;
     uint32_t x[128];
     uint32_t y[ND > 0 ? ND : 1][8];
 #pragma unroll
-    for (int i = kRepPrefetch; i < kBsK; ++i) bs_ld_row<kBsRepLdNt>(slot_ptr(s, i, c), &x[8 * i]);
+    for (int i = PF; i < kBsK; ++i) bs_ld_row<kBsRepLdNt>(slot_ptr(s, i, c), &x[8 * i]);
 #pragma unroll
     for (int q = 0; q < ND; ++q) bs_ld_row<kBsRepLdNt>(input(s, kBsK - ND + q, c), y[q]);
     // the prefetched slots were issued before everything since (in-order retirement)
-    __builtin_amdgcn_s_waitcnt(bs_waitcnt_vm(2 * (kBsK - kRepPrefetch + ND)));
+    __builtin_amdgcn_s_waitcnt(bs_waitcnt_vm(2 * (kBsK - PF + ND)));
 #pragma unroll
-    for (int i = 0; i < kRepPrefetch; ++i) bs_lds_row(pre + i * kBsWaveBytes, lane, &x[8 * i]);
+    for (int i = 0; i < PF; ++i) bs_lds_row(pre + i * kBsWaveBytes, lane, &x[8 * i]);
     __builtin_amdgcn_s_waitcnt(kBsWaitLgkm0);
     __builtin_amdgcn_sched_barrier(0);
     // which slots are present, one bit each, re-read per tile (opaque) like the row masks
@@ -376,7 +489,7 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
     issue_ring();
     issue_ring();
     __builtin_amdgcn_sched_barrier(0);
-    prefetch(t + nw < ntiles ? t + nw : t);
+    prefetch(t + t_step < t_end ? t + t_step : t);
     __builtin_amdgcn_sched_barrier(0);
     uint32_t diff = 0, first_bad = 0;
     (void)first_bad;
@@ -388,6 +501,15 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
       if (pst >> p & 1) {
         bs_transpose8(o);
         bs_st_rebuilt(output(s, ND + p, c), o);
+        if constexpr (CRC) {  // checksummed row ND + (stored parity rows before p)
+          const uint32_t k = (uint32_t)ND + (uint32_t)__builtin_popcount(pst & ((1u << p) - 1u));
+          __builtin_amdgcn_sched_barrier(0);  // in the middle of the network: no lookups hoisted into it
+          const uint32_t u = bs_crc_tile_seq(ct, o);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int kk = ND; kk < kBsCrcRows; ++kk)
+            if (k == (uint32_t)kk) R[kk] ^= u;
+        }
       } else if (pcm >> p & 1) {
         // this row's copy; the next compared row's may still fly (anything issued between them is
         // waited for too: retirement is in order)
@@ -410,6 +532,50 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
     if (diff) {
       if constexpr (CFSEC_BS_DEBUG_FLAGS) __hip_atomic_store(a.flags + s, first_bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       else set_flag(a.flags, s);
+    }
+    if constexpr (CRC && ND > 0) {
+      // the rebuilt data rows' checksums after the network, from their planes in x (kept as bytes
+      // through the network they spill): an odd slot holds d, an even slot the pair sum d ^ x_odd
+      uint32_t slots = (uint32_t)r.slot[0] | (uint32_t)r.slot[1] << 8;
+      if constexpr (CFSEC_BS_REP_RELOAD) asm volatile("" : "+s"(slots));
+#pragma unroll
+      for (int j = 0; j < ND; ++j) {
+        const uint32_t slot_j = slots >> (8 * j) & 0xFFu;
+        uint32_t d[8];
+#pragma unroll
+        for (int w = 0; w < 8; ++w) d[w] = 0u;
+#pragma unroll
+        for (int i = 0; i < kBsK; ++i)
+          if (i == slot_j) {  // uniform
+#pragma unroll
+            for (int w = 0; w < 8; ++w)
+              d[w] = (BsEc16p20l2::Paired && !(i & 1)) ? x[8 * i + w] ^ x[8 * (i + 1) + w] : x[8 * i + w];
+          }
+        bs_transpose8(d);
+        R[j] ^= bs_crc_tile_seq(ct, d);
+      }
+    }
+    if constexpr (CRC) {
+      if (t + 1 == t_end || c + 1 == tiles_per_stripe) {
+        // the segment [seg_c0, c] of stripe s: lanes folded, moved to the row's end, XOR-ed into the
+        // row's word (the row's first segment also folds in shift(~0, S) ^ ~0)
+        const uint32_t mv = r.cpow[tiles_per_stripe - 1 - c];
+#pragma unroll
+        for (int k = 0; k < kBsCrcRows; ++k) {
+          if ((uint32_t)k < ncrc) {
+            uint32_t v = bs_mulmod(bs_crc_lanes(ct, R[k], lane), mv);
+            if (seg_c0 == 0) v ^= r.crc_ones;
+            if (lane == 0) atomicXor(r.crcw + (size_t)s * r.crc_stride + r.crc_slot[k], v);
+          }
+          R[k] = 0u;
+        }
+        seg_c0 = 0;
+      } else {
+        // the next tile of this segment: every register moves 2048 bytes on
+#pragma unroll
+        for (int k = 0; k < kBsCrcRows; ++k)
+          if ((uint32_t)k < ncrc) R[k] = bs_five7(ct + kBsCrcTabR * 32, R[k]);
+      }
     }
   }
   bs_drain_exit();
@@ -506,16 +672,127 @@ void coef_tables_host(uint8_t c, dev::u32x4& t01, uint32_t& t2) {  // gf_device.
   t2 = tt2;
 }
 
-template <int M, int TAB>
+template <int M, int TAB, bool CRC = false>
 hipError_t launch_rep_m(int nd, const dev::GfArgs& a, const BsRepairArgs& r, unsigned grid, uint32_t tps,
                         uint32_t nt, hipStream_t st) {
   switch (nd) {
-    case 0: hipLaunchKernelGGL((gf_bs16_repair_kernel<M, 0, TAB>), dim3(grid), dim3(64 * kBsWaves), 0, st, a, r, tps, nt); break;
-    case 1: hipLaunchKernelGGL((gf_bs16_repair_kernel<M, 1, TAB>), dim3(grid), dim3(64 * kBsWaves), 0, st, a, r, tps, nt); break;
-    case 2: hipLaunchKernelGGL((gf_bs16_repair_kernel<M, 2, TAB>), dim3(grid), dim3(64 * kBsWaves), 0, st, a, r, tps, nt); break;
+    case 0: hipLaunchKernelGGL((gf_bs16_repair_kernel<M, 0, TAB, CRC>), dim3(grid), dim3(64 * kBsWaves), 0, st, a, r, tps, nt); break;
+    case 1:  // (no CRC form: one missing data row spills ~130 VGPRs with the checksums, the separate pass is faster)
+      if constexpr (CRC) return hipErrorInvalidValue;
+      else hipLaunchKernelGGL((gf_bs16_repair_kernel<M, 1, TAB, CRC>), dim3(grid), dim3(64 * kBsWaves), 0, st, a, r, tps, nt);
+      break;
+    case 2: hipLaunchKernelGGL((gf_bs16_repair_kernel<M, 2, TAB, CRC>), dim3(grid), dim3(64 * kBsWaves), 0, st, a, r, tps, nt); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
+}
+
+// ---- host side of the fused checksums (bs_crc_tile / bs_crc_lanes) ----
+uint32_t crc_mulmod(uint32_t a, uint32_t b) {  // reflected: bit 31 = x^0
+  uint32_t p = 0;
+  for (uint32_t bit = 0x80000000u; bit; bit >>= 1) {
+    if (a & bit) p ^= b;
+    b = (b >> 1) ^ ((b & 1u) ? kBsCrcPoly : 0u);
+  }
+  return p;
+}
+uint32_t crc_xpow(uint64_t e) {  // x^e mod P
+  uint32_t base = 0x40000000u, p = 0x80000000u;
+  for (; e; e >>= 1) {
+    if (e & 1) p = crc_mulmod(p, base);
+    base = crc_mulmod(base, base);
+  }
+  return p;
+}
+// f(0, the 16-byte piece whose word w is v, the rest 0)
+uint32_t crc_piece_word(int w, uint32_t v) {
+  uint32_t c = 0;
+  for (int i = 0; i < 16; ++i) {
+    c ^= i / 4 == w ? (v >> (8 * (i % 4))) & 0xFFu : 0u;
+    for (int q = 0; q < 8; ++q) c = (c & 1u) ? (c >> 1) ^ kBsCrcPoly : c >> 1;
+  }
+  return c;
+}
+// kBsCrcTabs tables of 32 words, table (g, f) at (g * 7 + f) * 32 for field f (bits 5f..) of word g:
+// a pieces (their image moved 1024 bytes on), b pieces, the register moved 2048 bytes on, and the
+// lane tree's levels (moved 16 * 2^k bytes on)
+std::vector<uint32_t> bs_crc_host_tables() {
+  std::vector<uint32_t> t((size_t)kBsCrcTabs * 32, 0u);
+  const uint32_t k1024 = crc_xpow(8 * 1024), k2048 = crc_xpow(8 * 2048);
+  for (int f = 0; f < 7; ++f)
+    for (uint32_t e = 0; e < (f < 6 ? 32u : 4u); ++e) {
+      const uint32_t v = e << (5 * f);
+      for (int w = 0; w < 4; ++w) {
+        const uint32_t img = crc_piece_word(w, v);
+        t[(size_t)((kBsCrcTabA + 7 * w + f) * 32 + e)] = crc_mulmod(k1024, img);
+        t[(size_t)((kBsCrcTabB + 7 * w + f) * 32 + e)] = img;
+      }
+      t[(size_t)((kBsCrcTabR + f) * 32 + e)] = crc_mulmod(k2048, v);
+      for (int k = 0; k < 6; ++k) t[(size_t)((kBsCrcTabTree + 7 * k + f) * 32 + e)] = crc_mulmod(crc_xpow(8ull * (16u << k)), v);
+    }
+  return t;
+}
+
+// the tables on the current device (uploaded once), and x^(8 * 2048 * j), j < tps (once per tps)
+struct BsCrcDev {
+  std::mutex mu;
+  uint32_t* tab = nullptr;
+  std::map<uint32_t, uint32_t*> pow;
+};
+hipError_t bs_crc_device(uint32_t tps, const uint32_t** tab, const uint32_t** pw) {
+  static BsCrcDev per[64];
+  int d = 0;
+  hipError_t e = hipGetDevice(&d);
+  if (e != hipSuccess) return e;
+  if (d < 0 || d >= 64) return hipErrorInvalidDevice;
+  BsCrcDev& c = per[d];
+  std::lock_guard<std::mutex> lk(c.mu);
+  if (!c.tab) {
+    const std::vector<uint32_t> h = bs_crc_host_tables();
+    uint32_t* p = nullptr;
+    if ((e = hipMalloc(reinterpret_cast<void**>(&p), h.size() * 4)) != hipSuccess) return e;
+    if ((e = hipMemcpy(p, h.data(), h.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) {
+      (void)hipFree(p);
+      return e;
+    }
+    c.tab = p;
+  }
+  auto it = c.pow.find(tps);
+  if (it == c.pow.end()) {
+    std::vector<uint32_t> h(tps);
+    const uint32_t k = crc_xpow(8ull * 2048);
+    uint32_t v = 0x80000000u;  // x^0
+    for (uint32_t j = 0; j < tps; ++j, v = crc_mulmod(v, k)) h[j] = v;
+    uint32_t* p = nullptr;
+    if ((e = hipMalloc(reinterpret_cast<void**>(&p), (size_t)tps * 4)) != hipSuccess) return e;
+    if ((e = hipMemcpy(p, h.data(), (size_t)tps * 4, hipMemcpyHostToDevice)) != hipSuccess) {
+      (void)hipFree(p);
+      return e;
+    }
+    it = c.pow.emplace(tps, p).first;
+  }
+  *tab = c.tab;
+  *pw = it->second;
+  return hipSuccess;
+}
+
+// the CRC fields of a repair launch, or false (not eligible: more than kBsCrcRows checksummed rows,
+// a zeroing request the atomics would race with, too many tiles per stripe for the table)
+bool rep_crc_args(int nd, const dev::GfArgs& a, uint64_t len, const BsCrcReq* crc, uint32_t* words, BsRepairArgs& r) {
+  if (!crc || !words || a.nzw || nd == 1) return false;
+  const int ncrc = nd + __builtin_popcount(a.pstore);
+  if (ncrc != crc->nrows || ncrc > kBsCrcRows || len % dev::kBsWaveBytes || len / dev::kBsWaveBytes > (1u << 20))
+    return false;
+  const uint32_t tps = (uint32_t)(len / dev::kBsWaveBytes);
+  if (bs_crc_device(tps, &r.ctab, &r.cpow) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  r.crcw = words;
+  r.crc_stride = crc->stride;
+  r.crc_ones = crc32_shift_ones((size_t)len);
+  for (int k = 0; k < 4; ++k) r.crc_slot[k] = crc->slot[k];
+  return true;
 }
 
 bool rep_args(int nd, const uint8_t* missing, const uint8_t* prow, const uint8_t* ainv, BsRepairArgs& r) {
@@ -530,15 +807,23 @@ bool rep_args(int nd, const uint8_t* missing, const uint8_t* prow, const uint8_t
 }  // namespace
 
 hipError_t launch_bs16_repair(int nd, int ne, const uint8_t* missing, const uint8_t* prow, const uint8_t* ainv,
-                              const dev::GfArgs& a, unsigned ns, uint64_t len, hipStream_t st) {
+                              const dev::GfArgs& a, unsigned ns, uint64_t len, hipStream_t st, const BsCrcReq* crc,
+                              uint32_t* crc_words, bool* crc_done) {
   const uint32_t tps = (uint32_t)(len / dev::kBsWaveBytes);
   const uint64_t ntiles = (uint64_t)tps * ns;
+  if (crc_done) *crc_done = false;
   if (nd < 0 || nd > kBsRepairMaxNd || (ne != 0 && ne != 2) || a.tab != 1 || tps == 0 || ntiles > 0xFFFFFFFFull ||
       (len % dev::kBsWaveBytes) || (a.pcmp && !a.flags))
     return hipErrorInvalidValue;
   BsRepairArgs r{};
   if (!rep_args(nd, missing, prow, ainv, r)) return hipErrorOutOfMemory;
   const unsigned grid = (unsigned)std::min<uint64_t>((uint64_t)cu_count(), (ntiles + kBsWaves - 1) / kBsWaves);
+  if (rep_crc_args(nd, a, len, crc, crc_words, r)) {
+    const hipError_t e = ne == 2 ? launch_rep_m<22, 0, true>(nd, a, r, grid, tps, (uint32_t)ntiles, st)
+                                 : launch_rep_m<20, 0, true>(nd, a, r, grid, tps, (uint32_t)ntiles, st);
+    if (e == hipSuccess && crc_done) *crc_done = true;
+    return e;
+  }
   return ne == 2 ? launch_rep_m<22, 0>(nd, a, r, grid, tps, (uint32_t)ntiles, st)
                  : launch_rep_m<20, 0>(nd, a, r, grid, tps, (uint32_t)ntiles, st);
 }
@@ -609,10 +894,12 @@ BsDevTable* dev_table_reserve(BsDevTables& r, size_t n) {
 
 hipError_t launch_bs16_repair_tab(int nd, int ne, const uint8_t* missing, const uint8_t* prow, const uint8_t* ainv,
                                   const dev::GfArgs& a, const uint8_t* const* rows, unsigned ns, uint64_t len,
-                                  hipStream_t st, bool* ok) {
+                                  hipStream_t st, bool* ok, const BsCrcReq* crc, uint32_t* crc_words,
+                                  bool* crc_done) {
   const int mo = nd + 20 + ne, per = bs_tab_stripes(mo);
   const uint32_t tps = (uint32_t)(len / dev::kBsWaveBytes);
   *ok = false;
+  if (crc_done) *crc_done = false;
   if (nd < 0 || nd > kBsRepairMaxNd || (ne != 0 && ne != 2) || tps == 0 || (len % dev::kBsWaveBytes) ||
       (a.pcmp && !a.flags) || !rows || ns == 0)
     return hipErrorInvalidValue;
@@ -642,9 +929,15 @@ hipError_t launch_bs16_repair_tab(int nd, int ne, const uint8_t* missing, const 
       const uint64_t ntiles = (uint64_t)tps * ns;
       if (ntiles > 0xFFFFFFFFull) return hipErrorInvalidValue;
       const unsigned grid = (unsigned)std::min<uint64_t>((uint64_t)cu_count(), (ntiles + kBsWaves - 1) / kBsWaves);
-      e = ne == 2 ? launch_rep_m<22, 2>(nd, t, r, grid, tps, (uint32_t)ntiles, st)
-                  : launch_rep_m<20, 2>(nd, t, r, grid, tps, (uint32_t)ntiles, st);
+      const bool fused = rep_crc_args(nd, t, len, crc, crc_words, r);
+      if (fused)
+        e = ne == 2 ? launch_rep_m<22, 2, true>(nd, t, r, grid, tps, (uint32_t)ntiles, st)
+                    : launch_rep_m<20, 2, true>(nd, t, r, grid, tps, (uint32_t)ntiles, st);
+      else
+        e = ne == 2 ? launch_rep_m<22, 2>(nd, t, r, grid, tps, (uint32_t)ntiles, st)
+                    : launch_rep_m<20, 2>(nd, t, r, grid, tps, (uint32_t)ntiles, st);
       if (e != hipSuccess) return e;
+      if (fused && crc_done) *crc_done = true;
       e = hipEventRecord(dt->done, st);
       if (e != hipSuccess) return e;
       dt->pending = true;

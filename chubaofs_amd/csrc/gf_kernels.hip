@@ -447,6 +447,17 @@ hipError_t launch_dy16_repair(const Dy16RepairJob& job, hipStream_t stream) {
   // Stripes at unrelated addresses (every shard its own buffer, as blobnode assembles a bid): the
   // bit-sliced repair over a table of 32-bit row offsets, ~20 stripes per launch, for the whole
   // 2 KiB column runs; the dyadic kernel below then covers only the rows' tails.
+  // the stored rows' checksums in the bit-sliced pass: rows = the missing data rows then the stored
+  // parity rows, in order (gf_bs16.hip's checksummed rows)
+  BsCrcReq crc_req;
+  if (job.crc_words && job.crc_done && !job.lens && job.syn && nd <= kBsRepairMaxNd) {
+    const int ncrc = nd + __builtin_popcount(job.pstore);
+    if (ncrc >= 1 && ncrc <= 4) {
+      crc_req.nrows = ncrc;
+      crc_req.stride = job.crc_stride;
+      for (int q = 0; q < 4; ++q) crc_req.slot[q] = job.crc_slot[q];
+    }
+  }
   uint64_t tab_full = 0;
   if (!sstride && job.nstripes > 1 && job.syn && kBs16 && nd <= kBsRepairMaxNd && !job.lens && kBsTab &&
       bs_matches(job.coef, 20 + ne, 16) && job.len >= kBs16Tile) {
@@ -464,11 +475,19 @@ hipError_t launch_dy16_repair(const Dy16RepairJob& job, hipStream_t stream) {
         if (job.src[i] >= 16) missing[job.src[i] - 16] = (uint8_t)i;
       dev::GfArgs t = a;
       t.flags = job.flags;
-      bool ok = false;
+      bool ok = false, fused = false;
       const uint64_t full = job.len / kBs16Tile * kBs16Tile;
+      const bool want_crc = crc_req.nrows && full == job.len;
+      if (want_crc) {  // the words are zeroed by the caller: no in-kernel zeroing to race the atomics
+        t.zw = nullptr;
+        t.nzw = 0;
+      }
       const hipError_t e = launch_bs16_repair_tab(nd, ne, missing, job.prow, job.ainv, t, rows.data(),
-                                                  (unsigned)job.nstripes, full, stream, &ok);
+                                                  (unsigned)job.nstripes, full, stream, &ok,
+                                                  want_crc ? &crc_req : nullptr, job.crc_words, &fused);
       if (e != hipSuccess) return e;
+      if (fused)
+        for (int s = 0; s < job.nstripes; ++s) job.crc_done[s] = 1;
       if (ok) {
         tab_full = full;
         a.zw = nullptr;  // the first launch zeroed them
@@ -508,8 +527,22 @@ hipError_t launch_dy16_repair(const Dy16RepairJob& job, hipStream_t stream) {
       uint8_t missing[4] = {};
       for (int i = 0; i < 16; ++i)
         if (job.src[i] >= 16) missing[job.src[i] - 16] = (uint8_t)i;
-      const hipError_t e = launch_bs16_repair(nd, ne, missing, job.prow, job.ainv, a, (unsigned)ns, full, stream);
+      const bool want_crc = crc_req.nrows && full == llen;
+      bool fused = false;
+      const dev::GfArgs* ra = &a;
+      static thread_local dev::GfArgs nz;
+      if (want_crc && a.nzw) {  // the words are zeroed by the caller: no in-kernel zeroing to race the atomics
+        std::memcpy(&nz, &a, sizeof(dev::GfArgs));
+        nz.zw = nullptr;
+        nz.nzw = 0;
+        ra = &nz;
+      }
+      const hipError_t e = launch_bs16_repair(nd, ne, missing, job.prow, job.ainv, *ra, (unsigned)ns, full, stream,
+                                              want_crc ? &crc_req : nullptr,
+                                              want_crc ? job.crc_words + (size_t)s0 * job.crc_stride : nullptr, &fused);
       if (e != hipSuccess) return e;
+      if (fused)
+        for (int s = 0; s < ns; ++s) job.crc_done[s0 + s] = 1;
     }
     const uint64_t done = full ? full : tab_full;  // columns the bit-sliced kernel covered
     if (done < llen) {

@@ -108,8 +108,19 @@ hipError_t launch_bs(int k, int m, const dev::GfArgs& a, unsigned ns, uint64_t l
 // (nd x nd, row stride 4) the inverse of those parity rows at the missing columns; columns [0, len),
 // len a multiple of kBs16Tile; nd <= kBsRepairMaxNd (3 and 4 missing data rows spill: dyadic kernel).
 constexpr int kBsRepairMaxNd = 2;
+// The rebuilt shards' checksums in the same pass (gf_bs16.hip, CRC launches): nrows (= nd + the stored
+// parity rows, at most 4) rows per stripe, row k's crc32.ChecksumIEEE XOR-accumulated into
+// words[s * stride + slot[k]] (the caller zeroes the words before the launch; a.nzw must be 0).
+// Taken only when len == the launch's columns (no row tail) and the device tables can be had:
+// *crc_done says whether this launch accumulated the words.
+struct BsCrcReq {
+  uint32_t stride = 0;
+  uint8_t slot[4] = {};
+  int nrows = 0;
+};
 hipError_t launch_bs16_repair(int nd, int ne, const uint8_t* missing, const uint8_t* prow, const uint8_t* ainv,
-                              const dev::GfArgs& a, unsigned ns, uint64_t len, hipStream_t st);
+                              const dev::GfArgs& a, unsigned ns, uint64_t len, hipStream_t st,
+                              const BsCrcReq* crc = nullptr, uint32_t* crc_words = nullptr, bool* crc_done = nullptr);
 // The same for stripes at unrelated addresses (every shard its own buffer): rows[s * (16 + mo) + i]
 // (the 16 inputs, then the mo = nd + 20 + ne outputs of stripe s) for ns stripes, every pointer
 // 16-byte aligned; a's other fields (flags, zw, pstore / pcmp, src) as for launch_bs16_repair.  The
@@ -123,7 +134,8 @@ hipError_t launch_bs_tab(int k, int m, const dev::GfArgs& a, const uint8_t* cons
                          hipStream_t st, bool* ok);
 hipError_t launch_bs16_repair_tab(int nd, int ne, const uint8_t* missing, const uint8_t* prow, const uint8_t* ainv,
                                   const dev::GfArgs& a, const uint8_t* const* rows, unsigned ns, uint64_t len,
-                                  hipStream_t st, bool* ok);
+                                  hipStream_t st, bool* ok, const BsCrcReq* crc = nullptr,
+                                  uint32_t* crc_words = nullptr, bool* crc_done = nullptr);
 
 // repair_dy16 on a GfArgs block (gf_dy16.hip); launch_dy16_repair (gf_kernels.hip) fills it.
 hipError_t launch_dy16_repair_args(int nd, int ne, const dev::GfArgs& a, unsigned ns, hipStream_t st);

@@ -56,8 +56,20 @@ struct Dy16RepairJob {
   bool syn = false;                    // the syndrome form below is set: the bit-sliced kernel may run
   uint8_t prow[4] = {};                // input 16 - nd + q is parity row prow[q]
   uint8_t ainv[16] = {};               // missing row j = sum_q ainv[j * 4 + q] * syndrome of prow[q]
+  // the stored rows' checksums in the same pass (bit-sliced kernel only): stripe s's checksummed row
+  // k (the missing data rows, then the stored parity rows in order) XOR-accumulates crc32.ChecksumIEEE
+  // into crc_words[s * crc_stride + crc_slot[k]] (zeroed by the caller, zero_words must be NULL);
+  // crc_done[s] is set to 1 for the stripes whose words the launches accumulated (host array)
+  uint32_t* crc_words = nullptr;
+  uint32_t crc_stride = 0;
+  uint8_t crc_slot[4] = {};
+  char* crc_done = nullptr;
 };
 hipError_t launch_dy16_repair(const Dy16RepairJob& job, hipStream_t stream);
+// what the bit-sliced repair (and its checksums) takes: whole 2 KiB column tiles, <= 2 missing data
+// rows (gf_launch.hpp kBs16Tile / kBsRepairMaxNd)
+constexpr uint64_t kBsRepairTileBytes = 2048;
+constexpr int kBsRepairMaxMissing = 2;
 
 // Verify flags of a batch call gathered per batch item (batch.cpp run_device): for every item o,
 // out[o] = OR of the per-task words tmp[word[j]] of the pairs (o, word[j]) -- `accumulate`: out[o] |=
