@@ -845,6 +845,21 @@ def segment_latency(args, torch, dev, cpu):
                         torch.cuda.synchronize()
 
                 r[kind + "_us"] = round(med(call), 1)
+                if kind == "device":
+                    # the C ABI alone, as cgo calls it: the shard vector marshalled once, a stream of
+                    # its own (the call is synchronous), no torch synchronize -- the Python layer's
+                    # Marshal and ctypes costs ~25-35 us of the figure above (tools/r5_latency.py)
+                    from chubaofs_amd._shards import Marshal
+                    m = Marshal(list(segs))
+                    badarr = (ctypes.c_int * 2)(*bad)
+                    own = torch.cuda.Stream(dev)
+                    torch.cuda.synchronize()
+
+                    def cabi():
+                        _lib.check(enc._L.cfsec_ec_reconstruct_data(enc._h, m.ptr(), m.n, badarr, 2, m.mem,
+                                                                     own.cuda_stream))
+
+                    r["device_cabi_us"] = round(med(cabi), 1)
                 got = [np.asarray(x.cpu().numpy() if kind == "device" else x) for x in segs[:N]]
                 assert all(np.array_equal(got[i], gold[i]) for i in range(N)), f"segment {name} {seg} {kind}"
             if cpu:
@@ -861,14 +876,16 @@ def segment_latency(args, torch, dev, cpu):
             del pin, pinned, devt
         wins = {}
         if cpu:
-            for kind in ("pageable", "pinned", "device"):
+            for kind in ("pageable", "pinned", "device", "device_cabi"):
                 w = [int(s) for s, r in rows.items()
                      if r[kind + "_us"] < min(r["cpu_port_4t_us"], r["cpu_port_1t_us"])]
                 wins[kind] = min(w) if w else None
         out["modes"][name] = {"by_segment_bytes": rows, "gpu_wins_from_bytes": wins}
     out["note"] = ("gpu_wins_from_bytes: smallest measured segment where the GPU call (wall, incl. staging and "
                    "sync) beats the faster of the CPU port's 1- and 4-thread calls; None: the CPU port wins at every "
-                   "measured size")
+                   "measured size.  *_us: through the Python ec.Encoder (Marshal + ctypes + torch synchronize); "
+                   "device_cabi_us: the C ABI call alone on HBM shards (what the Go shim's cgo call costs), "
+                   "synchronous on a stream of its own")
     return out
 
 
