@@ -830,11 +830,13 @@ hipError_t launch_bs16_repair(int nd, int ne, const uint8_t* missing, const uint
 
 int bs_tab_stripes(int mo) { return kBsTabWords / (kBsK + mo); }
 
-// The row-offset tables in device memory (TAB 2: any number of stripes in one launch): a small ring
-// per device, each slot a pinned staging copy and its device twin, free again once the launch that
-// read it has completed (its event, polled -- a launch never blocks the host on another caller's
-// work); with every slot still in flight the caller takes the argument-block route (TAB 1 launches,
-// or the encode's pointer-table chunks).  CFSEC_BS_DTAB=0 keeps the argument-block table (A/B).
+// The row-offset tables in device memory (TAB 2: any number of stripes in one launch): a ring of
+// kBsDevTables per device, each slot a pinned staging copy and its device twin, free again once the
+// launch that read it has completed (its event, polled).  A launch takes a free slot without
+// waiting; only when every slot is still in flight -- the host kBsDevTables launches ahead of the
+// GPU, e.g. back-to-back asynchronous tasklets -- does it wait for the oldest one, a bounded queue's
+// backpressure (the argument-block fallback measured 0.147 -> 0.205 ms per scattered C5 call when
+// taken instead).  CFSEC_BS_DTAB=0 keeps the argument-block table (A/B).
 #ifndef CFSEC_BS_DTAB
 #define CFSEC_BS_DTAB 1
 #endif
@@ -846,10 +848,12 @@ struct BsDevTable {
   size_t cap = 0;
   hipEvent_t done = nullptr;
   bool pending = false;
+  uint64_t seq = 0;  // when it was last taken
 };
 struct BsDevTables {
   std::mutex mu;
   BsDevTable slot[kBsDevTables];
+  uint64_t next = 0;
 };
 
 BsDevTables* dev_tables() {
@@ -859,21 +863,31 @@ BsDevTables* dev_tables() {
   return &t[d];
 }
 
-// A free slot with room for n words (under the ring's mutex), or nullptr: every slot still read by
-// a launch in flight, or no memory
+// A free slot with room for n words (under the ring's mutex) -- with every slot in flight, the oldest
+// once its launch completes -- or nullptr (no memory, a failed event)
 BsDevTable* dev_table_reserve(BsDevTables& r, size_t n) {
   BsDevTable* t = nullptr;
+  BsDevTable* oldest = nullptr;
   for (BsDevTable& c : r.slot) {
     if (c.pending) {
       const hipError_t q = hipEventQuery(c.done);
-      if (q == hipErrorNotReady) continue;
+      if (q == hipErrorNotReady) {
+        if (!oldest || c.seq < oldest->seq) oldest = &c;
+        continue;
+      }
       if (q != hipSuccess) return nullptr;
       c.pending = false;
     }
     if (!t || (t->cap < n && c.cap >= n)) t = &c;  // prefer a slot that needs no growth
     if (t->cap >= n) break;
   }
+  if (!t && oldest) {  // the host is kBsDevTables launches ahead: wait for the oldest
+    if (hipEventSynchronize(oldest->done) != hipSuccess) return nullptr;
+    oldest->pending = false;
+    t = oldest;
+  }
   if (!t) return nullptr;
+  t->seq = ++r.next;
   if (!t->done && hipEventCreateWithFlags(&t->done, hipEventDisableTiming) != hipSuccess) return nullptr;
   if (n <= t->cap) return t;
   if (t->host) (void)hipHostFree(t->host);
