@@ -61,6 +61,10 @@ __device__ __forceinline__ void piece(const uint8_t* p, uint64_t len, uint32_t o
 // The loads of CFSEC_CRC_AHEAD tiles are issued before any of them is folded (each thread's pieces
 // are independent loads; only the fold is a chain), so short runs -- a repair tasklet's 256 rebuilt
 // shards of 64 tiles, 8 per workgroup -- keep 8 loads per thread in flight instead of one.
+// CFSEC_CRC_DIAG (timing probes only, wrong words): 1 drops the alignment-basis multiply, 2 the fold
+#ifndef CFSEC_CRC_DIAG
+#define CFSEC_CRC_DIAG 0
+#endif
 #ifndef CFSEC_CRC_AHEAD
 #define CFSEC_CRC_AHEAD 8
 #endif
@@ -82,10 +86,19 @@ __global__ __launch_bounds__(256) void crc32_horner_kernel(const CrcArgs a) {
       if (t + k < t1) piece(p, a.len, (t + k) * kTile + lanepos, buf[k]);
 #pragma unroll
     for (int k = 0; k < A; ++k)
-      if (t + k < t1) R = crcdev::only_step(ct, R, buf[k]);
+      if (t + k < t1) {
+#if CFSEC_CRC_DIAG == 2
+        R = (R << 1 | R >> 31) ^ buf[k][0] ^ buf[k][1] ^ buf[k][2] ^ buf[k][3];
+#else
+        R = crcdev::only_step(ct, R, buf[k]);
+#endif
+      }
   }
   const u32x4* basis = reinterpret_cast<const u32x4*>(a.tabs + kTabWords + threadIdx.x * 32);
   uint32_t o = 0;
+#if CFSEC_CRC_DIAG == 1
+  o = R;
+#else
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const u32x4 v = basis[q];
@@ -94,6 +107,7 @@ __global__ __launch_bounds__(256) void crc32_horner_kernel(const CrcArgs a) {
     o ^= (0u - ((R >> (4 * q + 2)) & 1u)) & v.z;
     o ^= (0u - ((R >> (4 * q + 3)) & 1u)) & v.w;
   }
+#endif
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) o ^= (uint32_t)__shfl_xor((int)o, d);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = o;

@@ -192,6 +192,17 @@ __device__ __forceinline__ void st_chunk(uint8_t* p, const uint32_t (&x)[LW]) {
 #endif
 constexpr int fixed_lane_dwords(int K, int M) { return M >= CFSEC_LANE8_MIN_M ? 2 : 4; }
 
+// Tiles one workgroup of the fixed-K kernel codes, in sequence, for M <= CFSEC_FIXED_TPW_MAXM: a
+// single-output matrix (the LRC local stripes) does K loads and one store per lane, so the table
+// build and barrier are a visible share of a one-tile workgroup.
+#ifndef CFSEC_FIXED_TPW
+#define CFSEC_FIXED_TPW 1
+#endif
+#ifndef CFSEC_FIXED_TPW_MAXM
+#define CFSEC_FIXED_TPW_MAXM 1
+#endif
+constexpr int fixed_tiles_per_wg(int M) { return M <= CFSEC_FIXED_TPW_MAXM ? CFSEC_FIXED_TPW : 1; }
+
 // Product tables of one coefficient:
 //   t01 = {T0[0..3], T0[4..7], T1[0..3], T1[4..7]},  t2 = T2[0..3]
 // with T0[e] = coef*e, T1[e] = coef*(e<<3), T2[e] = coef*(e<<6).
@@ -495,7 +506,7 @@ __device__ __forceinline__ void lane_tile_k(int m, int nstore, const u32x4* tab0
 // one chunk of LW dwords per lane, tile = (256/OS)*4*LW bytes of every row, grid (tiles,
 // stripes); otherwise as matvec below.
 template <int K, int M, MatVecMode MODE, int D, int OS, bool NTL = true, bool NTS = true, bool PAIR = true,
-          int LW = 4>
+          int LW = 4, int TPW = 1>
 __device__ __forceinline__ void matvec_k(const GfArgs& a) {
   constexpr int MT = M * OS;
   __shared__ u32x4 tab01[K * MT];
@@ -508,23 +519,27 @@ __device__ __forceinline__ void matvec_k(const GfArgs& a) {
   const int cw = wave / OS;
   constexpr uint32_t kLB = 4 * LW;  // bytes per lane chunk
   constexpr uint32_t kTile = uint32_t(kThreads / OS) * kLB;
-  // 2-D grid (x: tiles of a stripe, y: stripes): a division of blockIdx.x would expand to VALU
-  // code and drag the row pointers into VGPRs
+  // 2-D grid (x: runs of TPW tiles of a stripe, y: stripes): a division of blockIdx.x would expand
+  // to VALU code and drag the row pointers into VGPRs
   const uint32_t stripe = blockIdx.y;
-  const uint32_t tile = blockIdx.x;
   const size_t tstripe = a.sstride ? 0 : (size_t)stripe;
   const int64_t sbase = (int64_t)stripe * a.sstride;
   const uint8_t* const* in = a.ptr + tstripe * K;
   uint8_t* const* out = const_cast<uint8_t* const*>(a.ptr + (size_t)a.tab * K + tstripe * a.m);
-  const uint32_t off = tile * kTile + (uint32_t)(cw * 64 + lane) * kLB;
   const uint64_t len = stripe_len(a, stripe);
   uint32_t diff = 0;
-  if (og < (int)a.m) {
-    if ((uint64_t)off + kLB <= len)
-      lane_tile_k<K, M, MT, MODE, D, NTL, NTS, PAIR, LW>((int)a.m, (int)a.nstore, tab01, tab2, in, out, og, sbase,
-                                                         off, diff);
-    else if (off < len)
-      lane_tail<M, MT, MODE>(a, tab01, tab2, in, out, og, (size_t)sbase + off, len - off, diff);
+#pragma unroll 1
+  for (int j = 0; j < TPW; ++j) {
+    const uint32_t tile = blockIdx.x * TPW + j;
+    if (TPW > 1 && tile >= a.tiles_per_stripe) break;
+    const uint32_t off = tile * kTile + (uint32_t)(cw * 64 + lane) * kLB;
+    if (og < (int)a.m) {
+      if ((uint64_t)off + kLB <= len)
+        lane_tile_k<K, M, MT, MODE, D, NTL, NTS, PAIR, LW>((int)a.m, (int)a.nstore, tab01, tab2, in, out, og, sbase,
+                                                           off, diff);
+      else if (off < len)
+        lane_tail<M, MT, MODE>(a, tab01, tab2, in, out, og, (size_t)sbase + off, len - off, diff);
+    }
   }
   if constexpr (MODE == MatVecMode::kVerify || MODE == MatVecMode::kStoreVerify) {
     if (diff) dev::set_flag(a.flags, stripe);

@@ -26,7 +26,8 @@ constexpr int fixed_d() {
 
 template <int K, int M, MatVecMode MODE>
 __global__ __launch_bounds__(256) void gf_matvec_k_kernel(const dev::GfArgs a) {
-  dev::matvec_k<K, M, MODE, fixed_d<MODE>(), 1, true, true, true, dev::fixed_lane_dwords(K, M)>(a);
+  dev::matvec_k<K, M, MODE, fixed_d<MODE>(), 1, true, true, true, dev::fixed_lane_dwords(K, M),
+                dev::fixed_tiles_per_wg(M)>(a);
 }
 
 template <int K, MatVecMode MODE, int M>
@@ -35,7 +36,9 @@ hipError_t launch_k(int m, const dev::GfArgs& a, dim3 grid, hipStream_t st) {
     return hipErrorInvalidValue;
   } else {
     if (m != M) return launch_k<K, MODE, M - 1>(m, a, grid, st);
-    hipLaunchKernelGGL((gf_matvec_k_kernel<K, M, MODE>), grid, dim3(256), 0, st, a);
+    constexpr unsigned T = dev::fixed_tiles_per_wg(M);
+    const dim3 g((grid.x + T - 1) / T, grid.y);
+    hipLaunchKernelGGL((gf_matvec_k_kernel<K, M, MODE>), g, dim3(256), 0, st, a);
     return hipGetLastError();
   }
 }
