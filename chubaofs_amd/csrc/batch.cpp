@@ -921,8 +921,10 @@ Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceCont
       const auto dptr = [&](const StripeTask* t, int idx) {
         return mem == CFSEC_MEM_DEVICE ? (const uint8_t*)t->shards[idx].data : (const uint8_t*)alias[{t, idx}];
       };
+      std::unique_ptr<HostTimer> gt(new HostTimer("      make_groups"));
       std::vector<Group> groups = make_groups(dph, &next_flag, dptr);
       route(groups);
+      gt.reset();
       // dy16 groups that checksum their rebuilt rows in the repair pass itself
       std::vector<std::vector<char>> crc_done(groups.size());
       bool any_crc_fused = false;
@@ -946,7 +948,10 @@ Status RSEngine::run_device(std::vector<StripeTask*>& tasks, int mem, DeviceCont
           fused.insert(gr.tasks.begin(), gr.tasks.end());
           continue;
         }
-        st = hip_status(launch_group(gr, ws->bflags, lane[0]), "launch_matvec(batch)");
+        {
+          HostTimer lt("      launch_group");
+          st = hip_status(launch_group(gr, ws->bflags, lane[0]), "launch_matvec(batch)");
+        }
         if (gr.crc_done) {
           int nf = 0;
           for (size_t i = 0; i < gr.tasks.size(); ++i)

@@ -47,9 +47,12 @@ __device__ __forceinline__ const uint8_t* shard_ptr(const CrcArgs& a, uint32_t i
   return reinterpret_cast<const uint8_t* const*>(a.flex + a.pw)[i];
 }
 
+#ifndef CFSEC_CRC_LDNT
+#define CFSEC_CRC_LDNT 1  // shard loads non-temporal (A/B: rows a repair pass just wrote)
+#endif
 __device__ __forceinline__ void piece(const uint8_t* p, uint64_t len, uint32_t off, uint32_t (&d)[4]) {
   if ((uint64_t)off + dev::kLaneBytes <= len) {
-    const u32x4 v = dev::ld16<true>(p + off);
+    const u32x4 v = dev::ld16<CFSEC_CRC_LDNT != 0>(p + off);
     d[0] = v.x, d[1] = v.y, d[2] = v.z, d[3] = v.w;
   } else {
     const size_t rem = off < len ? (size_t)(len - off) : 0;  // zero padding past the shard end

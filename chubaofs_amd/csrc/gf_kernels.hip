@@ -459,7 +459,12 @@ hipError_t launch_dy16_repair(const Dy16RepairJob& job, hipStream_t stream) {
     }
   }
   uint64_t tab_full = 0;
-  if (!sstride && job.nstripes > 1 && job.syn && kBs16 && nd <= kBsRepairMaxNd && !job.lens && kBsTab &&
+  // CFSEC_BS_FORCE_TAB=1 (A/B, read once): affine batches through the table launch too
+  static const bool kForceTab = [] {
+    const char* v = std::getenv("CFSEC_BS_FORCE_TAB");
+    return v && v[0] == '1';
+  }();
+  if ((!sstride || kForceTab) && job.nstripes > 1 && job.syn && kBs16 && nd <= kBsRepairMaxNd && !job.lens && kBsTab &&
       bs_matches(job.coef, 20 + ne, 16) && job.len >= kBs16Tile) {
     static thread_local std::vector<const uint8_t*> rows;
     rows.resize((size_t)job.nstripes * (16 + mo));

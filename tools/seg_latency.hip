@@ -28,6 +28,23 @@ __global__ void nop_kernel(int* p) {
   if (p && threadIdx.x == 0 && blockIdx.x == 0) p[0] = 1;
 }
 
+// the same with a kernel argument block the size of dev::GfArgs (3.5 KiB)
+struct BigArgs {
+  int* p;
+  uint8_t pad[3584 - 8];
+};
+__global__ void nop_big_kernel(const BigArgs a) {
+  if (a.p && threadIdx.x == 0 && blockIdx.x == 0) a.p[0] = a.pad[5];
+}
+
+// the same, ending with its own completion word in host memory (system-scope release store)
+__global__ void nop_mark_kernel(int* p, uint32_t* mark, uint32_t seq) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    p[0] = 1;
+    __hip_atomic_store(mark, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 static double now_us() {
   return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -69,8 +86,47 @@ int main(int argc, char** argv) {
     CK(hipStreamWriteValue32(st, dm, seq, 0));
     while (__atomic_load_n(hm, __ATOMIC_ACQUIRE) != seq) __builtin_ia32_pause();
   }, reps);
-  std::printf("{\"stream\": \"%s\", \"sync_floor_us\": %.1f, \"poll_floor_us\": %.1f", null_stream ? "null" : "own",
-              f_sync, f_poll);
+  const double f_kmark = median_us([&] {
+    ++seq;
+    hipLaunchKernelGGL(nop_mark_kernel, dim3(1), dim3(64), 0, st, flag, dm, seq);
+    while (__atomic_load_n(hm, __ATOMIC_ACQUIRE) != seq) __builtin_ia32_pause();
+  }, reps);
+  BigArgs big{};
+  big.p = flag;
+  const double f_big = median_us([&] {
+    hipLaunchKernelGGL(nop_big_kernel, dim3(1), dim3(64), 0, st, big);
+    ++seq;
+    CK(hipStreamWriteValue32(st, dm, seq, 0));
+    while (__atomic_load_n(hm, __ATOMIC_ACQUIRE) != seq) __builtin_ia32_pause();
+  }, reps);
+  // host cost of the launch calls alone (no wait): 64 B vs 3.5 KiB of arguments
+  const auto launch_cost = [&](bool large) {
+    CK(hipStreamSynchronize(st));
+    const double t0 = now_us();
+    for (int i = 0; i < 64; ++i) {
+      if (large) hipLaunchKernelGGL(nop_big_kernel, dim3(1), dim3(64), 0, st, big);
+      else hipLaunchKernelGGL(nop_kernel, dim3(1), dim3(64), 0, st, flag);
+    }
+    const double t = (now_us() - t0) / 64;
+    CK(hipStreamSynchronize(st));
+    return t;
+  };
+  double l_small = 1e9, l_big = 1e9;
+  for (int r = 0; r < 20; ++r) {
+    l_small = std::min(l_small, launch_cost(false));
+    l_big = std::min(l_big, launch_cost(true));
+  }
+  hipEvent_t ev;
+  CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  const double f_event = median_us([&] {
+    hipLaunchKernelGGL(nop_kernel, dim3(1), dim3(64), 0, st, flag);
+    CK(hipEventRecord(ev, st));
+    while (hipEventQuery(ev) == hipErrorNotReady) __builtin_ia32_pause();
+  }, reps);
+  std::printf("{\"stream\": \"%s\", \"sync_floor_us\": %.1f, \"poll_floor_us\": %.1f, \"kernel_mark_floor_us\": %.1f, "
+              "\"event_query_floor_us\": %.1f, \"poll_floor_3.5KiB_args_us\": %.1f, \"launch_call_us\": %.2f, "
+              "\"launch_call_3.5KiB_args_us\": %.2f", null_stream ? "null" : "own", f_sync, f_poll, f_kmark, f_event, f_big,
+              l_small, l_big);
   const int modes[2] = {2, 9};  // codemode.EC6P6, codemode.EC12P4 (codemode.go:30-60)
   const char* names[2] = {"EC6P6", "EC12P4"};
   for (int mi = 0; mi < 2; ++mi) {
