@@ -57,6 +57,9 @@ struct __attribute__((aligned(16))) GfArgs {
   const uint8_t* ptr[kPtrSlots];  // [tab*k inputs][tab*m outputs]
 };
 static_assert(sizeof(GfArgs) <= 3584, "kernel argument block must stay below 4 KiB");
+// Register-table launches of the fixed-K kernels (gf_fixed.hpp): the packed tables start this many
+// bytes into coef[], 16-byte aligned within the block
+constexpr size_t kRegTabOff = (16 - offsetof(GfArgs, coef) % 16) % 16;
 
 // Bytes in stripe s of the launch.
 __device__ __forceinline__ uint64_t stripe_len(const GfArgs& a, uint32_t s) {
@@ -170,10 +173,11 @@ __device__ __forceinline__ void ld_chunk(const uint8_t* p, uint32_t (&x)[LW]) {
   }
 }
 
-template <int LW, bool NTS>
+template <int LW, bool NTS, int SP = CFSEC_STORE_POL>
 __device__ __forceinline__ void st_chunk(uint8_t* p, const uint32_t (&x)[LW]) {
   if constexpr (LW == 4) {
-    st16_out<NTS>(p, u32x4{x[0], x[1], x[2], x[3]});
+    if constexpr (NTS) st16_pol<SP>(p, u32x4{x[0], x[1], x[2], x[3]});
+    else st16<false>(p, u32x4{x[0], x[1], x[2], x[3]});
   } else if constexpr (LW == 1) {
     if constexpr (NTS) asm volatile("global_store_dword %0, %1, off nt" ::"v"(p), "v"(x[0]) : "memory");
     else *reinterpret_cast<u32_ua*>(p) = x[0];
@@ -316,6 +320,34 @@ __device__ __forceinline__ void lane_tail(const GfArgs& a, const u32x4* tab01, c
   }
 }
 
+// lane_tail for a compile-time input count, one input row at a time (a rolled loop: unrolled, every
+// row's 16 byte loads were hoisted together and this rarely-taken path set the kernel's register
+// count -- C4's (8, 1) kernel 72 VGPRs against 48 for the full-tile path)
+template <int K, int M, int MT, MatVecMode MODE>
+__device__ __forceinline__ void lane_tail_k(const GfArgs& a, const u32x4* tab01, const uint32_t* tab2,
+                                            const uint8_t* const* in, uint8_t* const* out, int og,
+                                            size_t off, size_t rem, uint32_t& diff) {
+  const int m = (int)a.m;
+  u32x4 acc[M];
+#pragma unroll
+  for (int r = 0; r < M; ++r) acc[r] = u32x4{0u, 0u, 0u, 0u};
+#pragma unroll 1
+  for (int c = 0; c < K; ++c)
+    mac_row<M>(acc, ld_tail(in[c] + off, rem), tab01 + c * MT + og, tab2 + c * MT + og);
+#pragma unroll
+  for (int r = 0; r < M; ++r) {
+    if (og + r < m) {
+      uint8_t* p = out[og + r] + off;
+      if (row_compared<MODE>(a, og + r)) {
+        const u32x4 d = acc[r] ^ ld_tail(p, rem);
+        diff |= d.x | d.y | d.z | d.w;
+      } else {
+        st_tail(p, acc[r], rem);
+      }
+    }
+  }
+}
+
 // Full tile: W chunks per lane, all in bounds.  Input rows are loaded G at a time.
 template <int M, int MT, MatVecMode MODE, int W, int G, bool NTL, bool NTS>
 __device__ __forceinline__ void lane_tile(const GfArgs& a, const u32x4* tab01, const uint32_t* tab2,
@@ -413,8 +445,11 @@ __device__ __forceinline__ void mac_pair_k(uint32_t (&acc)[M][W], const uint32_t
 // VGPRs for K=12, M=4: one or two waves per SIMD), so each row ends by pinning the accumulators
 // (empty asm) behind a sched_barrier, and the row pointers (uniform: SGPR bases, 32-bit lane
 // offsets) are loaded once up front.  tools/gf_pipe.hip measured the effect.
-template <int K, int M, int MT, MatVecMode MODE, int D, bool NTL, bool NTS, bool PAIR = true, int LW = 4>
-__device__ __forceinline__ void lane_tile_k(int m, int nstore, const u32x4* tab01, const uint32_t* tab2,
+// PIN: the product tables are uniform values (register tables, matvec_k REG) -- read with the row
+// pointers, before the first barrier, so that both arrive in one round trip.
+template <int K, int M, int MT, MatVecMode MODE, int D, bool NTL, bool NTS, bool PAIR = true, int LW = 4,
+          int SP = CFSEC_STORE_POL, bool PIN = false>
+__device__ __forceinline__ void lane_tile_k(int m, int nstore, const u32x4* tab01_in, const uint32_t* tab2_in,
                                             const uint8_t* const* in, uint8_t* const* out, int og,
                                             int64_t sbase, uint32_t loff, uint32_t& diff) {
   static_assert(D >= 2, "the fixed-K tile consumes input rows in pairs, a pair ahead");
@@ -428,6 +463,18 @@ __device__ __forceinline__ void lane_tile_k(int m, int nstore, const u32x4* tab0
   for (int c = 0; c < K; ++c) row[c] = in[c] + sbase;
 #pragma unroll
   for (int r = 0; r < R - K; ++r) row[K + r] = out[og + r < m ? og + r : og] + sbase;
+  u32x4 p01[PIN ? K * MT : 1];
+  uint32_t p2[PIN ? K * MT : 1];
+  if constexpr (PIN) {
+#pragma unroll
+    for (int i = 0; i < K * MT; ++i) {
+      p01[i] = tab01_in[i];
+      p2[i] = tab2_in[i];
+      asm volatile("" : "+s"(p01[i].x), "+s"(p01[i].y), "+s"(p01[i].z), "+s"(p01[i].w), "+s"(p2[i]));
+    }
+  }
+  const u32x4* tab01 = PIN ? p01 : tab01_in;
+  const uint32_t* tab2 = PIN ? p2 : tab2_in;
   __builtin_amdgcn_sched_barrier(0);
 
   uint32_t acc[M][LW];
@@ -496,7 +543,7 @@ __device__ __forceinline__ void lane_tile_k(int m, int nstore, const u32x4* tab0
 #pragma unroll
           for (int w = 0; w < LW; ++w) acc[r][w] ^= y[w];
         }
-        st_chunk<LW, NTS>(p, acc[r]);
+        st_chunk<LW, NTS, SP>(p, acc[r]);
       }
     }
   }
@@ -506,13 +553,38 @@ __device__ __forceinline__ void lane_tile_k(int m, int nstore, const u32x4* tab0
 // one chunk of LW dwords per lane, tile = (256/OS)*4*LW bytes of every row, grid (tiles,
 // stripes); otherwise as matvec below.
 template <int K, int M, MatVecMode MODE, int D, int OS, bool NTL = true, bool NTS = true, bool PAIR = true,
-          int LW = 4, int TPW = 1>
+          int LW = 4, int TPW = 1, bool REG = false, int SP = CFSEC_STORE_POL>
 __device__ __forceinline__ void matvec_k(const GfArgs& a) {
+  static_assert(!REG || OS == 1, "register tables: one wave per column chunk");
+  static_assert(MODE != MatVecMode::kAccum, "the clamped row end re-codes bytes: stores and compares only");
   constexpr int MT = M * OS;
-  __shared__ u32x4 tab01[K * MT];
-  __shared__ uint32_t tab2[K * MT];
-  build_tables<MT>(a, tab01, tab2);
-  __syncthreads();
+  // REG: the host packed each coefficient's tables into the argument block's coef area, from byte
+  // kRegTabOff (16-byte aligned in the block): t01 of coefficient (c, r) as the (c * M + r)-th
+  // u32x4, then the t2 words -- read straight from the argument block (scalar loads), no LDS build,
+  // no barrier (single-output products: 0.65 -> 0.74-0.77 of 8 TB/s, tools/c4l_pattern_probe.hip)
+  // The full-tile path takes them as register copies made up front (read through the argument-block
+  // pointer inside the tile, each row's table waited for its own scalar load: 57 vs 51 us on C4's
+  // (8, 1)); the rarely-taken tail path indexes the argument block row by row.
+  __shared__ u32x4 lds01[REG ? 1 : K * MT];
+  __shared__ uint32_t lds2[REG ? 1 : K * MT];
+  const u32x4* ktab01 = reinterpret_cast<const u32x4*>(a.coef + kRegTabOff);
+  const uint32_t* ktab2 = reinterpret_cast<const uint32_t*>(a.coef + kRegTabOff + 16 * K * MT);
+  u32x4 reg01[REG ? K * MT : 1];
+  uint32_t reg2[REG ? K * MT : 1];
+  if constexpr (REG) {
+#pragma unroll
+    for (int i = 0; i < K * MT; ++i) {
+      reg01[i] = ktab01[i];
+      reg2[i] = ktab2[i];
+    }
+  } else {
+    build_tables<MT>(a, lds01, lds2);
+    __syncthreads();
+  }
+  const u32x4* tab01 = REG ? reg01 : lds01;
+  const uint32_t* tab2 = REG ? reg2 : lds2;
+  const u32x4* tail01 = REG ? ktab01 : lds01;
+  const uint32_t* tail2 = REG ? ktab2 : lds2;
 
   const int wave = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
   const int og = (wave % OS) * M;
@@ -522,23 +594,44 @@ __device__ __forceinline__ void matvec_k(const GfArgs& a) {
   // 2-D grid (x: runs of TPW tiles of a stripe, y: stripes): a division of blockIdx.x would expand
   // to VALU code and drag the row pointers into VGPRs
   const uint32_t stripe = blockIdx.y;
-  const size_t tstripe = a.sstride ? 0 : (size_t)stripe;
-  const int64_t sbase = (int64_t)stripe * a.sstride;
+  // Every argument word the row pointers and the stripe's length depend on, read in one round (the
+  // empty asm makes all of them live at once, so no load waits behind a branch on another): a
+  // workgroup codes one tile, so each dependent round trip to the argument block before its first
+  // row load shows (the stripe's length is selected, not branched on)
+  uint32_t varlen = a.varlen, tab = a.tab;
+  uint32_t slen = a.slen[stripe < (uint32_t)kLenSlots ? stripe : (uint32_t)kLenSlots - 1];
+  uint64_t len0 = a.len;
+  int64_t sstride = a.sstride;
+  asm volatile("" : "+s"(varlen), "+s"(tab), "+s"(slen), "+s"(len0), "+s"(sstride));
+  const uint32_t mrows = a.m;
+  const uint64_t len = varlen ? (uint64_t)slen : len0;
+  const size_t tstripe = sstride ? 0 : (size_t)stripe;
+  const int64_t sbase = (int64_t)stripe * sstride;
   const uint8_t* const* in = a.ptr + tstripe * K;
-  uint8_t* const* out = const_cast<uint8_t* const*>(a.ptr + (size_t)a.tab * K + tstripe * a.m);
-  const uint64_t len = stripe_len(a, stripe);
+  uint8_t* const* out = const_cast<uint8_t* const*>(a.ptr + (size_t)tab * K + tstripe * mrows);
   uint32_t diff = 0;
 #pragma unroll 1
   for (int j = 0; j < TPW; ++j) {
     const uint32_t tile = blockIdx.x * TPW + j;
     if (TPW > 1 && tile >= a.tiles_per_stripe) break;
     const uint32_t off = tile * kTile + (uint32_t)(cw * 64 + lane) * kLB;
-    if (og < (int)a.m) {
-      if ((uint64_t)off + kLB <= len)
-        lane_tile_k<K, M, MT, MODE, D, NTL, NTS, PAIR, LW>((int)a.m, (int)a.nstore, tab01, tab2, in, out, og, sbase,
-                                                           off, diff);
-      else if (off < len)
-        lane_tail<M, MT, MODE>(a, tab01, tab2, in, out, og, (size_t)sbase + off, len - off, diff);
+    // (m stays the launch's run-time value although it equals M here: with the compile-time M the
+    // StoreVerify kernels of (10, 4) / (12, 4) returned a wrong second row in
+    // test_reconstruct_stripes_mock_bids -- not understood, not taken)
+    // The ragged end of a row: the lane holding it codes the last full chunk of the row instead
+    // (clamped to end at len: its bytes before the end repeat its neighbour's, with the same values --
+    // plain stores and compares, never an accumulate), so every lane takes the one full-chunk path.
+    // A per-lane byte tail beside it cost 10 % on C4's (8, 1) product (56 vs 50 us,
+    // tools/c4l_pattern_probe.hip "regx F1" / "F8"); rows shorter than a chunk keep the byte path,
+    // under a branch uniform over the stripe.
+    if (og < (int)mrows && off < len) {
+      if (len >= kLB) {
+        const uint32_t loff = (uint64_t)off + kLB <= len ? off : (uint32_t)(len - kLB);
+        lane_tile_k<K, M, MT, MODE, D, NTL, NTS, PAIR, LW, SP>((int)mrows, (int)a.nstore, tab01, tab2, in, out, og,
+                                                               sbase, loff, diff);
+      } else {
+        lane_tail_k<K, M, MT, MODE>(a, tail01, tail2, in, out, og, (size_t)sbase + off, len - off, diff);
+      }
     }
   }
   if constexpr (MODE == MatVecMode::kVerify || MODE == MatVecMode::kStoreVerify) {

@@ -306,3 +306,27 @@ def test_large_stripe_roundtrip_ec12p4(rs):
     flags = torch.zeros(2, dtype=torch.int32, device="cuda")
     enc.verify_batch(ptrs, S, 2, flags.data_ptr())
     assert flags.cpu().tolist() == [0, 0]
+
+
+@pytest.mark.parametrize("k,m", [(8, 1), (12, 1), (6, 2), (3, 4), (10, 4), (12, 4), (16, 4)])
+@pytest.mark.parametrize("size", [16, 17, 31, 4096 + 5, 65536 + 15, 174763])
+def test_ragged_row_end_encode_verify_reconstruct(rs, k, m, size):
+    """The fixed-K kernels code a row's ragged end as the last full 16-byte chunk of the row (the
+    lane's bytes before the end repeat its neighbour's with the same values): encode equals the
+    oracle to the last byte, Verify catches a flip in the last byte of any row (and in the first byte
+    of the overlapped chunk), Reconstruct rebuilds the last bytes of lost rows."""
+    want = oracle_encoded(k, m, size, seed=size * 7 + k)
+    enc = engine(rs, k, m)
+    d = to_dev([s if i < k else np.zeros(size, np.uint8) for i, s in enumerate(want)])
+    enc.Encode(d)
+    got = to_host(d)
+    for i in range(k + m):
+        assert np.array_equal(got[i], want[i]), (i, size)
+    assert enc.Verify(to_dev(want))
+    for idx in (k + m - 1, k, 0):
+        for pos in (size - 1, max(0, size - 16)):
+            bad = [s.copy() for s in want]
+            bad[idx][pos] ^= 0x80
+            assert not enc.Verify(to_dev(bad)), (idx, pos, size)
+    for erased, data_only in (({0}, True), (set(range(min(m, k))), False), ({k - 1, k + m - 1} if m > 1 else {k}, False)):
+        _check_recon(rs, k, m, size, erased, data_only, seed=size + len(erased))
