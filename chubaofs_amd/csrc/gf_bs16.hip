@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstddef>
 #include <cstring>
 #include <map>
@@ -830,9 +831,13 @@ hipError_t launch_bs16_repair(int nd, int ne, const uint8_t* missing, const uint
 
 int bs_tab_stripes(int mo) { return kBsTabWords / (kBsK + mo); }
 
-// The row-offset tables in device memory (TAB 2: any number of stripes in one launch): a ring of
-// kBsDevTables per device, each slot a pinned staging copy and its device twin, free again once the
-// launch that read it has completed (its event, polled).  A launch takes a free slot without
+// The row-offset tables (TAB 2: any number of stripes in one launch): a ring of kBsDevTables per
+// device, each slot a table in mapped, coherent host memory that the kernel reads directly (no copy
+// launch: a blit copy into a device twin, read through another XCD's L2 by the next kernel's scalar
+// loads, is the one cross-launch hand-off this path had, and round 4's and round 5's false Verify
+// flags on the scattered layout came only from it; the direct read measured the same time per call,
+// profiles/r05/scattered_c5_upload.txt "host"), free again once the launch that read it has
+// completed (its event, polled).  A launch takes a free slot without
 // waiting; only when every slot is still in flight -- the host kBsDevTables launches ahead of the
 // GPU, e.g. back-to-back asynchronous tasklets -- does it wait for the oldest one, a bounded queue's
 // backpressure (the argument-block fallback measured 0.147 -> 0.205 ms per scattered C5 call when
@@ -891,13 +896,15 @@ BsDevTable* dev_table_reserve(BsDevTables& r, size_t n) {
   if (!t->done && hipEventCreateWithFlags(&t->done, hipEventDisableTiming) != hipSuccess) return nullptr;
   if (n <= t->cap) return t;
   if (t->host) (void)hipHostFree(t->host);
-  if (t->dev) (void)hipFree(t->dev);
   t->host = nullptr;
   t->dev = nullptr;
   t->cap = 0;
   const size_t cap = std::max<size_t>(n, kBsDevTableMin);
-  if (hipHostMalloc(reinterpret_cast<void**>(&t->host), cap * 4, hipHostMallocDefault) != hipSuccess) return nullptr;
-  if (hipMalloc(reinterpret_cast<void**>(&t->dev), cap * 4) != hipSuccess) {
+  if (hipHostMalloc(reinterpret_cast<void**>(&t->host), cap * 4, hipHostMallocMapped | hipHostMallocCoherent) !=
+      hipSuccess)
+    return nullptr;
+  if (hipHostGetDevicePointer(reinterpret_cast<void**>(&t->dev), t->host, 0) != hipSuccess) {
+    (void)hipGetLastError();
     (void)hipHostFree(t->host);
     t->host = nullptr;
     return nullptr;
@@ -936,8 +943,8 @@ hipError_t launch_bs16_repair_tab(int nd, int ne, const uint8_t* missing, const 
     std::lock_guard<std::mutex> lk(ring->mu);
     if (BsDevTable* dt = dev_table_reserve(*ring, nrows)) {
       for (size_t i = 0; i < nrows; ++i) dt->host[i] = (uint32_t)((uintptr_t)rows[i] - lo);
-      hipError_t e = hipMemcpyAsync(dt->dev, dt->host, nrows * 4, hipMemcpyHostToDevice, st);
-      if (e != hipSuccess) return e;
+      std::atomic_thread_fence(std::memory_order_release);  // the table before the launch that reads it
+      hipError_t e = hipSuccess;
       r.dtab = dt->dev;
       t.nstripes = ns;
       const uint64_t ntiles = (uint64_t)tps * ns;
@@ -999,8 +1006,7 @@ hipError_t launch_bs_tab(int k, int m, const dev::GfArgs& a, const uint8_t* cons
   BsDevTable* dt = dev_table_reserve(*ring, nrows);
   if (!dt) return hipSuccess;  // not ok: every table in flight, the caller keeps its route
   for (size_t i = 0; i < nrows; ++i) dt->host[i] = (uint32_t)((uintptr_t)rows[i] - lo);
-  hipError_t e = hipMemcpyAsync(dt->dev, dt->host, nrows * 4, hipMemcpyHostToDevice, st);
-  if (e != hipSuccess) return e;
+  std::atomic_thread_fence(std::memory_order_release);  // the table before the launch that reads it
   *ok = true;
   static thread_local dev::GfArgs t;
   std::memcpy(&t, &a, sizeof(dev::GfArgs));
@@ -1009,8 +1015,8 @@ hipError_t launch_bs_tab(int k, int m, const dev::GfArgs& a, const uint8_t* cons
   t.nstripes = ns;
   const BsTabArgs tb{reinterpret_cast<const uint8_t*>(lo), dt->dev};
   const unsigned grid = (unsigned)std::min<uint64_t>((uint64_t)cu_count(), (ntiles + kBsWaves - 1) / kBsWaves);
-  e = m == 22 ? launch_net<dev::BsEc16p20l2, 22, 2>(t, grid, tps, (uint32_t)ntiles, st, tb)
-              : launch_net<dev::BsEc16p20l2, 20, 2>(t, grid, tps, (uint32_t)ntiles, st, tb);
+  hipError_t e = m == 22 ? launch_net<dev::BsEc16p20l2, 22, 2>(t, grid, tps, (uint32_t)ntiles, st, tb)
+                         : launch_net<dev::BsEc16p20l2, 20, 2>(t, grid, tps, (uint32_t)ntiles, st, tb);
   if (e != hipSuccess) return e;
   e = hipEventRecord(dt->done, st);
   if (e != hipSuccess) return e;
