@@ -237,6 +237,7 @@ __device__ __forceinline__ void matvec_dy(const GfArgs& a) {
   static_assert(K % B == 0 && MD % B == 0 && (B == 2 || B == 4), "dyadic shape");
   using Sh = DyShape<MD, B, RBW_>;
   static_assert(E == 0 || Sh::OS == 1, "plain rows ride along single-wave shapes only");
+  static_assert(MODE == MatVecMode::kStore || MODE == MatVecMode::kVerify, "the clamped row end: stores, compares");
   constexpr int KB = K / B, MB = MD / B, NC = Dy<B>::NC, RBW = Sh::RBW, MW = RBW * B;
   constexpr int MBP = Sh::OS * RBW;  // row blocks incl. the last wave's padding
   constexpr int ND = MBP * KB * NC;  // dyadic table slots; the plain rows' follow
@@ -254,7 +255,7 @@ __device__ __forceinline__ void matvec_dy(const GfArgs& a) {
   const uint32_t stripe = blockIdx.y, tile = blockIdx.x;
   const size_t ts = a.sstride ? 0 : (size_t)stripe;
   const int64_t sbase = (int64_t)stripe * a.sstride;
-  const uint32_t off = tile * (uint32_t)Sh::kTileBytes + (uint32_t)(cw * 64 + lane) * kLaneBytes;
+  uint32_t off = tile * (uint32_t)Sh::kTileBytes + (uint32_t)(cw * 64 + lane) * kLaneBytes;
   const uint8_t* row[K + MW + E];
 #pragma unroll
   for (int c = 0; c < K; ++c) row[c] = a.ptr[ts * K + c] + sbase;
@@ -284,9 +285,15 @@ __device__ __forceinline__ void matvec_dy(const GfArgs& a) {
   const auto sb = [&]() {
     if constexpr (PIN) __builtin_amdgcn_sched_barrier(0);
   };
+  // The ragged end of a row: the lane holding it codes the row's last full 16-byte chunk instead (its
+  // bytes before the end repeat its neighbour's, same values: stores and compares only), so in rows of
+  // at least 16 bytes no lane takes the byte path -- whose dependent byte loads made each row's last
+  // workgroup a straggler that ended the launch late (gf_lut.hpp).  One body, `off` moved.
   const uint64_t slen = stripe_len(a, stripe);
+  const bool inrow = off < slen;
+  if (inrow && slen >= kLaneBytes && (uint64_t)off + kLaneBytes > slen) off = (uint32_t)(slen - kLaneBytes);
   const bool full = (uint64_t)off + kLaneBytes <= slen;
-  const size_t rem = off < slen ? (size_t)(slen - off) : 0;
+  const size_t rem = inrow ? (size_t)(slen - off) : 0;
   uint32_t diff = 0;
   if (full || rem) {
     uint32_t x[K][4];

@@ -259,10 +259,19 @@ __global__ __launch_bounds__(256) void gf_lut_kernel(const dev::GfArgs a) {
   const uint32_t off = tile * (256u * kLB) + threadIdx.x * kLB;
   const uint64_t len = dev::stripe_len(a, stripe);
   uint32_t diff = 0;
+  // The ragged end of a row: the lane holding it codes the row's last full chunk instead (its bytes
+  // before the end repeat its neighbour's, same values: stores and compares only), so in rows of at
+  // least one chunk no lane takes the byte path.  That path -- 16 dependent byte loads per input row
+  // -- made the row's last workgroup a straggler, and the last stripe's last one ended the launch
+  // ~10 us late: EC15P12 encode 75.6 -> 65.8 us, EC12P9 56.6 -> 46.6 (tools/gf_shapes.hip,
+  // profiles/r05/shape_sweep_lut_clamp.txt).  (Calling the chunk body from a second, byte-path-free
+  // instantiation instead returned wrong rows for the mixed lookup + v_perm shapes: one body.)
+  static_assert(MODE != MatVecMode::kAccum, "the clamped row end re-codes bytes: stores and compares only");
   if ((uint64_t)off < len) {
-    const uint32_t rem = (uint64_t)off + kLB <= len ? kLB : (uint32_t)(len - off);
-    lut_chunk<K, M, ML, MODE, LA, LW>(reinterpret_cast<const char*>(T), tab01, tab2, in, out, (int)a.nstore, sbase, off, rem,
-                              diff);
+    const uint32_t loff = len >= kLB && (uint64_t)off + kLB > len ? (uint32_t)(len - kLB) : off;
+    const uint32_t rem = (uint64_t)loff + kLB <= len ? kLB : (uint32_t)(len - loff);
+    lut_chunk<K, M, ML, MODE, LA, LW>(reinterpret_cast<const char*>(T), tab01, tab2, in, out, (int)a.nstore, sbase, loff,
+                                      rem, diff);
   }
   if constexpr (MODE == MatVecMode::kVerify || MODE == MatVecMode::kStoreVerify) {
     if (diff) dev::set_flag(a.flags, stripe);
