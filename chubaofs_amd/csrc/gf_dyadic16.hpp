@@ -224,7 +224,7 @@ __device__ __forceinline__ void matvec_dy16(const GfArgs& a) {
   const uint32_t stripe = blockIdx.y, tile = blockIdx.x;
   const size_t ts = a.sstride ? 0 : (size_t)stripe;
   const int64_t sbase = (int64_t)stripe * a.sstride;
-  const uint32_t off = tile * (256u * kLane) + (uint32_t)threadIdx.x * kLane;
+  uint32_t off = tile * (256u * kLane) + (uint32_t)threadIdx.x * kLane;
   const uint8_t* row[K + M];
 #pragma unroll
   for (int c = 0; c < K; ++c) row[c] = a.ptr[ts * K + c] + sbase;
@@ -232,9 +232,13 @@ __device__ __forceinline__ void matvec_dy16(const GfArgs& a) {
   for (int r = 0; r < M; ++r) row[K + r] = a.ptr[(size_t)a.tab * K + ts * M + r] + sbase;
   __builtin_amdgcn_sched_barrier(0);
 
+  // the ragged end of a row as the row's last full lane chunk (gf_dyadic.hpp matvec_dy): no lane of a
+  // row of at least one chunk takes the byte path
   const uint64_t slen = stripe_len(a, stripe);
+  const bool inrow = off < slen;
+  if (inrow && slen >= kLane && (uint64_t)off + kLane > slen) off = (uint32_t)(slen - kLane);
   const bool full = (uint64_t)off + kLane <= slen;
-  const size_t rem = off < slen ? (size_t)(slen - off) : 0;
+  const size_t rem = inrow ? (size_t)(slen - off) : 0;
   uint32_t diff = 0;
   if (full || rem) {
     uint32_t x[K][W];
@@ -296,10 +300,14 @@ __device__ __forceinline__ void repair_dy16(const GfArgs& a) {
   const uint32_t stripe = blockIdx.y, tile = blockIdx.x;
   const size_t ts = a.sstride ? 0 : (size_t)stripe;
   const int64_t sbase = (int64_t)stripe * a.sstride;
-  const uint32_t off = tile * (256u * kLane) + (uint32_t)threadIdx.x * kLane;
+  uint32_t off = tile * (256u * kLane) + (uint32_t)threadIdx.x * kLane;
+  // the ragged end of a row as the row's last full lane chunk (gf_dyadic.hpp matvec_dy): no lane of a
+  // row of at least one chunk takes the byte path
   const uint64_t slen = stripe_len(a, stripe);
+  const bool inrow = off < slen;
+  if (inrow && slen >= kLane && (uint64_t)off + kLane > slen) off = (uint32_t)(slen - kLane);
   const bool full = (uint64_t)off + kLane <= slen;
-  const size_t rem = off < slen ? (size_t)(slen - off) : 0;
+  const size_t rem = inrow ? (size_t)(slen - off) : 0;
   uint32_t diff = 0;
   if (full || rem) {
     const uint8_t* const* in = a.ptr + ts * K;
