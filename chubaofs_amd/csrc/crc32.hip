@@ -56,7 +56,7 @@ __device__ __forceinline__ void piece(const uint8_t* p, uint64_t len, uint32_t o
     d[0] = v.x, d[1] = v.y, d[2] = v.z, d[3] = v.w;
   } else {
     const size_t rem = off < len ? (size_t)(len - off) : 0;  // zero padding past the shard end
-    const u32x4 v = rem ? dev::ld_tail(p + off, rem) : u32x4{0u, 0u, 0u, 0u};
+    const u32x4 v = rem ? dev::ld_tail_row(p + off, rem, len) : u32x4{0u, 0u, 0u, 0u};
     d[0] = v.x, d[1] = v.y, d[2] = v.z, d[3] = v.w;
   }
 }

@@ -273,7 +273,7 @@ __device__ __forceinline__ void crc_tile(uint64_t len, const u32x4* tab01, const
     for (int c = 0; c < K; ++c) {
       uint32_t xv[4] = {0u, 0u, 0u, 0u};
       if (rem) {
-        const u32x4 v = dev::ld_tail(row[c] + off, rem);
+        const u32x4 v = dev::ld_tail_row(row[c] + off, rem, len);
         xv[0] = v.x;
         xv[1] = v.y;
         xv[2] = v.z;
@@ -365,7 +365,7 @@ __device__ __forceinline__ void crc_tile_dy(uint64_t len, const u32x4* tab01, co
     for (int cb = 0; cb < KB; ++cb) {
       uint32_t x[B][4];
       for (int c = 0; c < B; ++c) {
-        const u32x4 v = rem ? dev::ld_tail(row[B * cb + c] + off, rem) : u32x4{0u, 0u, 0u, 0u};
+        const u32x4 v = rem ? dev::ld_tail_row(row[B * cb + c] + off, rem, len) : u32x4{0u, 0u, 0u, 0u};
         x[c][0] = v.x;
         x[c][1] = v.y;
         x[c][2] = v.z;
@@ -576,7 +576,7 @@ __device__ __forceinline__ void crc_tile_lds(uint64_t len, const char* E, const 
   const auto load = [&](int c, uint32_t o, bool f) {
     u32x4 v;
     if (f) v = dev::ld16<true>(row[c] + o);
-    else v = rem ? dev::ld_tail(row[c] + o, rem) : u32x4{0u, 0u, 0u, 0u};
+    else v = rem ? dev::ld_tail_row(row[c] + o, rem, len) : u32x4{0u, 0u, 0u, 0u};
     x[c][0] = v.x;
     x[c][1] = v.y;
     x[c][2] = v.z;

@@ -146,6 +146,25 @@ __device__ __forceinline__ u32x4 ld_tail(const uint8_t* p, size_t rem) {
   return u32x4{w[0], w[1], w[2], w[3]};
 }
 
+// ld_tail of a row's last piece (p + rem is the row's end, rem < 16): with a row of at least 16
+// bytes, one 16-byte load of the row's last 16 bytes shifted down by 16 - rem bytes, zeros in --
+// the byte loads' 16 dependent round trips made the lane holding a row's end a straggler that ended
+// a launch late (the fused checksum kernels, whose pieces cannot overlap their neighbours' bytes).
+__device__ __forceinline__ u32x4 ld_tail_row(const uint8_t* p, size_t rem, uint64_t len) {
+  if (len < 16) return ld_tail(p, rem);
+  const u32x4 v = ld16<true>(p + rem - 16);
+  const uint32_t s = 16u - (uint32_t)rem, d = s >> 2, b = s & 3u;
+  const uint32_t w[5] = {v.x, v.y, v.z, v.w, 0u};
+  uint32_t a[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) a[j] = b ? __builtin_amdgcn_alignbyte(w[j + 1], w[j], b) : w[j];
+  const uint32_t r0 = d == 0 ? a[0] : d == 1 ? a[1] : d == 2 ? a[2] : a[3];
+  const uint32_t r1 = d == 0 ? a[1] : d == 1 ? a[2] : d == 2 ? a[3] : 0u;
+  const uint32_t r2 = d == 0 ? a[2] : d == 1 ? a[3] : 0u;
+  const uint32_t r3 = d == 0 ? a[3] : 0u;
+  return u32x4{r0, r1, r2, r3};
+}
+
 __device__ __forceinline__ void st_tail(uint8_t* p, u32x4 v, size_t rem) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
