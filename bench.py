@@ -938,6 +938,12 @@ def gated_calls(torch, stream, call, nbatch, seconds, zero, check, sync_call):
     sum of the pairs is the device time of the calls' kernels alone ("kernel-only"), and the first
     to last event the pipelined rate (host planning of call i+1 overlapping the kernels of call i).
     Returns dict(calls_per_s=..., kernel_ms_per_call=..., n=...)."""
+    # Whatever the caller prepared on other streams (torch's copies onto its current stream, e.g. the
+    # scattered C5 pool) is complete before the first call: the asynchronous calls run on `stream`,
+    # which does not wait for torch's stream.  Without this the scattered C5 run's first warm calls
+    # could read half-copied rows under load -- the "false Verify" flags of the N = 2 rehearsals in
+    # rounds 4 and 5 (flags set by those warm calls, never cleared; the rows right at the end).
+    torch.cuda.synchronize()
     for i in range(2 * nbatch):
         call(i)
     torch.cuda.synchronize()
@@ -1299,6 +1305,7 @@ def other_configs(args, torch, dev, stream, cpu):
             got = torch.stack([torch.stack([scv5[b][bid][i] for i in er5]) for bid in range(nb5)])
             assert torch.equal(got, gold5[b, :, er5]), "C5 scattered: rebuilt rows differ from the golden"
 
+    fl5.zero_()  # this run's flags only
     rsc = gated_calls(torch, stream, rep5s, NBATCH, secs, zero5s, check5s, sync_call=False)
     check5_status("scattered run")
     del sc5, scv5, pool5
