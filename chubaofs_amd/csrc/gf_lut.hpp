@@ -111,6 +111,17 @@ __device__ __forceinline__ void untranspose4(const uint32_t (&g)[4 * LW], uint32
 #ifndef CFSEC_LUT_LOOKAHEAD
 #define CFSEC_LUT_LOOKAHEAD 2
 #endif
+// Verify: the compared rows' loads issued right after the last input row's (overlapping the last
+// D + 1 columns' lookups) instead of after the product, where the held words fit: EC16P20's 8-row
+// repair verify 77 -> 69 us, EC15P12 verify 72 -> 66 us; at 32-36 held words (EC16P20 16 rows,
+// EC12P9) the occupancy halves and Verify slows 1.4-2.4x, and K = 16, M = 12 takes 106 VGPRs
+// (profiles/r05/lut_verify_early_loads.txt).  0 = off (A/B).
+#ifndef CFSEC_LUT_VPRE
+#define CFSEC_LUT_VPRE 1
+#endif
+#ifndef CFSEC_LUT_VPRE_MAXW
+#define CFSEC_LUT_VPRE_MAXW 24  // compared words per lane held early, at most
+#endif
 
 // One 16-byte chunk of every row at byte `off` of the stripe (all in bounds, or the tail chunk with
 // rem < 16 valid bytes).  Outputs [0, ML) come from the lookups, [ML, M) from the v_perm product
@@ -139,6 +150,9 @@ __device__ __forceinline__ void lut_chunk(const char* T, const u32x4* tab01, con
 #pragma unroll
     for (int w = 0; w < LW; ++w) accp[r][w] = 0u;
   uint32_t x[K][LW];
+  constexpr bool kPre = CFSEC_LUT_VPRE && MODE == MatVecMode::kVerify && M * LW <= CFSEC_LUT_VPRE_MAXW &&
+                          K * M <= 180;
+  uint32_t y[kPre ? M : 1][LW];
   const auto load = [&](int c) {
     if (full) {
       dev::ld_chunk<LW, true>(in[c] + sbase + off, x[c]);
@@ -154,6 +168,22 @@ __device__ __forceinline__ void lut_chunk(const char* T, const u32x4* tab01, con
 #pragma unroll
   for (int c = 0; c < K; ++c) {
     if (c + D < K) load(c + D);
+    if constexpr (kPre) {
+      if (c == K - D - 1 || (D >= K && c == 0)) {
+#pragma unroll
+        for (int r = 0; r < M; ++r) {
+          const uint8_t* p = out[r] + sbase + off;
+          if (full) {
+            dev::ld_chunk<LW, true>(p, y[r]);
+          } else {
+            const u32x4 v = dev::ld_tail(p, rem);
+            const uint32_t t[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int w = 0; w < LW; ++w) y[r][w] = t[w];
+          }
+        }
+      }
+    }
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (NQ > 0) {
       const char* tc = T + c * 2 * 16 * EB;
@@ -196,6 +226,13 @@ __device__ __forceinline__ void lut_chunk(const char* T, const u32x4* tab01, con
   const auto finish = [&](int r, const uint32_t (&o)[LW]) {
     uint8_t* p = out[r] + sbase + off;
     const bool cmp = kVer || (kMix && r >= nstore);
+    if constexpr (kPre) {
+      uint32_t d = 0;
+#pragma unroll
+      for (int w = 0; w < LW; ++w) d |= o[w] ^ y[r][w];
+      diff |= d;  // (the tail's bytes past rem: zeros in both)
+      return;
+    }
     if (full) {
       if (cmp) {
         uint32_t y[LW];
