@@ -30,7 +30,10 @@ inline int lut_outputs(int k, int m, bool dyadic = false) {
 // Lane chunk of the lookup kernel for k inputs: 8 bytes (EC15P12: 64 instead of 107 VGPRs, 8 waves
 // per SIMD instead of 4; encode 96 -> 81 us, verify unchanged: profiles/r03/lut_probe4.txt), 16 bytes
 // for k = 12 (EC12P9: no difference).  The launch grid's tiles are 256 lanes of it.
-constexpr int lut_lane_dwords(int k) { return k == 12 ? 4 : 2; }
+#ifndef CFSEC_LUT_K12_LW
+#define CFSEC_LUT_K12_LW 4
+#endif
+constexpr int lut_lane_dwords(int k) { return k == 12 ? CFSEC_LUT_K12_LW : 2; }
 constexpr size_t lut_tile_bytes(int k) { return size_t(256) * 4 * lut_lane_dwords(k); }
 
 template <int K>
