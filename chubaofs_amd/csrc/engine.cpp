@@ -969,11 +969,11 @@ Status RSEngine::reconstruct_batch(uint8_t* const* ptrs, size_t S, int nstripes,
   return hip_status(launch_matvec(job, stream), "launch_matvec(reconstruct_batch)");
 }
 
-// Product + checksums: the fused kernel where it exists, else the product then the standalone
-// CRC kernel over the same shards (one more read of each).
+// Product + checksums: the fused kernel where it takes the job, else the product then the
+// standalone CRC kernel over the same shards (one more read of each).
 static Status matvec_with_crc(const MatVecJob& job, uint8_t* const* ptrs, int total, const std::vector<int>& slot,
                               size_t S, uint32_t* crcs, hipStream_t stream) {
-  if (matvec_crc_supported(job.k, job.m, S, job.coef))
+  if (matvec_crc_accepts(job, total, slot.data()))
     return hip_status(launch_matvec_crc(job, crcs, total, slot.data(), stream), "launch_matvec_crc");
   Status st = hip_status(launch_matvec(job, stream), "launch_matvec");
   if (st != CFSEC_OK) return st;

@@ -853,7 +853,8 @@ struct BsDevTable {
   size_t cap = 0;
   hipEvent_t done = nullptr;
   bool pending = false;
-  uint64_t seq = 0;  // when it was last taken
+  bool dead = false;  // a launch may still read it and no event says when it ends: never reused
+  uint64_t seq = 0;   // when it was last taken
 };
 struct BsDevTables {
   std::mutex mu;
@@ -874,6 +875,7 @@ BsDevTable* dev_table_reserve(BsDevTables& r, size_t n) {
   BsDevTable* t = nullptr;
   BsDevTable* oldest = nullptr;
   for (BsDevTable& c : r.slot) {
+    if (c.dead) continue;
     if (c.pending) {
       const hipError_t q = hipEventQuery(c.done);
       if (q == hipErrorNotReady) {
@@ -911,6 +913,20 @@ BsDevTable* dev_table_reserve(BsDevTables& r, size_t n) {
   }
   t->cap = cap;
   return t;
+}
+
+// After a launch that reads dt's table: the event that frees the slot.  If it cannot be recorded the
+// launch may still be reading the row offsets, so the slot is not handed out again before the stream
+// has drained (or ever, when even that fails) -- a later reservation would rewrite the mapped table
+// under the kernel.
+hipError_t dev_table_fence(BsDevTable* dt, hipStream_t st) {
+  const hipError_t e = hipEventRecord(dt->done, st);
+  if (e == hipSuccess) {
+    dt->pending = true;
+    return hipSuccess;
+  }
+  if (hipStreamSynchronize(st) != hipSuccess) dt->dead = true;
+  return e;
 }
 
 hipError_t launch_bs16_repair_tab(int nd, int ne, const uint8_t* missing, const uint8_t* prow, const uint8_t* ainv,
@@ -959,10 +975,7 @@ hipError_t launch_bs16_repair_tab(int nd, int ne, const uint8_t* missing, const 
                     : launch_rep_m<20, 2>(nd, t, r, grid, tps, (uint32_t)ntiles, st);
       if (e != hipSuccess) return e;
       if (fused && crc_done) *crc_done = true;
-      e = hipEventRecord(dt->done, st);
-      if (e != hipSuccess) return e;
-      dt->pending = true;
-      return hipSuccess;
+      return dev_table_fence(dt, st);
     }
   }
   for (unsigned s0 = 0; s0 < ns; s0 += (unsigned)per) {
@@ -1018,10 +1031,7 @@ hipError_t launch_bs_tab(int k, int m, const dev::GfArgs& a, const uint8_t* cons
   hipError_t e = m == 22 ? launch_net<dev::BsEc16p20l2, 22, 2>(t, grid, tps, (uint32_t)ntiles, st, tb)
                          : launch_net<dev::BsEc16p20l2, 20, 2>(t, grid, tps, (uint32_t)ntiles, st, tb);
   if (e != hipSuccess) return e;
-  e = hipEventRecord(dt->done, st);
-  if (e != hipSuccess) return e;
-  dt->pending = true;
-  return hipSuccess;
+  return dev_table_fence(dt, st);
 }
 
 }  // namespace cfsec

@@ -153,11 +153,11 @@ int64_t affine_stride(const MatVecJob& job) {
 template <bool CIN>
 int lds_per_cu(int k, int m) {
   static std::mutex mu;
-  static std::map<std::pair<int, int>, int> cache;  // (device, k * 8 + m)
+  static std::map<std::pair<int, int>, int> cache;  // (device, k * 64 + m)
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   std::lock_guard<std::mutex> l(mu);
-  const auto key = std::make_pair(dev, k * 8 + m);
+  const auto key = std::make_pair(dev, k * 64 + m);
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
   int n = 0;
@@ -201,17 +201,24 @@ bool matvec_crc_supported(int k, int m, size_t len, const uint8_t* coef) {
 
 uint32_t crc32_shift_ones(size_t len) { return mulmod(xpow(8 * (int64_t)len), 0xFFFFFFFFu) ^ 0xFFFFFFFFu; }
 
+bool matvec_crc_accepts(const MatVecJob& job, int crc_stride, const int* slot) {
+  if (job.mode != MatVecMode::kStore || !matvec_crc_supported(job.k, job.m, job.len, job.coef) || !slot ||
+      crc_stride <= 0 || crc_stride > 256 || job.nstripes < 0 || !job.coef || !job.in || !job.out)
+    return false;
+  const bool cin = slot[0] >= 0;
+  for (int i = 0; i < job.k + job.m; ++i) {
+    const bool want = i >= job.k || cin;
+    if (want && (slot[i] < 0 || slot[i] >= crc_stride)) return false;
+  }
+  // EC6P10L2's fused encode is instantiated with its inputs checksummed only (every shard, as Put does)
+  return !(job.m > 6 && !cin);
+}
+
 hipError_t launch_matvec_crc(const MatVecJob& job, uint32_t* crc, int crc_stride, const int* slot,
                              hipStream_t stream, bool zero) {
-  if (job.mode != MatVecMode::kStore || !matvec_crc_supported(job.k, job.m, job.len, job.coef) || !crc || !slot ||
-      crc_stride <= 0 || crc_stride > 256 || job.nstripes < 0 || !job.coef || !job.in || !job.out)
-    return hipErrorInvalidValue;
+  if (!crc || !matvec_crc_accepts(job, crc_stride, slot)) return hipErrorInvalidValue;
   const int k = job.k, m = job.m;
   const bool cin = slot[0] >= 0;
-  for (int i = 0; i < k + m; ++i) {
-    const bool want = i >= k || cin;
-    if (want && (slot[i] < 0 || slot[i] >= crc_stride)) return hipErrorInvalidValue;
-  }
   hipError_t e = zero ? hipMemsetAsync(crc, 0, sizeof(uint32_t) * (size_t)crc_stride * job.nstripes, stream)
                       : hipSuccess;
   if (e != hipSuccess || job.nstripes == 0 || job.len == 0) return e;

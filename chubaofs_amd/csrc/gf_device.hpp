@@ -102,17 +102,30 @@ __device__ __forceinline__ void st16(uint8_t* p, u32x4 v) {
   else *reinterpret_cast<u32x4_ua*>(p) = v;
 }
 
-// 16-byte vector store with explicit gfx950 cache-policy bits (measurement variants; SP = 0: none,
-// 1: nt, 2: sc1, 3: sc0 sc1, 4: nt sc1, 5: nt sc0 sc1, 6: sc0).
+// 16-byte vector store with explicit gfx950 cache-policy bits (SP = 0: none, 1: nt, 2: sc1, 3: sc0 sc1,
+// 4: nt sc1, 5: nt sc0 sc1, 6: sc0).
+//
+// The store-data hazard (round 6): a store of more than 64 bits reads its data VGPRs after it issues,
+// and on gfx940+ a VALU write of one of them within 2 wait states changes what it stores (LLVM
+// GCNHazardRecognizer::createsVALUHazard).  hipcc pads the stores it emits itself, but an inline-asm
+// store is opaque to the hazard recognizer, so the asm forms here end in `s_nop 1` (2 wait states)
+// inside the string, and the non-temporal form -- the shipped policy -- is the compiler's own store.
+// Without that, whether a kernel stored the right bytes depended on its schedule: round 5's "wrong
+// rows, not understood" (a compile-time output count in matvec_k, a second instantiation of the
+// lookup kernel's body) were schedules that put a VALU write of a store's data right behind it, and six
+// shipped (K, 1) kStoreVerify kernels had one too (tools/store_hazard_check.py checks a built library).
 template <int SP>
 __device__ __forceinline__ void st16_pol(uint8_t* p, u32x4 v) {
-  if constexpr (SP == 0) asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(p), "v"(v) : "memory");
-  else if constexpr (SP == 1) asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(p), "v"(v) : "memory");
-  else if constexpr (SP == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-  else if constexpr (SP == 3) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
-  else if constexpr (SP == 4) asm volatile("global_store_dwordx4 %0, %1, off nt sc1" ::"v"(p), "v"(v) : "memory");
-  else if constexpr (SP == 5) asm volatile("global_store_dwordx4 %0, %1, off nt sc0 sc1" ::"v"(p), "v"(v) : "memory");
-  else asm volatile("global_store_dwordx4 %0, %1, off sc0" ::"v"(p), "v"(v) : "memory");
+  if constexpr (SP == 1) __builtin_nontemporal_store(v, reinterpret_cast<u32x4_ua*>(p));
+  else if constexpr (SP == 0) asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+  else if constexpr (SP == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+  else if constexpr (SP == 3)
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+  else if constexpr (SP == 4)
+    asm volatile("global_store_dwordx4 %0, %1, off nt sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+  else if constexpr (SP == 5)
+    asm volatile("global_store_dwordx4 %0, %1, off nt sc0 sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+  else asm volatile("global_store_dwordx4 %0, %1, off sc0\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
 
 // 16-byte load at base + off through a raw buffer descriptor with explicit cache-policy bits
@@ -198,10 +211,10 @@ __device__ __forceinline__ void st_chunk(uint8_t* p, const uint32_t (&x)[LW]) {
     if constexpr (NTS) st16_pol<SP>(p, u32x4{x[0], x[1], x[2], x[3]});
     else st16<false>(p, u32x4{x[0], x[1], x[2], x[3]});
   } else if constexpr (LW == 1) {
-    if constexpr (NTS) asm volatile("global_store_dword %0, %1, off nt" ::"v"(p), "v"(x[0]) : "memory");
+    if constexpr (NTS) __builtin_nontemporal_store(x[0], reinterpret_cast<u32_ua*>(p));
     else *reinterpret_cast<u32_ua*>(p) = x[0];
   } else if constexpr (NTS) {
-    asm volatile("global_store_dwordx2 %0, %1, off nt" ::"v"(p), "v"(u32x2{x[0], x[1]}) : "memory");
+    __builtin_nontemporal_store(u32x2{x[0], x[1]}, reinterpret_cast<u32x2_ua*>(p));
   } else {
     *reinterpret_cast<u32x2_ua*>(p) = u32x2{x[0], x[1]};
   }
@@ -312,27 +325,29 @@ __device__ __forceinline__ void finish(const GfArgs& a, u32x4 (&acc)[M], uint8_t
   }
 }
 
-// One lane's chunk at the end of a shard (rem < 16 bytes), byte-granular.
+// One lane's chunk at the end of a shard (rem < 16 bytes): byte stores; the loads are one 16-byte
+// load of the row's last 16 bytes shifted down (ld_tail_row; `len` is the row's length), not 16
+// dependent byte loads per row.
 template <int M, int MT, MatVecMode MODE>
 __device__ __forceinline__ void lane_tail(const GfArgs& a, const u32x4* tab01, const uint32_t* tab2,
                                           const uint8_t* const* in, uint8_t* const* out, int og,
-                                          size_t off, size_t rem, uint32_t& diff) {
+                                          size_t off, size_t rem, uint64_t len, uint32_t& diff) {
   const int k = (int)a.k, m = (int)a.m;
   u32x4 acc[M];
 #pragma unroll
   for (int r = 0; r < M; ++r) acc[r] = u32x4{0u, 0u, 0u, 0u};
   for (int c = 0; c < k; ++c)
-    mac_row<M>(acc, ld_tail(in[c] + off, rem), tab01 + c * MT + og, tab2 + c * MT + og);
+    mac_row<M>(acc, ld_tail_row(in[c] + off, rem, len), tab01 + c * MT + og, tab2 + c * MT + og);
 #pragma unroll
   for (int r = 0; r < M; ++r) {
     if (og + r < m) {
       uint8_t* p = out[og + r] + off;
       if (row_compared<MODE>(a, og + r)) {
-        const u32x4 d = acc[r] ^ ld_tail(p, rem);
+        const u32x4 d = acc[r] ^ ld_tail_row(p, rem, len);
         diff |= d.x | d.y | d.z | d.w;
       } else {
         u32x4 v = acc[r];
-        if constexpr (MODE == MatVecMode::kAccum) v ^= ld_tail(p, rem);
+        if constexpr (MODE == MatVecMode::kAccum) v ^= ld_tail_row(p, rem, len);
         st_tail(p, v, rem);
       }
     }
@@ -634,9 +649,9 @@ __device__ __forceinline__ void matvec_k(const GfArgs& a) {
     const uint32_t tile = blockIdx.x * TPW + j;
     if (TPW > 1 && tile >= a.tiles_per_stripe) break;
     const uint32_t off = tile * kTile + (uint32_t)(cw * 64 + lane) * kLB;
-    // (m stays the launch's run-time value although it equals M here: with the compile-time M the
-    // StoreVerify kernels of (10, 4) / (12, 4) returned a wrong second row in
-    // test_reconstruct_stripes_mock_bids -- not understood, not taken)
+    // (m stays the launch's run-time value although it equals M here.  Round 5 saw the compile-time M
+    // return wrong rows -- the store-data hazard of st16_pol, above; with hazard-free stores that
+    // form is bit-exact and measured no faster, profiles/r06/shape_sweep_store_variants.txt)
     // The ragged end of a row: the lane holding it codes the last full chunk of the row instead
     // (clamped to end at len: its bytes before the end repeat its neighbour's, with the same values --
     // plain stores and compares, never an accumulate), so every lane takes the one full-chunk path.
@@ -703,10 +718,18 @@ __device__ __forceinline__ void matvec(const GfArgs& a) {
 #pragma unroll
         for (int w = 0; w < W; ++w) {
           const size_t o = off + w * kStep;
-          if (o + kLaneBytes <= len)
+          if (o + kLaneBytes <= len) {
             lane_tile<M, MT, MODE, 1, G, NTL, NTS>(a, tab01, tab2, in, out, og, soff + o, kStep, diff);
-          else if (o < len)
-            lane_tail<M, MT, MODE>(a, tab01, tab2, in, out, og, soff + o, len - o, diff);
+          } else if (o < len) {
+            // The ragged end of a row: stores and compares code the row's last full chunk instead (its
+            // bytes before the end repeat a neighbour's, with the same values), as the fixed-K, dyadic
+            // and lookup kernels do; an accumulate cannot re-code bytes and keeps the byte stores.
+            if (MODE != MatVecMode::kAccum && len >= kLaneBytes)
+              lane_tile<M, MT, MODE, 1, G, NTL, NTS>(a, tab01, tab2, in, out, og, soff + (len - kLaneBytes), kStep,
+                                                     diff);
+            else
+              lane_tail<M, MT, MODE>(a, tab01, tab2, in, out, og, soff + o, len - o, len, diff);
+          }
         }
       }
     }

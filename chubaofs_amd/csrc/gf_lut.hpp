@@ -130,7 +130,8 @@ __device__ __forceinline__ void untranspose4(const uint32_t (&g)[4 * LW], uint32
 // tools/lds_rate.hip) and the VALU ~13 cycles for 8 outputs, the v_perm product ~4.7 VALU cycles
 // per output.  MODE: kStore (outputs written), kVerify (compared: diff), kStoreVerify (rows < nstore
 // written, the rest compared).
-template <int K, int M, int ML, MatVecMode MODE, int LA = CFSEC_LUT_LOOKAHEAD, int LW = 4>
+// FULL: the caller guarantees a whole chunk (rem == 4 * LW), so the tail paths are not compiled in.
+template <int K, int M, int ML, MatVecMode MODE, int LA = CFSEC_LUT_LOOKAHEAD, int LW = 4, bool FULL = false>
 __device__ __forceinline__ void lut_chunk(const char* T, const u32x4* tab01, const uint32_t* tab2,
                                           const uint8_t* const* in, uint8_t* const* out, int nstore, int64_t sbase,
                                           uint32_t off, uint32_t rem, uint32_t& diff) {
@@ -138,7 +139,7 @@ __device__ __forceinline__ void lut_chunk(const char* T, const u32x4* tab01, con
   constexpr int D = LA < K ? LA : K;
   constexpr int SHIFT = EW == 1 ? 2 : (EW == 2 ? 3 : 4);  // log2 of the entry bytes
   constexpr int NP = 4 * LW;                              // bytes per lane chunk
-  const bool full = rem >= (uint32_t)NP;
+  const bool full = FULL || rem >= (uint32_t)NP;
   uint32_t acc[NP][NQ > 0 ? NQ : 1];
   uint32_t accp[MP > 0 ? MP : 1][LW];
 #pragma unroll
@@ -301,14 +302,20 @@ __global__ __launch_bounds__(256) void gf_lut_kernel(const dev::GfArgs a) {
   // least one chunk no lane takes the byte path.  That path -- 16 dependent byte loads per input row
   // -- made the row's last workgroup a straggler, and the last stripe's last one ended the launch
   // ~10 us late: EC15P12 encode 75.6 -> 65.8 us, EC12P9 56.6 -> 46.6 (tools/gf_shapes.hip,
-  // profiles/r05/shape_sweep_lut_clamp.txt).  (Calling the chunk body from a second, byte-path-free
-  // instantiation instead returned wrong rows for the mixed lookup + v_perm shapes: one body.)
+  // profiles/r05/shape_sweep_lut_clamp.txt).  Whole chunks take a byte-path-free instantiation of the
+  // body (FULL: no tail loads or stores compiled in, fewer registers): EC16P20's 16-row repair verify
+  // 128 -> 101 us, EC12P9 encode 46.5 -> 44.0, EC15P12 66.3 -> 63.4, EC16P20's 8-row repair 73.3 ->
+  // 70.8 (profiles/r06/shape_sweep_store_variants.txt).  Round 5 measured this form returning wrong
+  // rows -- the inline-asm store hazard of gf_device.hpp st16_pol, since removed.
   static_assert(MODE != MatVecMode::kAccum, "the clamped row end re-codes bytes: stores and compares only");
   if ((uint64_t)off < len) {
     const uint32_t loff = len >= kLB && (uint64_t)off + kLB > len ? (uint32_t)(len - kLB) : off;
     const uint32_t rem = (uint64_t)loff + kLB <= len ? kLB : (uint32_t)(len - loff);
-    lut_chunk<K, M, ML, MODE, LA, LW>(reinterpret_cast<const char*>(T), tab01, tab2, in, out, (int)a.nstore, sbase, loff,
-                                      rem, diff);
+    const char* t = reinterpret_cast<const char*>(T);
+    if (rem == kLB)
+      lut_chunk<K, M, ML, MODE, LA, LW, true>(t, tab01, tab2, in, out, (int)a.nstore, sbase, loff, rem, diff);
+    else
+      lut_chunk<K, M, ML, MODE, LA, LW, false>(t, tab01, tab2, in, out, (int)a.nstore, sbase, loff, rem, diff);
   }
   if constexpr (MODE == MatVecMode::kVerify || MODE == MatVecMode::kStoreVerify) {
     if (diff) dev::set_flag(a.flags, stripe);

@@ -106,6 +106,10 @@ hipError_t launch_crc32_to(const uint8_t* const* ptrs, size_t len, int n, uint32
 // Only for matvec_crc_supported shapes (k in {6,8,12,16,18}, m <= 6; and k = 6, m = 12 when coef is
 // EC6P10L2's fused LRC matrix: 10 rows of 2x2 dyadic blocks + 2 plain rows).
 bool matvec_crc_supported(int k, int m, size_t len, const uint8_t* coef = nullptr);
+// launch_matvec_crc takes exactly the jobs this accepts (a supported shape, kStore, checksum slots
+// inside [0, crc_stride) with crc_stride <= 256, the inputs checksummed where the only instantiated
+// form does so); callers route everything else to the product and the separate pass.
+bool matvec_crc_accepts(const MatVecJob& job, int crc_stride, const int* slot);
 hipError_t launch_matvec_crc(const MatVecJob& job, uint32_t* crc, int crc_stride, const int* slot,
                              hipStream_t stream, bool zero = true);
 // shift(~0, len) ^ ~0: XOR it into a raw (zero-preset) CRC of len bytes to get crc32.ChecksumIEEE.

@@ -3,9 +3,10 @@
 //
 // It implements github.com/klauspost/reedsolomon.Encoder (the seam that
 // blobstore/common/ec/encoder.go:86 and :95 construct) over the C ABI in
-// include/cfsec.h.  The six methods CubeFS calls -- Encode, Verify, Reconstruct,
-// ReconstructData, Split, Join -- go to libcfsec.so; EncodeIdx, ReconstructSome
-// and Update, which CubeFS never calls, return reedsolomon.ErrNotSupported.
+// include/cfsec.h.  The methods CubeFS calls go to libcfsec.so -- Encode, Verify, Reconstruct,
+// ReconstructData -- or, for Split and Join (host bookkeeping, no coding), stay in Go as the
+// reference writes them; EncodeIdx, ReconstructSome and Update, which CubeFS never calls, return
+// reedsolomon.ErrNotSupported.
 //
 // Go releases.  CubeFS builds with Go 1.17 (go.mod:3, docker/Dockerfile:1), whose cgo rules forbid a
 // C array holding Go pointers.  So every call first looks for the one-allocation layout that
@@ -326,106 +327,92 @@ func (e *Engine) Reconstruct(shards [][]byte) error { return e.reconstruct(shard
 
 func (e *Engine) ReconstructData(shards [][]byte) error { return e.reconstruct(shards, true) }
 
-// Split is the engine's cfsec_rs_split (KRS/reedsolomon.go:1574-1632, the restatement tests/
-// test_capi.py pins): the data shards are views data[off:off+per:off+per] of data itself, the
-// padding shards views of one Go buffer the engine lays out as AllocAligned does (64-byte aligned,
-// stride and capacity per rounded up to 64).  The engine returns addresses; they are turned back
-// into offsets of the two Go buffers here, so no Go pointer outlives the call on the C side.
+// Split and Join are host bookkeeping -- slice headers, a zero fill, one copy of the partial tail --
+// with no coding arithmetic, so the shim keeps them in Go (KRS/reedsolomon.go:1574-1684) rather
+// than sending Go memory through C: the C ABI's cfsec_rs_split / cfsec_rs_join run the same
+// algorithm for C callers (pinned by tests/test_capi.py), but a C function that writes addresses of
+// Go buffers into an array outlives the cgo call's pointer rules, and a Join through C costs two
+// copies of the object where the reference writes the shard slices straight to dst.
+
+// Split: the data shards are views of data itself (its spare capacity zeroed and used), the shards
+// past the end of data come from AllocAligned (64-byte aligned, stride and capacity rounded up to
+// 64), the bytes after the last full shard copied into them in order.
 func (e *Engine) Split(data []byte) ([][]byte, error) {
+	n := len(data)
+	if n == 0 {
+		return nil, reedsolomon.ErrShortData
+	}
 	tot := e.dataShards + e.parityShards
-	arr := (*C.cfsec_shard)(C.malloc(C.size_t(tot) * C.size_t(unsafe.Sizeof(C.cfsec_shard{}))))
-	defer C.free(unsafe.Pointer(arr))
-	out := unsafe.Slice(arr, tot)
-	var dp *C.uint8_t
-	full := data[:cap(data)]
-	if len(full) > 0 {
-		dp = (*C.uint8_t)(unsafe.Pointer(&full[0]))
+	if tot == 1 {
+		return [][]byte{data}, nil
 	}
-	var need C.size_t
-	st := C.cfsec_rs_split(e.h, dp, C.size_t(len(data)), C.size_t(cap(data)), arr, nil, 0, &need)
-	var pad []byte
-	if st == C.CFSEC_ERR_INVALID_ARG && need > 0 {
-		pad = make([]byte, int(need))
-		st = C.cfsec_rs_split(e.h, dp, C.size_t(len(data)), C.size_t(cap(data)), arr,
-			(*C.uint8_t)(unsafe.Pointer(&pad[0])), need, &need)
-	}
-	if err := toError(st); err != nil {
-		return nil, err
-	}
-	view := func(buf []byte, el C.cfsec_shard) ([]byte, bool) {
-		if len(buf) == 0 {
-			return nil, false
+	per := (n + e.dataShards - 1) / e.dataShards
+	// usable bytes of data: its length, or its capacity up to tot*per (zeroed past the length)
+	usable := n
+	if c := cap(data); c > n {
+		usable = tot * per
+		if c < usable {
+			usable = c
 		}
-		off := int(uintptr(unsafe.Pointer(el.data)) - uintptr(unsafe.Pointer(&buf[0])))
-		if off < 0 || off+int(el.cap) > len(buf) {
-			return nil, false
+		tail := data[n:usable]
+		for i := range tail {
+			tail[i] = 0
 		}
-		return buf[off : off+int(el.len) : off+int(el.cap)], true
 	}
-	dst := make([][]byte, tot)
-	for i, el := range out {
-		v, ok := view(full, el)
-		if !ok {
-			if v, ok = view(pad, el); !ok {
-				return nil, fmt.Errorf("%w: split returned a shard outside its buffers", errInvalidArg)
-			}
+	buf := data[:usable]
+	inPlace := usable / per
+	if inPlace > tot {
+		inPlace = tot
+	}
+	out := make([][]byte, tot)
+	for i := 0; i < inPlace; i++ {
+		out[i] = buf[i*per : (i+1)*per : (i+1)*per]
+	}
+	if inPlace < tot {
+		pad := reedsolomon.AllocAligned(tot-inPlace, per)
+		var rest []byte
+		if inPlace*per < n {
+			rest = data[inPlace*per : n]
 		}
-		dst[i] = v
+		for j := range pad {
+			rest = rest[copy(pad[j], rest):]
+			out[inPlace+j] = pad[j]
+		}
 	}
-	return dst, nil
+	return out, nil
 }
 
-// Join is the engine's cfsec_rs_join (KRS/reedsolomon.go:1646-1684): the same argument checks and
-// errors (ErrTooFewShards, ErrReconstructRequired for a nil data shard, ErrShortData), the first
-// outSize bytes of the data shards gathered by the engine, then written to dst shard by shard as the
-// reference writes them (a Write per data shard, the last one cut at outSize).
+// Join: ErrTooFewShards, ErrReconstructRequired (a nil data shard before outSize bytes are covered)
+// and ErrShortData are decided before anything is written or allocated; then one Write per data
+// shard, the last cut at outSize.
 func (e *Engine) Join(dst io.Writer, shards [][]byte, outSize int) error {
-	k := len(shards)
-	if k > e.dataShards {
-		k = e.dataShards
+	if len(shards) < e.dataShards {
+		return reedsolomon.ErrTooFewShards
 	}
-	data := shards[:k]
-	// the engine reads at most outSize bytes of the data shards: those bytes cross in C memory (Go
-	// 1.17 forbids Go pointers inside a C array), each shard's true length beside them
-	arr := (*C.cfsec_shard)(C.malloc(C.size_t(k+1) * C.size_t(unsafe.Sizeof(C.cfsec_shard{}))))
-	defer C.free(unsafe.Pointer(arr))
-	els := unsafe.Slice(arr, k+1)
-	stage := C.malloc(C.size_t(outSize + 1))
-	defer C.free(stage)
-	mem := unsafe.Slice((*byte)(stage), outSize+1)
-	used := 0
-	for i, s := range data {
-		els[i] = C.cfsec_shard{data: nil, len: C.size_t(len(s)), cap: C.size_t(len(s))}
-		if s == nil {
-			continue // a nil data shard: ErrReconstructRequired
-		}
-		n := len(s)
-		if n > outSize-used {
-			n = outSize - used
-		}
-		copy(mem[used:used+n], s[:n])
-		// non-nil: a non-NULL address even for an empty shard (never read beyond its n bytes)
-		els[i].data = (*C.uint8_t)(unsafe.Add(stage, used))
-		used += n
-	}
-	out := make([]byte, outSize+1)
-	if err := toError(C.cfsec_rs_join(e.h, (*C.uint8_t)(unsafe.Pointer(&out[0])), C.size_t(outSize), arr,
-		C.int(len(shards)), C.size_t(outSize))); err != nil {
-		return err
-	}
-	write := outSize
-	pos := 0
+	data := shards[:e.dataShards]
+	have := 0
 	for _, s := range data {
-		if write < len(s) {
-			_, err := dst.Write(out[pos : pos+write])
+		if s == nil {
+			return reedsolomon.ErrReconstructRequired
+		}
+		if have += len(s); have >= outSize {
+			break
+		}
+	}
+	if have < outSize {
+		return reedsolomon.ErrShortData
+	}
+	left := outSize
+	for _, s := range data {
+		if left < len(s) {
+			_, err := dst.Write(s[:left])
 			return err
 		}
-		n, err := dst.Write(out[pos : pos+len(s)])
+		w, err := dst.Write(s)
 		if err != nil {
 			return err
 		}
-		write -= n
-		pos += n
+		left -= w
 	}
 	return nil
 }
