@@ -512,7 +512,13 @@ def main():
     }
     out["gate_failures"] = GATE_FAILURES  # [] when every secondary leg's gate held
     out.update(extra)
-    if "device_copy_GBps" in extra:
+    if "stream_copy_GBps" in extra:
+        out["roofline"]["measured_peak_GBps"] = extra["stream_copy_GBps"]
+        out["roofline"]["frac_of_measured_copy"] = round(achieved / extra["stream_copy_GBps"], 4)
+        out["roofline"]["measured_peak_note"] = ("cfsec_stream_copy: a flat float4 non-temporal copy (1 read : 1 write) "
+                                                 "on the same rotated batches; the step kernel's 12 : 4 pattern may sit "
+                                                 "above or below it")
+    elif "device_copy_GBps" in extra:
         out["roofline"]["frac_of_measured_copy"] = round(achieved / extra["device_copy_GBps"], 4)
     print(json.dumps(out), flush=True)
     if world > 1:
@@ -628,7 +634,17 @@ def secondary(args, torch, enc, batch, ptrs, stream, S, nst, pitch, dev, launch_
     copy_bytes = 2 * batch[0].numel()
     out["device_copy_GBps"] = rate(copy_bytes, copy_ms)
     out["device_copy_note"] = ("torch copy_ of one rotated batch into a scratch batch (the HIP runtime D2D copy, "
-                               "__amd_rocclr_copyBuffer), read + write bytes / time: a measured streaming peak")
+                               "__amd_rocclr_copyBuffer), read + write bytes / time")
+    # the measured streaming ceiling: a flat float4 non-temporal copy (cfsec_stream_copy, the form of
+    # tools/rot_probe.hip), same bytes and rotation -- the roofline's second denominator
+    from chubaofs_amd import _lib
+    nb = batch[0].numel() // 16 * 16
+    with torch.cuda.stream(stream):
+        fcopy_ms = timed(lambda b: _lib.check(_lib.lib().cfsec_stream_copy(
+            ctypes.c_void_p(scratch.data_ptr()), ctypes.c_void_p(batch[b].data_ptr()), nb, stream.cuda_stream)))
+    out["stream_copy_GBps"] = rate(2 * nb, fcopy_ms)
+    out["stream_copy_note"] = ("cfsec_stream_copy (flat 16-byte non-temporal grid-stride copy) of one rotated batch: "
+                               "read + write bytes / time, the device's measured 1:1 streaming ceiling")
     del scratch
     return out
 
@@ -670,6 +686,44 @@ def host_path(args, torch, dev, world):
                      "pcie_GBps": round(world * nst * (K + M) * S * reps / dt / 1e9, 2),
                      "per_gpu_data_GBps": round(nst * K * S * reps / dt / 1e9, 2), "n_gpus": world}
         del stripes, buf
+    # the link's measured peaks on this rank (page-locked <-> HBM copies of 256 MiB, each direction alone and
+    # both at once on two streams): the path moves 12 S host-to-device and 4 S device-to-host per stripe, so
+    # its host-to-device bytes (= data bytes) against the H2D peak is how close it runs to the PCIe roofline
+    n = 256 << 20
+    h_src = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    h_dst = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    d_a = torch.empty(n, dtype=torch.uint8, device=dev)
+    d_b = torch.empty(n, dtype=torch.uint8, device=dev)
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+
+    def copies(h2d, d2h, reps=8):
+        for _ in range(2):
+            if h2d:
+                with torch.cuda.stream(s1):
+                    d_a.copy_(h_src, non_blocking=True)
+            if d2h:
+                with torch.cuda.stream(s2):
+                    h_dst.copy_(d_b, non_blocking=True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            if h2d:
+                with torch.cuda.stream(s1):
+                    d_a.copy_(h_src, non_blocking=True)
+            if d2h:
+                with torch.cuda.stream(s2):
+                    h_dst.copy_(d_b, non_blocking=True)
+        torch.cuda.synchronize()
+        return reps * n / (time.perf_counter() - t0) / 1e9
+
+    h2d, d2h = copies(True, False), copies(False, True)
+    both = copies(True, True)
+    out["pcie_peaks"] = {"h2d_GBps": round(h2d, 2), "d2h_GBps": round(d2h, 2),
+                         "bidirectional_each_GBps": round(both, 2),
+                         "note": "torch copies between page-locked host memory and HBM, 256 MiB, per rank"}
+    for kind in ("pinned", "pageable"):
+        out[kind]["h2d_frac_of_measured_peak"] = round(out[kind]["per_gpu_data_GBps"] / h2d, 3)
+    del h_src, h_dst, d_a, d_b
     return out
 
 
@@ -845,21 +899,23 @@ def segment_latency(args, torch, dev, cpu):
                         torch.cuda.synchronize()
 
                 r[kind + "_us"] = round(med(call), 1)
-                if kind == "device":
-                    # the C ABI alone, as cgo calls it: the shard vector marshalled once, a stream of
-                    # its own (the call is synchronous), no torch synchronize -- the Python layer's
-                    # Marshal and ctypes costs ~25-35 us of the figure above (tools/r5_latency.py)
-                    from chubaofs_amd._shards import Marshal
-                    m = Marshal(list(segs))
-                    badarr = (ctypes.c_int * 2)(*bad)
-                    own = torch.cuda.Stream(dev)
-                    torch.cuda.synchronize()
+                # the C ABI alone, as cgo calls it: the shard vector marshalled once, no torch
+                # synchronize -- the Python layer's Marshal and ctypes costs ~25-35 us of the figure
+                # above (tools/r5_latency.py).  HBM shards on a stream of their own (the call is
+                # synchronous); host shards with a NULL stream, as the Go shim passes them
+                # (CFSEC_MEM_HOST: page-locked rows read and written by the kernel over PCIe,
+                # pageable rows staged through HBM).
+                from chubaofs_amd._shards import Marshal
+                m = Marshal(list(segs))
+                badarr = (ctypes.c_int * 2)(*bad)
+                own = torch.cuda.Stream(dev)
+                torch.cuda.synchronize()
+                cst = own.cuda_stream if kind == "device" else None
 
-                    def cabi():
-                        _lib.check(enc._L.cfsec_ec_reconstruct_data(enc._h, m.ptr(), m.n, badarr, 2, m.mem,
-                                                                     own.cuda_stream))
+                def cabi():
+                    _lib.check(enc._L.cfsec_ec_reconstruct_data(enc._h, m.ptr(), m.n, badarr, 2, m.mem, cst))
 
-                    r["device_cabi_us"] = round(med(cabi), 1)
+                r[kind + "_cabi_us"] = round(med(cabi), 1)
                 got = [np.asarray(x.cpu().numpy() if kind == "device" else x) for x in segs[:N]]
                 assert all(np.array_equal(got[i], gold[i]) for i in range(N)), f"segment {name} {seg} {kind}"
             if cpu:
@@ -876,7 +932,7 @@ def segment_latency(args, torch, dev, cpu):
             del pin, pinned, devt
         wins = {}
         if cpu:
-            for kind in ("pageable", "pinned", "device", "device_cabi"):
+            for kind in ("pageable", "pinned", "device", "pageable_cabi", "pinned_cabi", "device_cabi"):
                 w = [int(s) for s, r in rows.items()
                      if r[kind + "_us"] < min(r["cpu_port_4t_us"], r["cpu_port_1t_us"])]
                 wins[kind] = min(w) if w else None
@@ -884,8 +940,9 @@ def segment_latency(args, torch, dev, cpu):
     out["note"] = ("gpu_wins_from_bytes: smallest measured segment where the GPU call (wall, incl. staging and "
                    "sync) beats the faster of the CPU port's 1- and 4-thread calls; None: the CPU port wins at every "
                    "measured size.  *_us: through the Python ec.Encoder (Marshal + ctypes + torch synchronize); "
-                   "device_cabi_us: the C ABI call alone on HBM shards (what the Go shim's cgo call costs), "
-                   "synchronous on a stream of its own")
+                   "*_cabi_us: the C ABI call alone (what the Go shim's cgo call costs): HBM shards synchronous on a "
+                   "stream of their own, host shards (pageable, or page-locked by cfsec_host_alloc) with a NULL stream "
+                   "as the shim passes")
     return out
 
 

@@ -131,6 +131,7 @@ SIGNATURES = {
     "cfsec_crc32_ieee_batch": ([_V, _S, _I, _V, _I, _V], _I),
     "cfsec_crc32_combine": ([ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int64], ctypes.c_uint32),
     "cfsec_crc32_shift": ([_V, _I, ctypes.c_int64], _I),
+    "cfsec_stream_copy": ([_V, _V, _S, _V], _I),
     "cfsec_host_alloc": ([_S, _P(_V)], _I),
     "cfsec_host_free": ([_V], _I),
     "cfsec_crc32block_encode_size": ([ctypes.c_int64, ctypes.c_int64], ctypes.c_int64),

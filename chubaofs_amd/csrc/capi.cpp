@@ -527,13 +527,18 @@ int cfsec_host_alloc(size_t size, void** out) {
   *out = nullptr;
   if (size == 0) return CFSEC_OK;
   return guarded([&] {
-    return (int)cfsec::hip_status(hipHostMalloc(out, size, hipHostMallocPortable), "hipHostMalloc");
+    const int st = (int)cfsec::hip_status(hipHostMalloc(out, size, hipHostMallocPortable), "hipHostMalloc");
+    if (st == CFSEC_OK) cfsec::host_range_add(*out, size);
+    return st;
   });
 }
 
 int cfsec_host_free(void* p) {
   if (!p) return CFSEC_OK;
-  return guarded([&] { return (int)cfsec::hip_status(hipHostFree(p), "hipHostFree"); });
+  return guarded([&] {
+    cfsec::host_range_remove(p);
+    return (int)cfsec::hip_status(hipHostFree(p), "hipHostFree");
+  });
 }
 
 // ---------------- CRC32 ----------------
@@ -583,6 +588,13 @@ int cfsec_crc32_shift(uint32_t* words, int n, int64_t nbytes) {
   const uint32_t xp = cfsec::crc_xpow(8 * nbytes);
   for (int i = 0; i < n; ++i) words[i] = cfsec::crc_mulmod(xp, words[i]);
   return CFSEC_OK;
+}
+
+int cfsec_stream_copy(void* dst, const void* src, size_t bytes, void* stream) {
+  return guarded([&] {
+    return (int)cfsec::hip_status(cfsec::launch_stream_copy(dst, src, bytes, static_cast<hipStream_t>(stream)),
+                                  "launch_stream_copy");
+  });
 }
 
 // ---------------- crc32block ----------------

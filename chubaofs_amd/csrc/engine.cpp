@@ -7,6 +7,8 @@
 
 #include <algorithm>
 #include <cstring>
+#include <map>
+#include <shared_mutex>
 #include <unordered_map>
 
 namespace cfsec {
@@ -383,7 +385,54 @@ static Status matvec_with_crc(const MatVecJob& job, uint8_t* const* ptrs, int to
 
 // The device address of page-locked host memory (hipHostMalloc / cfsec_host_alloc); false for
 // pageable memory.
+namespace {
+struct HostRange {
+  size_t size;
+  uint8_t* dev;  // device address of the base
+};
+struct HostRanges {
+  std::shared_mutex mu;
+  std::map<uintptr_t, HostRange> by_base;
+};
+HostRanges& host_ranges() {
+  static HostRanges r;
+  return r;
+}
+}  // namespace
+
+void host_range_add(void* base, size_t size) {
+  hipPointerAttribute_t attr;
+  if (!base || hipPointerGetAttributes(&attr, base) != hipSuccess || !attr.devicePointer) {
+    (void)hipGetLastError();
+    return;
+  }
+  HostRanges& r = host_ranges();
+  std::unique_lock<std::shared_mutex> lk(r.mu);
+  r.by_base[(uintptr_t)base] = HostRange{size, static_cast<uint8_t*>(attr.devicePointer)};
+}
+
+void host_range_remove(void* base) {
+  HostRanges& r = host_ranges();
+  std::unique_lock<std::shared_mutex> lk(r.mu);
+  r.by_base.erase((uintptr_t)base);
+}
+
 bool device_alias(uint8_t* p, uint8_t** dptr) {
+  {
+    HostRanges& r = host_ranges();
+    std::shared_lock<std::shared_mutex> lk(r.mu);
+    if (!r.by_base.empty()) {
+      auto it = r.by_base.upper_bound((uintptr_t)p);
+      if (it != r.by_base.begin()) {
+        --it;
+        const uintptr_t off = (uintptr_t)p - it->first;
+        if (off < it->second.size) {
+          *dptr = it->second.dev + off;
+          return true;
+        }
+      }
+    }
+  }
   hipPointerAttribute_t attr;
   if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
     (void)hipGetLastError();

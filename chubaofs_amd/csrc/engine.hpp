@@ -57,6 +57,11 @@ Status hip_status(hipError_t e, const char* what);
 // The device address of page-locked host memory (hipHostMalloc / cfsec_host_alloc); false for
 // pageable memory.
 bool device_alias(uint8_t* p, uint8_t** dptr);
+// The library's own page-locked allocations (cfsec_host_alloc / cfsec_host_free), looked up by
+// device_alias before it asks the runtime: hipPointerGetAttributes costs microseconds per shard,
+// which a small host-memory call (a degraded range read's segment) pays for every row.
+void host_range_add(void* base, size_t size);
+void host_range_remove(void* base);
 
 // Per-device streams and staging workspaces, shared by every engine on the device.
 class DeviceContext {

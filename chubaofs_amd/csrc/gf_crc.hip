@@ -186,12 +186,25 @@ hipError_t launch_crc(int k, int m, const GfCrcArgs& a, dim3 grid, hipStream_t s
 
 }  // namespace
 
+// The lookup-product fused kernel (gf_crc_lds_kernel): m <= 4, k <= 16, and (round 6) k = 6, m = 12 --
+// EC6P10L2's fused LRC encode with every shard checksummed, any 6 x 12 matrix (CFSEC_CRC_LDS=0 /
+// CFSEC_CRC_LDS12=0 keep the v_perm kernels for A/B, which need the 2x2-dyadic + 2 plain-row form).
+static bool crc_lds_on() {
+  static const bool v = env_u32("CFSEC_CRC_LDS", 1) != 0;
+  return v;
+}
+static bool crc_lds12_on() {
+  static const bool v = crc_lds_on() && env_u32("CFSEC_CRC_LDS12", 1) != 0;
+  return v;
+}
+
 bool matvec_crc_supported(int k, int m, size_t len, const uint8_t* coef) {
   // the fused kernels exist for the input counts of the code modes of SURVEY §8, m <= 6 outputs, and
   // EC6P10L2's fused encode (6 x (10 dyadic + 2 local) rows)
   const bool crc_k = k == 6 || k == 8 || k == 12 || k == 16 || k == 18;
   if (!crc_k || m < 1 || len > 0xFFFFFFFFull - crcdev::kTile) return false;
   if (m <= 6) return true;
+  if (k == 6 && m == 12 && crc_lds12_on()) return true;
   if (k == 6 && m == 12 && coef) {
     const DyPlan dp = dyadic_plan(coef, m, k);
     return dp.B == 2 && dp.E == 2;
@@ -247,8 +260,10 @@ hipError_t launch_matvec_crc(const MatVecJob& job, uint32_t* crc, int crc_stride
   // m <= 4, k <= 16: the lookup-product kernel (gf_crc_lds_kernel; CFSEC_CRC_LDS=0 keeps the v_perm
   // kernels for A/B): EC12P4 8 x 64 MiB encode + 16 checksums 225-230 -> 200 us
   // (profiles/r03/crc_lds_ab*.txt)
-  static const uint32_t kLds = env_u32("CFSEC_CRC_LDS", 1);
-  if (kLds && m <= 4 && k <= 16) dy = -1;
+  if (crc_lds_on() && m <= 4 && k <= 16) dy = -1;
+  // EC6P10L2's fused LRC encode + 18 checksums (C4) on the same lookup kernel with 16-byte entries
+  // (round 6): C4's put batch 245 -> 211 us per call against the v_perm form (profiles/r06/c4_crc_lds12.txt)
+  if (crc_lds12_on() && k == 6 && m == 12 && cin) dy = -1;
   // Workgroups per launch.  The v_perm kernels: ~1024, each folding ~11 tiles per row before its
   // per-thread basis epilogue (16 rows x 32 columns); 512 / 2048 / 4096 were 3-7 % slower
   // (profiles/r01/crc_wgs_sweep.txt).  The lookup kernel: exactly the resident count (its 48-64 KiB

@@ -467,7 +467,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DY ? 3 : 4,
 }
 
 // ---------------------------------------------------------------------------------------------
-// Product and checksum from one set of lookups (m <= 4 outputs).
+// Product and checksum from one set of lookups (m <= 4 outputs: 8-byte entries; m <= 12: 16-byte).
 //
 // The CRC step needs a table lookup per field of every piece anyway; a ds_read_b64 costs the LDS
 // the same 2 cycles as a ds_read_b32 (bank = dword mod 64 per 32-lane group, MI355X_MICROARCH.md
@@ -478,9 +478,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DY ? 3 : 4,
 // every output (XOR-accumulated byte-transposed: g[p] byte r = output r's byte p), so the GF product
 // costs no v_perm_b32 at all -- the fused kernel was VALU-issue-bound on half-rate v_perm /
 // v_bitop3.  Output rows are transposed once per tile (8 v_perm per dword) and
-// checksummed through the first words of E_0 (ds_read_b32 at stride 8 B: 16 even banks, no
+// checksummed through the first words of E_0 (ds_read_b32 at the entry stride: 16 distinct banks, no
 // conflicts).  The Horner jump shift(R, 4096) takes the 5-bit tables of the register word (7 reads).
 // E is 4 KiB per input row (K = 12: 48 KiB; 3 workgroups per CU).
+//
+// Round 6: up to 12 outputs with 16-byte entries (the CRC word + three product words, one
+// ds_read_b128 per nibble, 16 entries span the 64 banks four times over at 16 B: still one cycle per
+// quarter-wave, no conflicts; a b96 read would cost 8 LDS cycles, so m = 5..8 pad to 16 B too), for
+// EC6P10L2's fused LRC encode with all 18 checksums (C4; stream_put.go:249-253): 6 inputs x 12
+// outputs, E = 6 x 8 KiB.  The v_perm form of that kernel issued 2750 VALU per 64-lane column (the
+// 2x2-dyadic product plus 18 rows of 5-bit Horner steps, profiles/r05/pmc_c4_crc_probe.txt).
 __device__ __forceinline__ uint32_t gf_mul_dev(uint32_t c, uint32_t v) {
   uint32_t p = 0;
 #pragma unroll
@@ -491,36 +498,44 @@ __device__ __forceinline__ uint32_t gf_mul_dev(uint32_t c, uint32_t v) {
   return p;
 }
 
-constexpr int kLdsRowBytes = 16 * 2 * 16 * 8;  // E_c: 16 positions x 2 nibbles x 16 values x 8 B
+constexpr int lds_nq(int M) { return (M + 3) / 4; }       // product words per entry
+constexpr int lds_ew(int M) { return M <= 4 ? 2 : 4; }    // entry words: CRC word + products (padded)
+constexpr int lds_row_bytes(int M) { return 16 * 2 * 16 * 4 * lds_ew(M); }  // E_c: 16 pos x 2 nibbles x 16
+constexpr int kLdsRowBytes = lds_row_bytes(4);
 
-// Lookups of one 16-byte piece d in E (bytes; E_c for an input row, E_0 for an output row).  GF:
-// accumulate the second words into g as well (input rows).
-template <bool GF>
-__device__ __forceinline__ uint32_t piece_lookup(const char* E, const uint32_t (&d)[4], uint32_t (&g)[16]) {
-  uint32_t cr0 = 0u, cr1 = 0u;
-#pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    // byte j of lo / hi = 8 x (low / high nibble of byte j): the byte offset of the entry
-    uint32_t lo = (d[w] << 3) & 0x78787878u, hi = (d[w] >> 1) & 0x78787878u;
-    asm volatile("" : "+v"(lo), "+v"(hi));
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int p = 4 * w + j;
-      const uint32_t al = (lo >> (8 * j)) & 0xFFu, ah = (hi >> (8 * j)) & 0xFFu;
-      uint32_t& cr = (w & 1) ? cr1 : cr0;
-      if constexpr (GF) {
-        const dev::u32x2 el = *reinterpret_cast<const dev::u32x2*>(E + p * 256 + al);
-        const dev::u32x2 eh = *reinterpret_cast<const dev::u32x2*>(E + p * 256 + 128 + ah);
-        cr = __builtin_amdgcn_bitop3_b32(cr, el.x, eh.x, 0x96);
-        g[p] = __builtin_amdgcn_bitop3_b32(g[p], el.y, eh.y, 0x96);
-      } else {
-        const uint32_t el = *reinterpret_cast<const uint32_t*>(E + p * 256 + al);
-        const uint32_t eh = *reinterpret_cast<const uint32_t*>(E + p * 256 + 128 + ah);
-        cr = __builtin_amdgcn_bitop3_b32(cr, el, eh, 0x96);
-      }
-    }
+template <int EW>
+struct LdsEnt {
+  uint32_t w[EW];
+};
+
+template <int EW>
+__device__ __forceinline__ LdsEnt<EW> ld_ent(const char* p) {
+  LdsEnt<EW> e;
+  if constexpr (EW == 2) {
+    const dev::u32x2 v = *reinterpret_cast<const dev::u32x2*>(p);
+    e.w[0] = v.x;
+    e.w[1] = v.y;
+  } else {
+    const u32x4 v = *reinterpret_cast<const u32x4*>(p);
+    e.w[0] = v.x;
+    e.w[1] = v.y;
+    e.w[2] = v.z;
+    e.w[3] = v.w;
   }
-  return cr0 ^ cr1;
+  return e;
+}
+
+// Byte j of lo / hi = the entry offset (4 * EW * nibble) of the low / high nibble of byte j of v.
+template <int EW>
+__device__ __forceinline__ void ent_offsets(uint32_t v, uint32_t& lo, uint32_t& hi) {
+  if constexpr (EW == 2) {
+    lo = (v << 3) & 0x78787878u;
+    hi = (v >> 1) & 0x78787878u;
+  } else {
+    lo = (v << 4) & 0xF0F0F0F0u;
+    hi = v & 0xF0F0F0F0u;
+  }
+  asm volatile("" : "+v"(lo), "+v"(hi));
 }
 
 // shift(r, 4096) from the 5-bit tables of the register word (rt = Q(4, .), 7 x 32 words)
@@ -555,20 +570,38 @@ __device__ __forceinline__ void untranspose(const uint32_t (&g)[16], uint32_t (&
 #endif
 // Lookups in flight: the 8 reads of word step s + P are issued before word step s is consumed
 // (a step = one dword of one row's piece), so a wave keeps ~8P reads outstanding instead of
-// draining its LDS queue after every few (lgkmcnt counts to 15).  P = 0: one row at a time.
+// draining its LDS queue after every few (lgkmcnt counts to 15).  P = 0: each step's 8 reads, then
+// their use.  The 16-byte entries take P = 0 by default: P = 1 holds 64 VGPRs of entries.
 #ifndef CFSEC_LDS_PIPE
 #define CFSEC_LDS_PIPE 1
 #endif
+#ifndef CFSEC_LDS_PIPE_W
+#define CFSEC_LDS_PIPE_W 0
+#endif
+// Output rows' checksums from the 5-bit tables (35 conflict-free reads per 16-byte piece, the
+// register jump included) instead of E_0's nibble words + the jump (32 + 7).  Bit 0: the 8-byte-entry
+// kernels (m <= 4), bit 1: the 16-byte-entry kernels.
+#ifndef CFSEC_LDS_OUT5
+#define CFSEC_LDS_OUT5 0
+#endif
+template <int M>
+constexpr bool lds_out5() {
+  return (CFSEC_LDS_OUT5 >> (lds_ew(M) == 2 ? 0 : 1)) & 1;
+}
+
 template <int K, int M, bool CIN>
-__device__ __forceinline__ void crc_tile_lds(uint64_t len, const char* E, const uint32_t* rt,
+__device__ __forceinline__ void crc_tile_lds(uint64_t len, const char* E, const uint32_t* ft, const uint32_t* rt,
                                              const uint8_t* const (&row)[K + M], uint32_t off, bool pre, bool next,
                                              uint32_t (&x)[K][4], uint32_t (&R)[(CIN ? K : 0) + M]) {
   constexpr int RO = CIN ? K : 0;
   constexpr int D = CFSEC_LDS_LOOKAHEAD < K ? CFSEC_LDS_LOOKAHEAD : K;
-  constexpr int P = CFSEC_LDS_PIPE;
-  uint32_t g[16];
+  constexpr int NQ = lds_nq(M), EW = lds_ew(M), EB = 4 * EW, RB = lds_row_bytes(M);
+  constexpr int P = EW == 2 ? CFSEC_LDS_PIPE : CFSEC_LDS_PIPE_W;
+  uint32_t g[16][NQ];
 #pragma unroll
-  for (int p = 0; p < 16; ++p) g[p] = 0u;
+  for (int p = 0; p < 16; ++p)
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) g[p][q] = 0u;
   // one pipelined pass; the thread holding the shard end (or past it) loads its piece
   // byte-granular, zero-padded
   const bool full = (uint64_t)off + dev::kLaneBytes <= len;
@@ -590,23 +623,9 @@ __device__ __forceinline__ void crc_tile_lds(uint64_t len, const char* E, const 
   if (!pre)
 #pragma unroll
     for (int c = 0; c < D; ++c) load(c, off, full);
-  if constexpr (P == 0) {
-#pragma unroll
-    for (int c = 0; c < K; ++c) {
-      load_ahead(c);
-      __builtin_amdgcn_sched_barrier(0);
-      const uint32_t cr = piece_lookup<true>(E + c * kLdsRowBytes, x[c], g);
-      if constexpr (CIN) {
-        R[c] = cr ^ rshift4096(rt, R[c]);
-        asm volatile("" : "+v"(R[c]));  // computed here, not sunk to its next use (all the reads would stay live)
-      }
-#pragma unroll
-      for (int p = 0; p < 16; ++p) asm volatile("" : "+v"(g[p]));
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  } else {
-    // input steps s = 4c + w: 8 ds_read_b64 each (+ the 7 register-shift reads of row c at w = 0)
-    dev::u32x2 L[P + 1][8];
+  {
+    // input steps s = 4c + w: 8 entry reads each (+ the 7 register-shift reads of row c at w = 0)
+    LdsEnt<EW> L[P + 1][8];
     uint32_t rs[2][kFiveFields];
     uint32_t cr0 = 0u, cr1 = 0u;
     const auto issue = [&](int s) {
@@ -615,23 +634,25 @@ __device__ __forceinline__ void crc_tile_lds(uint64_t len, const char* E, const 
         load_ahead(c);
         if constexpr (CIN) five_word<0>(rt, R[c], rs[c & 1]);
       }
-      uint32_t lo = (x[c][w] << 3) & 0x78787878u, hi = (x[c][w] >> 1) & 0x78787878u;
-      asm volatile("" : "+v"(lo), "+v"(hi));
-      const char* t = E + c * kLdsRowBytes + 4 * w * 256;
+      uint32_t lo, hi;
+      ent_offsets<EW>(x[c][w], lo, hi);
+      const char* t = E + c * RB + 4 * w * (32 * EB);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        L[s % (P + 1)][2 * j] = *reinterpret_cast<const dev::u32x2*>(t + j * 256 + ((lo >> (8 * j)) & 0xFFu));
-        L[s % (P + 1)][2 * j + 1] = *reinterpret_cast<const dev::u32x2*>(t + j * 256 + 128 + ((hi >> (8 * j)) & 0xFFu));
+        L[s % (P + 1)][2 * j] = ld_ent<EW>(t + j * (32 * EB) + ((lo >> (8 * j)) & 0xFFu));
+        L[s % (P + 1)][2 * j + 1] = ld_ent<EW>(t + j * (32 * EB) + 16 * EB + ((hi >> (8 * j)) & 0xFFu));
       }
     };
     const auto consume = [&](int s) {
       const int c = s >> 2, w = s & 3;
-      const dev::u32x2(&l)[8] = L[s % (P + 1)];
+      const LdsEnt<EW>(&l)[8] = L[s % (P + 1)];
       uint32_t& cr = (w & 1) ? cr1 : cr0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        cr = __builtin_amdgcn_bitop3_b32(cr, l[2 * j].x, l[2 * j + 1].x, 0x96);
-        g[4 * w + j] = __builtin_amdgcn_bitop3_b32(g[4 * w + j], l[2 * j].y, l[2 * j + 1].y, 0x96);
+        cr = __builtin_amdgcn_bitop3_b32(cr, l[2 * j].w[0], l[2 * j + 1].w[0], 0x96);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q)
+          g[4 * w + j][q] = __builtin_amdgcn_bitop3_b32(g[4 * w + j][q], l[2 * j].w[1 + q], l[2 * j + 1].w[1 + q], 0x96);
       }
       if (w == 3) {
         if constexpr (CIN) {
@@ -639,12 +660,14 @@ __device__ __forceinline__ void crc_tile_lds(uint64_t len, const char* E, const 
           R[c] = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(cr0, cr1, t[0], 0x96),
                                              __builtin_amdgcn_bitop3_b32(t[1], t[2], t[3], 0x96),
                                              __builtin_amdgcn_bitop3_b32(t[4], t[5], t[6], 0x96), 0x96);
-          asm volatile("" : "+v"(R[c]));
+          asm volatile("" : "+v"(R[c]));  // computed here, not sunk to its next use (the reads would stay live)
         }
         cr0 = cr1 = 0u;
       }
 #pragma unroll
-      for (int p = 0; p < 4; ++p) asm volatile("" : "+v"(g[4 * w + p]));
+      for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) asm volatile("" : "+v"(g[4 * w + p][q]));
     };
 #pragma unroll
     for (int s = 0; s < P && s < 4 * K; ++s) issue(s);
@@ -656,39 +679,56 @@ __device__ __forceinline__ void crc_tile_lds(uint64_t len, const char* E, const 
       __builtin_amdgcn_sched_barrier(0);
     }
   }
-  uint32_t o[M][4];
-  untranspose<M>(g, o);
-  if (full) {
+  // output rows, one quad of the byte-transposed accumulators at a time: transposed back, stored,
+  // checksummed through the CRC words of E_0 (output steps s = 4r + w: 8 ds_read_b32 each)
 #pragma unroll
-    for (int r = 0; r < M; ++r)
-      dev::st16_out<true>(const_cast<uint8_t*>(row[K + r]) + off, u32x4{o[r][0], o[r][1], o[r][2], o[r][3]});
-  } else if (rem) {
+  for (int q = 0; q < NQ; ++q) {
+    constexpr int kLast = M - 4 * (NQ - 1);
+    uint32_t gq[16];
 #pragma unroll
-    for (int r = 0; r < M; ++r)
-      dev::st_tail(const_cast<uint8_t*>(row[K + r]) + off, u32x4{o[r][0], o[r][1], o[r][2], o[r][3]}, rem);
-  }
-  if constexpr (P == 0) {
+    for (int p = 0; p < 16; ++p) gq[p] = g[p][q];
+    uint32_t o[4][4];
+    untranspose<4>(gq, o);
+    const int mq = q + 1 < NQ ? 4 : kLast;  // rows of this quad
+    if (full) {
 #pragma unroll
-    for (int r = 0; r < M; ++r) {
-      R[RO + r] = piece_lookup<false>(E, o[r], g) ^ rshift4096(rt, R[RO + r]);
-      asm volatile("" : "+v"(R[RO + r]));
+      for (int r = 0; r < 4; ++r)
+        if (r < mq)
+          dev::st16_out<true>(const_cast<uint8_t*>(row[K + 4 * q + r]) + off, u32x4{o[r][0], o[r][1], o[r][2], o[r][3]});
+    } else if (rem) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (r < mq)
+          dev::st_tail(const_cast<uint8_t*>(row[K + 4 * q + r]) + off, u32x4{o[r][0], o[r][1], o[r][2], o[r][3]}, rem);
     }
-  } else {
-    // output steps s = 4r + w: 8 ds_read_b32 of the first words of E_0
-    uint32_t L[P + 1][8];
-    uint32_t rs[M][kFiveFields];
+    if constexpr (lds_out5<M>()) {
 #pragma unroll
-    for (int r = 0; r < M; ++r) five_word<0>(rt, R[RO + r], rs[r]);
+      for (int r = 0; r < 4; ++r) {
+        if (r < mq) {
+          R[RO + 4 * q + r] = crc_step5(ft, R[RO + 4 * q + r], o[r]);
+          asm volatile("" : "+v"(R[RO + 4 * q + r]));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      continue;
+    }
+    uint32_t L[P + 1][8];
+    uint32_t rs[4][kFiveFields];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (r < mq) five_word<0>(rt, R[RO + 4 * q + r], rs[r]);
     uint32_t cr0 = 0u, cr1 = 0u;
+    const int ns = 4 * mq;
     const auto issue = [&](int s) {
       const int r = s >> 2, w = s & 3;
-      uint32_t lo = (o[r][w] << 3) & 0x78787878u, hi = (o[r][w] >> 1) & 0x78787878u;
-      asm volatile("" : "+v"(lo), "+v"(hi));
-      const char* t = E + 4 * w * 256;
+      uint32_t lo, hi;
+      ent_offsets<EW>(o[r][w], lo, hi);
+      const char* t = E + 4 * w * (32 * EB);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        L[s % (P + 1)][2 * j] = *reinterpret_cast<const uint32_t*>(t + j * 256 + ((lo >> (8 * j)) & 0xFFu));
-        L[s % (P + 1)][2 * j + 1] = *reinterpret_cast<const uint32_t*>(t + j * 256 + 128 + ((hi >> (8 * j)) & 0xFFu));
+        L[s % (P + 1)][2 * j] = *reinterpret_cast<const uint32_t*>(t + j * (32 * EB) + ((lo >> (8 * j)) & 0xFFu));
+        L[s % (P + 1)][2 * j + 1] =
+            *reinterpret_cast<const uint32_t*>(t + j * (32 * EB) + 16 * EB + ((hi >> (8 * j)) & 0xFFu));
       }
     };
     const auto consume = [&](int s) {
@@ -699,21 +739,24 @@ __device__ __forceinline__ void crc_tile_lds(uint64_t len, const char* E, const 
       for (int j = 0; j < 4; ++j) cr = __builtin_amdgcn_bitop3_b32(cr, l[2 * j], l[2 * j + 1], 0x96);
       if (w == 3) {
         const uint32_t(&t)[kFiveFields] = rs[r];
-        R[RO + r] = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(cr0, cr1, t[0], 0x96),
-                                                __builtin_amdgcn_bitop3_b32(t[1], t[2], t[3], 0x96),
-                                                __builtin_amdgcn_bitop3_b32(t[4], t[5], t[6], 0x96), 0x96);
-        asm volatile("" : "+v"(R[RO + r]));
+        R[RO + 4 * q + r] = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(cr0, cr1, t[0], 0x96),
+                                                        __builtin_amdgcn_bitop3_b32(t[1], t[2], t[3], 0x96),
+                                                        __builtin_amdgcn_bitop3_b32(t[4], t[5], t[6], 0x96), 0x96);
+        asm volatile("" : "+v"(R[RO + 4 * q + r]));
         cr0 = cr1 = 0u;
       }
     };
 #pragma unroll
-    for (int s = 0; s < P && s < 4 * M; ++s) issue(s);
+    for (int s = 0; s < P && s < 16; ++s)
+      if (s < ns) issue(s);
 #pragma clang loop unroll(full)
-    for (int s = 0; s < 4 * M; ++s) {
-      if (s + P < 4 * M) issue(s + P);
-      __builtin_amdgcn_sched_barrier(0);
-      consume(s);
-      __builtin_amdgcn_sched_barrier(0);
+    for (int s = 0; s < 16; ++s) {
+      if (s < ns) {
+        if (s + P < ns) issue(s + P);
+        __builtin_amdgcn_sched_barrier(0);
+        consume(s);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
   }
 }
@@ -730,35 +773,55 @@ constexpr int kLdsV = CFSEC_LDS_V;
 template <int K, int M, bool CIN>
 __global__ __launch_bounds__(256 * kLdsV) __attribute__((amdgpu_waves_per_eu(CFSEC_LDS_WPE, 8))) void gf_crc_lds_kernel(
     const GfCrcArgs a) {
-  static_assert(M >= 1 && M <= 4, "the second word of an entry holds at most 4 products");
+  static_assert(M >= 1 && M <= 12, "an entry holds at most 12 products");
   constexpr int NR = (CIN ? K : 0) + M;
   constexpr int NT = 256 * kLdsV;
-  __shared__ dev::u32x2 E[K * kLdsRowBytes / 8];
-  __shared__ uint32_t rt[kFiveFields * 32];
-  __shared__ uint32_t gfw[K * 32];
+  constexpr int NQ = lds_nq(M), EW = lds_ew(M);
+  __shared__ u32x4 E[K * lds_row_bytes(M) / 16];
+  constexpr bool kO5 = lds_out5<M>();
+  constexpr int kFtWords = (kO5 ? 5 : 1) * kFiveFields * 32, kGfWords = K * 32 * NQ;
+  // the register word's 5-bit tables Q(4, .) (kO5: all five words' tables, Q(4, .) last; the product
+  // words gfw, needed only while E is built, then live in the same words, so E_c + tables stay
+  // within a third of the LDS)
+  constexpr bool kShare = kO5 && kGfWords <= kFtWords;
+  __shared__ uint32_t ft[kFtWords];
+  __shared__ uint32_t gfw_own[kShare ? 1 : kGfWords];
+  uint32_t* gfw = kShare ? ft : gfw_own;
+  const uint32_t* rt = ft + (kO5 ? 4 * kFiveFields * 32 : 0);
   __shared__ uint32_t red[kLdsV][4][NR];
-  // gfw[c][h][n]: the M products of input row c's coefficients with n << 4h
-  for (int i = threadIdx.x; i < K * 32; i += NT) {
-    const int c = i >> 5;
-    const uint32_t v = (uint32_t)(i & 15) << (4 * ((i >> 4) & 1));
+  // gfw[(c * 32 + h * 16 + n) * NQ + q]: the products of input row c's coefficients of outputs
+  // 4q .. 4q + 3 with n << 4h
+  for (int i = threadIdx.x; i < K * 32 * NQ; i += NT) {
+    const int q = i % NQ, e = i / NQ, c = e >> 5;
+    const uint32_t v = (uint32_t)(e & 15) << (4 * ((e >> 4) & 1));
     uint32_t w = 0;
 #pragma unroll
-    for (int r = 0; r < M; ++r) w |= gf_mul_dev(a.coef[r * K + c], v) << (8 * r);
+    for (int b = 0; b < 4; ++b)
+      if (4 * q + b < M) w |= gf_mul_dev(a.coef[(4 * q + b) * K + c], v) << (8 * b);
     gfw[i] = w;
   }
-  // Q(4, f): the register word's 5-bit tables
-  for (int i = threadIdx.x; i < kFiveFields * 32; i += NT)
-    rt[i] = a.tabs[kByteTabWords + kNibTabWords + 4 * kFiveFields * 32 + i];
+  if constexpr (!kShare)
+    for (int i = threadIdx.x; i < kFtWords; i += NT)
+      ft[i] = a.tabs[kByteTabWords + kNibTabWords + (kO5 ? 0 : 4 * kFiveFields * 32) + i];
   __syncthreads();
-  // E_c[q][n] (q = 2p + h) = (N_q[n], gfw[c][h][n]); N_q are the device block's nibble tables
+  // E_c[q][n] (q = 2p + h) = (N_q[n], gfw[c][h][n][..]); N_q are the device block's nibble tables
   // (entry i & 511 of E_c takes N word i & 511: a thread meets at most two of them)
   const uint32_t* nt = a.tabs + kByteTabWords;
   const uint32_t nA = nt[threadIdx.x & 511], nB = nt[(threadIdx.x + 256) & 511];
+  uint32_t* Ew = reinterpret_cast<uint32_t*>(E);
   for (int i = threadIdx.x; i < K * 512; i += NT) {
     const int c = i >> 9, q = (i >> 4) & 31, n = i & 15;
-    E[i] = dev::u32x2{(i & 511) == (int)(threadIdx.x & 511) ? nA : nB, gfw[c * 32 + (q & 1) * 16 + n]};
+    const uint32_t* pw = gfw + (c * 32 + (q & 1) * 16 + n) * NQ;
+    uint32_t* dst = Ew + (size_t)i * EW;
+    dst[0] = (i & 511) == (int)(threadIdx.x & 511) ? nA : nB;
+#pragma unroll
+    for (int w = 1; w < EW; ++w) dst[w] = w - 1 < NQ ? pw[w - 1] : 0u;
   }
   __syncthreads();
+  if constexpr (kShare) {
+    for (int i = threadIdx.x; i < kFtWords; i += NT) ft[i] = a.tabs[kByteTabWords + kNibTabWords + i];
+    __syncthreads();
+  }
 
   const uint32_t vg = threadIdx.x >> 8, tid = threadIdx.x & 255;
   const uint32_t g = blockIdx.x * kLdsV + vg, stripe = blockIdx.y;
@@ -780,7 +843,7 @@ __global__ __launch_bounds__(256 * kLdsV) __attribute__((amdgpu_waves_per_eu(CFS
   for (uint32_t t = t0; t < t1; ++t) {
     const uint32_t off = t * kTile + lanepos;
     const bool next = t + 1 < t1 && (uint64_t)off + kTile + dev::kLaneBytes <= a.len;
-    crc_tile_lds<K, M, CIN>(a.len, reinterpret_cast<const char*>(E), rt, row, off, pre, next, x, R);
+    crc_tile_lds<K, M, CIN>(a.len, reinterpret_cast<const char*>(E), ft, rt, row, off, pre, next, x, R);
     pre = next && (uint64_t)off + dev::kLaneBytes <= a.len;
   }
   crc_epilogue<K, NR, CIN>(a, R, red[vg], g, stripe, tid, t0 < a.tiles);
@@ -788,7 +851,7 @@ __global__ __launch_bounds__(256 * kLdsV) __attribute__((amdgpu_waves_per_eu(CFS
 
 // Launch gf_crc_kernel<K, m, CIN> (instantiated for m = 1..6 in gf_crc_k<K>.hip); dy: the dyadic
 // block size of the product (4: m = 4, K a multiple of 4; 2: K = m = 6; 0: plain); dy = -1: the
-// lookup-product kernel gf_crc_lds_kernel (m <= 4).
+// lookup-product kernel gf_crc_lds_kernel (m <= 4; K = 6, m = 12 with the inputs checksummed).
 template <int K, bool CIN>
 hipError_t launch_crc_k(int m, const GfCrcArgs& a, dim3 grid, hipStream_t st, int dy) {
   if (dy == -1) {
@@ -800,6 +863,12 @@ hipError_t launch_crc_k(int m, const GfCrcArgs& a, dim3 grid, hipStream_t st, in
         case 2: hipLaunchKernelGGL((gf_crc_lds_kernel<K, 2, CIN>), grid, dim3(256 * kLdsV), 0, st, a); break;
         case 3: hipLaunchKernelGGL((gf_crc_lds_kernel<K, 3, CIN>), grid, dim3(256 * kLdsV), 0, st, a); break;
         case 4: hipLaunchKernelGGL((gf_crc_lds_kernel<K, 4, CIN>), grid, dim3(256 * kLdsV), 0, st, a); break;
+        case 12:
+          if constexpr (K == 6 && CIN) {  // EC6P10L2's fused LRC encode + its 18 checksums
+            hipLaunchKernelGGL((gf_crc_lds_kernel<K, 12, CIN>), grid, dim3(256 * kLdsV), 0, st, a);
+            break;
+          }
+          return hipErrorInvalidValue;
         default: return hipErrorInvalidValue;
       }
       return hipGetLastError();
@@ -859,6 +928,12 @@ int lds_blocks_per_cu(int m) {
       case 2: f = reinterpret_cast<const void*>(&gf_crc_lds_kernel<K, 2, CIN>); break;
       case 3: f = reinterpret_cast<const void*>(&gf_crc_lds_kernel<K, 3, CIN>); break;
       case 4: f = reinterpret_cast<const void*>(&gf_crc_lds_kernel<K, 4, CIN>); break;
+      case 12:
+        if constexpr (K == 6 && CIN) {
+          f = reinterpret_cast<const void*>(&gf_crc_lds_kernel<K, 12, CIN>);
+          break;
+        }
+        return 0;
       default: return 0;
     }
     int n = 0;

@@ -374,6 +374,26 @@ __global__ __launch_bounds__(kGatherSlots) void flag_gather_kernel(const GatherA
 }
 }  // namespace
 
+namespace {
+__global__ __launch_bounds__(256) void stream_copy_kernel(const dev::u32x4* __restrict__ src, dev::u32x4* __restrict__ dst,
+                                                          size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+}
+}  // namespace
+
+hipError_t launch_stream_copy(void* dst, const void* src, size_t bytes, hipStream_t stream) {
+  if ((bytes & 15) || ((uintptr_t)dst & 15) || ((uintptr_t)src & 15) || (bytes && (!dst || !src)))
+    return hipErrorInvalidValue;
+  if (bytes == 0) return hipSuccess;
+  const size_t n = bytes / 16;
+  // 8192 x 256 threads: tools/rot_probe.hip's flat copy (32 resident workgroups per CU)
+  const unsigned grid = (unsigned)std::min<size_t>(8192, (n + 255) / 256);
+  hipLaunchKernelGGL(stream_copy_kernel, dim3(grid), dim3(256), 0, stream, static_cast<const dev::u32x4*>(src),
+                     static_cast<dev::u32x4*>(dst), n);
+  return hipGetLastError();
+}
+
 hipError_t launch_flag_gather(uint32_t* tmp, uint32_t* out, const int* item, const int* word, int n,
                               bool accumulate, hipStream_t stream) {
   if (n <= 0) return hipSuccess;

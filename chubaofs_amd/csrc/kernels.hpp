@@ -76,6 +76,8 @@ constexpr int kBsRepairMaxMissing = 2;
 // (v != 0), else out[o] = (v != 0) -- and those tmp words are reset to 0, so a workspace's flag words
 // stay zero between calls (no memset per call).  pairs: n (item, word) entries sorted by item; out
 // may be host-mapped pinned memory (the synchronous calls read it after the sync, no D2H copy).
+// cfsec_stream_copy: dst[0, bytes) <- src, 16-byte non-temporal grid-stride copy (bytes % 16 == 0).
+hipError_t launch_stream_copy(void* dst, const void* src, size_t bytes, hipStream_t stream);
 hipError_t launch_flag_gather(uint32_t* tmp, uint32_t* out, const int* item, const int* word, int n,
                               bool accumulate, hipStream_t stream);
 

@@ -331,6 +331,13 @@ int cfsec_crc32_ieee_batch(uint8_t* const* ptrs, size_t shard_size, int n, uint3
 uint32_t cfsec_crc32_combine(uint32_t crc1, uint32_t crc2, int64_t len2);
 int cfsec_crc32_shift(uint32_t* words, int n, int64_t nbytes);
 
+/* Measurement helper (no reference counterpart): a flat grid-stride copy of `bytes` bytes (a
+ * multiple of 16; both pointers device memory, 16-byte aligned) with non-temporal 16-byte loads and
+ * stores, asynchronous on `stream` -- the device's streaming ceiling for a 1:1 read/write pattern,
+ * which bench.py reports beside the HBM spec peak (tools/rot_probe.hip measured this form at 72-75 %
+ * of 8 TB/s, above the HIP runtime's own copy). */
+int cfsec_stream_copy(void* dst, const void* src, size_t bytes, void* stream);
+
 /* ---------------- crc32block framing (blobstore/common/crc32block) ---------------- */
 /* A framed object is a run of block_len-byte blocks (default 64 KiB; block_len a positive multiple
  * of 4096), each the little-endian crc32.ChecksumIEEE of its payload followed by the payload

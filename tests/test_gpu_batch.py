@@ -672,6 +672,36 @@ def test_ec_reconstruct_batch_async_crc():
             assert got[b][i] == (crc_of(shards[i]) if i in bads[b] else 0), (b, i)
 
 
+@pytest.mark.parametrize("size", [1, 17, 4095, 4097, 65539, 699051])
+def test_lrc_fused_encode_crc_ragged(size, monkeypatch, capfd):
+    """EC6P10L2's fused LRC encode + all 18 checksums (C4's put, stream_put.go:249-253) on the
+    lookup-product kernel with 16-byte entries (round 6): 5 equal-length bids in device memory (one
+    fused launch), ragged and whole-tile sizes; parity against the ec oracle's Encode, every word
+    against crc32.ChecksumIEEE."""
+    monkeypatch.setenv("CFSEC_TRACE_BATCH", "1")
+    from chubaofs_amd import ec
+    t = cm.GetTactic(cm.EC6P10L2)
+    total = t.N + t.M + t.L
+    enc = ec.NewEncoder(ec.Config(CodeMode=t, EnableVerify=False), device=0)
+    orc = ECOracle.from_tactic(t, enable_verify=False)
+    stripes, want = [], []
+    for b in range(5):
+        src = [gen_mock_bytes(b * 13 + i, size) for i in range(t.N)] + \
+              [np.full(size, 0x5A, np.uint8) for _ in range(total - t.N)]
+        ref = [Slice.of(x) for x in src]
+        assert orc.encode(ref) == 0
+        want.append([x.view().copy() for x in ref])
+        stripes.append(to_mem(src, "device"))
+    capfd.readouterr()
+    st, crcs = enc.EncodeBatch(stripes, crcs=True)
+    assert "fused crc group k=6 m=12 tasks=5" in capfd.readouterr().err
+    assert st == [0] * 5
+    for b in range(5):
+        for i in range(total):
+            assert np.array_equal(host(stripes[b][i]), want[b][i]), (b, i)
+            assert crcs[b][i] == crc_of(want[b][i]), (b, i)
+
+
 @pytest.mark.parametrize("gap", [False, True])
 @pytest.mark.parametrize("memory", ["host", "device"])
 @pytest.mark.parametrize("mode", [cm.EC12P4, cm.EC6P6, cm.EC6P10L2])

@@ -1,7 +1,8 @@
 """C4's put batch (EC6P10L2, 48 blobs x S = 699,051) through cfsec_ec_encode_batch_async with and
 without all 18 checksums per blob: device time per call from HIP events (back-to-back calls), the
 words of blob 0 against zlib.  CFSEC_BATCH_FUSED_CRC=0 runs the checksums as the separate pass
-(A/B of the fused 6 x (10 + 2) encode + CRC kernel)."""
+(A/B of the fused 6 x (10 + 2) encode + CRC kernel); CFSEC_CRC_LDS12=0 the round-5 v_perm form of it.
+Every blob's parity and 18 words are checked after the timing.""" 
 import ctypes
 import os
 import sys
@@ -43,10 +44,17 @@ for crc in (False, True, False, True):
     torch.cuda.synchronize()
     print(f"crcs={crc}: {e0.elapsed_time(e1) * 1e3 / reps:8.1f} us per call", flush=True)
     assert list(st) == [0] * nb
+call(0, False)
+torch.cuda.synchronize()
+plain = bufs[0][:, t.N:].clone()
+bufs[0][:, t.N:] = 0
+torch.cuda.synchronize()  # the zero fill ran on torch's stream, the calls run on `stream`
 call(0, True)
 torch.cuda.synchronize()
+assert torch.equal(bufs[0][:, t.N:], plain), "parity rows of the checksummed call differ from the plain encode"
 w = words.cpu().numpy().view("uint32").reshape(nb, tot)
-h = bufs[0][0].cpu().numpy()
-for i in range(tot):
-    assert int(w[0, i]) == zlib.crc32(h[i].tobytes()) & 0xFFFFFFFF, i
-print("blob 0 checksums equal zlib")
+h = bufs[0].cpu().numpy()
+for b in range(nb):
+    for i in range(tot):
+        assert int(w[b, i]) == zlib.crc32(h[b, i].tobytes()) & 0xFFFFFFFF, (b, i)
+print(f"all {nb} blobs: parity equal to the plain encode, {tot} checksums each equal zlib")

@@ -82,7 +82,7 @@ int main() {
   uint32_t* crcs;
   CK(hipMalloc(&crcs, 4 * 64 * 1024));
   printf("%-30s %3s %3s %9s %4s %9s %8s %6s %9s %9s %6s %9s %6s %11s\n", "shape", "k", "m", "S", "nst", "us/launch", "GB/s",
-         "%8TB", "Tlaneop/s", "verify us", "%8TB", "+crc us", "%8TB", "crc-only us");
+         "%8TB", "Tlaneop/s", "verify us", "%8TB", "+crc us", "%8TB", "crc-only us");  // + the +crc route
   for (auto& sh : shapes) {
     const size_t pitch = (sh.S + 255) / 256 * 256;
     Matrix mat;
@@ -101,6 +101,21 @@ int main() {
     if (sh.k == 16 && sh.m == 22)  // EC16P20L2's fused encode: the 2 AZ-local rows over the data, as the engine builds them
       for (int r = 20; r < 22; ++r)
         for (int c = 0; c < 16; ++c) coef[(size_t)r * 16 + c] = dev::kBsEc16p20l2Rows[r][c];
+    if (sh.k == 6 && sh.m == 12) {  // EC6P10L2's fused encode: the 2 AZ-local rows over the data (lrcencoder.go)
+      // AZ a's local stripe = data [3a, 3a+3) + global parities [5a, 5a+5) (N/AZ, M/AZ per AZ), one
+      // local parity from RS(8, 1); over the data: l[c] = sum over the stripe's members of their row
+      Matrix lm;
+      build_matrix(8, 9, lm);
+      const GF& gf = GF::get();
+      for (int a = 0; a < 2; ++a)
+        for (int c = 0; c < 6; ++c) {
+          uint8_t v = 0;
+          for (int j = 0; j < 3; ++j)
+            if (c == 3 * a + j) v ^= lm.at(8, j);
+          for (int j = 0; j < 5; ++j) v ^= gf.mul(lm.at(8, 3 + j), mat.at(6 + 5 * a + j, c));
+          coef[(size_t)(10 + a) * 6 + c] = v;
+        }
+    }
     MatVecJob job;
     job.k = sh.k;
     job.m = sh.m;
@@ -141,14 +156,30 @@ int main() {
     float vms;
     CK(hipEventElapsedTime(&vms, e0, e1));
     const double vus = vms * 1e3 / reps;
-    // encode + crc32.ChecksumIEEE of every shard, fused (same algorithmic bytes as the encode)
+    // encode + crc32.ChecksumIEEE of every shard: the fused kernel where it takes the job (same
+    // algorithmic bytes as the encode), else what the engine runs then -- the product and the
+    // standalone checksum pass (route 's')
     double cus = 0;
-    if (matvec_crc_supported(sh.k, sh.m, sh.S)) {
-      std::vector<int> slot(sh.k + sh.m);
-      for (int i = 0; i < sh.k + sh.m; ++i) slot[i] = i;
-      for (int i = 0; i < 5; ++i) CK(launch_matvec_crc(job, crcs, sh.k + sh.m, slot.data(), 0));
+    std::vector<const uint8_t*> all;
+    for (int s = 0; s < sh.stripes; ++s) {
+      for (int c = 0; c < sh.k; ++c) all.push_back(in[(size_t)s * sh.k + c]);
+      for (int r = 0; r < sh.m; ++r) all.push_back(out[(size_t)s * sh.m + r]);
+    }
+    std::vector<int> slot(sh.k + sh.m);
+    for (int i = 0; i < sh.k + sh.m; ++i) slot[i] = i;
+    const bool fused = matvec_crc_accepts(job, sh.k + sh.m, slot.data());
+    const auto with_crc = [&]() {
+      if (fused) {
+        CK(launch_matvec_crc(job, crcs, sh.k + sh.m, slot.data(), 0));
+      } else {
+        CK(launch_matvec(job, 0));
+        CK(launch_crc32(all.data(), sh.S, (int)all.size(), crcs, 0));
+      }
+    };
+    {
+      for (int i = 0; i < 5; ++i) with_crc();
       CK(hipEventRecord(e0, 0));
-      for (int i = 0; i < reps; ++i) CK(launch_matvec_crc(job, crcs, sh.k + sh.m, slot.data(), 0));
+      for (int i = 0; i < reps; ++i) with_crc();
       CK(hipEventRecord(e1, 0));
       CK(hipEventSynchronize(e1));
       float cms;
@@ -158,11 +189,6 @@ int main() {
     // the standalone checksum pass over the same shards (what the fused kernel saves)
     double ous = 0;
     {
-      std::vector<const uint8_t*> all;
-      for (int s = 0; s < sh.stripes; ++s) {
-        for (int c = 0; c < sh.k; ++c) all.push_back(in[(size_t)s * sh.k + c]);
-        for (int r = 0; r < sh.m; ++r) all.push_back(out[(size_t)s * sh.m + r]);
-      }
       for (int i = 0; i < 3; ++i) CK(launch_crc32(all.data(), sh.S, (int)all.size(), crcs, 0));
       const int creps = std::max(5, reps / 4);
       CK(hipEventRecord(e0, 0));
@@ -176,9 +202,10 @@ int main() {
     const double bytes = double(sh.k + sh.m) * sh.S * sh.stripes;
     // lane-ops: per 16-B lane chunk, k inputs x (20 selector ops + m x 20 perm/xor ops)
     const double laneops = double(sh.S) / 16 * sh.stripes * sh.k * (20.0 + 20.0 * sh.m);
-    printf("%-30s %3d %3d %9zu %4d %9.1f %8.1f %6.1f %9.1f %9.1f %6.1f %9.1f %6.1f %11.1f\n", sh.name, sh.k, sh.m, sh.S,
+    printf("%-30s %3d %3d %9zu %4d %9.1f %8.1f %6.1f %9.1f %9.1f %6.1f %9.1f %6.1f %11.1f %s\n", sh.name, sh.k, sh.m, sh.S,
            sh.stripes, us, bytes / (us * 1e-6) / 1e9, 100 * bytes / (us * 1e-6) / 8e12, laneops / (us * 1e-6) / 1e12,
-           vus, 100 * bytes / (vus * 1e-6) / 8e12, cus, cus > 0 ? 100 * bytes / (cus * 1e-6) / 8e12 : 0.0, ous);
+           vus, 100 * bytes / (vus * 1e-6) / 8e12, cus, cus > 0 ? 100 * bytes / (cus * 1e-6) / 8e12 : 0.0, ous,
+           fused ? "fused" : "sep");
   }
   return 0;
 }

@@ -2,7 +2,8 @@
 // range read: ReconstructData of one segment per shard, access/stream_get.go:420-427), without
 // Python: cfsec_ec_reconstruct_data on HBM shards, median over repeated calls, beside the floor a
 // synchronous call cannot go under (one trivial kernel launched and waited for, by
-// hipStreamSynchronize and by a polled marker word).  Build: make -C tools seg_latency (links
+// hipStreamSynchronize and by a polled marker word); round 6: the same segments in page-locked and in
+// pageable host memory with a NULL stream (the Go shim's CFSEC_MEM_HOST call).  Build: make -C tools seg_latency (links
 // ../chubaofs_amd/libcfsec.so).  CFSEC_HOST_TIMING=1 adds the engine's phase times on stderr.
 #include <hip/hip_runtime.h>
 
@@ -160,6 +161,34 @@ int main(int argc, char** argv) {
         return 6;
       }
       std::printf(", \"%s_%zu_us\": %.1f", names[mi], seg, us);
+      // the same call on host memory with a NULL stream, as the Go shim makes it: page-locked rows
+      // (cfsec_host_alloc: the kernel reads and writes them over PCIe) and pageable rows (staged)
+      for (int pinned = 1; pinned >= 0; --pinned) {
+        std::vector<uint8_t*> hrow(n);
+        uint8_t* block = nullptr;
+        std::vector<uint8_t> pageable;
+        if (pinned) {
+          if (cfsec_host_alloc((size_t)n * seg, reinterpret_cast<void**>(&block))) return 7;
+        } else {
+          pageable.resize((size_t)n * seg);
+          block = pageable.data();
+        }
+        for (int i = 0; i < n; ++i) {
+          hrow[i] = block + (size_t)i * seg;
+          CK(hipMemcpy(hrow[i], d[i], seg, hipMemcpyDeviceToHost));
+        }
+        const double hus = median_us([&] {
+          for (int i = 0; i < n; ++i) sh[i] = cfsec_shard{hrow[i], seg, seg};
+          const int e = cfsec_ec_reconstruct_data(h, sh.data(), n, bad, 2, CFSEC_MEM_HOST, nullptr);
+          if (e) std::exit(8);
+        }, reps);
+        if (std::memcmp(hrow[0], want.data(), seg) != 0) {
+          std::fprintf(stderr, "rebuilt host segment differs\n");
+          return 9;
+        }
+        std::printf(", \"%s_%zu_%s_us\": %.1f", names[mi], seg, pinned ? "pinned" : "pageable", hus);
+        if (pinned) cfsec_host_free(block);
+      }
       for (int i = 0; i < n; ++i) CK(hipFree(d[i]));
     }
     cfsec_ec_free(h);
