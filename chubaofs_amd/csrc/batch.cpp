@@ -68,6 +68,7 @@ struct Group {
   uint32_t* crc_words = nullptr;
   uint32_t crc_stride = 0;
   uint8_t crc_slot[4] = {};
+  int crc_mode = 1;
   std::vector<char>* crc_done = nullptr;
 };
 
@@ -155,6 +156,7 @@ hipError_t launch_group_run(const Group& g, size_t t0, size_t t1, uint32_t* dfla
     if (g.crc_words && g.crc_done) {
       job.crc_words = g.crc_words + t0 * g.crc_stride;
       job.crc_stride = g.crc_stride;
+      job.crc_mode = g.crc_mode;
       std::memcpy(job.crc_slot, g.crc_slot, 4);
       job.crc_done = g.crc_done->data() + t0;
     }
@@ -257,12 +259,15 @@ bool fused_crc_group(const Group& g, uint32_t* dcrc, size_t nwords, const std::m
 // tasks they covered (crc_done), the rest keep the separate pass.  The words must be zeroed before.
 bool dy16_crc_group(Group& g, uint32_t* dcrc, size_t nwords, const std::map<int, int>& tasks_per_owner,
                     std::vector<char>* done) {
-  // Off unless CFSEC_BS_REPAIR_CRC=1 (read per call): measured slower than the separate pass on
-  // C5's tasklet (profiles/r05/c5_repair_crc.txt: 178-183 vs 154-156 us per call) -- the repair
-  // kernel sits at 253 of 256 VGPRs at 2 waves per SIMD, so the Horner registers and lookups spill
-  // or serialise, and the block tile order it needs costs 8 % by itself
+  // CFSEC_BS_REPAIR_CRC (read per call) = 1: the Horner steps inside the network -- measured slower
+  // than the separate pass on C5's tasklet (profiles/r05/c5_repair_crc.txt: 178-183 vs 154-156 us
+  // per call): the repair kernel sits at 253 of 256 VGPRs at 2 waves per SIMD, so the Horner
+  // registers and lookups spill or serialise, and the block tile order it needs costs 8 % by itself;
+  // = 2: each wave checksums the rebuilt rows of its own tiles after its last tile (round 6, a second
+  // phase of the same kernel: no launch, no dependence on other waves, the network's registers free)
   const char* on = std::getenv("CFSEC_BS_REPAIR_CRC");
-  if (!on || on[0] != '1') return false;
+  if (!on || (on[0] != '1' && on[0] != '2')) return false;
+  g.crc_mode = on[0] - '0';
   const Dy16Plan* d = g.plan->dy16.get();
   const size_t nt = g.tasks.size();
   if (!d || !d->syn || d->nd > kBsRepairMaxMissing || nt == 0 || !dcrc) return false;

@@ -185,6 +185,8 @@ struct BsRepairArgs {
   const uint32_t* cpow;  // tiles_per_stripe words: x^(8 * 2048 * j) mod P
   uint32_t crc_stride, crc_ones;  // crc_ones: shift(~0, S) ^ ~0, folded in by each row's first segment
   uint8_t crc_slot[4];
+  const uint32_t* lbasis;  // P2 launches: lane l's 32 columns of shift(., 16 * (63 - l)) (bs_crc_device)
+  const uint32_t* ccols;   // P2 launches: tile j's 32 columns of the multiply by x^(8 * 2048 * j), j < tps
 };
 
 // TAB launches keep their row offsets where a repair launch does not read its GfArgs: from coef to
@@ -327,9 +329,20 @@ __device__ __forceinline__ void bs_mul_acc8(uint32_t* acc, const uint32_t* s0, c
 
 // (GfArgs must stay the first parameter: bs_kernarg_ptr / bs_kernarg_u32 read it at offset 0 of
 // the arguments)
-template <int M, int ND, int TAB, bool CRC = false>
+// P2 (round 6, CFSEC_BS_REPAIR_CRC=2): the rebuilt rows' checksums as a second phase of each wave --
+// after its last tile it re-reads the rows it stored (2 KiB of each per tile, from L2 / the Infinity
+// Cache), takes each lane's 32 bytes through the 5-bit tables (bs_crc_tile, its own copy in its LDS
+// slice), moves the lane's term to the tile's end by a per-lane GF(2) basis (64 VALU, no lookups),
+// XOR-reduces the wave and moves the tile's term to the row's end (x^(8 * 2048 * j), scalar): no
+// Horner registers through the network, the tile order unchanged, no second launch, and the waves
+// that finish first checksum while the others still repair.  (The tile-to-row-end multiply is done
+// per lane from the tile's 32 columns in scalar registers before the wave's XOR: as a scalar
+// bit-serial multiply after it, 256 SALU per row and tile that a CU issues for all its waves, the
+// phase cost 34 us per C5 call instead of the separate pass's 20.)
+template <int M, int ND, int TAB, bool CRC = false, bool P2 = false>
 __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2, 2))) void gf_bs16_repair_kernel(
     const dev::GfArgs a, const BsRepairArgs r, uint32_t tiles_per_stripe, uint32_t ntiles) {
+  static_assert(!(CRC && P2), "one checksum form per launch");
   using namespace dev;
   constexpr int MO = ND + M;  // output rows per stripe: missing data rows, 20 parity rows, extras
   constexpr int PF = CRC ? kRepPrefetchCrc : kRepPrefetch;
@@ -579,6 +592,105 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
       }
     }
   }
+#ifndef CFSEC_BS_P2_PROBE
+#define CFSEC_BS_P2_PROBE 0  // 1: plain stores for the atomics, 2: phase 2 skipped (timing probes only)
+#endif
+  if constexpr (P2 && CFSEC_BS_P2_PROBE != 2) {
+    // phase 2: the checksummed rows of this wave's own tiles (written by its own stores above)
+    // its stores and the last re-prefetch complete: the rows re-read below come from L2 (this CU never
+    // read them before, so no L1 line is stale; an agent-scope acquire here -- an L2 invalidate per
+    // wave -- measured +18 us on C5's call)
+    __builtin_amdgcn_s_waitcnt(bs_waitcnt_vm(0));
+    uint32_t* tb = reinterpret_cast<uint32_t*>(pre);     // tables A and B (56 x 32 words) in its own slice
+    constexpr int kTabVec = (kBsCrcTabR - kBsCrcTabA) * 8;
+    static_assert(kTabVec * 16 <= kWaveLds, "the tables fit the wave's LDS slice");
+    for (uint32_t i = lane; i < (uint32_t)kTabVec; i += 64)
+      reinterpret_cast<u32x4*>(tb)[i] = reinterpret_cast<const u32x4*>(r.ctab)[i];
+    uint32_t col[32];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const u32x4 v = reinterpret_cast<const u32x4*>(r.lbasis + lane * 32)[q];
+      col[4 * q] = v.x;
+      col[4 * q + 1] = v.y;
+      col[4 * q + 2] = v.z;
+      col[4 * q + 3] = v.w;
+    }
+    __builtin_amdgcn_s_waitcnt(kBsWaitLgkm0);  // the table stores before any lane's lookups (one wave: in order)
+    uint32_t pst = a.pstore;
+    if constexpr (CFSEC_BS_REP_RELOAD) asm volatile("" : "+s"(pst));
+    const uint32_t ncrc = __builtin_amdgcn_readfirstlane((uint32_t)ND + (uint32_t)__builtin_popcount(pst));
+    int orow[kBsCrcRows];  // output row of checksummed row k: the rebuilt data rows, then the stored parities
+    {
+      uint32_t rest = pst;
+#pragma unroll
+      for (int k = 0; k < kBsCrcRows; ++k) {
+        orow[k] = k;
+        if (k >= ND && rest) {
+          orow[k] = ND + __builtin_ctz(rest);
+          rest &= rest - 1;
+        }
+      }
+    }
+    // a tile's checksummed rows, loaded one tile ahead (the re-reads' latency under the previous
+    // tile's lookups)
+    uint32_t cur[kBsCrcRows][8], nxt[kBsCrcRows][8];
+    const auto load_tile = [&](uint32_t tt, uint32_t (&buf)[kBsCrcRows][8]) {
+      const uint32_t s = tt / tiles_per_stripe, c = tt % tiles_per_stripe;
+#pragma unroll
+      for (int k = 0; k < kBsCrcRows; ++k)
+        if ((uint32_t)k < ncrc) bs_ld_row<false>(output(s, orow[k], c), buf[k]);
+    };
+    if (wid < ntiles) load_tile(wid, cur);
+    for (uint32_t t2 = wid; t2 < ntiles; t2 += nw) {
+      if (t2 + nw < ntiles) load_tile(t2 + nw, nxt);
+      const uint32_t s = t2 / tiles_per_stripe, c = t2 % tiles_per_stripe;
+      uint32_t m[kBsCrcRows];
+#pragma unroll
+      for (int k = 0; k < kBsCrcRows; ++k) {
+        m[k] = 0u;
+        if ((uint32_t)k < ncrc) {
+          const uint32_t u = bs_crc_tile(tb, cur[k]);
+#pragma unroll
+          for (int b = 0; b < 32; ++b) m[k] ^= (0u - ((u >> b) & 1u)) & col[b];  // the lane's term to the tile's end
+        }
+      }
+      // the tile's end to the row's end, lane by lane (linear: the wave's sum moves the same), by the
+      // tile's 32 columns in scalar registers -- a scalar bit-serial multiply per row and tile cost
+      // 256 SALU, which one CU issues for all its waves (~13 us of C5's call)
+      const uint32_t* cc = r.ccols + (size_t)(tiles_per_stripe - 1 - c) * 32;
+      uint32_t scol[32];
+#pragma unroll
+      for (int b = 0; b < 32; ++b) scol[b] = __builtin_amdgcn_readfirstlane(cc[b]);
+#pragma unroll
+      for (int k = 0; k < kBsCrcRows; ++k) {
+        uint32_t z = 0;
+#pragma unroll
+        for (int b = 0; b < 32; ++b) z ^= (0u - ((m[k] >> b) & 1u)) & scol[b];
+        m[k] = z;
+      }
+      // the wave's sums, the rows' four reductions interleaved
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1)
+#pragma unroll
+        for (int k = 0; k < kBsCrcRows; ++k) m[k] ^= (uint32_t)__shfl_xor((int)m[k], d, 64);
+#pragma unroll
+      for (int k = 0; k < kBsCrcRows; ++k) {
+        if ((uint32_t)k < ncrc) {
+          uint32_t w = m[k];
+          if (c == 0) w ^= r.crc_ones;
+#if CFSEC_BS_P2_PROBE == 1  // timing probe only (wrong words): a plain store instead of the atomic
+          if (lane == 0) r.crcw[(size_t)s * r.crc_stride + r.crc_slot[k]] = w;
+#else
+          if (lane == 0) atomicXor(r.crcw + (size_t)s * r.crc_stride + r.crc_slot[k], w);
+#endif
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < kBsCrcRows; ++k)
+#pragma unroll
+        for (int w = 0; w < 8; ++w) cur[k][w] = nxt[k][w];
+    }
+  }
   bs_drain_exit();
 }
 
@@ -673,19 +785,33 @@ void coef_tables_host(uint8_t c, dev::u32x4& t01, uint32_t& t2) {  // gf_device.
   t2 = tt2;
 }
 
-template <int M, int TAB, bool CRC = false>
+template <int M, int TAB, bool CRC = false, bool P2 = false>
 hipError_t launch_rep_m(int nd, const dev::GfArgs& a, const BsRepairArgs& r, unsigned grid, uint32_t tps,
                         uint32_t nt, hipStream_t st) {
   switch (nd) {
-    case 0: hipLaunchKernelGGL((gf_bs16_repair_kernel<M, 0, TAB, CRC>), dim3(grid), dim3(64 * kBsWaves), 0, st, a, r, tps, nt); break;
+    case 0:
+      hipLaunchKernelGGL((gf_bs16_repair_kernel<M, 0, TAB, CRC, P2>), dim3(grid), dim3(64 * kBsWaves), 0, st, a, r, tps, nt);
+      break;
     case 1:  // (no CRC form: one missing data row spills ~130 VGPRs with the checksums, the separate pass is faster)
       if constexpr (CRC) return hipErrorInvalidValue;
-      else hipLaunchKernelGGL((gf_bs16_repair_kernel<M, 1, TAB, CRC>), dim3(grid), dim3(64 * kBsWaves), 0, st, a, r, tps, nt);
+      else hipLaunchKernelGGL((gf_bs16_repair_kernel<M, 1, TAB, CRC, P2>), dim3(grid), dim3(64 * kBsWaves), 0, st, a, r, tps, nt);
       break;
-    case 2: hipLaunchKernelGGL((gf_bs16_repair_kernel<M, 2, TAB, CRC>), dim3(grid), dim3(64 * kBsWaves), 0, st, a, r, tps, nt); break;
+    case 2:
+      hipLaunchKernelGGL((gf_bs16_repair_kernel<M, 2, TAB, CRC, P2>), dim3(grid), dim3(64 * kBsWaves), 0, st, a, r, tps, nt);
+      break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
+}
+
+// the repair launch with the checksum form r asks for (rep_crc_args): none, Horner in the network
+// (crc mode 1), or the second phase (mode 2)
+template <int M, int TAB>
+hipError_t launch_rep_crc(int nd, int mode, const dev::GfArgs& a, const BsRepairArgs& r, unsigned grid, uint32_t tps,
+                          uint32_t nt, hipStream_t st) {
+  if (mode == 2) return launch_rep_m<M, TAB, false, true>(nd, a, r, grid, tps, nt, st);
+  if (mode == 1) return launch_rep_m<M, TAB, true>(nd, a, r, grid, tps, nt, st);
+  return launch_rep_m<M, TAB>(nd, a, r, grid, tps, nt, st);
 }
 
 // ---- host side of the fused checksums (bs_crc_tile / bs_crc_lanes) ----
@@ -738,9 +864,11 @@ std::vector<uint32_t> bs_crc_host_tables() {
 struct BsCrcDev {
   std::mutex mu;
   uint32_t* tab = nullptr;
-  std::map<uint32_t, uint32_t*> pow;
+  uint32_t* lbasis = nullptr;
+  std::map<uint32_t, uint32_t*> pow, cols;
 };
-hipError_t bs_crc_device(uint32_t tps, const uint32_t** tab, const uint32_t** pw) {
+hipError_t bs_crc_device(uint32_t tps, const uint32_t** tab, const uint32_t** pw, const uint32_t** lbasis,
+                         const uint32_t** ccols) {
   static BsCrcDev per[64];
   int d = 0;
   hipError_t e = hipGetDevice(&d);
@@ -758,6 +886,20 @@ hipError_t bs_crc_device(uint32_t tps, const uint32_t** tab, const uint32_t** pw
     }
     c.tab = p;
   }
+  if (!c.lbasis) {  // lane l: the columns (bit b of a word) of the multiply by x^(8 * 16 * (63 - l))
+    std::vector<uint32_t> h(64 * 32);
+    for (int l = 0; l < 64; ++l) {
+      const uint32_t k = crc_xpow(8ull * 16 * (63 - l));
+      for (int b = 0; b < 32; ++b) h[(size_t)l * 32 + b] = crc_mulmod(k, 1u << b);
+    }
+    uint32_t* p = nullptr;
+    if ((e = hipMalloc(reinterpret_cast<void**>(&p), h.size() * 4)) != hipSuccess) return e;
+    if ((e = hipMemcpy(p, h.data(), h.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) {
+      (void)hipFree(p);
+      return e;
+    }
+    c.lbasis = p;
+  }
   auto it = c.pow.find(tps);
   if (it == c.pow.end()) {
     std::vector<uint32_t> h(tps);
@@ -772,20 +914,37 @@ hipError_t bs_crc_device(uint32_t tps, const uint32_t** tab, const uint32_t** pw
     }
     it = c.pow.emplace(tps, p).first;
   }
+  auto jt = c.cols.find(tps);
+  if (jt == c.cols.end()) {  // tile j: the columns (bit b) of the multiply by x^(8 * 2048 * j)
+    std::vector<uint32_t> h((size_t)tps * 32);
+    const uint32_t k = crc_xpow(8ull * 2048);
+    uint32_t v = 0x80000000u;
+    for (uint32_t j = 0; j < tps; ++j, v = crc_mulmod(v, k))
+      for (int b = 0; b < 32; ++b) h[(size_t)j * 32 + b] = crc_mulmod(v, 1u << b);
+    uint32_t* p = nullptr;
+    if ((e = hipMalloc(reinterpret_cast<void**>(&p), h.size() * 4)) != hipSuccess) return e;
+    if ((e = hipMemcpy(p, h.data(), h.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) {
+      (void)hipFree(p);
+      return e;
+    }
+    jt = c.cols.emplace(tps, p).first;
+  }
   *tab = c.tab;
   *pw = it->second;
+  *lbasis = c.lbasis;
+  *ccols = jt->second;
   return hipSuccess;
 }
 
 // the CRC fields of a repair launch, or false (not eligible: more than kBsCrcRows checksummed rows,
 // a zeroing request the atomics would race with, too many tiles per stripe for the table)
 bool rep_crc_args(int nd, const dev::GfArgs& a, uint64_t len, const BsCrcReq* crc, uint32_t* words, BsRepairArgs& r) {
-  if (!crc || !words || a.nzw || nd == 1) return false;
+  if (!crc || !words || a.nzw || (nd == 1 && crc->mode == 1) || (crc->mode != 1 && crc->mode != 2)) return false;
   const int ncrc = nd + __builtin_popcount(a.pstore);
   if (ncrc != crc->nrows || ncrc > kBsCrcRows || len % dev::kBsWaveBytes || len / dev::kBsWaveBytes > (1u << 20))
     return false;
   const uint32_t tps = (uint32_t)(len / dev::kBsWaveBytes);
-  if (bs_crc_device(tps, &r.ctab, &r.cpow) != hipSuccess) {
+  if (bs_crc_device(tps, &r.ctab, &r.cpow, &r.lbasis, &r.ccols) != hipSuccess) {
     (void)hipGetLastError();
     return false;
   }
@@ -820,8 +979,8 @@ hipError_t launch_bs16_repair(int nd, int ne, const uint8_t* missing, const uint
   if (!rep_args(nd, missing, prow, ainv, r)) return hipErrorOutOfMemory;
   const unsigned grid = (unsigned)std::min<uint64_t>((uint64_t)cu_count(), (ntiles + kBsWaves - 1) / kBsWaves);
   if (rep_crc_args(nd, a, len, crc, crc_words, r)) {
-    const hipError_t e = ne == 2 ? launch_rep_m<22, 0, true>(nd, a, r, grid, tps, (uint32_t)ntiles, st)
-                                 : launch_rep_m<20, 0, true>(nd, a, r, grid, tps, (uint32_t)ntiles, st);
+    const hipError_t e = ne == 2 ? launch_rep_crc<22, 0>(nd, crc->mode, a, r, grid, tps, (uint32_t)ntiles, st)
+                                 : launch_rep_crc<20, 0>(nd, crc->mode, a, r, grid, tps, (uint32_t)ntiles, st);
     if (e == hipSuccess && crc_done) *crc_done = true;
     return e;
   }
@@ -967,12 +1126,9 @@ hipError_t launch_bs16_repair_tab(int nd, int ne, const uint8_t* missing, const 
       if (ntiles > 0xFFFFFFFFull) return hipErrorInvalidValue;
       const unsigned grid = (unsigned)std::min<uint64_t>((uint64_t)cu_count(), (ntiles + kBsWaves - 1) / kBsWaves);
       const bool fused = rep_crc_args(nd, t, len, crc, crc_words, r);
-      if (fused)
-        e = ne == 2 ? launch_rep_m<22, 2, true>(nd, t, r, grid, tps, (uint32_t)ntiles, st)
-                    : launch_rep_m<20, 2, true>(nd, t, r, grid, tps, (uint32_t)ntiles, st);
-      else
-        e = ne == 2 ? launch_rep_m<22, 2>(nd, t, r, grid, tps, (uint32_t)ntiles, st)
-                    : launch_rep_m<20, 2>(nd, t, r, grid, tps, (uint32_t)ntiles, st);
+      const int mode = fused ? crc->mode : 0;
+      e = ne == 2 ? launch_rep_crc<22, 2>(nd, mode, t, r, grid, tps, (uint32_t)ntiles, st)
+                  : launch_rep_crc<20, 2>(nd, mode, t, r, grid, tps, (uint32_t)ntiles, st);
       if (e != hipSuccess) return e;
       if (fused && crc_done) *crc_done = true;
       return dev_table_fence(dt, st);

@@ -475,6 +475,7 @@ hipError_t launch_dy16_repair(const Dy16RepairJob& job, hipStream_t stream) {
     if (ncrc >= 1 && ncrc <= 4) {
       crc_req.nrows = ncrc;
       crc_req.stride = job.crc_stride;
+      crc_req.mode = job.crc_mode;
       for (int q = 0; q < 4; ++q) crc_req.slot[q] = job.crc_slot[q];
     }
   }

@@ -117,6 +117,7 @@ struct BsCrcReq {
   uint32_t stride = 0;
   uint8_t slot[4] = {};
   int nrows = 0;
+  int mode = 1;  // 1: Horner inside the network (blocked tile order); 2: a pass over the wave's own tiles after them
 };
 hipError_t launch_bs16_repair(int nd, int ne, const uint8_t* missing, const uint8_t* prow, const uint8_t* ainv,
                               const dev::GfArgs& a, unsigned ns, uint64_t len, hipStream_t st,

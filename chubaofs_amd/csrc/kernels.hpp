@@ -63,6 +63,7 @@ struct Dy16RepairJob {
   uint32_t* crc_words = nullptr;
   uint32_t crc_stride = 0;
   uint8_t crc_slot[4] = {};
+  int crc_mode = 1;  // gf_launch.hpp BsCrcReq::mode
   char* crc_done = nullptr;
 };
 hipError_t launch_dy16_repair(const Dy16RepairJob& job, hipStream_t stream);

@@ -6,8 +6,9 @@ gf_bs16.hip's CRC launches fold crc32.ChecksumIEEE of the stored rows into the r
 (batch.cpp dy16_crc_group).  Every case here compares statuses, every shard and the words with the
 ec oracle's repair and zlib; CFSEC_TRACE_BATCH names which groups the repair pass checksummed, so
 the routing (fused: whole 2 KiB tiles, <= 4 stored rows, 0 or 2 missing data rows; else the
-separate pass) is pinned too.  The route is off by default (CFSEC_BS_REPAIR_CRC=1 turns it on: it
-measured slower than the separate pass), so these tests turn it on.
+separate pass) is pinned too.  The route is off by default, so these tests turn it on: mode 1 (the
+Horner steps inside the network, measured slower than the separate pass) and mode 2
+(round 6: each wave checksums the rows of its own tiles after its last tile).
 """
 import random
 import re
@@ -66,16 +67,18 @@ def test_repair_pass_checksums_off_by_default(monkeypatch, capfd):
     assert [crcs[0][i] for i in range(n) if i not in bad] == [0] * (n - len(bad))
 
 
+@pytest.mark.parametrize("mode", ["1", "2"])
 @pytest.mark.parametrize("layout", ["slab", "scattered"])
 @pytest.mark.parametrize("bad,fused", [([0, 1, 16, 17], True), ([16, 17], True), ([5, 12, 30], True),
                                        ([3, 20], False), ([0, 1, 16, 17, 18], False)])
-def test_repair_pass_checksums(layout, bad, fused, monkeypatch, capfd):
+def test_repair_pass_checksums(mode, layout, bad, fused, monkeypatch, capfd):
     """24 bids of one erasure pattern at S = 3 x 2 KiB: one slab at a bid stride (one affine launch)
     or every shard at its own address (the device row-offset table); bids 4 and 17 carry a corrupted
     compared parity (ErrVerify; their words are 0, clear_failed_crcs).  ([3, 20]: one missing data row
-    -- no CRC form, the separate pass; five rows rebuilt -- more than the kernel's 4.)"""
+    -- no mode-1 form, the separate pass; mode 2 takes it.  Five rows rebuilt -- more than the kernel's 4.)"""
     monkeypatch.setenv("CFSEC_TRACE_BATCH", "1")
-    monkeypatch.setenv("CFSEC_BS_REPAIR_CRC", "1")
+    monkeypatch.setenv("CFSEC_BS_REPAIR_CRC", mode)
+    fused = fused or (mode == "2" and bad == [3, 20])
     enc = enc_new()
     t = cm.GetTactic(MODE)
     n = t.N + t.M + t.L
@@ -117,11 +120,12 @@ def test_repair_pass_checksums(layout, bad, fused, monkeypatch, capfd):
         assert sum(f for _, f in counts) == 0, err
 
 
-def test_repair_pass_checksums_c5_async_and_tail(monkeypatch):
+@pytest.mark.parametrize("mode", ["1", "2"])
+def test_repair_pass_checksums_c5_async_and_tail(mode, monkeypatch):
     """C5's tasklet (64 bids x 262,144 B) through the asynchronous call with device words -- every
     rebuilt shard's word equals zlib's, the Verify flags of the two corrupted bids set -- and the same
     tasklet at S = 262,144 + 48 (a row tail: the separate pass), equal words."""
-    monkeypatch.setenv("CFSEC_BS_REPAIR_CRC", "1")
+    monkeypatch.setenv("CFSEC_BS_REPAIR_CRC", mode)
     enc = enc_new()
     t = cm.GetTactic(MODE)
     n = t.N + t.M + t.L
