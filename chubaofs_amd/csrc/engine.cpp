@@ -417,6 +417,48 @@ void host_range_remove(void* base) {
   r.by_base.erase((uintptr_t)base);
 }
 
+// Page-locked staging for small pageable host calls (RSEngine::run): a free list of cfsec-owned
+// hipHostMalloc blocks (registered in the host-range registry, so the zero-copy path takes them),
+// one per concurrent call, kept for reuse.
+namespace {
+struct PinnedStages {
+  std::mutex mu;
+  std::vector<std::pair<uint8_t*, size_t>> free;
+};
+PinnedStages& pinned_stages() {
+  static PinnedStages p;
+  return p;
+}
+}  // namespace
+
+static std::pair<uint8_t*, size_t> pinned_stage_take(size_t bytes) {
+  PinnedStages& p = pinned_stages();
+  {
+    std::lock_guard<std::mutex> lk(p.mu);
+    for (size_t i = 0; i < p.free.size(); ++i)
+      if (p.free[i].second >= bytes) {
+        const auto b = p.free[i];
+        p.free.erase(p.free.begin() + (long)i);
+        return b;
+      }
+  }
+  const size_t cap = std::max<size_t>(bytes, (size_t)256 << 10);
+  void* h = nullptr;
+  if (hipHostMalloc(&h, cap, hipHostMallocPortable) != hipSuccess) {
+    (void)hipGetLastError();
+    return {nullptr, 0};
+  }
+  host_range_add(h, cap);
+  return {static_cast<uint8_t*>(h), cap};
+}
+
+static void pinned_stage_give(std::pair<uint8_t*, size_t> b) {
+  if (!b.first) return;
+  PinnedStages& p = pinned_stages();
+  std::lock_guard<std::mutex> lk(p.mu);
+  p.free.push_back(b);
+}
+
 bool device_alias(uint8_t* p, uint8_t** dptr) {
   {
     HostRanges& r = host_ranges();
@@ -488,6 +530,33 @@ Status RSEngine::run(const Matrix& rows, const std::vector<cfsec_shard*>& ins,
       for (int i = 0; i < nin; ++i) pin[i] = &zin[i];
       for (int r = 0; r < nout; ++r) pout[r] = &zout[r];
       return run(rows, pin, pout, S, CFSEC_MEM_DEVICE, nullptr, mode, ok);
+    }
+    // Small pageable calls (a degraded range read's segments): the rows copied on the CPU into
+    // page-locked staging and coded there in place, instead of HIP's staged copies of pageable memory
+    // (~130 us per call whatever the size up to 64 KiB, profiles/r06/bench_s1).
+    const size_t total = S * (size_t)(nin + nout);
+    if (!two_step_verify && total <= kSmallPageable) {
+      std::pair<uint8_t*, size_t> stage = pinned_stage_take(total);
+      if (stage.first) {
+        std::vector<cfsec_shard> sin(nin), sout(nout);
+        std::vector<cfsec_shard*> pin(nin), pout(nout);
+        for (int i = 0; i < nin; ++i) {
+          std::memcpy(stage.first + S * i, ins[i]->data, S);
+          sin[i] = cfsec_shard{stage.first + S * i, S, S};
+          pin[i] = &sin[i];
+        }
+        for (int r = 0; r < nout; ++r) {
+          uint8_t* d = stage.first + S * (nin + r);
+          if (mode != MatVecMode::kStore) std::memcpy(d, outs[r]->data, S);
+          sout[r] = cfsec_shard{d, S, S};
+          pout[r] = &sout[r];
+        }
+        Status st = run(rows, pin, pout, S, CFSEC_MEM_HOST, nullptr, mode, ok);
+        if (st == CFSEC_OK && mode != MatVecMode::kVerify)
+          for (int r = 0; r < nout; ++r) std::memcpy(outs[r]->data, sout[r].data, S);
+        pinned_stage_give(stage);
+        return st;
+      }
     }
     if (!two_step_verify) return run_host(rows, ins, outs, S, mode, ok);
   }

@@ -337,6 +337,8 @@ class RSEngine {
 
   // Columns of a host-memory call per chunk (bytes per row) through the two-stream pipeline.
   static constexpr size_t kHostChunk = 1 << 20;
+  // pageable host calls moving at most this many bytes take the page-locked staging path (run)
+  static constexpr size_t kSmallPageable = 1 << 20;
 
  private:
   Status run_host(const Matrix& rows, const std::vector<cfsec_shard*>& ins,

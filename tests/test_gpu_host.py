@@ -77,3 +77,31 @@ def test_pinned_alloc_roundtrip():
     a[:] = 7
     assert int(a.sum()) == 7 << 20
     assert _lib.pinned_empty(0).size == 0
+
+
+@pytest.mark.parametrize("k,m", [(12, 4), (6, 6)])
+@pytest.mark.parametrize("delta", [-1, 0, 1])
+def test_small_pageable_staging_boundary(k, m, delta):
+    """Pageable host calls moving at most 1 MiB (rows x S) are copied into page-locked staging on the
+    CPU and coded there (round 6: a degraded range read's segments, ~130 -> ~20 us); one byte more per
+    row takes the chunked pipeline.  Encode, Verify (a flipped byte caught), ReconstructData and
+    Reconstruct at both sides of the boundary, bytes equal to the oracle."""
+    S = (1 << 20) // (k + m) + delta
+    sh = make(k, m, S, False, False, seed=S * 3 + k)
+    want = [s.copy() for s in sh]
+    assert O.encode(k, m, want) == 0
+    enc = rs().New(k, m)
+    enc.Encode(sh)
+    for i in range(k + m):
+        assert np.array_equal(sh[i], want[i]), i
+    assert enc.Verify(sh)
+    sh[k][S // 2] ^= 0x10
+    assert not enc.Verify(sh)
+    sh[k][S // 2] ^= 0x10
+    work = [s[:0] if i in (0, 1) else s.copy() for i, s in enumerate(sh)]
+    enc.ReconstructData(work)
+    assert np.array_equal(work[0], want[0]) and np.array_equal(work[1], want[1])
+    work = [s[:0] if i in (1, k) else s.copy() for i, s in enumerate(sh)]
+    enc.Reconstruct(work)
+    for i in range(k + m):
+        assert np.array_equal(work[i], want[i]), i
