@@ -235,6 +235,9 @@ hipError_t launch_matvec_crc(const MatVecJob& job, uint32_t* crc, int crc_stride
   hipError_t e = zero ? hipMemsetAsync(crc, 0, sizeof(uint32_t) * (size_t)crc_stride * job.nstripes, stream)
                       : hipSuccess;
   if (e != hipSuccess || job.nstripes == 0 || job.len == 0) return e;
+  // EC6P10L2's fused LRC encode and EC12P4's encode with every shard checksummed: the bit-sliced
+  // network, checksums from its bit planes (gf_bs_crc.hip, round 6)
+  if (cin && bs_crc_takes(job, crc_stride, slot)) return launch_bs_crc(job, crc, crc_stride, slot, stream);
 
   GfCrcArgs a{};
   e = crc_device_tables(&a.tabs);

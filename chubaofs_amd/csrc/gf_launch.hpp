@@ -138,6 +138,15 @@ hipError_t launch_bs16_repair_tab(int nd, int ne, const uint8_t* missing, const 
                                   hipStream_t st, bool* ok, const BsCrcReq* crc = nullptr,
                                   uint32_t* crc_words = nullptr, bool* crc_done = nullptr);
 
+// Fused encode + crc32.ChecksumIEEE of every row on the bit-sliced networks (gf_bs_crc.hip, round 6):
+// EC6P10L2's fused LRC encode (6 x 12) and EC12P4's encode (12 x 4), coef equal to the network's
+// constants, the inputs checksummed too (slot[0] >= 0), any row alignment and length; words as
+// launch_matvec_crc (zeroed by the caller).  CFSEC_BS_CRC (bit 0: 6 x 12, bit 1: 12 x 4) = 0 keeps
+// the lookup-product kernels.
+bool bs_crc_matches(int k, int m, const uint8_t* coef);
+bool bs_crc_takes(const MatVecJob& job, int crc_stride, const int* slot);
+hipError_t launch_bs_crc(const MatVecJob& job, uint32_t* crc, int crc_stride, const int* slot, hipStream_t st);
+
 // repair_dy16 on a GfArgs block (gf_dy16.hip); launch_dy16_repair (gf_kernels.hip) fills it.
 hipError_t launch_dy16_repair_args(int nd, int ne, const dev::GfArgs& a, unsigned ns, hipStream_t st);
 

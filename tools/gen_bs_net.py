@@ -17,6 +17,9 @@ checks its engine's coefficients against these constants before it takes the net
 
   python3 tools/gen_bs_net.py ec16p20l2 --paired --joint > chubaofs_amd/csrc/bs_net_ec16p20l2.hpp
   python3 tools/gen_bs_net.py ec15p12 | ec12p9   (measured, not shipped: profiles/r04/bsk_ab.txt)
+  python3 tools/gen_bs_net.py ec6p10l2 --paired --joint > chubaofs_amd/csrc/bs_net_ec6p10l2.hpp
+  python3 tools/gen_bs_net.py ec12p4 --paired --joint > chubaofs_amd/csrc/bs_net_ec12p4.hpp
+    (round 6: the fused encode + checksum kernels, gf_bs_crc.hip)
 """
 import sys
 
@@ -86,6 +89,25 @@ def ec16p20l2_rows():
         for t in range(10):
             for c in range(16):
                 row[c] ^= gmul(lc[8 + t], g[10 * a + t][c])
+        rows.append(row)
+    return rows
+
+
+def lrc_rows(k, m, azs, ln):
+    """An LRC's fused encode rows (as the engine's ECEncoder::create builds them): the m KRS global
+    rows, then each AZ's local parity over the data -- AZ a holds data k/azs * a .. and global parities
+    m/azs * a .., its one local row is the KRS (ln, 1) parity row over those ln members."""
+    g = parity_rows(k, m)
+    lc = parity_rows(ln, 1)[0]
+    rows = [r[:] for r in g]
+    dk, dm = k // azs, m // azs
+    for a in range(azs):
+        row = [0] * k
+        for t in range(dk):
+            row[dk * a + t] ^= lc[t]
+        for t in range(dm):
+            for c in range(k):
+                row[c] ^= gmul(lc[dk + t], g[dm * a + t][c])
         rows.append(row)
     return rows
 
@@ -374,6 +396,9 @@ CODES = {
     # name: (title, rows, note on NR)
     "ec16p20l2": ("The EC16P20L2 parity (20 KRS global rows, then the 2 AZ-local rows over the data)",
                   ec16p20l2_rows, "NR = 20: EC16P20's global parity; 22: with the local rows"),
+    "ec6p10l2": ("The EC6P10L2 fused LRC encode rows (10 KRS global rows, then the 2 AZ-local rows over the data)",
+                 lambda: lrc_rows(6, 10, 2, 8), "NR = 12"),
+    "ec12p4": ("The EC12P4 parity (KRS buildMatrix(12, 16) rows 12..15)", lambda: parity_rows(12, 4), "NR = 4"),
     "ec15p12": ("The EC15P12 parity (KRS buildMatrix(15, 27) rows 15..26)", lambda: parity_rows(15, 12), "NR = 12"),
     "ec12p9": ("The EC12P9 parity (KRS buildMatrix(12, 21) rows 12..20)", lambda: parity_rows(12, 9), "NR = 9"),
 }
