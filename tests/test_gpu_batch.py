@@ -674,10 +674,10 @@ def test_ec_reconstruct_batch_async_crc():
 
 @pytest.mark.parametrize("size", [1, 17, 4095, 4097, 65539, 699051])
 def test_lrc_fused_encode_crc_ragged(size, monkeypatch, capfd):
-    """EC6P10L2's fused LRC encode + all 18 checksums (C4's put, stream_put.go:249-253) on the
-    lookup-product kernel with 16-byte entries (round 6): 5 equal-length bids in device memory (one
-    fused launch), ragged and whole-tile sizes; parity against the ec oracle's Encode, every word
-    against crc32.ChecksumIEEE."""
+    """EC6P10L2's fused LRC encode + all 18 checksums (C4's put, stream_put.go:249-253; round 6: the
+    bit-sliced network with checksums from its bit planes, gf_bs_crc.hip): 5 equal-length bids in
+    device memory (one fused launch), ragged and whole-tile sizes; parity against the ec oracle's
+    Encode, every word against crc32.ChecksumIEEE."""
     monkeypatch.setenv("CFSEC_TRACE_BATCH", "1")
     from chubaofs_amd import ec
     t = cm.GetTactic(cm.EC6P10L2)

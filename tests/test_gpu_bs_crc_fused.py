@@ -3,16 +3,15 @@
 access checksums every data and parity shard right after Encode (blobstore/access/stream_put.go:
 249-253).  For EC12P4 and EC6P10L2's fused LRC encode the product now runs as the bit-sliced XOR
 network and every checksum comes from the bit planes it holds (56 lookups per lane and row, no row
-re-read).  Checked here against the C oracle's Encode (KRS/reedsolomon.go:707-738 restated) and zlib's
+re-read), W waves per stripe on every W-th tile, each folding its lanes' Horner registers once.  Checked here against the C oracle's Encode (KRS/reedsolomon.go:707-738 restated) and zlib's
 CRC-32 at lengths around the 2 KiB column tile (a partial last tile, tiles shorter than a lane's
 piece, lengths below 16), with rows at odd byte offsets, stripes in one allocation (one affine launch)
 and in separate allocations (pointer-table launches), and with checksum words at a stride and slots
 of the caller's choosing (the ec batch seam).  CFSEC_TRACE_CRC names the launches, so each case also
 asserts that the bit-sliced route ran.
 
-EC6P10L2 runs the plane-residue form by default (every output checksum from the input rows' bit-plane
-residues); the per-row form (CFSEC_BS_CRC bit 2) and EC12P4's route (bit 1, off by default: no faster
-than the lookup-product kernel) are re-run in a child process with CFSEC_BS_CRC=7.
+EC6P10L2's route is on by default; EC12P4's (CFSEC_BS_CRC bit 1) is off -- no faster than the
+lookup-product kernel -- and is exercised in a child process with CFSEC_BS_CRC=3.
 """
 import os
 import subprocess
@@ -29,7 +28,7 @@ pytestmark = pytest.mark.gpu
 
 SIZES = [1, 15, 16, 17, 1023, 1024, 1025, 2047, 2048, 2049, 4095, 4097, 6144, 65539, 174763]
 MASK = int(os.environ.get("CFSEC_BS_CRC", "1"), 0)
-ec12p4 = pytest.mark.skipif(not MASK & 2, reason="EC12P4's route is off by default (run in the child, CFSEC_BS_CRC=7)")
+ec12p4 = pytest.mark.skipif(not MASK & 2, reason="EC12P4's route is off by default (run in the child, CFSEC_BS_CRC=3)")
 
 
 @pytest.fixture(scope="module")
@@ -172,8 +171,8 @@ def test_ec12p4_large_stripe_vs_separate_pass(rs, monkeypatch, capfd):
 
 @pytest.mark.skipif(os.environ.get("CFSEC_BS_CRC") is not None, reason="the child process itself")
 def test_per_row_form_and_ec12p4_in_child():
-    """This module again with CFSEC_BS_CRC=7: EC6P10L2 in the per-row form, EC12P4's route on."""
-    env = dict(os.environ, CFSEC_BS_CRC="7")
+    """This module again with CFSEC_BS_CRC=3: EC12P4's route on too."""
+    env = dict(os.environ, CFSEC_BS_CRC="3")
     r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", __file__],
                        env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
