@@ -30,7 +30,10 @@
 // per register: 189); 1-4 tiles per wave and stripe 194-249 us (more folds); the product alone in this
 // structure 156 us, in gf_bs_kernel's every-nw-th-tile order 143 us (that order leaves no run of one
 // row per wave for the Horner registers).  Kept off for EC12P4 (bit 1): 197-207 us against 181-203 for
-// the lookup-product kernel.  A plane-residue form -- the 12 output checksums as linear functions of
+// the lookup-product kernel.  The 16 + 20 code (EC16P20 / EC16P20L2's fused encode, all 36 / 38 rows
+// checksummed) had no fused form: 256 VGPRs with 79 spilled at 2 waves per SIMD, still 243.6 -> 218.5 us
+// (EC16P20L2, 64 x 262,144) and 227.5 -> 206.5 us (EC16P20) against the product + separate pass
+// (profiles/r06/bs_crc/shape_sweep_ec16.txt).  A plane-residue form -- the 12 output checksums as linear functions of
 // the 6 input rows' 48 bit-plane residues, 3x fewer lookups -- ran at 192-211 us (2 waves per SIMD at
 // 172 VGPRs) and was dropped.
 //
@@ -48,6 +51,7 @@
 #include <vector>
 
 #include "bs_net_ec12p4.hpp"
+#include "bs_net_ec16p20l2.hpp"
 #include "bs_net_ec6p10l2.hpp"
 #include "gf_bitslice.hpp"
 #include "gf_launch.hpp"
@@ -81,7 +85,7 @@ struct __attribute__((aligned(16))) BcArgs {
   uint32_t fin, pad0;    // shift(~0, len) ^ ~0
   uint32_t* crc;         // [stripe][crc_stride] checksum words (XOR-accumulated)
   const uint32_t* tabs;  // kBcTabs x 32 words
-  uint8_t slot[32];      // checksum word of kernel row i (inputs, then outputs)
+  uint8_t slot[40];      // checksum word of kernel row i (inputs, then outputs)
   // tile j's end to the row's end is x^(8 (2048 e - pad)), e = tps - 1 - j:
   // pw[0][e % 64] (pad folded in) * pw[1][(e / 64) % 64] * pw[2][e / 4096]
   uint32_t pw[3][kBcPow];
@@ -157,9 +161,10 @@ __global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(N
     const BcArgs a) {
   constexpr int K = Net::K;
   constexpr int NR = K + M;  // checksummed rows: the inputs, then the outputs
-  static_assert(NR <= 32, "one lane per row's word");
+  static_assert(NR <= 64, "one lane per row's word");
+  constexpr int NP = NR <= 32 ? 32 : 64;  // the rows padded for the lane fold
   __shared__ uint32_t tb[kBcTabs * 32];  // planes, the jump, the lane tree
-  __shared__ uint32_t slot[32];  // the rows' word offsets, indexed per lane at the segment ends
+  __shared__ uint32_t slot[64];  // the rows' word offsets, indexed per lane at the segment ends
   for (uint32_t i = threadIdx.x; i < kBcPlaneTabs * 8; i += blockDim.x)
     reinterpret_cast<u32x4*>(tb)[i] = reinterpret_cast<const u32x4*>(a.tabs)[i];
   for (uint32_t i = threadIdx.x; i < 6 * kBcFields * 8; i += blockDim.x)
@@ -245,17 +250,18 @@ __global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(N
     // of a 32-column basis per register -- so lane l holds row bitrev5(l mod 32)'s sum at the tile's end
     uint32_t mine;
     {
-      uint32_t v[32];
+      uint32_t v[NP];
 #pragma unroll
-      for (int i = 0; i < 32; ++i) v[i] = i < NR ? R[i] : 0u;
+      for (int i = 0; i < NP; ++i) v[i] = i < NR ? R[i] : 0u;
 #pragma unroll
       for (int k = 0; k < 6; ++k) {
-        const int half = k < 5 ? 16 >> k : 1;
+        const int half = NP >> (k + 1) ? NP >> (k + 1) : 1;  // NP = 32: the 6th level combines halves
+        const bool halving = (NP >> (k + 1)) != 0;
         const bool up = (lane >> k) & 1u;
 #pragma unroll
         for (int i = 0; i < half; ++i) {
-          const uint32_t send = k == 5 ? v[i] : (up ? v[i] : v[half + i]);
-          const uint32_t keep = k == 5 ? v[i] : (up ? v[half + i] : v[i]);
+          const uint32_t send = !halving ? v[i] : (up ? v[i] : v[half + i]);
+          const uint32_t keep = !halving ? v[i] : (up ? v[half + i] : v[i]);
           const uint32_t recv = (uint32_t)__shfl_xor((int)send, 1 << k, 64);
           const uint32_t lo = up ? recv : keep, hi = up ? keep : recv;
           v[i] = bc_five7(tb + (kBcTree + k * kBcFields) * 32, lo) ^ hi;
@@ -264,13 +270,14 @@ __global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(N
       }
       mine = v[0];
     }
-    const uint32_t row = __builtin_bitreverse32(lane & 31u) >> 27;
+    // lane l holds row bitrev(l) (6 bits for 64 padded rows, 5 of l mod 32 for 32)
+    const uint32_t row = NP == 64 ? __builtin_bitreverse32(lane) >> 26 : __builtin_bitreverse32(lane & 31u) >> 27;
     const uint32_t e = tps - 1 - c;
     const uint32_t k = bc_mulmod(bc_mulmod(a.pw[0][e % kBcPow], a.pw[1][(e / kBcPow) % kBcPow]),
                                  a.pw[2][e / (kBcPow * kBcPow)]);
     uint32_t w = bc_mulmod(mine, k);
     if (j == 0) w ^= a.fin;
-    if (lane < 32 && row < (uint32_t)NR) atomicXor(a.crc + (size_t)s * a.crc_stride + slot[row], w);
+    if ((NP == 64 || lane < 32) && row < (uint32_t)NR) atomicXor(a.crc + (size_t)s * a.crc_stride + slot[row], w);
   }
 }
 
@@ -280,10 +287,11 @@ uint32_t env_mask(const char* name, uint32_t dflt) {
   const char* v = std::getenv(name);
   return v && *v ? (uint32_t)std::strtoul(v, nullptr, 0) : dflt;
 }
-// CFSEC_BS_CRC: bit 0 EC6P10L2's fused LRC encode (6 x 12, on by default), bit 1 EC12P4 (12 x 4: off
-// by default, no faster than the lookup-product kernel); 0 keeps the lookup-product kernels (A/B)
+// CFSEC_BS_CRC: bit 0 EC6P10L2's fused LRC encode (6 x 12), bit 2 EC16P20 / EC16P20L2 (16 x 20 / 22:
+// the product + separate pass otherwise) -- both on by default --, bit 1 EC12P4 (12 x 4: off, no faster
+// than the lookup-product kernel); 0 keeps the lookup-product kernels / the separate pass (A/B)
 #ifndef CFSEC_BS_CRC_DEFAULT
-#define CFSEC_BS_CRC_DEFAULT 1
+#define CFSEC_BS_CRC_DEFAULT 5
 #endif
 uint32_t bs_crc_mask() {
   static const uint32_t v = env_mask("CFSEC_BS_CRC", CFSEC_BS_CRC_DEFAULT);
@@ -464,6 +472,7 @@ bool bs_crc_matches(int k, int m, const uint8_t* coef) {
   const uint32_t mask = bs_crc_mask();
   if ((mask & 1u) && k == 6 && m == 12) return rows_equal<dev::BsEc6p10l2>(coef, 12);
   if ((mask & 2u) && k == 12 && m == 4) return rows_equal<dev::BsEc12p4>(coef, 4);
+  if ((mask & 4u) && k == 16 && (m == 20 || m == 22)) return rows_equal<dev::BsEc16p20l2>(coef, m);
   return false;
 }
 
@@ -478,6 +487,8 @@ hipError_t launch_bs_crc(const MatVecJob& job, uint32_t* crc, int crc_stride, co
   if (trace) std::fprintf(stderr, "cfsec: bs crc k=%d m=%d stripes=%d len=%llu\n", job.k, job.m, job.nstripes,
                           (unsigned long long)job.len);
   if (job.k == 6) return bc_launch<dev::BsEc6p10l2, 12>(job, crc, crc_stride, slot, st);
+  if (job.k == 16 && job.m == 22) return bc_launch<dev::BsEc16p20l2, 22>(job, crc, crc_stride, slot, st);
+  if (job.k == 16) return bc_launch<dev::BsEc16p20l2, 20>(job, crc, crc_stride, slot, st);
   return bc_launch<dev::BsEc12p4, 4>(job, crc, crc_stride, slot, st);
 }
 

@@ -205,6 +205,7 @@ bool matvec_crc_supported(int k, int m, size_t len, const uint8_t* coef) {
   if (!crc_k || m < 1 || len > 0xFFFFFFFFull - crcdev::kTile) return false;
   if (m <= 6) return true;
   if (k == 6 && m == 12 && crc_lds12_on()) return true;
+  if (bs_crc_matches(k, m, coef)) return true;  // the bit-sliced fused kernels (gf_bs_crc.hip)
   if (k == 6 && m == 12 && coef) {
     const DyPlan dp = dyadic_plan(coef, m, k);
     return dp.B == 2 && dp.E == 2;

@@ -10,8 +10,9 @@ and in separate allocations (pointer-table launches), and with checksum words at
 of the caller's choosing (the ec batch seam).  CFSEC_TRACE_CRC names the launches, so each case also
 asserts that the bit-sliced route ran.
 
-EC6P10L2's route is on by default; EC12P4's (CFSEC_BS_CRC bit 1) is off -- no faster than the
-lookup-product kernel -- and is exercised in a child process with CFSEC_BS_CRC=3.
+EC6P10L2's and the 16 + 20 code's routes (EC16P20, EC16P20L2: CFSEC_BS_CRC bits 0 and 2) are on by
+default; EC12P4's (bit 1, no faster than the lookup-product kernel) is exercised in a child process
+with CFSEC_BS_CRC=7.
 """
 import os
 import subprocess
@@ -27,8 +28,9 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 SIZES = [1, 15, 16, 17, 1023, 1024, 1025, 2047, 2048, 2049, 4095, 4097, 6144, 65539, 174763]
-MASK = int(os.environ.get("CFSEC_BS_CRC", "1"), 0)
-ec12p4 = pytest.mark.skipif(not MASK & 2, reason="EC12P4's route is off by default (run in the child, CFSEC_BS_CRC=3)")
+MASK = int(os.environ.get("CFSEC_BS_CRC", "5"), 0)  # the library default: EC6P10L2 and the 16 + 20 code
+ec12p4 = pytest.mark.skipif(not MASK & 2, reason="EC12P4's route is off by default (run in the child, CFSEC_BS_CRC=7)")
+ec16 = pytest.mark.skipif(not MASK & 4, reason="the 16 + 20 code's route is off (CFSEC_BS_CRC without bit 2)")
 
 
 @pytest.fixture(scope="module")
@@ -171,8 +173,8 @@ def test_ec12p4_large_stripe_vs_separate_pass(rs, monkeypatch, capfd):
 
 @pytest.mark.skipif(os.environ.get("CFSEC_BS_CRC") is not None, reason="the child process itself")
 def test_per_row_form_and_ec12p4_in_child():
-    """This module again with CFSEC_BS_CRC=3: EC12P4's route on too."""
-    env = dict(os.environ, CFSEC_BS_CRC="3")
+    """This module again with CFSEC_BS_CRC=7: EC12P4's and the 16 + 20 code's routes on too."""
+    env = dict(os.environ, CFSEC_BS_CRC="7")
     r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", __file__],
                        env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
@@ -205,4 +207,65 @@ def test_c4_fused_lrc_encode_crc_scattered(S, monkeypatch, capfd):
         for i in range(total):
             w = ref[i].view()
             assert np.array_equal(stripes[b][i].cpu().numpy(), w), (b, i)
+            assert crcs[b][i] == crc(w), (b, i)
+
+
+@ec16
+@pytest.mark.parametrize("S", [1, 2047, 2049, 65539, 262144])
+@pytest.mark.parametrize("offset", [0, 5])
+def test_ec16p20_encode_crc(rs, S, offset, monkeypatch, capfd):
+    """EC16P20's encode + 36 checksums (16 x 20 on the EC16P20L2 network's first 20 rows), 3 stripes
+    in one allocation at pitch S + offset."""
+    monkeypatch.setenv("CFSEC_TRACE_CRC", "1")
+    k, m, nst = 16, 20, 3
+    pitch = S + offset
+    r = np.random.default_rng(S * 3 + offset)
+    flat = np.zeros(nst * (k + m) * pitch + 64, np.uint8)
+    for s_ in range(nst):
+        for i in range(k):
+            base = (s_ * (k + m) + i) * pitch
+            flat[base:base + S] = r.integers(0, 256, S, dtype=np.uint8)
+    dev = torch.from_numpy(flat).cuda()
+    ptrs = [dev.data_ptr() + (s_ * (k + m) + i) * pitch for s_ in range(nst) for i in range(k + m)]
+    crcs = torch.full((nst * (k + m),), 0x3C3C3C3C, dtype=torch.int32, device="cuda")
+    capfd.readouterr()
+    rs.New(k, m).encode_crc_batch(ptrs, S, nst, crcs.data_ptr())
+    torch.cuda.synchronize()
+    assert routed(capfd.readouterr().err, k, m)
+    got = dev.cpu().numpy()
+    words = crcs.cpu().numpy().view(np.uint32).reshape(nst, k + m)
+    rows = lambda a, s_, i: a[(s_ * (k + m) + i) * pitch:(s_ * (k + m) + i) * pitch + S]
+    check_stripes(k, m, [[rows(flat, s_, i) for i in range(k + m)] for s_ in range(nst)],
+                  [[rows(got, s_, i) for i in range(k + m)] for s_ in range(nst)], words)
+
+
+@ec16
+@pytest.mark.parametrize("S", [17, 4097, 262144])
+def test_ec16p20l2_fused_encode_crc(S, monkeypatch, capfd):
+    """EC16P20L2's fused LRC encode (20 global + 2 local rows) with all 38 checksums through the ec
+    batch seam, 4 bids in one allocation, against the ec oracle and zlib."""
+    monkeypatch.setenv("CFSEC_TRACE_CRC", "1")
+    from chubaofs_amd import codemode as cm, ec
+    from oracle.ec_oracle import ECOracle, Slice
+    t = cm.GetTactic(cm.EC16P20L2)
+    total, nb = t.N + t.M + t.L, 4
+    enc = ec.NewEncoder(ec.Config(CodeMode=t, EnableVerify=False), device=0)
+    orc = ECOracle.from_tactic(t, enable_verify=False)
+    r = np.random.default_rng(S + 16)
+    data = r.integers(0, 256, (nb, t.N, S), dtype=np.uint8)
+    buf = torch.zeros((nb, total, S), dtype=torch.uint8, device="cuda")
+    buf[:, :t.N] = torch.from_numpy(data).cuda()
+    stripes = [[buf[b, i] for i in range(total)] for b in range(nb)]
+    capfd.readouterr()
+    st, crcs = enc.EncodeBatch(stripes, crcs=True)
+    torch.cuda.synchronize()
+    assert routed(capfd.readouterr().err, t.N, t.M + t.L)
+    assert st == [0] * nb
+    got = buf.cpu().numpy()
+    for b in range(nb):
+        ref = [Slice.of(data[b, i].copy()) for i in range(t.N)] + [Slice.of(np.zeros(S, np.uint8)) for _ in range(total - t.N)]
+        assert orc.encode(ref) == 0
+        for i in range(total):
+            w = ref[i].view()
+            assert np.array_equal(got[b, i], w), (b, i)
             assert crcs[b][i] == crc(w), (b, i)
