@@ -29,8 +29,9 @@
 // consecutive tiles per wave 195 us, this order 189 us, with the tree fold 184-186 us (a 32-column basis
 // per register: 189); 1-4 tiles per wave and stripe 194-249 us (more folds); the product alone in this
 // structure 156 us, in gf_bs_kernel's every-nw-th-tile order 143 us (that order leaves no run of one
-// row per wave for the Horner registers).  Kept off for EC12P4 (bit 1): 197-207 us against 181-203 for
-// the lookup-product kernel.  The 16 + 20 code (EC16P20 / EC16P20L2's fused encode, all 36 / 38 rows
+// row per wave for the Horner registers).  EC12P4 with its input rows' registers in LDS (LI below, 3
+// waves per SIMD): 64 MiB blobs 190 us against 207 on the lookup-product kernel, 4 MiB blobs 194 vs 185,
+// so it takes rows of 2 MiB and more.  The 16 + 20 code (EC16P20 / EC16P20L2's fused encode, all 36 / 38 rows
 // checksummed) had no fused form: 256 VGPRs with 79 spilled at 2 waves per SIMD, still 243.6 -> 218.5 us
 // (EC16P20L2, 64 x 262,144) and 227.5 -> 206.5 us (EC16P20) against the product + separate pass
 // (profiles/r06/bs_crc/shape_sweep_ec16.txt).  A plane-residue form -- the 12 output checksums as linear functions of
@@ -157,7 +158,7 @@ __device__ __forceinline__ void bc_st(uint8_t* row, uint64_t po, uint64_t len, u
 }
 
 template <class Net, int M>
-__global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(Net::K > 8 ? 2 : CFSEC_BC_WPE, 4))) void gf_bs_crc_kernel(
+__global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(Net::K > 12 ? 2 : CFSEC_BC_WPE, 4))) void gf_bs_crc_kernel(
     const BcArgs a) {
   constexpr int K = Net::K;
   constexpr int NR = K + M;  // checksummed rows: the inputs, then the outputs
@@ -165,6 +166,11 @@ __global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(N
   constexpr int NP = NR <= 32 ? 32 : 64;  // the rows padded for the lane fold
   __shared__ uint32_t tb[kBcTabs * 32];  // planes, the jump, the lane tree
   __shared__ uint32_t slot[64];  // the rows' word offsets, indexed per lane at the segment ends
+  // LI (k > 8: the 16 + 20 code, 38 registers beside 128 input planes): the input rows' Horner registers
+  // live in LDS across the network -- read, jumped and updated at each tile's input phase -- instead of
+  // in VGPRs the network needs (79 spilled at 2 waves per SIMD otherwise)
+  constexpr bool LI = K > 8;
+  __shared__ uint32_t rin[LI ? kBcWaves * K * 64 : 1];
   for (uint32_t i = threadIdx.x; i < kBcPlaneTabs * 8; i += blockDim.x)
     reinterpret_cast<u32x4*>(tb)[i] = reinterpret_cast<const u32x4*>(a.tabs)[i];
   for (uint32_t i = threadIdx.x; i < 6 * kBcFields * 8; i += blockDim.x)
@@ -193,6 +199,7 @@ __global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(N
                                           : a.ptr[(size_t)a.tab * K + (size_t)s * M + r]);
   };
   uint32_t R[NR];
+  bool fresh = true;  // LI: the wave's first tile of a stripe (the LDS registers hold nothing yet)
   // one column tile: loads, transposes, the inputs' terms, the network, the outputs' terms and stores
   // (FULL: every piece in bounds -- straight-line code; else the stripe's partial last tile)
   const auto tile = [&](uint32_t s, uint64_t po, auto full_tag) {
@@ -210,8 +217,15 @@ __global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(N
     for (int i = 0; i < K; ++i) {
       dev::bs_transpose8(&x[8 * i]);
       uint32_t(&pl)[8] = *reinterpret_cast<uint32_t(*)[8]>(&x[8 * i]);
-      if constexpr (!(CFSEC_BC_PROBE & 1)) R[i] ^= bc_planes(tb, pl);
-      asm volatile("" : "+v"(R[i]));
+      if constexpr (LI) {
+        uint32_t* ri = rin + (wave * K + i) * 64 + lane;
+        uint32_t v = fresh ? 0u : bc_five7(tb + kBcJump * 32, *ri);
+        if constexpr (!(CFSEC_BC_PROBE & 1)) v ^= bc_planes(tb, pl);
+        *ri = v;
+      } else {
+        if constexpr (!(CFSEC_BC_PROBE & 1)) R[i] ^= bc_planes(tb, pl);
+        asm volatile("" : "+v"(R[i]));
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
     if constexpr (Net::Paired) dev::bs_pair_basis<K>(x);
@@ -233,6 +247,7 @@ __global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(N
   for (uint32_t s = g0; s < a.nst; s += a.groups) {
 #pragma unroll
     for (int i = 0; i < NR; ++i) R[i] = 0u;
+    fresh = true;
     uint32_t c = j;
     for (;;) {
       const uint64_t po = (uint64_t)c * kBcTile + lane * 16;
@@ -241,7 +256,8 @@ __global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(N
       if (c + W >= tps) break;
       c += W;
 #pragma unroll
-      for (int i = 0; i < NR; ++i) R[i] = bc_five7(tb + kBcJump * 32, R[i]);
+      for (int i = LI ? K : 0; i < NR; ++i) R[i] = bc_five7(tb + kBcJump * 32, R[i]);
+      fresh = false;
     }
     // the stripe's end of this wave: the 64 lanes' registers folded by recursive halving -- at level k
     // lane pairs l, l ^ 2^k swap halves of their registers and each keeps the sum of one half, the
@@ -252,7 +268,7 @@ __global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(N
     {
       uint32_t v[NP];
 #pragma unroll
-      for (int i = 0; i < NP; ++i) v[i] = i < NR ? R[i] : 0u;
+      for (int i = 0; i < NP; ++i) v[i] = i < NR ? (LI && i < K ? rin[(wave * K + i) * 64 + lane] : R[i]) : 0u;
 #pragma unroll
       for (int k = 0; k < 6; ++k) {
         const int half = NP >> (k + 1) ? NP >> (k + 1) : 1;  // NP = 32: the 6th level combines halves
@@ -287,11 +303,11 @@ uint32_t env_mask(const char* name, uint32_t dflt) {
   const char* v = std::getenv(name);
   return v && *v ? (uint32_t)std::strtoul(v, nullptr, 0) : dflt;
 }
-// CFSEC_BS_CRC: bit 0 EC6P10L2's fused LRC encode (6 x 12), bit 2 EC16P20 / EC16P20L2 (16 x 20 / 22:
-// the product + separate pass otherwise) -- both on by default --, bit 1 EC12P4 (12 x 4: off, no faster
-// than the lookup-product kernel); 0 keeps the lookup-product kernels / the separate pass (A/B)
+// CFSEC_BS_CRC: bit 0 EC6P10L2's fused LRC encode (6 x 12), bit 1 EC12P4 (12 x 4) with rows of >= 2 MiB,
+// bit 2 EC16P20 / EC16P20L2 (16 x 20 / 22: the product + separate pass otherwise) -- all on by default
+// --, bit 3 EC12P4 at every length (tests); 0 keeps the lookup-product kernels / the separate pass (A/B)
 #ifndef CFSEC_BS_CRC_DEFAULT
-#define CFSEC_BS_CRC_DEFAULT 5
+#define CFSEC_BS_CRC_DEFAULT 7
 #endif
 uint32_t bs_crc_mask() {
   static const uint32_t v = env_mask("CFSEC_BS_CRC", CFSEC_BS_CRC_DEFAULT);
@@ -471,7 +487,7 @@ bool bs_crc_matches(int k, int m, const uint8_t* coef) {
   if (!coef) return false;
   const uint32_t mask = bs_crc_mask();
   if ((mask & 1u) && k == 6 && m == 12) return rows_equal<dev::BsEc6p10l2>(coef, 12);
-  if ((mask & 2u) && k == 12 && m == 4) return rows_equal<dev::BsEc12p4>(coef, 4);
+  if ((mask & 10u) && k == 12 && m == 4) return rows_equal<dev::BsEc12p4>(coef, 4);
   if ((mask & 4u) && k == 16 && (m == 20 || m == 22)) return rows_equal<dev::BsEc16p20l2>(coef, m);
   return false;
 }
@@ -483,8 +499,8 @@ hipError_t launch_bs_crc(const MatVecJob& job, uint32_t* crc, int crc_stride, co
     return hipErrorInvalidValue;
   for (int i = 0; i < job.k + job.m; ++i)
     if (slot[i] < 0 || slot[i] >= crc_stride) return hipErrorInvalidValue;
-  static const bool trace = env_mask("CFSEC_TRACE_CRC", 0) != 0;
-  if (trace) std::fprintf(stderr, "cfsec: bs crc k=%d m=%d stripes=%d len=%llu\n", job.k, job.m, job.nstripes,
+  if (env_mask("CFSEC_TRACE_CRC", 0))  // read per call: tests turn it on mid-process
+    std::fprintf(stderr, "cfsec: bs crc k=%d m=%d stripes=%d len=%llu\n", job.k, job.m, job.nstripes,
                           (unsigned long long)job.len);
   if (job.k == 6) return bc_launch<dev::BsEc6p10l2, 12>(job, crc, crc_stride, slot, st);
   if (job.k == 16 && job.m == 22) return bc_launch<dev::BsEc16p20l2, 22>(job, crc, crc_stride, slot, st);
@@ -495,6 +511,9 @@ hipError_t launch_bs_crc(const MatVecJob& job, uint32_t* crc, int crc_stride, co
 bool bs_crc_takes(const MatVecJob& job, int crc_stride, const int* slot) {
   if (!slot || slot[0] < 0 || job.len == 0 || crc_stride > 256 || !bs_crc_matches(job.k, job.m, job.coef)) return false;
   const uint64_t tps = (job.len + kBcTile - 1) / kBcTile;
+  // EC12P4: rows of at least 1024 tiles (2 MiB: the 64 MiB-blob put 207 -> 190 us; 4 MiB blobs are
+  // faster on the lookup-product kernel, 185 vs 194 us), any length with bit 3
+  if (job.k == 12 && !(bs_crc_mask() & 8u) && tps < 1024) return false;
   return tps <= (uint64_t)kBcPow * kBcPow * kBcPow && tps * (uint64_t)std::max(job.nstripes, 1) <= 0xFFFFFFFFull;
 }
 
