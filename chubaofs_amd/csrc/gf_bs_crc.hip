@@ -30,8 +30,10 @@
 // per register: 189); 1-4 tiles per wave and stripe 194-249 us (more folds); the product alone in this
 // structure 156 us, in gf_bs_kernel's every-nw-th-tile order 143 us (that order leaves no run of one
 // row per wave for the Horner registers).  EC12P4 with its input rows' registers in LDS (LI below, 3
-// waves per SIMD): 64 MiB blobs 190 us against 207 on the lookup-product kernel, 4 MiB blobs 194 vs 185,
-// so it takes rows of 2 MiB and more.  The 16 + 20 code (EC16P20 / EC16P20L2's fused encode, all 36 / 38 rows
+// waves per SIMD): in the shape sweep 64 MiB blobs 190 us against 207 on the lookup-product kernel,
+// 4 MiB blobs 194 vs 185, but in the bench's rotated batches no faster (encode_crc_roofline_frac
+// 0.473-0.481 vs 0.479-0.482, the ec seam 0.463-0.466 vs 0.471-0.475: profiles/r06/bs_crc/
+// bench_ec12p4_ab.txt), so its route (rows of >= 2 MiB) is off by default.  The 16 + 20 code (EC16P20 / EC16P20L2's fused encode, all 36 / 38 rows
 // checksummed) had no fused form: 256 VGPRs with 79 spilled at 2 waves per SIMD, still 243.6 -> 218.5 us
 // (EC16P20L2, 64 x 262,144) and 227.5 -> 206.5 us (EC16P20) against the product + separate pass
 // (profiles/r06/bs_crc/shape_sweep_ec16.txt).  A plane-residue form -- the 12 output checksums as linear functions of
@@ -303,11 +305,12 @@ uint32_t env_mask(const char* name, uint32_t dflt) {
   const char* v = std::getenv(name);
   return v && *v ? (uint32_t)std::strtoul(v, nullptr, 0) : dflt;
 }
-// CFSEC_BS_CRC: bit 0 EC6P10L2's fused LRC encode (6 x 12), bit 1 EC12P4 (12 x 4) with rows of >= 2 MiB,
-// bit 2 EC16P20 / EC16P20L2 (16 x 20 / 22: the product + separate pass otherwise) -- all on by default
-// --, bit 3 EC12P4 at every length (tests); 0 keeps the lookup-product kernels / the separate pass (A/B)
+// CFSEC_BS_CRC: bit 0 EC6P10L2's fused LRC encode (6 x 12), bit 2 EC16P20 / EC16P20L2 (16 x 20 / 22: the
+// product + separate pass otherwise) -- both on by default --, bit 1 EC12P4 (12 x 4) with rows of >= 2 MiB
+// (off: no faster than the lookup-product kernel in the bench), bit 3 EC12P4 at every length (tests);
+// 0 keeps the lookup-product kernels / the separate pass (A/B)
 #ifndef CFSEC_BS_CRC_DEFAULT
-#define CFSEC_BS_CRC_DEFAULT 7
+#define CFSEC_BS_CRC_DEFAULT 5
 #endif
 uint32_t bs_crc_mask() {
   static const uint32_t v = env_mask("CFSEC_BS_CRC", CFSEC_BS_CRC_DEFAULT);
