@@ -115,6 +115,9 @@ __device__ __forceinline__ uint32_t bc_five7(const uint32_t* tb, uint32_t v) {
   return bc_x3(bc_x3(t[0], t[1], t[2]), bc_x3(t[3], t[4], t[5]), t[6]);
 }
 
+#ifndef CFSEC_BC_LO
+#define CFSEC_BC_LO 1  // the 16 + 20 code's output rows' registers in LDS too (A/B)
+#endif
 #ifndef CFSEC_BC_WPE
 #define CFSEC_BC_WPE 3  // waves per SIMD the per-row form is compiled for
 #endif
@@ -172,7 +175,11 @@ __global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(N
   // live in LDS across the network -- read, jumped and updated at each tile's input phase -- instead of
   // in VGPRs the network needs (79 spilled at 2 waves per SIMD otherwise)
   constexpr bool LI = K > 8;
-  __shared__ uint32_t rin[LI ? kBcWaves * K * 64 : 1];
+  // LO (k > 12: the 16 + 20 code): the output rows' registers too, read, jumped and updated where the
+  // network emits each row
+  constexpr bool LO = K > 12 && CFSEC_BC_LO;
+  constexpr int NL = (LI ? K : 0) + (LO ? M : 0);  // rows whose registers live in LDS (the first NL)
+  __shared__ uint32_t rin[NL ? kBcWaves * NL * 64 : 1];
   for (uint32_t i = threadIdx.x; i < kBcPlaneTabs * 8; i += blockDim.x)
     reinterpret_cast<u32x4*>(tb)[i] = reinterpret_cast<const u32x4*>(a.tabs)[i];
   for (uint32_t i = threadIdx.x; i < 6 * kBcFields * 8; i += blockDim.x)
@@ -220,7 +227,7 @@ __global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(N
       dev::bs_transpose8(&x[8 * i]);
       uint32_t(&pl)[8] = *reinterpret_cast<uint32_t(*)[8]>(&x[8 * i]);
       if constexpr (LI) {
-        uint32_t* ri = rin + (wave * K + i) * 64 + lane;
+        uint32_t* ri = rin + (wave * NL + i) * 64 + lane;
         uint32_t v = fresh ? 0u : bc_five7(tb + kBcJump * 32, *ri);
         if constexpr (!(CFSEC_BC_PROBE & 1)) v ^= bc_planes(tb, pl);
         *ri = v;
@@ -233,8 +240,15 @@ __global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(N
     if constexpr (Net::Paired) dev::bs_pair_basis<K>(x);
     __builtin_amdgcn_sched_barrier(0);
     Net::template net<M>(x, [&](int r, uint32_t (&o)[8]) {
-      if constexpr (!(CFSEC_BC_PROBE & 2)) R[K + r] ^= bc_planes(tb, o);
-      asm volatile("" : "+v"(R[K + r]));
+      if constexpr (LO) {
+        uint32_t* ri = rin + (wave * NL + K + r) * 64 + lane;
+        uint32_t v = fresh ? 0u : bc_five7(tb + kBcJump * 32, *ri);
+        if constexpr (!(CFSEC_BC_PROBE & 2)) v ^= bc_planes(tb, o);
+        *ri = v;
+      } else {
+        if constexpr (!(CFSEC_BC_PROBE & 2)) R[K + r] ^= bc_planes(tb, o);
+        asm volatile("" : "+v"(R[K + r]));
+      }
       dev::bs_transpose8(o);
       uint8_t* p = out_row(s, r);
       if constexpr (FULL) {
@@ -258,7 +272,7 @@ __global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(N
       if (c + W >= tps) break;
       c += W;
 #pragma unroll
-      for (int i = LI ? K : 0; i < NR; ++i) R[i] = bc_five7(tb + kBcJump * 32, R[i]);
+      for (int i = NL; i < NR; ++i) R[i] = bc_five7(tb + kBcJump * 32, R[i]);
       fresh = false;
     }
     // the stripe's end of this wave: the 64 lanes' registers folded by recursive halving -- at level k
@@ -270,7 +284,7 @@ __global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(N
     {
       uint32_t v[NP];
 #pragma unroll
-      for (int i = 0; i < NP; ++i) v[i] = i < NR ? (LI && i < K ? rin[(wave * K + i) * 64 + lane] : R[i]) : 0u;
+      for (int i = 0; i < NP; ++i) v[i] = i < NR ? (i < NL ? rin[(wave * NL + i) * 64 + lane] : R[i]) : 0u;
 #pragma unroll
       for (int k = 0; k < 6; ++k) {
         const int half = NP >> (k + 1) ? NP >> (k + 1) : 1;  // NP = 32: the 6th level combines halves
