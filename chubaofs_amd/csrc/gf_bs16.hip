@@ -187,6 +187,7 @@ struct BsRepairArgs {
   uint8_t crc_slot[4];
   const uint32_t* lbasis;  // P2 launches: lane l's 32 columns of shift(., 16 * (63 - l)) (bs_crc_device)
   const uint32_t* ccols;   // P2 launches: tile j's 32 columns of the multiply by x^(8 * 2048 * j), j < tps
+  uint32_t xjump;          // CRC launches: x^(8 * 2048 * W), W the waves per stripe (bs_rep_waves)
 };
 
 // TAB launches keep their row offsets where a repair launch does not read its GfArgs: from coef to
@@ -225,6 +226,9 @@ __device__ __forceinline__ uint32_t bs_kernarg_u32(uint32_t j) {
 // 1: a failed compare writes 0x80000000 | row << 24 | column tile (the stripe's first mismatching
 // compared row of the lane that wrote last) instead of 1 into the stripe's flag word (diagnosis)
 #define CFSEC_BS_DEBUG_FLAGS 0
+#endif
+#ifndef CFSEC_BS_PERBID
+#define CFSEC_BS_PERBID 0  // timing probe: the repair's tiles in per-stripe order (see the kernel)
 #endif
 #ifndef CFSEC_BS_BLOCKED
 #define CFSEC_BS_BLOCKED 0  // 1: every repair launch maps each wave to a block of consecutive tiles (A/B)
@@ -355,8 +359,14 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
   const uint32_t* ct = reinterpret_cast<const uint32_t*>(lds + kBsWaves * kWaveLds);
   const uint32_t nw = gridDim.x * kBsWaves;
   if constexpr (CRC) {  // the checksum tables, once per workgroup (before any wave may leave)
+    uint32_t* ctw = reinterpret_cast<uint32_t*>(lds + kBsWaves * kWaveLds);
     for (uint32_t i = threadIdx.x; i < kBsCrcTabs * 8; i += blockDim.x)
-      reinterpret_cast<u32x4*>(lds + kBsWaves * kWaveLds)[i] = reinterpret_cast<const u32x4*>(r.ctab)[i];
+      reinterpret_cast<u32x4*>(ctw)[i] = reinterpret_cast<const u32x4*>(r.ctab)[i];
+    __syncthreads();
+    // a wave's tiles of a stripe are W apart (per-stripe order below): the register's jump table moves
+    // it 2048 W bytes on instead of 2048
+    for (uint32_t i = threadIdx.x; i < 7 * 32; i += blockDim.x)
+      ctw[kBsCrcTabR * 32 + i] = bs_mulmod((i & 31u) << (5 * (i >> 5)), r.xjump);
     __syncthreads();
   }
   if (blockIdx.x == 0)  // the checksum words the pass after this one accumulates into
@@ -391,12 +401,32 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
 #pragma unroll
     for (int i = 0; i < PF; ++i) bs_glds_row<kBsRepGlds>(slot_ptr(s, i, c), pre + i * kBsWaveBytes);
   };
-  // tiles: every nw-th (t0 = the wave's index), or for CRC launches one block of consecutive tiles
-  constexpr bool kBlocked = CRC || CFSEC_BS_BLOCKED;
+  // tiles: every nw-th (t0 = the wave's index); CRC launches: per-stripe order (W waves per stripe,
+  // each on every W-th tile of its stripes: one run of one row per wave for the Horner registers, +2 %
+  // against the every-nw-th order on C5, profiles/r06/c5_perbid_order.txt; blocks of consecutive tiles,
+  // round 5's CRC order, cost 8 %)
+  constexpr bool kBlocked = CFSEC_BS_BLOCKED && !CRC;
   const uint32_t wid = blockIdx.x * kBsWaves + wave;
   const uint32_t per_wave = kBlocked ? (ntiles + nw - 1) / nw : 0;
   uint32_t t = kBlocked ? wid * per_wave : wid;
   const uint32_t t_end = kBlocked ? min(t + per_wave, ntiles) : ntiles, t_step = kBlocked ? 1u : nw;
+  // CFSEC_BS_PERBID (timing probe, no checksum form): W = nw / stripes waves per stripe, wave (g, j)
+  // on tiles j, j + W, ... of stripes g, g + nw / W, ... -- the order a per-row checksum run needs
+  constexpr bool kPerBid = (CRC || CFSEC_BS_PERBID) && !kBlocked;
+  const uint32_t nst = ntiles / tiles_per_stripe;
+  const uint32_t pbW = kPerBid ? max(1u, min(tiles_per_stripe, nw / max(nst, 1u))) : 1u, pbG = nw / pbW;
+  const auto next_tile = [&](uint32_t u) -> uint32_t {
+    if constexpr (!kPerBid) return u + t_step;
+    const uint32_t su = u / tiles_per_stripe, cu = u - su * tiles_per_stripe + pbW;
+    if (cu < tiles_per_stripe) return su * tiles_per_stripe + cu;
+    const uint32_t s2 = su + pbG;
+    return s2 < nst ? s2 * tiles_per_stripe + (wid % pbW) : ntiles;
+  };
+  if constexpr (kPerBid) {
+    if (wid / pbW >= pbG || wid % pbW >= tiles_per_stripe) return;
+    t = (wid / pbW) * tiles_per_stripe + wid % pbW;
+    if (t >= ntiles) return;
+  }
   if (t >= t_end) return;
   prefetch(t);
   __builtin_amdgcn_s_waitcnt(bs_waitcnt_vm(0));
@@ -409,7 +439,7 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
   }
   (void)ncrc;
   (void)seg_c0;
-  for (; t < t_end; t += t_step) {
+  for (; t < t_end; t = next_tile(t)) {
     const uint32_t s = t / tiles_per_stripe, c = t % tiles_per_stripe;
     uint32_t x[128];
     uint32_t y[ND > 0 ? ND : 1][8];
@@ -503,7 +533,7 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
     issue_ring();
     issue_ring();
     __builtin_amdgcn_sched_barrier(0);
-    prefetch(t + t_step < t_end ? t + t_step : t);
+    prefetch(next_tile(t) < t_end ? next_tile(t) : t);
     __builtin_amdgcn_sched_barrier(0);
     uint32_t diff = 0, first_bad = 0;
     (void)first_bad;
@@ -570,7 +600,8 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
       }
     }
     if constexpr (CRC) {
-      if (t + 1 == t_end || c + 1 == tiles_per_stripe) {
+      const uint32_t tn = next_tile(t);
+      if (tn >= t_end || tn / tiles_per_stripe != s) {
         // the segment [seg_c0, c] of stripe s: lanes folded, moved to the row's end, XOR-ed into the
         // row's word (the row's first segment also folds in shift(~0, S) ^ ~0)
         const uint32_t mv = r.cpow[tiles_per_stripe - 1 - c];
@@ -583,9 +614,9 @@ __global__ __launch_bounds__(64 * kBsWaves) __attribute__((amdgpu_waves_per_eu(2
           }
           R[k] = 0u;
         }
-        seg_c0 = 0;
+        seg_c0 = tn % tiles_per_stripe;  // the next segment's first tile
       } else {
-        // the next tile of this segment: every register moves 2048 bytes on
+        // the next tile of this segment: every register moves 2048 W bytes on (the rebuilt jump table)
 #pragma unroll
         for (int k = 0; k < kBsCrcRows; ++k)
           if ((uint32_t)k < ncrc) R[k] = bs_five7(ct + kBsCrcTabR * 32, R[k]);
@@ -955,6 +986,13 @@ bool rep_crc_args(int nd, const dev::GfArgs& a, uint64_t len, const BsCrcReq* cr
   return true;
 }
 
+// x^(8 * 2048 * W) for a CRC launch of `grid` workgroups: W waves per stripe, as the kernel computes it
+uint32_t bs_rep_xjump(unsigned grid, uint32_t tps, uint64_t ntiles) {
+  const uint64_t nw = (uint64_t)grid * kBsWaves, nst = tps ? ntiles / tps : 0;
+  const uint64_t W = std::max<uint64_t>(1, std::min<uint64_t>(tps, nw / std::max<uint64_t>(nst, 1)));
+  return crc_xpow(8ull * 2048 * W);
+}
+
 bool rep_args(int nd, const uint8_t* missing, const uint8_t* prow, const uint8_t* ainv, BsRepairArgs& r) {
   for (int q = 0; q < nd; ++q) {
     r.slot[q] = missing[q];
@@ -979,6 +1017,7 @@ hipError_t launch_bs16_repair(int nd, int ne, const uint8_t* missing, const uint
   if (!rep_args(nd, missing, prow, ainv, r)) return hipErrorOutOfMemory;
   const unsigned grid = (unsigned)std::min<uint64_t>((uint64_t)cu_count(), (ntiles + kBsWaves - 1) / kBsWaves);
   if (rep_crc_args(nd, a, len, crc, crc_words, r)) {
+    r.xjump = bs_rep_xjump(grid, tps, ntiles);
     const hipError_t e = ne == 2 ? launch_rep_crc<22, 0>(nd, crc->mode, a, r, grid, tps, (uint32_t)ntiles, st)
                                  : launch_rep_crc<20, 0>(nd, crc->mode, a, r, grid, tps, (uint32_t)ntiles, st);
     if (e == hipSuccess && crc_done) *crc_done = true;
@@ -1127,6 +1166,7 @@ hipError_t launch_bs16_repair_tab(int nd, int ne, const uint8_t* missing, const 
       const unsigned grid = (unsigned)std::min<uint64_t>((uint64_t)cu_count(), (ntiles + kBsWaves - 1) / kBsWaves);
       const bool fused = rep_crc_args(nd, t, len, crc, crc_words, r);
       const int mode = fused ? crc->mode : 0;
+      r.xjump = bs_rep_xjump(grid, tps, ntiles);
       e = ne == 2 ? launch_rep_crc<22, 2>(nd, mode, t, r, grid, tps, (uint32_t)ntiles, st)
                   : launch_rep_crc<20, 2>(nd, mode, t, r, grid, tps, (uint32_t)ntiles, st);
       if (e != hipSuccess) return e;
