@@ -53,7 +53,12 @@
 #include <type_traits>
 #include <vector>
 
+#include "bs_net_ec10p4.hpp"
+#include "bs_net_ec3p3.hpp"
+#include "bs_net_ec4p4.hpp"
 #include "bs_net_ec12p4.hpp"
+#include "bs_net_ec12p9.hpp"
+#include "bs_net_ec15p12.hpp"
 #include "bs_net_ec16p20l2.hpp"
 #include "bs_net_ec6p10l2.hpp"
 #include "gf_bitslice.hpp"
@@ -163,7 +168,7 @@ __device__ __forceinline__ void bc_st(uint8_t* row, uint64_t po, uint64_t len, u
 }
 
 template <class Net, int M>
-__global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(Net::K > 12 ? 2 : CFSEC_BC_WPE, 4))) void gf_bs_crc_kernel(
+__global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(Net::K > 12 || (Net::K > 8 && M > 4) ? 2 : CFSEC_BC_WPE, 4))) void gf_bs_crc_kernel(
     const BcArgs a) {
   constexpr int K = Net::K;
   constexpr int NR = K + M;  // checksummed rows: the inputs, then the outputs
@@ -319,12 +324,13 @@ uint32_t env_mask(const char* name, uint32_t dflt) {
   const char* v = std::getenv(name);
   return v && *v ? (uint32_t)std::strtoul(v, nullptr, 0) : dflt;
 }
-// CFSEC_BS_CRC: bit 0 EC6P10L2's fused LRC encode (6 x 12), bit 2 EC16P20 / EC16P20L2 (16 x 20 / 22: the
-// product + separate pass otherwise) -- both on by default --, bit 1 EC12P4 (12 x 4) with rows of >= 2 MiB
-// (off: no faster than the lookup-product kernel in the bench), bit 3 EC12P4 at every length (tests);
-// 0 keeps the lookup-product kernels / the separate pass (A/B)
+// CFSEC_BS_CRC: bit 0 EC6P10L2's fused LRC encode (6 x 12), bit 2 EC16P20 / EC16P20L2 (16 x 20 / 22),
+// bit 4 EC6P8, EC6P10, EC12P9, EC15P12, EC10P4, EC4P4, EC3P3 (the product + separate pass otherwise) --
+// on by default --, bit 1 EC12P4 (12 x 4) with rows of >= 2 MiB (off: no faster than the
+// lookup-product kernel in the bench), bit 3 EC12P4 at every length (tests); 0 keeps the lookup-product
+// kernels / the separate pass (A/B)
 #ifndef CFSEC_BS_CRC_DEFAULT
-#define CFSEC_BS_CRC_DEFAULT 5
+#define CFSEC_BS_CRC_DEFAULT 21
 #endif
 uint32_t bs_crc_mask() {
   static const uint32_t v = env_mask("CFSEC_BS_CRC", CFSEC_BS_CRC_DEFAULT);
@@ -506,6 +512,15 @@ bool bs_crc_matches(int k, int m, const uint8_t* coef) {
   if ((mask & 1u) && k == 6 && m == 12) return rows_equal<dev::BsEc6p10l2>(coef, 12);
   if ((mask & 10u) && k == 12 && m == 4) return rows_equal<dev::BsEc12p4>(coef, 4);
   if ((mask & 4u) && k == 16 && (m == 20 || m == 22)) return rows_equal<dev::BsEc16p20l2>(coef, m);
+  if (mask & 16u) {  // the other RS modes' encodes (EC6P8 / EC6P10 on the EC6P10L2 network's first rows;
+                     // EC6P6 / EC6P3 / EC16P4 / EC12P4 keep their product kernels' fused forms)
+    if (k == 6 && (m == 8 || m == 10)) return rows_equal<dev::BsEc6p10l2>(coef, m);
+    if (k == 12 && m == 9) return rows_equal<dev::BsEc12p9>(coef, 9);
+    if (k == 15 && m == 12) return rows_equal<dev::BsEc15p12>(coef, 12);
+    if (k == 10 && m == 4) return rows_equal<dev::BsEc10p4>(coef, 4);
+    if (k == 4 && m == 4) return rows_equal<dev::BsEc4p4>(coef, 4);
+    if (k == 3 && m == 3) return rows_equal<dev::BsEc3p3>(coef, 3);
+  }
   return false;
 }
 
@@ -519,7 +534,14 @@ hipError_t launch_bs_crc(const MatVecJob& job, uint32_t* crc, int crc_stride, co
   if (env_mask("CFSEC_TRACE_CRC", 0))  // read per call: tests turn it on mid-process
     std::fprintf(stderr, "cfsec: bs crc k=%d m=%d stripes=%d len=%llu\n", job.k, job.m, job.nstripes,
                           (unsigned long long)job.len);
-  if (job.k == 6) return bc_launch<dev::BsEc6p10l2, 12>(job, crc, crc_stride, slot, st);
+  if (job.k == 6 && job.m == 12) return bc_launch<dev::BsEc6p10l2, 12>(job, crc, crc_stride, slot, st);
+  if (job.k == 6 && job.m == 10) return bc_launch<dev::BsEc6p10l2, 10>(job, crc, crc_stride, slot, st);
+  if (job.k == 6) return bc_launch<dev::BsEc6p10l2, 8>(job, crc, crc_stride, slot, st);
+  if (job.k == 12 && job.m == 9) return bc_launch<dev::BsEc12p9, 9>(job, crc, crc_stride, slot, st);
+  if (job.k == 15) return bc_launch<dev::BsEc15p12, 12>(job, crc, crc_stride, slot, st);
+  if (job.k == 10) return bc_launch<dev::BsEc10p4, 4>(job, crc, crc_stride, slot, st);
+  if (job.k == 4) return bc_launch<dev::BsEc4p4, 4>(job, crc, crc_stride, slot, st);
+  if (job.k == 3) return bc_launch<dev::BsEc3p3, 3>(job, crc, crc_stride, slot, st);
   if (job.k == 16 && job.m == 22) return bc_launch<dev::BsEc16p20l2, 22>(job, crc, crc_stride, slot, st);
   if (job.k == 16) return bc_launch<dev::BsEc16p20l2, 20>(job, crc, crc_stride, slot, st);
   return bc_launch<dev::BsEc12p4, 4>(job, crc, crc_stride, slot, st);
@@ -530,7 +552,7 @@ bool bs_crc_takes(const MatVecJob& job, int crc_stride, const int* slot) {
   const uint64_t tps = (job.len + kBcTile - 1) / kBcTile;
   // EC12P4: rows of at least 1024 tiles (2 MiB: the 64 MiB-blob put 207 -> 190 us; 4 MiB blobs are
   // faster on the lookup-product kernel, 185 vs 194 us), any length with bit 3
-  if (job.k == 12 && !(bs_crc_mask() & 8u) && tps < 1024) return false;
+  if (job.k == 12 && job.m == 4 && !(bs_crc_mask() & 8u) && tps < 1024) return false;
   return tps <= (uint64_t)kBcPow * kBcPow * kBcPow && tps * (uint64_t)std::max(job.nstripes, 1) <= 0xFFFFFFFFull;
 }
 

@@ -201,11 +201,12 @@ static bool crc_lds12_on() {
 bool matvec_crc_supported(int k, int m, size_t len, const uint8_t* coef) {
   // the fused kernels exist for the input counts of the code modes of SURVEY §8, m <= 6 outputs, and
   // EC6P10L2's fused encode (6 x (10 dyadic + 2 local) rows)
+  if (m < 1 || len > 0xFFFFFFFFull - crcdev::kTile) return false;
+  if (bs_crc_matches(k, m, coef)) return true;  // the bit-sliced fused kernels (gf_bs_crc.hip)
   const bool crc_k = k == 6 || k == 8 || k == 12 || k == 16 || k == 18;
-  if (!crc_k || m < 1 || len > 0xFFFFFFFFull - crcdev::kTile) return false;
+  if (!crc_k) return false;
   if (m <= 6) return true;
   if (k == 6 && m == 12 && crc_lds12_on()) return true;
-  if (bs_crc_matches(k, m, coef)) return true;  // the bit-sliced fused kernels (gf_bs_crc.hip)
   if (k == 6 && m == 12 && coef) {
     const DyPlan dp = dyadic_plan(coef, m, k);
     return dp.B == 2 && dp.E == 2;

@@ -10,9 +10,10 @@ and in separate allocations (pointer-table launches), and with checksum words at
 of the caller's choosing (the ec batch seam).  CFSEC_TRACE_CRC names the launches, so each case also
 asserts that the bit-sliced route ran.
 
-EC6P10L2's and the 16 + 20 code's routes (EC16P20, EC16P20L2: CFSEC_BS_CRC bits 0 and 2) are on by
-default; EC12P4's (bit 1: rows of 2 MiB and more; bit 3: every length) is off -- no faster than the
-lookup-product kernel in the bench -- and its cases run in a child process with CFSEC_BS_CRC=15.
+EC6P10L2's, the 16 + 20 code's (EC16P20, EC16P20L2) and the other RS modes' routes (EC6P8, EC6P10,
+EC12P9, EC15P12, EC10P4, EC4P4, EC3P3: CFSEC_BS_CRC bits 0, 2, 4) are on by default; EC12P4's (bit 1:
+rows of 2 MiB and more; bit 3: every length) is off -- no faster than the lookup-product kernel in the
+bench -- and its cases run in a child process with CFSEC_BS_CRC=31.
 """
 import os
 import subprocess
@@ -28,9 +29,10 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 SIZES = [1, 15, 16, 17, 1023, 1024, 1025, 2047, 2048, 2049, 4095, 4097, 6144, 65539, 174763]
-MASK = int(os.environ.get("CFSEC_BS_CRC", "5"), 0)  # the library default
-ec12p4 = pytest.mark.skipif(not MASK & 8, reason="EC12P4's route is off by default (every length in the child, CFSEC_BS_CRC=15)")
+MASK = int(os.environ.get("CFSEC_BS_CRC", "21"), 0)  # the library default
+ec12p4 = pytest.mark.skipif(not MASK & 8, reason="EC12P4's route is off by default (every length in the child, CFSEC_BS_CRC=31)")
 ec12p4_long = pytest.mark.skipif(not MASK & 10, reason="EC12P4's route is off (CFSEC_BS_CRC without bits 1, 3)")
+rs_more = pytest.mark.skipif(not MASK & 16, reason="the other RS modes' route is off (CFSEC_BS_CRC without bit 4)")
 ec16 = pytest.mark.skipif(not MASK & 4, reason="the 16 + 20 code's route is off (CFSEC_BS_CRC without bit 2)")
 
 
@@ -174,8 +176,8 @@ def test_ec12p4_large_stripe_vs_separate_pass(rs, monkeypatch, capfd):
 
 @pytest.mark.skipif(os.environ.get("CFSEC_BS_CRC") is not None, reason="the child process itself")
 def test_per_row_form_and_ec12p4_in_child():
-    """This module again with CFSEC_BS_CRC=15: EC12P4's route on, at every length."""
-    env = dict(os.environ, CFSEC_BS_CRC="15")
+    """This module again with CFSEC_BS_CRC=31: every route on (EC12P4's at every length)."""
+    env = dict(os.environ, CFSEC_BS_CRC="31")
     r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", __file__],
                        env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
@@ -270,3 +272,31 @@ def test_ec16p20l2_fused_encode_crc(S, monkeypatch, capfd):
             w = ref[i].view()
             assert np.array_equal(got[b, i], w), (b, i)
             assert crcs[b][i] == crc(w), (b, i)
+
+
+@rs_more
+@pytest.mark.parametrize("k,m", [(6, 8), (6, 10), (12, 9), (15, 12), (10, 4), (4, 4), (3, 3)])
+@pytest.mark.parametrize("S", [1, 2049, 65539])
+def test_other_rs_modes_encode_crc(rs, k, m, S, monkeypatch, capfd):
+    """EC6P8 / EC6P10 (the EC6P10L2 network's first rows), EC12P9, EC15P12 and EC3P3 (unpaired: k
+    odd), EC10P4 and EC4P4 encodes with every shard checksummed, 3 stripes at an odd pitch."""
+    monkeypatch.setenv("CFSEC_TRACE_CRC", "1")
+    nst, pitch = 3, S + 3
+    r = np.random.default_rng(k * 1000 + m * 10 + S)
+    flat = np.zeros(nst * (k + m) * pitch + 64, np.uint8)
+    for s_ in range(nst):
+        for i in range(k):
+            base = (s_ * (k + m) + i) * pitch
+            flat[base:base + S] = r.integers(0, 256, S, dtype=np.uint8)
+    dev = torch.from_numpy(flat).cuda()
+    ptrs = [dev.data_ptr() + (s_ * (k + m) + i) * pitch for s_ in range(nst) for i in range(k + m)]
+    crcs = torch.full((nst * (k + m),), 0x77, dtype=torch.int32, device="cuda")
+    capfd.readouterr()
+    rs.New(k, m).encode_crc_batch(ptrs, S, nst, crcs.data_ptr())
+    torch.cuda.synchronize()
+    assert routed(capfd.readouterr().err, k, m)
+    got = dev.cpu().numpy()
+    words = crcs.cpu().numpy().view(np.uint32).reshape(nst, k + m)
+    rows = lambda a, s_, i: a[(s_ * (k + m) + i) * pitch:(s_ * (k + m) + i) * pitch + S]
+    check_stripes(k, m, [[rows(flat, s_, i) for i in range(k + m)] for s_ in range(nst)],
+                  [[rows(got, s_, i) for i in range(k + m)] for s_ in range(nst)], words)

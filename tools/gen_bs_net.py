@@ -19,7 +19,13 @@ checks its engine's coefficients against these constants before it takes the net
   python3 tools/gen_bs_net.py ec15p12 | ec12p9   (measured, not shipped: profiles/r04/bsk_ab.txt)
   python3 tools/gen_bs_net.py ec6p10l2 --paired --joint > chubaofs_amd/csrc/bs_net_ec6p10l2.hpp
   python3 tools/gen_bs_net.py ec12p4 --paired --joint > chubaofs_amd/csrc/bs_net_ec12p4.hpp
-    (round 6: the fused encode + checksum kernels, gf_bs_crc.hip)
+  python3 tools/gen_bs_net.py ec12p9 --paired --joint > chubaofs_amd/csrc/bs_net_ec12p9.hpp
+  python3 tools/gen_bs_net.py ec15p12 > chubaofs_amd/csrc/bs_net_ec15p12.hpp   (k odd: no paired basis)
+  python3 tools/gen_bs_net.py ec10p4 --paired --joint > chubaofs_amd/csrc/bs_net_ec10p4.hpp
+  python3 tools/gen_bs_net.py ec4p4 --paired --joint > chubaofs_amd/csrc/bs_net_ec4p4.hpp
+  python3 tools/gen_bs_net.py ec3p3 > chubaofs_amd/csrc/bs_net_ec3p3.hpp
+    (round 6: the fused encode + checksum kernels, gf_bs_crc.hip; EC6P8 / EC6P10 use the first 8 / 10
+    rows of the EC6P10L2 network -- a KRS parity row does not depend on m)
 """
 import sys
 
@@ -399,6 +405,9 @@ CODES = {
     "ec6p10l2": ("The EC6P10L2 fused LRC encode rows (10 KRS global rows, then the 2 AZ-local rows over the data)",
                  lambda: lrc_rows(6, 10, 2, 8), "NR = 12"),
     "ec12p4": ("The EC12P4 parity (KRS buildMatrix(12, 16) rows 12..15)", lambda: parity_rows(12, 4), "NR = 4"),
+    "ec4p4": ("The EC4P4 parity (KRS buildMatrix(4, 8) rows 4..7)", lambda: parity_rows(4, 4), "NR = 4"),
+    "ec3p3": ("The EC3P3 parity (KRS buildMatrix(3, 6) rows 3..5)", lambda: parity_rows(3, 3), "NR = 3"),
+    "ec10p4": ("The EC10P4 parity (KRS buildMatrix(10, 14) rows 10..13)", lambda: parity_rows(10, 4), "NR = 4"),
     "ec15p12": ("The EC15P12 parity (KRS buildMatrix(15, 27) rows 15..26)", lambda: parity_rows(15, 12), "NR = 12"),
     "ec12p9": ("The EC12P9 parity (KRS buildMatrix(12, 21) rows 12..20)", lambda: parity_rows(12, 9), "NR = 9"),
 }
