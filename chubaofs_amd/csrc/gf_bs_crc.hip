@@ -56,6 +56,10 @@
 #include "bs_net_ec10p4.hpp"
 #include "bs_net_ec3p3.hpp"
 #include "bs_net_ec4p4.hpp"
+#include "bs_net_ec4p4l2.hpp"
+#include "bs_net_ec6p3l3.hpp"
+#include "bs_net_ec6p6l9.hpp"
+#include "bs_net_ec6p8l10.hpp"
 #include "bs_net_ec12p4.hpp"
 #include "bs_net_ec12p9.hpp"
 #include "bs_net_ec15p12.hpp"
@@ -168,7 +172,7 @@ __device__ __forceinline__ void bc_st(uint8_t* row, uint64_t po, uint64_t len, u
 }
 
 template <class Net, int M>
-__global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(Net::K > 12 || (Net::K > 8 && M > 4) ? 2 : CFSEC_BC_WPE, 4))) void gf_bs_crc_kernel(
+__global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(Net::K > 12 || (Net::K > 8 && M > 4) || M > 12 ? 2 : CFSEC_BC_WPE, 4))) void gf_bs_crc_kernel(
     const BcArgs a) {
   constexpr int K = Net::K;
   constexpr int NR = K + M;  // checksummed rows: the inputs, then the outputs
@@ -180,10 +184,13 @@ __global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(N
   // live in LDS across the network -- read, jumped and updated at each tile's input phase -- instead of
   // in VGPRs the network needs (79 spilled at 2 waves per SIMD otherwise)
   constexpr bool LI = K > 8;
-  // LO (k > 12: the 16 + 20 code): the output rows' registers too, read, jumped and updated where the
+  // LO (k > 12 or m > 12: the 16 + 20 code, EC6P6L9, EC6P8L10): the output rows' registers too, read, jumped and updated where the
   // network emits each row
-  constexpr bool LO = K > 12 && CFSEC_BC_LO;
-  constexpr int NL = (LI ? K : 0) + (LO ? M : 0);  // rows whose registers live in LDS (the first NL)
+  constexpr bool LO = (K > 12 || M > 12) && CFSEC_BC_LO;
+  constexpr int NL = (LI ? K : 0) + (LO ? M : 0);  // rows whose registers live in LDS
+  // row i's LDS slot (in_lds(i)): the inputs first when LI, then the outputs when LO
+  const auto in_lds = [](int i) { return (LI && i < K) || (LO && i >= K); };
+  const auto lds_row = [](int i) { return i < K ? i : (LI ? K : 0) + (i - K); };
   __shared__ uint32_t rin[NL ? kBcWaves * NL * 64 : 1];
   for (uint32_t i = threadIdx.x; i < kBcPlaneTabs * 8; i += blockDim.x)
     reinterpret_cast<u32x4*>(tb)[i] = reinterpret_cast<const u32x4*>(a.tabs)[i];
@@ -246,7 +253,7 @@ __global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(N
     __builtin_amdgcn_sched_barrier(0);
     Net::template net<M>(x, [&](int r, uint32_t (&o)[8]) {
       if constexpr (LO) {
-        uint32_t* ri = rin + (wave * NL + K + r) * 64 + lane;
+        uint32_t* ri = rin + (wave * NL + lds_row(K + r)) * 64 + lane;
         uint32_t v = fresh ? 0u : bc_five7(tb + kBcJump * 32, *ri);
         if constexpr (!(CFSEC_BC_PROBE & 2)) v ^= bc_planes(tb, o);
         *ri = v;
@@ -277,7 +284,8 @@ __global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(N
       if (c + W >= tps) break;
       c += W;
 #pragma unroll
-      for (int i = NL; i < NR; ++i) R[i] = bc_five7(tb + kBcJump * 32, R[i]);
+      for (int i = 0; i < NR; ++i)
+        if (!in_lds(i)) R[i] = bc_five7(tb + kBcJump * 32, R[i]);
       fresh = false;
     }
     // the stripe's end of this wave: the 64 lanes' registers folded by recursive halving -- at level k
@@ -289,7 +297,7 @@ __global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(N
     {
       uint32_t v[NP];
 #pragma unroll
-      for (int i = 0; i < NP; ++i) v[i] = i < NR ? (i < NL ? rin[(wave * NL + i) * 64 + lane] : R[i]) : 0u;
+      for (int i = 0; i < NP; ++i) v[i] = i < NR ? (in_lds(i) ? rin[(wave * NL + lds_row(i)) * 64 + lane] : R[i]) : 0u;
 #pragma unroll
       for (int k = 0; k < 6; ++k) {
         const int half = NP >> (k + 1) ? NP >> (k + 1) : 1;  // NP = 32: the 6th level combines halves
@@ -325,7 +333,8 @@ uint32_t env_mask(const char* name, uint32_t dflt) {
   return v && *v ? (uint32_t)std::strtoul(v, nullptr, 0) : dflt;
 }
 // CFSEC_BS_CRC: bit 0 EC6P10L2's fused LRC encode (6 x 12), bit 2 EC16P20 / EC16P20L2 (16 x 20 / 22),
-// bit 4 EC6P8, EC6P10, EC12P9, EC15P12, EC10P4, EC4P4, EC3P3 (the product + separate pass otherwise) --
+// bit 4 EC6P8, EC6P10, EC12P9, EC15P12, EC10P4, EC4P4, EC3P3 and the LRC modes EC6P3L3, EC4P4L2,
+// EC6P6L9, EC6P8L10 (the product + separate pass, or for EC6P3L3 the v_perm fused kernel, otherwise) --
 // on by default --, bit 1 EC12P4 (12 x 4) with rows of >= 2 MiB (off: no faster than the
 // lookup-product kernel in the bench), bit 3 EC12P4 at every length (tests); 0 keeps the lookup-product
 // kernels / the separate pass (A/B)
@@ -520,6 +529,11 @@ bool bs_crc_matches(int k, int m, const uint8_t* coef) {
     if (k == 10 && m == 4) return rows_equal<dev::BsEc10p4>(coef, 4);
     if (k == 4 && m == 4) return rows_equal<dev::BsEc4p4>(coef, 4);
     if (k == 3 && m == 3) return rows_equal<dev::BsEc3p3>(coef, 3);
+    // the other LRC modes' fused encodes (global + every AZ's local rows over the data)
+    if (k == 6 && m == 6 && rows_equal<dev::BsEc6p3l3>(coef, 6)) return true;
+    if (k == 4 && m == 6) return rows_equal<dev::BsEc4p4l2>(coef, 6);
+    if (k == 6 && m == 15) return rows_equal<dev::BsEc6p6l9>(coef, 15);
+    if (k == 6 && m == 18) return rows_equal<dev::BsEc6p8l10>(coef, 18);
   }
   return false;
 }
@@ -535,6 +549,10 @@ hipError_t launch_bs_crc(const MatVecJob& job, uint32_t* crc, int crc_stride, co
     std::fprintf(stderr, "cfsec: bs crc k=%d m=%d stripes=%d len=%llu\n", job.k, job.m, job.nstripes,
                           (unsigned long long)job.len);
   if (job.k == 6 && job.m == 12) return bc_launch<dev::BsEc6p10l2, 12>(job, crc, crc_stride, slot, st);
+  if (job.k == 6 && job.m == 6) return bc_launch<dev::BsEc6p3l3, 6>(job, crc, crc_stride, slot, st);
+  if (job.k == 6 && job.m == 15) return bc_launch<dev::BsEc6p6l9, 15>(job, crc, crc_stride, slot, st);
+  if (job.k == 6 && job.m == 18) return bc_launch<dev::BsEc6p8l10, 18>(job, crc, crc_stride, slot, st);
+  if (job.k == 4 && job.m == 6) return bc_launch<dev::BsEc4p4l2, 6>(job, crc, crc_stride, slot, st);
   if (job.k == 6 && job.m == 10) return bc_launch<dev::BsEc6p10l2, 10>(job, crc, crc_stride, slot, st);
   if (job.k == 6) return bc_launch<dev::BsEc6p10l2, 8>(job, crc, crc_stride, slot, st);
   if (job.k == 12 && job.m == 9) return bc_launch<dev::BsEc12p9, 9>(job, crc, crc_stride, slot, st);

@@ -10,8 +10,9 @@ and in separate allocations (pointer-table launches), and with checksum words at
 of the caller's choosing (the ec batch seam).  CFSEC_TRACE_CRC names the launches, so each case also
 asserts that the bit-sliced route ran.
 
-EC6P10L2's, the 16 + 20 code's (EC16P20, EC16P20L2) and the other RS modes' routes (EC6P8, EC6P10,
-EC12P9, EC15P12, EC10P4, EC4P4, EC3P3: CFSEC_BS_CRC bits 0, 2, 4) are on by default; EC12P4's (bit 1:
+EC6P10L2's, the 16 + 20 code's (EC16P20, EC16P20L2) and the other modes' routes (EC6P8, EC6P10,
+EC12P9, EC15P12, EC10P4, EC4P4, EC3P3 and the LRC modes EC6P3L3, EC4P4L2, EC6P6L9, EC6P8L10:
+CFSEC_BS_CRC bits 0, 2, 4) are on by default; EC12P4's (bit 1:
 rows of 2 MiB and more; bit 3: every length) is off -- no faster than the lookup-product kernel in the
 bench -- and its cases run in a child process with CFSEC_BS_CRC=31.
 """
@@ -300,3 +301,37 @@ def test_other_rs_modes_encode_crc(rs, k, m, S, monkeypatch, capfd):
     rows = lambda a, s_, i: a[(s_ * (k + m) + i) * pitch:(s_ * (k + m) + i) * pitch + S]
     check_stripes(k, m, [[rows(flat, s_, i) for i in range(k + m)] for s_ in range(nst)],
                   [[rows(got, s_, i) for i in range(k + m)] for s_ in range(nst)], words)
+
+
+@rs_more
+@pytest.mark.parametrize("mode", ["EC6P3L3", "EC4P4L2", "EC6P6L9", "EC6P8L10"])
+@pytest.mark.parametrize("S", [17, 2049, 65539])
+def test_other_lrc_fused_encode_crc(mode, S, monkeypatch, capfd):
+    """The other LRC modes' fused encodes (global + every AZ's local rows over the data, as
+    lrcencoder.go's Encode fills them) with every shard checksummed, through the ec batch seam: 3 bids
+    in one allocation, against the ec oracle's Encode and zlib."""
+    monkeypatch.setenv("CFSEC_TRACE_CRC", "1")
+    from chubaofs_amd import codemode as cm, ec
+    from oracle.ec_oracle import ECOracle, Slice
+    t = cm.GetTactic(getattr(cm, mode))
+    total, nb = t.N + t.M + t.L, 3
+    enc = ec.NewEncoder(ec.Config(CodeMode=t, EnableVerify=False), device=0)
+    orc = ECOracle.from_tactic(t, enable_verify=False)
+    r = np.random.default_rng(S + total)
+    data = r.integers(0, 256, (nb, t.N, S), dtype=np.uint8)
+    buf = torch.zeros((nb, total, S), dtype=torch.uint8, device="cuda")
+    buf[:, :t.N] = torch.from_numpy(data).cuda()
+    stripes = [[buf[b, i] for i in range(total)] for b in range(nb)]
+    capfd.readouterr()
+    st, crcs = enc.EncodeBatch(stripes, crcs=True)
+    torch.cuda.synchronize()
+    assert routed(capfd.readouterr().err, t.N, t.M + t.L), mode
+    assert st == [0] * nb
+    got = buf.cpu().numpy()
+    for b in range(nb):
+        ref = [Slice.of(data[b, i].copy()) for i in range(t.N)] + [Slice.of(np.zeros(S, np.uint8)) for _ in range(total - t.N)]
+        assert orc.encode(ref) == 0
+        for i in range(total):
+            w = ref[i].view()
+            assert np.array_equal(got[b, i], w), (mode, b, i)
+            assert crcs[b][i] == crc(w), (mode, b, i)

@@ -24,6 +24,10 @@ checks its engine's coefficients against these constants before it takes the net
   python3 tools/gen_bs_net.py ec10p4 --paired --joint > chubaofs_amd/csrc/bs_net_ec10p4.hpp
   python3 tools/gen_bs_net.py ec4p4 --paired --joint > chubaofs_amd/csrc/bs_net_ec4p4.hpp
   python3 tools/gen_bs_net.py ec3p3 > chubaofs_amd/csrc/bs_net_ec3p3.hpp
+  python3 tools/gen_bs_net.py ec6p3l3 --paired --joint > chubaofs_amd/csrc/bs_net_ec6p3l3.hpp
+  python3 tools/gen_bs_net.py ec4p4l2 --paired --joint > chubaofs_amd/csrc/bs_net_ec4p4l2.hpp
+  python3 tools/gen_bs_net.py ec6p6l9 --paired --joint > chubaofs_amd/csrc/bs_net_ec6p6l9.hpp
+  python3 tools/gen_bs_net.py ec6p8l10 --paired --joint > chubaofs_amd/csrc/bs_net_ec6p8l10.hpp
     (round 6: the fused encode + checksum kernels, gf_bs_crc.hip; EC6P8 / EC6P10 use the first 8 / 10
     rows of the EC6P10L2 network -- a KRS parity row does not depend on m)
 """
@@ -99,22 +103,23 @@ def ec16p20l2_rows():
     return rows
 
 
-def lrc_rows(k, m, azs, ln):
+def lrc_rows(k, m, azs, ln, lm=1):
     """An LRC's fused encode rows (as the engine's ECEncoder::create builds them): the m KRS global
-    rows, then each AZ's local parity over the data -- AZ a holds data k/azs * a .. and global parities
-    m/azs * a .., its one local row is the KRS (ln, 1) parity row over those ln members."""
+    rows, then each AZ's lm local parities over the data -- AZ a holds data k/azs * a .. and global
+    parities m/azs * a .., its local rows are the KRS (ln, lm) parity rows over those ln members."""
     g = parity_rows(k, m)
-    lc = parity_rows(ln, 1)[0]
+    lc = parity_rows(ln, lm)
     rows = [r[:] for r in g]
     dk, dm = k // azs, m // azs
     for a in range(azs):
-        row = [0] * k
-        for t in range(dk):
-            row[dk * a + t] ^= lc[t]
-        for t in range(dm):
-            for c in range(k):
-                row[c] ^= gmul(lc[dk + t], g[dm * a + t][c])
-        rows.append(row)
+        for j in range(lm):
+            row = [0] * k
+            for t in range(dk):
+                row[dk * a + t] ^= lc[j][t]
+            for t in range(dm):
+                for c in range(k):
+                    row[c] ^= gmul(lc[j][dk + t], g[dm * a + t][c])
+            rows.append(row)
     return rows
 
 
@@ -405,6 +410,14 @@ CODES = {
     "ec6p10l2": ("The EC6P10L2 fused LRC encode rows (10 KRS global rows, then the 2 AZ-local rows over the data)",
                  lambda: lrc_rows(6, 10, 2, 8), "NR = 12"),
     "ec12p4": ("The EC12P4 parity (KRS buildMatrix(12, 16) rows 12..15)", lambda: parity_rows(12, 4), "NR = 4"),
+    "ec6p3l3": ("The EC6P3L3 fused LRC encode rows (3 global, then 3 AZ-local rows over the data)",
+                lambda: lrc_rows(6, 3, 3, 3), "NR = 6"),
+    "ec4p4l2": ("The EC4P4L2 fused LRC encode rows (4 global, then 2 AZ-local rows over the data)",
+                lambda: lrc_rows(4, 4, 2, 4), "NR = 6"),
+    "ec6p6l9": ("The EC6P6L9 fused LRC encode rows (6 global, then 3 AZs x 3 local rows over the data)",
+                lambda: lrc_rows(6, 6, 3, 4, 3), "NR = 15"),
+    "ec6p8l10": ("The EC6P8L10 fused LRC encode rows (8 global, then 2 AZs x 5 local rows over the data)",
+                 lambda: lrc_rows(6, 8, 2, 7, 5), "NR = 18"),
     "ec4p4": ("The EC4P4 parity (KRS buildMatrix(4, 8) rows 4..7)", lambda: parity_rows(4, 4), "NR = 4"),
     "ec3p3": ("The EC3P3 parity (KRS buildMatrix(3, 6) rows 3..5)", lambda: parity_rows(3, 3), "NR = 3"),
     "ec10p4": ("The EC10P4 parity (KRS buildMatrix(10, 14) rows 10..13)", lambda: parity_rows(10, 4), "NR = 4"),
