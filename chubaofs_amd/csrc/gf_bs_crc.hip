@@ -171,39 +171,43 @@ __device__ __forceinline__ void bc_st(uint8_t* row, uint64_t po, uint64_t len, u
   else if (po < len) dev::st_tail(row + po, v, (size_t)(len - po));
 }
 
-template <class Net, int M>
-__global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(Net::K > 12 || (Net::K > 8 && M > 4) || M > 12 ? 2 : CFSEC_BC_WPE, 4))) void gf_bs_crc_kernel(
-    const BcArgs a) {
+// CRC = false: the product alone (bs_plain_matches: the wide LRC modes, whose fused rows outgrow
+// the fixed-K kernels' 12 outputs and ran as two products)
+template <class Net, int M, bool CRC = true>
+__global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(
+    Net::K > 12 || (Net::K > 8 && M > 4) || M > 12 ? 2 : CFSEC_BC_WPE, 4))) void gf_bs_crc_kernel(const BcArgs a) {
   constexpr int K = Net::K;
   constexpr int NR = K + M;  // checksummed rows: the inputs, then the outputs
   static_assert(NR <= 64, "one lane per row's word");
   constexpr int NP = NR <= 32 ? 32 : 64;  // the rows padded for the lane fold
-  __shared__ uint32_t tb[kBcTabs * 32];  // planes, the jump, the lane tree
+  __shared__ uint32_t tb[CRC ? kBcTabs * 32 : 1];  // planes, the jump, the lane tree
   __shared__ uint32_t slot[64];  // the rows' word offsets, indexed per lane at the segment ends
   // LI (k > 8: the 16 + 20 code, 38 registers beside 128 input planes): the input rows' Horner registers
   // live in LDS across the network -- read, jumped and updated at each tile's input phase -- instead of
   // in VGPRs the network needs (79 spilled at 2 waves per SIMD otherwise)
-  constexpr bool LI = K > 8;
+  constexpr bool LI = CRC && K > 8;
   // LO (k > 12 or m > 12: the 16 + 20 code, EC6P6L9, EC6P8L10): the output rows' registers too, read, jumped and updated where the
   // network emits each row
-  constexpr bool LO = (K > 12 || M > 12) && CFSEC_BC_LO;
+  constexpr bool LO = CRC && (K > 12 || M > 12) && CFSEC_BC_LO;
   constexpr int NL = (LI ? K : 0) + (LO ? M : 0);  // rows whose registers live in LDS
   // row i's LDS slot (in_lds(i)): the inputs first when LI, then the outputs when LO
   const auto in_lds = [](int i) { return (LI && i < K) || (LO && i >= K); };
   const auto lds_row = [](int i) { return i < K ? i : (LI ? K : 0) + (i - K); };
   __shared__ uint32_t rin[NL ? kBcWaves * NL * 64 : 1];
-  for (uint32_t i = threadIdx.x; i < kBcPlaneTabs * 8; i += blockDim.x)
-    reinterpret_cast<u32x4*>(tb)[i] = reinterpret_cast<const u32x4*>(a.tabs)[i];
-  for (uint32_t i = threadIdx.x; i < 6 * kBcFields * 8; i += blockDim.x)
-    reinterpret_cast<u32x4*>(tb + kBcTree * 32)[i] = reinterpret_cast<const u32x4*>(a.tabs + kBcTree * 32)[i];
-  // the register's jump over the launch's tile stride (2048 W bytes): table (kBcJump + f)[e] =
-  // shift(e << 5f, 2048 W), built here from x^(8 * 2048 * W)
-  for (uint32_t i = threadIdx.x; i < kBcFields * 32; i += blockDim.x)
-    tb[kBcJump * 32 + i] = bc_mulmod((i & 31u) << (5 * (i >> 5)), a.xjump);
-  if (threadIdx.x == 0)  // constant indices: a lane-indexed read of the argument block would copy it to scratch
+  if constexpr (CRC) {
+    for (uint32_t i = threadIdx.x; i < kBcPlaneTabs * 8; i += blockDim.x)
+      reinterpret_cast<u32x4*>(tb)[i] = reinterpret_cast<const u32x4*>(a.tabs)[i];
+    for (uint32_t i = threadIdx.x; i < 6 * kBcFields * 8; i += blockDim.x)
+      reinterpret_cast<u32x4*>(tb + kBcTree * 32)[i] = reinterpret_cast<const u32x4*>(a.tabs + kBcTree * 32)[i];
+    // the register's jump over the launch's tile stride (2048 W bytes): table (kBcJump + f)[e] =
+    // shift(e << 5f, 2048 W), built here from x^(8 * 2048 * W)
+    for (uint32_t i = threadIdx.x; i < kBcFields * 32; i += blockDim.x)
+      tb[kBcJump * 32 + i] = bc_mulmod((i & 31u) << (5 * (i >> 5)), a.xjump);
+    if (threadIdx.x == 0)  // constant indices: a lane-indexed read of the argument block would copy it to scratch
 #pragma unroll
-    for (int i = 0; i < NR; ++i) slot[i] = a.slot[i];
-  __syncthreads();
+      for (int i = 0; i < NR; ++i) slot[i] = a.slot[i];
+    __syncthreads();
+  }
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const uint32_t wid = blockIdx.x * kBcWaves + wave;
   // wave (g, j) = (wid / W, wid % W) takes tiles j, j + W, j + 2W, ... of stripes g, g + groups, ...
@@ -238,7 +242,8 @@ __global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(N
     for (int i = 0; i < K; ++i) {
       dev::bs_transpose8(&x[8 * i]);
       uint32_t(&pl)[8] = *reinterpret_cast<uint32_t(*)[8]>(&x[8 * i]);
-      if constexpr (LI) {
+      if constexpr (!CRC) {
+      } else if constexpr (LI) {
         uint32_t* ri = rin + (wave * NL + i) * 64 + lane;
         uint32_t v = fresh ? 0u : bc_five7(tb + kBcJump * 32, *ri);
         if constexpr (!(CFSEC_BC_PROBE & 1)) v ^= bc_planes(tb, pl);
@@ -252,7 +257,8 @@ __global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(N
     if constexpr (Net::Paired) dev::bs_pair_basis<K>(x);
     __builtin_amdgcn_sched_barrier(0);
     Net::template net<M>(x, [&](int r, uint32_t (&o)[8]) {
-      if constexpr (LO) {
+      if constexpr (!CRC) {
+      } else if constexpr (LO) {
         uint32_t* ri = rin + (wave * NL + lds_row(K + r)) * 64 + lane;
         uint32_t v = fresh ? 0u : bc_five7(tb + kBcJump * 32, *ri);
         if constexpr (!(CFSEC_BC_PROBE & 2)) v ^= bc_planes(tb, o);
@@ -283,11 +289,14 @@ __global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(N
       else tile(s, po, std::false_type{});
       if (c + W >= tps) break;
       c += W;
+      if constexpr (CRC) {
 #pragma unroll
-      for (int i = 0; i < NR; ++i)
-        if (!in_lds(i)) R[i] = bc_five7(tb + kBcJump * 32, R[i]);
+        for (int i = 0; i < NR; ++i)
+          if (!in_lds(i)) R[i] = bc_five7(tb + kBcJump * 32, R[i]);
+      }
       fresh = false;
     }
+    if constexpr (!CRC) continue;
     // the stripe's end of this wave: the 64 lanes' registers folded by recursive halving -- at level k
     // lane pairs l, l ^ 2^k swap halves of their registers and each keeps the sum of one half, the
     // earlier group's value moved 16 * 2^k bytes on (7 lookups); the 32 padded registers are one per
@@ -335,7 +344,8 @@ uint32_t env_mask(const char* name, uint32_t dflt) {
 // CFSEC_BS_CRC: bit 0 EC6P10L2's fused LRC encode (6 x 12), bit 2 EC16P20 / EC16P20L2 (16 x 20 / 22),
 // bit 4 EC6P8, EC6P10, EC12P9, EC15P12, EC10P4, EC4P4, EC3P3 and the LRC modes EC6P3L3, EC4P4L2,
 // EC6P6L9, EC6P8L10 (the product + separate pass, or for EC6P3L3 the v_perm fused kernel, otherwise) --
-// on by default --, bit 1 EC12P4 (12 x 4) with rows of >= 2 MiB (off: no faster than the
+// on by default --, bit 5 the product alone for EC6P6L9 / EC6P8L10's plain fused encodes (on), bit 1
+// EC12P4 (12 x 4) with rows of >= 2 MiB (off: no faster than the
 // lookup-product kernel in the bench), bit 3 EC12P4 at every length (tests); 0 keeps the lookup-product
 // kernels / the separate pass (A/B)
 #ifndef CFSEC_BS_CRC_DEFAULT
@@ -434,7 +444,7 @@ int64_t bc_affine_stride(const MatVecJob& job) {  // as gf_crc.hip's
   return ss;
 }
 
-template <class Net, int M>
+template <class Net, int M, bool CRC = true>
 int bc_groups() {  // resident workgroups on the device (one wave of workgroups)
   static std::mutex mu;
   static std::map<int, int> cache;
@@ -444,7 +454,7 @@ int bc_groups() {  // resident workgroups on the device (one wave of workgroups)
   auto it = cache.find(dev);
   if (it != cache.end()) return it->second;
   int per = 0, cus = 0;
-  const void* f = reinterpret_cast<const void*>(&gf_bs_crc_kernel<Net, M>);
+  const void* f = reinterpret_cast<const void*>(&gf_bs_crc_kernel<Net, M, CRC>);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, f, 64 * kBcWaves, 0) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
     (void)hipGetLastError();
@@ -455,7 +465,7 @@ int bc_groups() {  // resident workgroups on the device (one wave of workgroups)
   return n;
 }
 
-template <class Net, int M>
+template <class Net, int M, bool CRC = true>
 hipError_t bc_launch(const MatVecJob& job, uint32_t* crc, int crc_stride, const int* slot, hipStream_t st) {
   constexpr int K = Net::K;
   BcArgs a{};
@@ -479,16 +489,17 @@ hipError_t bc_launch(const MatVecJob& job, uint32_t* crc, int crc_stride, const 
   a.tps = (uint32_t)tps;
   a.crc_stride = (uint32_t)crc_stride;
   a.fin = crc32_shift_ones((size_t)len);
-  for (int i = 0; i < K + M; ++i) a.slot[i] = (uint8_t)slot[i];
+  if (CRC)
+    for (int i = 0; i < K + M; ++i) a.slot[i] = (uint8_t)slot[i];
   const int64_t ss = bc_affine_stride(job);
   a.sstride = ss;
   const int per = ss ? job.nstripes : kBcPtr / (K + M);
-  const int groups = bc_groups<Net, M>();
+  const int groups = bc_groups<Net, M, CRC>();
   for (int s0 = 0; s0 < job.nstripes; s0 += per) {
     const int ns = std::min(per, job.nstripes - s0);
     const int tab = ss ? 1 : ns;
     a.tab = (uint32_t)tab;
-    a.crc = crc + (size_t)s0 * crc_stride;
+    a.crc = CRC ? crc + (size_t)s0 * crc_stride : nullptr;
     for (int s = 0; s < tab; ++s) {
       for (int c = 0; c < K; ++c) a.ptr[s * K + c] = job.in[(size_t)(s0 + s) * K + c];
       for (int r = 0; r < M; ++r) a.ptr[tab * K + s * M + r] = job.out[(size_t)(s0 + s) * M + r];
@@ -507,7 +518,7 @@ hipError_t bc_launch(const MatVecJob& job, uint32_t* crc, int crc_stride, const 
     a.groups = (uint32_t)ng;
     a.xjump = crc_xpow(8 * (int64_t)kBcTile * (int64_t)W);
     const unsigned grid = (unsigned)((ng * W + kBcWaves - 1) / kBcWaves);
-    hipLaunchKernelGGL((gf_bs_crc_kernel<Net, M>), dim3(grid), dim3(64 * kBcWaves), 0, st, a);
+    hipLaunchKernelGGL((gf_bs_crc_kernel<Net, M, CRC>), dim3(grid), dim3(64 * kBcWaves), 0, st, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   return hipSuccess;
@@ -563,6 +574,29 @@ hipError_t launch_bs_crc(const MatVecJob& job, uint32_t* crc, int crc_stride, co
   if (job.k == 16 && job.m == 22) return bc_launch<dev::BsEc16p20l2, 22>(job, crc, crc_stride, slot, st);
   if (job.k == 16) return bc_launch<dev::BsEc16p20l2, 20>(job, crc, crc_stride, slot, st);
   return bc_launch<dev::BsEc12p4, 4>(job, crc, crc_stride, slot, st);
+}
+
+// The product alone on the bit-sliced kernel for the wide LRC modes' fused encodes (EC6P6L9 6 x 15,
+// EC6P8L10 6 x 18: over the fixed-K kernels' 12 outputs they ran as two products, 173 / 190 us for a
+// 32-bid put batch); CFSEC_BS_CRC bit 5
+bool bs_plain_matches(int k, int m, const uint8_t* coef) {
+  if (!coef || !(bs_crc_mask() & 32u) || k != 6) return false;
+  if (m == 15) return rows_equal<dev::BsEc6p6l9>(coef, 15);
+  if (m == 18) return rows_equal<dev::BsEc6p8l10>(coef, 18);
+  return false;
+}
+
+hipError_t launch_bs_plain(const MatVecJob& job, hipStream_t st) {
+  // (the caller has resolved the mode to a plain store: kStore, or kStoreVerify storing every row)
+  if (!bs_plain_matches(job.k, job.m, job.coef) || job.len == 0 || job.lens ||
+      (job.len + kBcTile - 1) / kBcTile > (uint64_t)kBcPow * kBcPow * kBcPow ||
+      (job.len + kBcTile - 1) / kBcTile * (uint64_t)std::max(job.nstripes, 1) > 0xFFFFFFFFull)
+    return hipErrorInvalidValue;
+  if (env_mask("CFSEC_TRACE_CRC", 0))
+    std::fprintf(stderr, "cfsec: bs plain k=%d m=%d stripes=%d len=%llu\n", job.k, job.m, job.nstripes,
+                 (unsigned long long)job.len);
+  if (job.m == 15) return bc_launch<dev::BsEc6p6l9, 15, false>(job, nullptr, 0, nullptr, st);
+  return bc_launch<dev::BsEc6p8l10, 18, false>(job, nullptr, 0, nullptr, st);
 }
 
 bool bs_crc_takes(const MatVecJob& job, int crc_stride, const int* slot) {

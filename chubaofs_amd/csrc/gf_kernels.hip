@@ -165,6 +165,9 @@ hipError_t launch_matvec(const MatVecJob& job, hipStream_t stream) {
     if (maxlen > 0xFFFFFFFFull) return hipErrorInvalidValue;  // slen[] is 32-bit
   }
   if (job.m == 0 || job.nstripes == 0 || maxlen == 0) return hipSuccess;
+  // the wide LRC modes' fused encodes (EC6P6L9, EC6P8L10): one bit-sliced product instead of two passes
+  if (jmode == MatVecMode::kStore && !job.lens && bs_plain_matches(job.k, job.m, job.coef))
+    return launch_bs_plain(job, stream);
   if ((jmode == MatVecMode::kVerify || jmode == MatVecMode::kStoreVerify) && (job.k > kMaxK || !job.flags))
     return hipErrorInvalidValue;
 

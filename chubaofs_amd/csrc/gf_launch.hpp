@@ -146,6 +146,10 @@ hipError_t launch_bs16_repair_tab(int nd, int ne, const uint8_t* missing, const 
 bool bs_crc_matches(int k, int m, const uint8_t* coef);
 bool bs_crc_takes(const MatVecJob& job, int crc_stride, const int* slot);
 hipError_t launch_bs_crc(const MatVecJob& job, uint32_t* crc, int crc_stride, const int* slot, hipStream_t st);
+// The product alone on the same kernel (no checksums) for the wide LRC modes' fused encodes (EC6P6L9,
+// EC6P8L10): a kStore job whose coef equals their networks, any alignment and length
+bool bs_plain_matches(int k, int m, const uint8_t* coef);
+hipError_t launch_bs_plain(const MatVecJob& job, hipStream_t st);
 
 // repair_dy16 on a GfArgs block (gf_dy16.hip); launch_dy16_repair (gf_kernels.hip) fills it.
 hipError_t launch_dy16_repair_args(int nd, int ne, const dev::GfArgs& a, unsigned ns, hipStream_t st);

@@ -14,7 +14,8 @@ EC6P10L2's, the 16 + 20 code's (EC16P20, EC16P20L2) and the other modes' routes 
 EC12P9, EC15P12, EC10P4, EC4P4, EC3P3 and the LRC modes EC6P3L3, EC4P4L2, EC6P6L9, EC6P8L10:
 CFSEC_BS_CRC bits 0, 2, 4) are on by default; EC12P4's (bit 1:
 rows of 2 MiB and more; bit 3: every length) is off -- no faster than the lookup-product kernel in the
-bench -- and its cases run in a child process with CFSEC_BS_CRC=31.
+bench -- and its cases run in a child process with CFSEC_BS_CRC=63.  The wide LRC modes' plain
+encodes (EC6P6L9, EC6P8L10) take the same kernel without the checksums (bit 5, on).
 """
 import os
 import subprocess
@@ -31,8 +32,9 @@ pytestmark = pytest.mark.gpu
 
 SIZES = [1, 15, 16, 17, 1023, 1024, 1025, 2047, 2048, 2049, 4095, 4097, 6144, 65539, 174763]
 MASK = int(os.environ.get("CFSEC_BS_CRC", "21"), 0)  # the library default
-ec12p4 = pytest.mark.skipif(not MASK & 8, reason="EC12P4's route is off by default (every length in the child, CFSEC_BS_CRC=31)")
+ec12p4 = pytest.mark.skipif(not MASK & 8, reason="EC12P4's route is off by default (every length in the child, CFSEC_BS_CRC=63)")
 ec12p4_long = pytest.mark.skipif(not MASK & 10, reason="EC12P4's route is off (CFSEC_BS_CRC without bits 1, 3)")
+plain = pytest.mark.skipif(not MASK & 32, reason="the wide LRC modes' plain route is off (CFSEC_BS_CRC without bit 5)")
 rs_more = pytest.mark.skipif(not MASK & 16, reason="the other RS modes' route is off (CFSEC_BS_CRC without bit 4)")
 ec16 = pytest.mark.skipif(not MASK & 4, reason="the 16 + 20 code's route is off (CFSEC_BS_CRC without bit 2)")
 
@@ -177,8 +179,8 @@ def test_ec12p4_large_stripe_vs_separate_pass(rs, monkeypatch, capfd):
 
 @pytest.mark.skipif(os.environ.get("CFSEC_BS_CRC") is not None, reason="the child process itself")
 def test_per_row_form_and_ec12p4_in_child():
-    """This module again with CFSEC_BS_CRC=31: every route on (EC12P4's at every length)."""
-    env = dict(os.environ, CFSEC_BS_CRC="31")
+    """This module again with CFSEC_BS_CRC=63: every route on (EC12P4's at every length)."""
+    env = dict(os.environ, CFSEC_BS_CRC="63")
     r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", __file__],
                        env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
@@ -335,3 +337,34 @@ def test_other_lrc_fused_encode_crc(mode, S, monkeypatch, capfd):
             w = ref[i].view()
             assert np.array_equal(got[b, i], w), (mode, b, i)
             assert crcs[b][i] == crc(w), (mode, b, i)
+
+
+@plain
+@pytest.mark.parametrize("mode", ["EC6P6L9", "EC6P8L10"])
+@pytest.mark.parametrize("S", [17, 2049, 65539])
+def test_wide_lrc_plain_encode(mode, S, monkeypatch, capfd):
+    """EC6P6L9's / EC6P8L10's fused encode without checksums on the bit-sliced product (one pass over
+    the inputs instead of two fixed-K products), 3 bids, against the ec oracle's Encode."""
+    monkeypatch.setenv("CFSEC_TRACE_CRC", "1")
+    from chubaofs_amd import codemode as cm, ec
+    from oracle.ec_oracle import ECOracle, Slice
+    t = cm.GetTactic(getattr(cm, mode))
+    total, nb = t.N + t.M + t.L, 3
+    enc = ec.NewEncoder(ec.Config(CodeMode=t, EnableVerify=False), device=0)
+    orc = ECOracle.from_tactic(t, enable_verify=False)
+    r = np.random.default_rng(S + 3 * total)
+    data = r.integers(0, 256, (nb, t.N, S), dtype=np.uint8)
+    buf = torch.zeros((nb, total, S), dtype=torch.uint8, device="cuda")
+    buf[:, :t.N] = torch.from_numpy(data).cuda()
+    stripes = [[buf[b, i] for i in range(total)] for b in range(nb)]
+    capfd.readouterr()
+    st = enc.EncodeBatch(stripes)
+    torch.cuda.synchronize()
+    assert f"bs plain k={t.N} m={t.M + t.L}" in capfd.readouterr().err, mode
+    assert list(st) == [0] * nb
+    got = buf.cpu().numpy()
+    for b in range(nb):
+        ref = [Slice.of(data[b, i].copy()) for i in range(t.N)] + [Slice.of(np.zeros(S, np.uint8)) for _ in range(total - t.N)]
+        assert orc.encode(ref) == 0
+        for i in range(total):
+            assert np.array_equal(got[b, i], ref[i].view()), (mode, b, i)
