@@ -349,7 +349,7 @@ uint32_t env_mask(const char* name, uint32_t dflt) {
 // lookup-product kernel in the bench), bit 3 EC12P4 at every length (tests); 0 keeps the lookup-product
 // kernels / the separate pass (A/B)
 #ifndef CFSEC_BS_CRC_DEFAULT
-#define CFSEC_BS_CRC_DEFAULT 21
+#define CFSEC_BS_CRC_DEFAULT 53
 #endif
 uint32_t bs_crc_mask() {
   static const uint32_t v = env_mask("CFSEC_BS_CRC", CFSEC_BS_CRC_DEFAULT);
@@ -577,8 +577,9 @@ hipError_t launch_bs_crc(const MatVecJob& job, uint32_t* crc, int crc_stride, co
 }
 
 // The product alone on the bit-sliced kernel for the wide LRC modes' fused encodes (EC6P6L9 6 x 15,
-// EC6P8L10 6 x 18: over the fixed-K kernels' 12 outputs they ran as two products, 173 / 190 us for a
-// 32-bid put batch); CFSEC_BS_CRC bit 5
+// EC6P8L10 6 x 18: over the fixed-K kernels' 12 outputs they ran as two products): a 32-bid put batch
+// (32 x 699,051 B) 173 -> 117 and 190 -> 128 us (profiles/r06/bs_crc/lrc_modes_put_batch.txt);
+// CFSEC_BS_CRC bit 5
 bool bs_plain_matches(int k, int m, const uint8_t* coef) {
   if (!coef || !(bs_crc_mask() & 32u) || k != 6) return false;
   if (m == 15) return rows_equal<dev::BsEc6p6l9>(coef, 15);

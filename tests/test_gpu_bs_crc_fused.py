@@ -31,7 +31,7 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 SIZES = [1, 15, 16, 17, 1023, 1024, 1025, 2047, 2048, 2049, 4095, 4097, 6144, 65539, 174763]
-MASK = int(os.environ.get("CFSEC_BS_CRC", "21"), 0)  # the library default
+MASK = int(os.environ.get("CFSEC_BS_CRC", "53"), 0)  # the library default
 ec12p4 = pytest.mark.skipif(not MASK & 8, reason="EC12P4's route is off by default (every length in the child, CFSEC_BS_CRC=63)")
 ec12p4_long = pytest.mark.skipif(not MASK & 10, reason="EC12P4's route is off (CFSEC_BS_CRC without bits 1, 3)")
 plain = pytest.mark.skipif(not MASK & 32, reason="the wide LRC modes' plain route is off (CFSEC_BS_CRC without bit 5)")
