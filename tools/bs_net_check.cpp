@@ -3,6 +3,7 @@
 // the kernels use (paired basis when the header says so), every row of the network emitted and
 // transposed back, compared byte by byte with the GF(2^8)/0x11D matrix product.
 //   g++ -O1 -std=c++17 -I../chubaofs_amd/csrc -DBS_NET_HDR='"bs_net_ec16p20l2.hpp"' bs_net_check.cpp -o /tmp/bs_net_check
+// (another network: -DBS_NET_CAP=Ec6p10l2 -DBS_NET_LOW=ec6p10l2 with its header)
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -13,6 +14,16 @@
 #define __builtin_amdgcn_sched_barrier(x) ((void)0)
 namespace cfsec { namespace dev { inline uint32_t bs_x3(uint32_t a, uint32_t b, uint32_t c) { return a ^ b ^ c; } } }
 #include BS_NET_HDR
+#ifndef BS_NET_CAP
+#define BS_NET_CAP Ec16p20l2
+#define BS_NET_LOW ec16p20l2
+#endif
+#define BS_CAT3(a, b, c) a##b##c
+#define BS_PASTE3(a, b, c) BS_CAT3(a, b, c)
+#define BS_NET_TYPE BS_PASTE3(Bs, BS_NET_CAP, )
+#define BS_NET_ROWS BS_PASTE3(kBs, BS_NET_CAP, Rows)
+#define BS_NET_FN BS_PASTE3(bs_net_, BS_NET_LOW, )
+#define BS_NET_ROW_RT BS_PASTE3(bs_row_, BS_NET_LOW, _rt)
 
 static void swapmove(uint32_t& a, uint32_t& b, int s, uint32_t m) {
   const uint32_t t = ((a >> s) ^ b) & m;
@@ -37,7 +48,7 @@ static uint8_t gmul(uint8_t a, uint8_t b) {
 
 int main() {
   using namespace cfsec::dev;
-  constexpr int K = BsEc16p20l2::K, M = BsEc16p20l2::M;
+  constexpr int K = BS_NET_TYPE::K, M = BS_NET_TYPE::M;
   srand(12345);
   long bad = 0;
   for (int trial = 0; trial < 200; ++trial) {
@@ -50,18 +61,18 @@ int main() {
         x[8 * c + w] = in[c][4 * w] | in[c][4 * w + 1] << 8 | in[c][4 * w + 2] << 16 | (uint32_t)in[c][4 * w + 3] << 24;
       transpose8(&x[8 * c]);
     }
-    if (kBsEc16p20l2Paired)
+    if (BS_NET_TYPE::Paired)
       for (int c = 0; c < K; c += 2)
         for (int j = 0; j < 8; ++j) x[8 * c + j] ^= x[8 * (c + 1) + j];
     int seen = 0;
-    bs_net_ec16p20l2<M>(x, [&](int r, uint32_t (&o)[8]) {
+    BS_NET_FN<M>(x, [&](int r, uint32_t (&o)[8]) {
       ++seen;
       uint32_t v[8];
       for (int w = 0; w < 8; ++w) v[w] = o[w];
       transpose8(v);
       for (int b = 0; b < 32; ++b) {
         uint8_t want = 0;
-        for (int c = 0; c < K; ++c) want ^= gmul(kBsEc16p20l2Rows[r][c], in[c][b]);
+        for (int c = 0; c < K; ++c) want ^= gmul(BS_NET_ROWS[r][c], in[c][b]);
         const uint8_t got = (uint8_t)(v[b / 4] >> (8 * (b % 4)));
         bad += got != want;
       }
@@ -69,11 +80,11 @@ int main() {
     // the run-time single rows too
     for (int r = 0; r < M; ++r) {
       uint32_t o[8];
-      bs_row_ec16p20l2_rt(r, x, o);
+      BS_NET_ROW_RT(r, x, o);
       transpose8(o);
       for (int b = 0; b < 32; ++b) {
         uint8_t want = 0;
-        for (int c = 0; c < K; ++c) want ^= gmul(kBsEc16p20l2Rows[r][c], in[c][b]);
+        for (int c = 0; c < K; ++c) want ^= gmul(BS_NET_ROWS[r][c], in[c][b]);
         bad += (uint8_t)(o[b / 4] >> (8 * (b % 4))) != want;
       }
     }

@@ -4,10 +4,13 @@
 set -o pipefail
 mkdir -p gpurun_out/r6l
 export TMPDIR=/tmp
+CFSEC_BS_CRC=1 timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_bs_crc_fused.py \
+  > gpurun_out/r6l/pytest_bs_crc_w.log 2>&1 || { tail -40 gpurun_out/r6l/pytest_bs_crc_w.log; exit 1; }
+tail -1 gpurun_out/r6l/pytest_bs_crc_w.log
 timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_bs_crc_fused.py \
   > gpurun_out/r6l/pytest_bs_crc.log 2>&1 || { tail -40 gpurun_out/r6l/pytest_bs_crc.log; exit 1; }
 tail -1 gpurun_out/r6l/pytest_bs_crc.log
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_crc.py \
+CFSEC_BS_CRC=1 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_crc.py \
   tests/test_gpu_batch.py -k "crc" > gpurun_out/r6l/pytest_crc.log 2>&1 || { tail -40 gpurun_out/r6l/pytest_crc.log; exit 1; }
 tail -1 gpurun_out/r6l/pytest_crc.log
 for v in 1 5 0 w3; do
@@ -16,6 +19,6 @@ for v in 1 5 0 w3; do
   CFSEC_LIB_PATH=$PWD/$lib CFSEC_BS_CRC=$m timeout -k 10 120 python tools/c4_crc_probe.py >> gpurun_out/r6l/c4.txt 2>&1 || exit $?
 done
 grep -E "==|us per call|all" gpurun_out/r6l/c4.txt
-timeout -k 10 200 ./tools/gf_shapes > gpurun_out/r6l/shapes.txt 2>&1 || exit $?
+CFSEC_BS_CRC=1 timeout -k 10 200 ./tools/gf_shapes > gpurun_out/r6l/shapes.txt 2>&1 || exit $?
 grep -E "EC12P4|EC6P10L2 fused" gpurun_out/r6l/shapes.txt
 exit 0
