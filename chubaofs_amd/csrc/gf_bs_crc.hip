@@ -94,7 +94,10 @@ struct __attribute__((aligned(16))) BcArgs {
   uint32_t tab, crc_stride;
   uint32_t nst, wps, groups;  // the per-row form: stripes, waves per stripe W, wave groups (<= nst)
   uint32_t xjump;             // the per-row form: x^(8 * 2048 * W)
-  uint32_t fin, pad0;    // shift(~0, len) ^ ~0
+  uint32_t fin;               // shift(~0, len) ^ ~0
+  uint32_t bend;              // tiles [0, bend) of a stripe go round the W waves (bend = W floor(tps / W))
+  uint32_t tail, tblk;        // the stripes' last tps - bend tiles: one per wave of workgroups >= tblk
+  uint32_t pad0;
   uint32_t* crc;         // [stripe][crc_stride] checksum words (XOR-accumulated)
   const uint32_t* tabs;  // kBcTabs x 32 words
   uint8_t slot[40];      // checksum word of kernel row i (inputs, then outputs)
@@ -210,12 +213,15 @@ __global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(
   }
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const uint32_t wid = blockIdx.x * kBcWaves + wave;
-  // wave (g, j) = (wid / W, wid % W) takes tiles j, j + W, j + 2W, ... of stripes g, g + groups, ...
+  // wave (g, j) = (wid / W, wid % W) takes tiles j, j + W, ... (< bend) of stripes g, g + groups, ...;
+  // a tail wave (workgroups from tblk on, dispatched as the round waves retire) one tile >= bend
   const uint32_t W = a.wps, g0 = wid / W, j = wid - g0 * W;
-  if (g0 >= a.groups) return;  // no barrier below
+  const bool tailw = blockIdx.x >= a.tblk;
+  const uint32_t tq = (blockIdx.x - a.tblk) * kBcWaves + wave;  // tail waves: stripe tq / tail's tile
+  if (tailw ? tq >= a.tail * a.nst : g0 >= a.groups) return;  // no barrier below
   const uint64_t len = a.len;
   const uint32_t tps = a.tps;
-  if (j >= tps) return;
+  if (!tailw && j >= tps) return;
   const auto in_row = [&](uint32_t s, int i) -> const uint8_t* {
     return a.sstride ? a.ptr[i] + (int64_t)s * a.sstride : a.ptr[(size_t)s * K + i];
   };
@@ -278,16 +284,18 @@ __global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(
       }
     });
   };
-  for (uint32_t s = g0; s < a.nst; s += a.groups) {
+  const uint32_t s0 = tailw ? tq / a.tail : g0, sstep = tailw ? a.nst : a.groups;
+  const uint32_t c0 = tailw ? a.bend + (tq - s0 * a.tail) : j, cend = tailw ? c0 + 1 : a.bend;
+  for (uint32_t s = s0; s < a.nst; s += sstep) {
 #pragma unroll
     for (int i = 0; i < NR; ++i) R[i] = 0u;
     fresh = true;
-    uint32_t c = j;
+    uint32_t c = c0;
     for (;;) {
       const uint64_t po = (uint64_t)c * kBcTile + lane * 16;
       if ((uint64_t)(c + 1) * kBcTile <= len) tile(s, po, std::true_type{});  // wave-uniform
       else tile(s, po, std::false_type{});
-      if (c + W >= tps) break;
+      if (c + W >= cend) break;
       c += W;
       if constexpr (CRC) {
 #pragma unroll
@@ -330,7 +338,7 @@ __global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(
     const uint32_t k = bc_mulmod(bc_mulmod(a.pw[0][e % kBcPow], a.pw[1][(e / kBcPow) % kBcPow]),
                                  a.pw[2][e / (kBcPow * kBcPow)]);
     uint32_t w = bc_mulmod(mine, k);
-    if (j == 0) w ^= a.fin;
+    if (!tailw && j == 0) w ^= a.fin;
     if ((NP == 64 || lane < 32) && row < (uint32_t)NR) atomicXor(a.crc + (size_t)s * a.crc_stride + slot[row], w);
   }
 }
@@ -517,7 +525,24 @@ hipError_t bc_launch(const MatVecJob& job, uint32_t* crc, int crc_stride, const 
     a.wps = (uint32_t)W;
     a.groups = (uint32_t)ng;
     a.xjump = crc_xpow(8 * (int64_t)kBcTile * (int64_t)W);
-    const unsigned grid = (unsigned)((ng * W + kBcWaves - 1) / kBcWaves);
+    unsigned grid = (unsigned)((ng * W + kBcWaves - 1) / kBcWaves);
+    // the remainder tps mod W: in W-strided rounds a third of the waves take one tile more, and a SIMD
+    // whose 3 waves all do leaves the launch a tile late (C4: 320 tiles per row 160 us, 321 tiles 178,
+    // profiles/r06/bs_crc/c4_tail_tiles.txt); as one tile per extra wave those tiles go wherever
+    // waves retire first: C4 187 -> 176 us per put batch, EC6P6L9 158 -> 151, EC12P9 184 -> 173,
+    // EC16P20L2 (32 x 699,051) 330 -> 305; moving a whole round more to tail waves: 181 (C4); plain
+    // products unchanged (profiles/r06/bs_crc/tail_waves_ab.txt).  CFSEC_BC_TAIL: the largest remainder
+    // (percent of W) taken this way (0: the strided rounds only)
+    static const uint32_t tail_pct = env_mask("CFSEC_BC_TAIL", 100);
+    const uint64_t rem = tps % W;
+    a.bend = (uint32_t)tps;
+    a.tail = 0;
+    a.tblk = grid;
+    if (rem && rem * 100 <= (uint64_t)tail_pct * W) {
+      a.bend = (uint32_t)(tps - rem);
+      a.tail = (uint32_t)rem;
+      grid += (unsigned)((rem * ns + kBcWaves - 1) / kBcWaves);
+    }
     hipLaunchKernelGGL((gf_bs_crc_kernel<Net, M, CRC>), dim3(grid), dim3(64 * kBcWaves), 0, st, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
