@@ -33,7 +33,8 @@
 // waves per SIMD): in the shape sweep 64 MiB blobs 190 us against 207 on the lookup-product kernel,
 // 4 MiB blobs 194 vs 185, but in the bench's rotated batches no faster (encode_crc_roofline_frac
 // 0.473-0.481 vs 0.479-0.482, the ec seam 0.463-0.466 vs 0.471-0.475: profiles/r06/bs_crc/
-// bench_ec12p4_ab.txt), so its route (rows of >= 2 MiB) is off by default.  The 16 + 20 code (EC16P20 / EC16P20L2's fused encode, all 36 / 38 rows
+// bench_ec12p4_ab.txt); with the remainder tiles as tail waves (below) it won there too (0.484 -> 0.506)
+// and is routed by default.  The 16 + 20 code (EC16P20 / EC16P20L2's fused encode, all 36 / 38 rows
 // checksummed) had no fused form: 256 VGPRs with 79 spilled at 2 waves per SIMD, still 243.6 -> 218.5 us
 // (EC16P20L2, 64 x 262,144) and 227.5 -> 206.5 us (EC16P20) against the product + separate pass
 // (profiles/r06/bs_crc/shape_sweep_ec16.txt).  A plane-residue form -- the 12 output checksums as linear functions of
@@ -349,15 +350,16 @@ uint32_t env_mask(const char* name, uint32_t dflt) {
   const char* v = std::getenv(name);
   return v && *v ? (uint32_t)std::strtoul(v, nullptr, 0) : dflt;
 }
-// CFSEC_BS_CRC: bit 0 EC6P10L2's fused LRC encode (6 x 12), bit 2 EC16P20 / EC16P20L2 (16 x 20 / 22),
-// bit 4 EC6P8, EC6P10, EC12P9, EC15P12, EC10P4, EC4P4, EC3P3 and the LRC modes EC6P3L3, EC4P4L2,
-// EC6P6L9, EC6P8L10 (the product + separate pass, or for EC6P3L3 the v_perm fused kernel, otherwise) --
-// on by default --, bit 5 the product alone for EC6P6L9 / EC6P8L10's plain fused encodes (on), bit 1
-// EC12P4 (12 x 4) with rows of >= 2 MiB (off: no faster than the
-// lookup-product kernel in the bench), bit 3 EC12P4 at every length (tests); 0 keeps the lookup-product
-// kernels / the separate pass (A/B)
+// CFSEC_BS_CRC: bit 0 EC6P10L2's fused LRC encode (6 x 12), bit 1 EC12P4 (12 x 4; bit 3 the same),
+// bit 2 EC16P20 / EC16P20L2 (16 x 20 / 22), bit 4 EC6P8, EC6P10, EC12P9, EC15P12, EC10P4, EC4P4,
+// EC3P3 and the LRC modes EC6P3L3, EC4P4L2, EC6P6L9, EC6P8L10 (the product + separate pass, or for
+// EC6P3L3 the v_perm fused kernel, otherwise), bit 5 the product alone for EC6P6L9 / EC6P8L10's plain
+// fused encodes -- all on by default; 0 keeps the lookup-product kernels / the separate pass (A/B).
+// EC12P4 was off until the remainder tiles became tail waves: the bench's fused encode + CRC 0.484 ->
+// 0.506, the ec seam 0.478 -> 0.498 (profiles/r06/bs_crc/bench_ec12p4_tail_ab.txt); 4 MiB blobs 183 ->
+// 178 us in the shape sweep (shape_sweep_ec12p4_tail.txt)
 #ifndef CFSEC_BS_CRC_DEFAULT
-#define CFSEC_BS_CRC_DEFAULT 53
+#define CFSEC_BS_CRC_DEFAULT 55
 #endif
 uint32_t bs_crc_mask() {
   static const uint32_t v = env_mask("CFSEC_BS_CRC", CFSEC_BS_CRC_DEFAULT);
@@ -628,9 +630,6 @@ hipError_t launch_bs_plain(const MatVecJob& job, hipStream_t st) {
 bool bs_crc_takes(const MatVecJob& job, int crc_stride, const int* slot) {
   if (!slot || slot[0] < 0 || job.len == 0 || crc_stride > 256 || !bs_crc_matches(job.k, job.m, job.coef)) return false;
   const uint64_t tps = (job.len + kBcTile - 1) / kBcTile;
-  // EC12P4: rows of at least 1024 tiles (2 MiB: the 64 MiB-blob put 207 -> 190 us; 4 MiB blobs are
-  // faster on the lookup-product kernel, 185 vs 194 us), any length with bit 3
-  if (job.k == 12 && job.m == 4 && !(bs_crc_mask() & 8u) && tps < 1024) return false;
   return tps <= (uint64_t)kBcPow * kBcPow * kBcPow && tps * (uint64_t)std::max(job.nstripes, 1) <= 0xFFFFFFFFull;
 }
 

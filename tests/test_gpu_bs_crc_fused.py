@@ -12,10 +12,9 @@ asserts that the bit-sliced route ran.
 
 EC6P10L2's, the 16 + 20 code's (EC16P20, EC16P20L2) and the other modes' routes (EC6P8, EC6P10,
 EC12P9, EC15P12, EC10P4, EC4P4, EC3P3 and the LRC modes EC6P3L3, EC4P4L2, EC6P6L9, EC6P8L10:
-CFSEC_BS_CRC bits 0, 2, 4) are on by default; EC12P4's (bit 1:
-rows of 2 MiB and more; bit 3: every length) is off -- no faster than the lookup-product kernel in the
-bench -- and its cases run in a child process with CFSEC_BS_CRC=63.  The wide LRC modes' plain
-encodes (EC6P6L9, EC6P8L10) take the same kernel without the checksums (bit 5, on).
+CFSEC_BS_CRC bits 0, 2, 4) and EC12P4's (bit 1, or bit 3) are on by default; a child process re-runs
+the module with CFSEC_BS_CRC=61 (EC12P4 through bit 3).  The wide LRC modes' plain encodes (EC6P6L9, EC6P8L10) take the same
+kernel without the checksums (bit 5, on).
 """
 import os
 import subprocess
@@ -31,9 +30,9 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 SIZES = [1, 15, 16, 17, 1023, 1024, 1025, 2047, 2048, 2049, 4095, 4097, 6144, 65539, 174763]
-MASK = int(os.environ.get("CFSEC_BS_CRC", "53"), 0)  # the library default
-ec12p4 = pytest.mark.skipif(not MASK & 8, reason="EC12P4's route is off by default (every length in the child, CFSEC_BS_CRC=63)")
-ec12p4_long = pytest.mark.skipif(not MASK & 10, reason="EC12P4's route is off (CFSEC_BS_CRC without bits 1, 3)")
+MASK = int(os.environ.get("CFSEC_BS_CRC", "55"), 0)  # the library default
+ec12p4 = pytest.mark.skipif(not MASK & 10, reason="EC12P4's route is off (CFSEC_BS_CRC without bits 1, 3)")
+ec12p4_long = ec12p4
 plain = pytest.mark.skipif(not MASK & 32, reason="the wide LRC modes' plain route is off (CFSEC_BS_CRC without bit 5)")
 rs_more = pytest.mark.skipif(not MASK & 16, reason="the other RS modes' route is off (CFSEC_BS_CRC without bit 4)")
 ec16 = pytest.mark.skipif(not MASK & 4, reason="the 16 + 20 code's route is off (CFSEC_BS_CRC without bit 2)")
@@ -179,8 +178,8 @@ def test_ec12p4_large_stripe_vs_separate_pass(rs, monkeypatch, capfd):
 
 @pytest.mark.skipif(os.environ.get("CFSEC_BS_CRC") is not None, reason="the child process itself")
 def test_per_row_form_and_ec12p4_in_child():
-    """This module again with CFSEC_BS_CRC=63: every route on (EC12P4's at every length)."""
-    env = dict(os.environ, CFSEC_BS_CRC="63")
+    """This module again with CFSEC_BS_CRC=61: every route on, EC12P4's through bit 3."""
+    env = dict(os.environ, CFSEC_BS_CRC="61")
     r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", __file__],
                        env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
