@@ -545,6 +545,9 @@ hipError_t bc_launch(const MatVecJob& job, uint32_t* crc, int crc_stride, const 
       a.tail = (uint32_t)rem;
       grid += (unsigned)((rem * ns + kBcWaves - 1) / kBcWaves);
     }
+    if (env_mask("CFSEC_TRACE_CRC", 0))
+      std::fprintf(stderr, "cfsec: bs launch stripes=%d tps=%llu W=%llu groups=%llu tail=%u\n", ns,
+                   (unsigned long long)tps, (unsigned long long)W, (unsigned long long)ng, a.tail);
     hipLaunchKernelGGL((gf_bs_crc_kernel<Net, M, CRC>), dim3(grid), dim3(64 * kBcWaves), 0, st, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
