@@ -354,12 +354,15 @@ uint32_t env_mask(const char* name, uint32_t dflt) {
 // bit 2 EC16P20 / EC16P20L2 (16 x 20 / 22), bit 4 EC6P8, EC6P10, EC12P9, EC15P12, EC10P4, EC4P4,
 // EC3P3 and the LRC modes EC6P3L3, EC4P4L2, EC6P6L9, EC6P8L10 (the product + separate pass, or for
 // EC6P3L3 the v_perm fused kernel, otherwise), bit 5 the product alone for EC6P6L9 / EC6P8L10's plain
-// fused encodes -- all on by default; 0 keeps the lookup-product kernels / the separate pass (A/B).
+// fused encodes, bit 6 EC6P6 and EC16P4 (the EC6P10L2 / 16 + 20 networks' first rows; their v_perm
+// fused kernels before: EC6P6's 1 MiB-blob put 152 -> 131 us, EC16P4 105 -> 103, the put-batch probe
+// 124 -> 117, profiles/r06/bs_crc/ec6p6_ec16p4_ab.txt) -- all on by default --, bit 7 EC6P3 (off: 62 vs
+// 64 us); 0 keeps the lookup-product kernels / the separate pass (A/B).
 // EC12P4 was off until the remainder tiles became tail waves: the bench's fused encode + CRC 0.484 ->
 // 0.506, the ec seam 0.478 -> 0.498 (profiles/r06/bs_crc/bench_ec12p4_tail_ab.txt); 4 MiB blobs 183 ->
 // 178 us in the shape sweep (shape_sweep_ec12p4_tail.txt)
 #ifndef CFSEC_BS_CRC_DEFAULT
-#define CFSEC_BS_CRC_DEFAULT 55
+#define CFSEC_BS_CRC_DEFAULT 119
 #endif
 uint32_t bs_crc_mask() {
   static const uint32_t v = env_mask("CFSEC_BS_CRC", CFSEC_BS_CRC_DEFAULT);
@@ -563,7 +566,7 @@ bool bs_crc_matches(int k, int m, const uint8_t* coef) {
   if ((mask & 10u) && k == 12 && m == 4) return rows_equal<dev::BsEc12p4>(coef, 4);
   if ((mask & 4u) && k == 16 && (m == 20 || m == 22)) return rows_equal<dev::BsEc16p20l2>(coef, m);
   if (mask & 16u) {  // the other RS modes' encodes (EC6P8 / EC6P10 on the EC6P10L2 network's first rows;
-                     // EC6P6 / EC6P3 / EC16P4 / EC12P4 keep their product kernels' fused forms)
+                     // EC6P6, EC16P4, EC6P3: bits 6, 7 below)
     if (k == 6 && (m == 8 || m == 10)) return rows_equal<dev::BsEc6p10l2>(coef, m);
     if (k == 12 && m == 9) return rows_equal<dev::BsEc12p9>(coef, 9);
     if (k == 15 && m == 12) return rows_equal<dev::BsEc15p12>(coef, 12);
@@ -576,6 +579,10 @@ bool bs_crc_matches(int k, int m, const uint8_t* coef) {
     if (k == 6 && m == 15) return rows_equal<dev::BsEc6p6l9>(coef, 15);
     if (k == 6 && m == 18) return rows_equal<dev::BsEc6p8l10>(coef, 18);
   }
+  // EC6P6 and EC16P4 (bit 6), EC6P3 (bit 7): the first rows of the EC6P10L2 / 16 + 20 networks
+  if ((mask & 64u) && k == 6 && m == 6) return rows_equal<dev::BsEc6p10l2>(coef, 6);
+  if ((mask & 64u) && k == 16 && m == 4) return rows_equal<dev::BsEc16p20l2>(coef, 4);
+  if ((mask & 128u) && k == 6 && m == 3) return rows_equal<dev::BsEc6p10l2>(coef, 3);
   return false;
 }
 
@@ -590,7 +597,11 @@ hipError_t launch_bs_crc(const MatVecJob& job, uint32_t* crc, int crc_stride, co
     std::fprintf(stderr, "cfsec: bs crc k=%d m=%d stripes=%d len=%llu\n", job.k, job.m, job.nstripes,
                           (unsigned long long)job.len);
   if (job.k == 6 && job.m == 12) return bc_launch<dev::BsEc6p10l2, 12>(job, crc, crc_stride, slot, st);
-  if (job.k == 6 && job.m == 6) return bc_launch<dev::BsEc6p3l3, 6>(job, crc, crc_stride, slot, st);
+  if (job.k == 6 && job.m == 6 && rows_equal<dev::BsEc6p3l3>(job.coef, 6))
+    return bc_launch<dev::BsEc6p3l3, 6>(job, crc, crc_stride, slot, st);
+  if (job.k == 6 && job.m == 6) return bc_launch<dev::BsEc6p10l2, 6>(job, crc, crc_stride, slot, st);
+  if (job.k == 6 && job.m == 3) return bc_launch<dev::BsEc6p10l2, 3>(job, crc, crc_stride, slot, st);
+  if (job.k == 16 && job.m == 4) return bc_launch<dev::BsEc16p20l2, 4>(job, crc, crc_stride, slot, st);
   if (job.k == 6 && job.m == 15) return bc_launch<dev::BsEc6p6l9, 15>(job, crc, crc_stride, slot, st);
   if (job.k == 6 && job.m == 18) return bc_launch<dev::BsEc6p8l10, 18>(job, crc, crc_stride, slot, st);
   if (job.k == 4 && job.m == 6) return bc_launch<dev::BsEc4p4l2, 6>(job, crc, crc_stride, slot, st);

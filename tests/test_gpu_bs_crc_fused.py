@@ -13,7 +13,7 @@ asserts that the bit-sliced route ran.
 EC6P10L2's, the 16 + 20 code's (EC16P20, EC16P20L2) and the other modes' routes (EC6P8, EC6P10,
 EC12P9, EC15P12, EC10P4, EC4P4, EC3P3 and the LRC modes EC6P3L3, EC4P4L2, EC6P6L9, EC6P8L10:
 CFSEC_BS_CRC bits 0, 2, 4) and EC12P4's (bit 1, or bit 3) are on by default; a child process re-runs
-the module with CFSEC_BS_CRC=61 (EC12P4 through bit 3).  The wide LRC modes' plain encodes (EC6P6L9, EC6P8L10) take the same
+the module with CFSEC_BS_CRC=253 (EC12P4 through bit 3, EC6P3's route on too).  The wide LRC modes' plain encodes (EC6P6L9, EC6P8L10) take the same
 kernel without the checksums (bit 5, on).
 """
 import os
@@ -30,7 +30,7 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 SIZES = [1, 15, 16, 17, 1023, 1024, 1025, 2047, 2048, 2049, 4095, 4097, 6144, 65539, 174763]
-MASK = int(os.environ.get("CFSEC_BS_CRC", "55"), 0)  # the library default
+MASK = int(os.environ.get("CFSEC_BS_CRC", "119"), 0)  # the library default
 ec12p4 = pytest.mark.skipif(not MASK & 10, reason="EC12P4's route is off (CFSEC_BS_CRC without bits 1, 3)")
 ec12p4_long = ec12p4
 plain = pytest.mark.skipif(not MASK & 32, reason="the wide LRC modes' plain route is off (CFSEC_BS_CRC without bit 5)")
@@ -178,8 +178,8 @@ def test_ec12p4_large_stripe_vs_separate_pass(rs, monkeypatch, capfd):
 
 @pytest.mark.skipif(os.environ.get("CFSEC_BS_CRC") is not None, reason="the child process itself")
 def test_per_row_form_and_ec12p4_in_child():
-    """This module again with CFSEC_BS_CRC=61: every route on, EC12P4's through bit 3."""
-    env = dict(os.environ, CFSEC_BS_CRC="61")
+    """This module again with CFSEC_BS_CRC=253: every route on, EC12P4's through bit 3."""
+    env = dict(os.environ, CFSEC_BS_CRC="253")
     r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", __file__],
                        env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
@@ -276,12 +276,18 @@ def test_ec16p20l2_fused_encode_crc(S, monkeypatch, capfd):
             assert crcs[b][i] == crc(w), (b, i)
 
 
-@rs_more
-@pytest.mark.parametrize("k,m", [(6, 8), (6, 10), (12, 9), (15, 12), (10, 4), (4, 4), (3, 3)])
+RS_MORE = [(6, 8), (6, 10), (12, 9), (15, 12), (10, 4), (4, 4), (3, 3)] if MASK & 16 else []
+RS_MORE += [(6, 6), (16, 4)] if MASK & 64 else []
+RS_MORE += [(6, 3)] if MASK & 128 else []
+
+
+@pytest.mark.skipif(not RS_MORE, reason="the other RS modes' routes are off (CFSEC_BS_CRC without bits 4, 6, 7)")
+@pytest.mark.parametrize("k,m", RS_MORE or [(0, 0)])
 @pytest.mark.parametrize("S", [1, 2049, 65539])
 def test_other_rs_modes_encode_crc(rs, k, m, S, monkeypatch, capfd):
-    """EC6P8 / EC6P10 (the EC6P10L2 network's first rows), EC12P9, EC15P12 and EC3P3 (unpaired: k
-    odd), EC10P4 and EC4P4 encodes with every shard checksummed, 3 stripes at an odd pitch."""
+    """EC6P8 / EC6P10 / EC6P6 / EC6P3 (the EC6P10L2 network's first rows), EC16P4 (the 16 + 20
+    network's), EC12P9, EC15P12 and EC3P3 (unpaired: k odd), EC10P4 and EC4P4 encodes with every
+    shard checksummed, 3 stripes at an odd pitch."""
     monkeypatch.setenv("CFSEC_TRACE_CRC", "1")
     nst, pitch = 3, S + 3
     r = np.random.default_rng(k * 1000 + m * 10 + S)
