@@ -1086,6 +1086,21 @@ def other_configs(args, torch, dev, stream, cpu):
           "roofline_frac": frac((k + m) * S1 * nb, ms),
           "avg_launch_ms": round(ms, 4), "algorithmic_bytes_per_launch": (k + m) * S1 * nb,
           "gate": "parity rows zeroed before the timed launches, equal to the golden parity after"}
+    # access's Put checksums every shard right after Encode (stream_put.go:249-253): the same batches
+    # through cfsec_rs_encode_crc_batch, all 12 checksums per blob (zlib-checked)
+    cw1 = torch.zeros((NBATCH, nb * (k + m)), dtype=torch.int32, device=dev)
+    rc = gated_calls(torch, stream, lambda i: r6.encode_crc_batch(pt[i % NBATCH], S1, nb, cw1[i % NBATCH].data_ptr(),
+                                                                   stream=stream),
+                     NBATCH, secs, lambda: b1[:, :, k:, :].zero_(), check1, sync_call=False)
+    w1h = cw1[0].cpu().numpy().view(np.uint32).reshape(nb, k + m)
+    g1h = b1[0, :, :, :S1].cpu().numpy()
+    for s_ in (0, nb - 1):
+        for i in range(k + m):
+            assert int(w1h[s_, i]) == zlib.crc32(g1h[s_, i].tobytes()) & 0xFFFFFFFF, f"C1 checksum {s_} {i}"
+    c1.update({"encode_crc_kernel_ms": round(rc["kernel_ms_per_call"], 4),
+               "encode_crc_roofline_frac": frac((k + m) * S1 * nb, rc["kernel_ms_per_call"]),
+               "encode_crc_over_encode": round(rc["kernel_ms_per_call"] / ms, 3)})
+    del cw1
     if cpu:
         full = O.build_matrix(k, k + m)
         h = b1[0, 0, :k, :S1].cpu().numpy()
