@@ -183,7 +183,14 @@ __global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(
   constexpr int K = Net::K;
   constexpr int NR = K + M;  // checksummed rows: the inputs, then the outputs
   static_assert(NR <= 64, "one lane per row's word");
-  constexpr int NP = NR <= 32 ? 32 : 64;  // the rows padded for the lane fold
+  // the rows padded for the lane fold: log2(NP) halving levels then 6 - log2(NP) lane butterflies, NP -
+  // 1 + 6 - log2(NP) register-steps (8 rows: 10 instead of the 32 a 32-row padding took)
+#ifndef CFSEC_BC_NPMIN
+#define CFSEC_BC_NPMIN 8
+#endif
+  constexpr int NP = NR <= CFSEC_BC_NPMIN ? CFSEC_BC_NPMIN : NR <= 16 ? (16 > CFSEC_BC_NPMIN ? 16 : CFSEC_BC_NPMIN)
+                     : NR <= 32 ? 32 : 64;
+  constexpr int LG = NP == 8 ? 3 : NP == 16 ? 4 : NP == 32 ? 5 : 6;
   __shared__ uint32_t tb[CRC ? kBcTabs * 32 : 1];  // planes, the jump, the lane tree
   __shared__ uint32_t slot[64];  // the rows' word offsets, indexed per lane at the segment ends
   // LI (k > 8: the 16 + 20 code, 38 registers beside 128 input planes): the input rows' Horner registers
@@ -308,9 +315,9 @@ __global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(
     if constexpr (!CRC) continue;
     // the stripe's end of this wave: the 64 lanes' registers folded by recursive halving -- at level k
     // lane pairs l, l ^ 2^k swap halves of their registers and each keeps the sum of one half, the
-    // earlier group's value moved 16 * 2^k bytes on (7 lookups); the 32 padded registers are one per
-    // lane after 5 levels, the 6th combines the two 32-lane halves: 32 register-steps in all instead
-    // of a 32-column basis per register -- so lane l holds row bitrev5(l mod 32)'s sum at the tile's end
+    // earlier group's value moved 16 * 2^k bytes on (7 lookups); the NP padded registers are one per
+    // lane after log2(NP) levels, the rest combine whole lane groups (32 rows: 32 register-steps in all
+    // instead of a 32-column basis per register) -- so lane l holds row bitrev(l mod NP)'s sum
     uint32_t mine;
     {
       uint32_t v[NP];
@@ -318,7 +325,7 @@ __global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(
       for (int i = 0; i < NP; ++i) v[i] = i < NR ? (in_lds(i) ? rin[(wave * NL + lds_row(i)) * 64 + lane] : R[i]) : 0u;
 #pragma unroll
       for (int k = 0; k < 6; ++k) {
-        const int half = NP >> (k + 1) ? NP >> (k + 1) : 1;  // NP = 32: the 6th level combines halves
+        const int half = NP >> (k + 1) ? NP >> (k + 1) : 1;  // past log2(NP): whole registers combined
         const bool halving = (NP >> (k + 1)) != 0;
         const bool up = (lane >> k) & 1u;
 #pragma unroll
@@ -333,14 +340,14 @@ __global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(
       }
       mine = v[0];
     }
-    // lane l holds row bitrev(l) (6 bits for 64 padded rows, 5 of l mod 32 for 32)
-    const uint32_t row = NP == 64 ? __builtin_bitreverse32(lane) >> 26 : __builtin_bitreverse32(lane & 31u) >> 27;
+    // lane l holds row bitrev(l mod NP) (log2(NP) bits)
+    const uint32_t row = __builtin_bitreverse32(lane & (NP - 1u)) >> (32 - LG);
     const uint32_t e = tps - 1 - c;
     const uint32_t k = bc_mulmod(bc_mulmod(a.pw[0][e % kBcPow], a.pw[1][(e / kBcPow) % kBcPow]),
                                  a.pw[2][e / (kBcPow * kBcPow)]);
     uint32_t w = bc_mulmod(mine, k);
     if (!tailw && j == 0) w ^= a.fin;
-    if ((NP == 64 || lane < 32) && row < (uint32_t)NR) atomicXor(a.crc + (size_t)s * a.crc_stride + slot[row], w);
+    if (lane < (uint32_t)NP && row < (uint32_t)NR) atomicXor(a.crc + (size_t)s * a.crc_stride + slot[row], w);
   }
 }
 
