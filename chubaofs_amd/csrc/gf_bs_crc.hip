@@ -135,7 +135,8 @@ __device__ __forceinline__ uint32_t bc_five7(const uint32_t* tb, uint32_t v) {
 #define CFSEC_BC_WPE 3  // waves per SIMD the per-row form is compiled for
 #endif
 #ifndef CFSEC_BC_PROBE
-#define CFSEC_BC_PROBE 0  // timing probes only (wrong words): bit 0 no input-row terms, bit 1 no output-row terms
+#define CFSEC_BC_PROBE 0  // timing probes only (wrong words): bit 0 no input-row terms, bit 1 no output-row terms,
+                          // bit 2 no register jumps
 #endif
 
 // The lane's term of a row from its 8 planes p: 56 lookups, BC_PL planes' worth in flight at a time
@@ -259,7 +260,7 @@ __global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(
       if constexpr (!CRC) {
       } else if constexpr (LI) {
         uint32_t* ri = rin + (wave * NL + i) * 64 + lane;
-        uint32_t v = fresh ? 0u : bc_five7(tb + kBcJump * 32, *ri);
+        uint32_t v = fresh ? 0u : (CFSEC_BC_PROBE & 4) ? *ri : bc_five7(tb + kBcJump * 32, *ri);
         if constexpr (!(CFSEC_BC_PROBE & 1)) v ^= bc_planes(tb, pl);
         *ri = v;
       } else {
@@ -274,7 +275,7 @@ __global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(
       if constexpr (!CRC) {
       } else if constexpr (LO) {
         uint32_t* ri = rin + (wave * NL + lds_row(K + r)) * 64 + lane;
-        uint32_t v = fresh ? 0u : bc_five7(tb + kBcJump * 32, *ri);
+        uint32_t v = fresh ? 0u : (CFSEC_BC_PROBE & 4) ? *ri : bc_five7(tb + kBcJump * 32, *ri);
         if constexpr (!(CFSEC_BC_PROBE & 2)) v ^= bc_planes(tb, o);
         *ri = v;
       } else {
@@ -308,7 +309,7 @@ __global__ __launch_bounds__(64 * kBcWaves) __attribute__((amdgpu_waves_per_eu(
       if constexpr (CRC) {
 #pragma unroll
         for (int i = 0; i < NR; ++i)
-          if (!in_lds(i)) R[i] = bc_five7(tb + kBcJump * 32, R[i]);
+          if (!in_lds(i) && !(CFSEC_BC_PROBE & 4)) R[i] = bc_five7(tb + kBcJump * 32, R[i]);
       }
       fresh = false;
     }
