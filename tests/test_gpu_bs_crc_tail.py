@@ -67,3 +67,44 @@ def test_tail_waves_put_batch(mode, nb, S, monkeypatch, capfd):
         assert orc.encode(ref) == 0
         for i in range(t.N, total):
             assert np.array_equal(got[b, i], ref[i].view()), (b, i)
+
+
+def test_tail_waves_pointer_table_launches(monkeypatch, capfd):
+    """Shards in separate allocations (pointer-table launches of 96 / 16 = 6 stripes, the last one
+    short) at BASELINE C2's row length, so W < tps in the full launches and the tail waves run there:
+    13 EC12P4 stripes through encode_crc_batch, parity vs the plain encode and the C oracle (first and
+    last stripe), every word vs zlib."""
+    from chubaofs_amd import reedsolomon
+    from oracle import oracle as O
+    k, m, S, nst = 12, 4, 5592406, 13
+    g = torch.Generator(device="cuda").manual_seed(0x7A11)
+    sh = [[torch.randint(0, 256, (S,), dtype=torch.uint8, device="cuda", generator=g) if i < k
+           else torch.zeros(S, dtype=torch.uint8, device="cuda") for i in range(k + m)] for _ in range(nst)]
+    ptrs = [t.data_ptr() for st in sh for t in st]
+    enc = reedsolomon.New(k, m)
+    monkeypatch.setenv("CFSEC_TRACE_CRC", "1")
+    crcs = torch.zeros(nst * (k + m), dtype=torch.int32, device="cuda")
+    capfd.readouterr()
+    enc.encode_crc_batch(ptrs, S, nst, crcs.data_ptr())
+    torch.cuda.synchronize()
+    err = capfd.readouterr().err
+    tails = _tails(err)
+    # 6 + 6 + 1 stripes: the two full launches have W = 512 < tps = 2731 (171 tail tiles per stripe),
+    # the lone stripe's launch W = tps
+    assert "bs crc" in err and len(tails) == 3 and all(tails[:2]) and tails[2] == 0, err[-2000:]
+    fused = [[t.cpu().numpy() for t in st] for st in sh]
+    for st in sh:
+        for t in st[k:]:
+            t.zero_()
+    enc.encode_batch(ptrs, S, nst)
+    torch.cuda.synchronize()
+    words = crcs.cpu().numpy().view(np.uint32).reshape(nst, k + m)
+    for s_ in range(nst):
+        for i in range(k + m):
+            assert np.array_equal(fused[s_][i], sh[s_][i].cpu().numpy()), (s_, i)
+            assert int(words[s_][i]) == zlib.crc32(fused[s_][i].tobytes()) & 0xFFFFFFFF, (s_, i)
+    for s_ in (0, nst - 1):
+        want = [fused[s_][i].copy() for i in range(k)] + [np.zeros(S, np.uint8) for _ in range(m)]
+        assert O.encode(k, m, want) == 0
+        for i in range(k, k + m):
+            assert np.array_equal(fused[s_][i], want[i]), (s_, i)
