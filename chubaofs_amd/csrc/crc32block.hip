@@ -22,6 +22,7 @@
 // with shift(~0, size) ^ ~0 folded in by the last block, so the accumulated word is ChecksumIEEE.
 // Every payload byte is read once and written once.
 #include <algorithm>
+#include <cstdlib>
 
 #include "gf_crc.hpp"
 #include "kernels.hpp"
@@ -480,8 +481,15 @@ hipError_t launch(const Crc32BlockJob& j, hipStream_t stream) {
         cap = resident_groups<RING, NTS>();
         cached_dev = dev;
       }
+      // CFSEC_BLK_GRID=1: the whole resident grid, (items mod cap) workgroups taking one block more, so
+      // every CU holds as many workgroups; 0: as few workgroups as give every one the same count (A/B)
+      static const bool full = [] {
+        const char* v = std::getenv("CFSEC_BLK_GRID");
+        return !(v && v[0] == '0');
+      }();
       const unsigned per = cap ? (a.items + cap - 1) / cap : 1;
-      hipLaunchKernelGGL((crc32block_block_kernel<RING, NTS, true>), dim3((a.items + per - 1) / per), dim3(256), 0, stream, a);
+      const unsigned g = full && cap ? std::min(cap, a.items) : (a.items + per - 1) / per;
+      hipLaunchKernelGGL((crc32block_block_kernel<RING, NTS, true>), dim3(g), dim3(256), 0, stream, a);
     } else if (FASTEPI && ONE && EPI && STORE && CRC)
       hipLaunchKernelGGL((crc32block_block_kernel<RING, NTS, false>), dim3(a.items), dim3(256), 0, stream, a);
     else
